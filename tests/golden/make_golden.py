@@ -1,0 +1,148 @@
+"""Generate golden vectors from the REFERENCE itself (run in the build container only).
+
+    OPENBLAS_NUM_THREADS=1 python tests/golden/make_golden.py [runs|prims|all] [config...]
+
+* imports `/root/reference/src/*` and `/root/reference/psd_system/*` as they lie, with the
+  reference's Cython kernels compiled from source into `oracle/_ref` (`oracle/build_ref.py`);
+* third-party packages absent from the image are replaced by `tests/golden/refshim/`
+  (opt_einsum -> numpy.einsum greedy; petsc4py KSPLGMRES -> oracle/petsc_lgmres.py restatement;
+  scikit-sparse / memory_profiler -> unused stubs);
+* the reference's `IneqMatVecWrapper.matvec` returns a memoryview (`cy_src/lgmres_cy.pyx:510`);
+  the "fixed" inequality runs wrap it in `np.asarray`, the "shipped" runs do not;
+* writes `tests/golden/runs.json` (per-seed final metrics + per-Newton-system trace) and
+  `tests/golden/prims.npz` (primitive-level input/output pairs).
+
+Only data is written; no reference source is copied.  The fixtures are consumed by tests/.
+"""
+import json
+import os
+import sys
+import time
+
+os.environ.setdefault("OPENBLAS_NUM_THREADS", "1")
+os.environ.setdefault("OMP_NUM_THREADS", "1")
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.abspath(os.path.join(HERE, "..", ".."))
+REF = "/root/reference"
+sys.path.insert(0, REPO)
+
+import numpy as np  # noqa: E402
+import yaml  # noqa: E402
+
+
+def _import_reference(fixed_ineq=True):
+    sys.path[:0] = [os.path.join(HERE, "refshim"), os.path.join(REPO, "oracle", "_ref"), REF]
+    from oracle.build_ref import build
+    build()
+    import src.tt_ops as rops  # noqa
+    import src.tt_als as rals  # noqa
+    import src.tt_ipm as ripm  # noqa
+    import warnings
+    warnings.simplefilter("default")  # tt_ipm sets "error" at import; re-enabled around runs
+    if fixed_ineq:
+        base = ripm.IneqMatVecWrapper
+
+        class FixedIneqMatVec(base):
+            def matvec(self, x):
+                return np.asarray(base.matvec(self, x))
+
+        ripm.IneqMatVecWrapper = FixedIneqMatVec
+    return rops, rals, ripm
+
+
+PROBLEM_MOD = {"maxcut": "psd_system.maxcut.maxcut", "corr_clust": "psd_system.corr_clust.corr_clust",
+               "graphm": "psd_system.graphm.graphm", "max_stable_set": "psd_system.max_stable_set.max_stable_set"}
+
+
+def run_reference(problem, cfg_name, seed, rank, fixed_ineq=True):
+    """Mirror of `src/utils.py:245-321` (run_and_record) with a per-Newton-system trace hook."""
+    import importlib
+    import warnings
+    rops, rals, ripm = _import_reference(fixed_ineq)
+    with open(os.path.join(REF, "configs", cfg_name + ".yaml")) as f:
+        config = yaml.safe_load(f)
+    mod = importlib.import_module(PROBLEM_MOD[problem])
+    trace = []
+    orig = ripm.tt_infeasible_newton_system
+
+    def hooked(lhs, obj, X, Y, Z, Tt, L, Ladj, b, mask, status):
+        out = orig(lhs, obj, X, Y, Z, Tt, L, Ladj, b, mask, status)
+        st = out[2]
+        trace.append({"mu": float(st.mu), "primal_error": float(st.primal_error),
+                      "dual_error": float(st.dual_error), "centrality_error": float(st.centrality_error),
+                      "sigma": float(st.sigma), "ranksX": rops.tt_ranks(X), "ranksZ": rops.tt_ranks(Z),
+                      "ranksY": rops.tt_ranks(Y), "is_last_iter": bool(st.is_last_iter)})
+        return out
+
+    ripm.tt_infeasible_newton_system = hooked
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")
+        np.random.seed(seed)
+        prob = mod.create_problem(config["dim"], rank)
+        if len(prob) == 5:
+            C, L, b, mask, lag = prob
+        else:
+            C, L, b, lag_y = prob
+            mask = None
+            lag = {"y": lag_y}
+        lag = {k: rops.tt_reshape(v, (4, 4)) for k, v in lag.items()}
+        C = rops.tt_reshape(C, (4,))
+        b = rops.tt_reshape(b, (4,))
+        t2 = time.time()
+        X, Y, Tt, Z, info = ripm.tt_ipm(lag, C, L, b, ineq_mask=mask, max_iter=config["max_iter"], verbose=False,
+                                        gap_tol=float(config["gap_tol"]), op_tol=float(config["op_tol"]),
+                                        warm_up=config["warm_up"], abs_tol=float(config["abs_tol"]),
+                                        aho_direction=False, mals_restarts=config["mals_restarts"],
+                                        max_refinement=config["max_refinement"],
+                                        lambdaStar=float(config.get("lambdaStar", 1)),
+                                        lambdaStarIneq=float(config.get("lambdaStarIneq", 1)))
+        t3 = time.time()
+        gap = abs(rops.tt_inner_prod(X, Z))
+        pr = rops.tt_rank_reduce(rops.tt_sub(rops.tt_fast_matrix_vec_mul(L, rops.tt_reshape(X, (4,))), b), eps=1e-12)
+        feas = rops.tt_inner_prod(pr, pr)
+        dr = rops.tt_rank_reduce(rops.tt_sub(rops.tt_fast_matrix_vec_mul(rops.tt_transpose(L), rops.tt_reshape(Y, (4,)), eps=1e-12),
+                                             rops.tt_rank_reduce(rops.tt_add(rops.tt_reshape(Z, (4,)), C), eps=1e-12)), eps=1e-12)
+        if info["status"].ineq_status is ripm.IneqStatus.ACTIVE:
+            dr = rops.tt_rank_reduce(rops.tt_sub(dr, rops.tt_reshape(Tt, (4,))), eps=1e-12)
+        dfeas = rops.tt_inner_prod(dr, dr)
+    ripm.tt_infeasible_newton_system = orig
+    return {"problem": problem, "config": cfg_name, "seed": seed, "rank": rank, "fixed_ineq": fixed_ineq,
+            "num_iters": int(info["num_iters"]), "runtime": t3 - t2,
+            "sec_per_iter": (t3 - t2) / max(1, int(info["num_iters"])), "gap": float(gap), "feas": float(feas),
+            "dual_feas": float(dfeas), "ranksX": info["ranksX"], "ranksY": info["ranksY"],
+            "ranksZ": info["ranksZ"], "trace": trace, "blas_threads": os.environ.get("OPENBLAS_NUM_THREADS")}
+
+
+RUNS = [
+    ("maxcut", "maxcut_5", 0, 1, True),
+    ("maxcut", "maxcut_5", 319, 1, True),
+    ("maxcut", "maxcut_10", 41, 1, True),
+    ("corr_clust", "corr_clust_9", 764, 1, True),
+    ("corr_clust", "corr_clust_9", 764, 1, False),
+]
+
+
+def make_runs(only=None):
+    path = os.path.join(HERE, "runs.json")
+    out = json.load(open(path)) if os.path.exists(path) else {}
+    for prob, cfg, seed, rank, fixed in RUNS:
+        key = f"{cfg}_r{rank}_s{seed}" + ("" if fixed else "_shipped")
+        if only and cfg not in only and key not in only:
+            continue
+        print("running reference", key, flush=True)
+        res = run_reference(prob, cfg, seed, rank, fixed)
+        print(key, {k: res[k] for k in ("num_iters", "gap", "feas", "dual_feas", "sec_per_iter")}, flush=True)
+        out[key] = res
+        with open(path, "w") as f:
+            json.dump(out, f, indent=1)
+
+
+if __name__ == "__main__":
+    what = sys.argv[1] if len(sys.argv) > 1 else "all"
+    rest = sys.argv[2:]
+    if what in ("runs", "all"):
+        make_runs(rest or None)
+    if what in ("prims", "all"):
+        from tests.golden import make_prims
+        make_prims.main(_import_reference)
