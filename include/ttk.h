@@ -1,0 +1,141 @@
+/*
+ * ttk.h -- C ABI of the MI355X (gfx950) TT-IPM hot-path library `libttk.so`.
+ *
+ * The reference has no C ABI: its native boundary is the Cython module surface
+ * (`cy_src/tt_ops_cy.pyx`, `cy_src/lgmres_cy.pyx`) plus LAPACK/PETSc reached through SciPy and
+ * petsc4py.  Every entry point below replaces one of those native calls; the
+ * reference interface each one stands in for is cited next to it.  The Python host layer
+ * (`ttipm_amd`) re-exposes them under the reference's names (tt_rank_reduce, MatVecWrapper, ...).
+ *
+ * Conventions
+ *   - all tensors are fp64, device-resident, caller-owned (the library never frees caller memory);
+ *   - strided operands are described by int64 offset tables that live in device memory
+ *     (built once per (equation, shapes) plan on the host and cached, like the reference's
+ *     LRU-cached opt_einsum expressions, `src/tt_ops.py:22-28`);
+ *   - `stream` is a hipStream_t passed as void* (NULL = default stream);
+ *   - every function returns an int status (TTK_OK = 0); no C++ exception crosses the ABI;
+ *     `ttk_last_error()` returns a thread-local message for the last failure;
+ *   - functions whose name ends in `_sync` block on `stream` and return host scalars that drive
+ *     host-side decisions (rank truncation, convergence tests).
+ */
+#ifndef TTK_H
+#define TTK_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum ttk_status {
+  TTK_OK = 0,
+  TTK_ERR_ARG = 1,          /* invalid argument / shape */
+  TTK_ERR_HIP = 2,          /* HIP runtime error */
+  TTK_ERR_NOT_PD = 3,       /* Cholesky: matrix not positive definite (scipy LinAlgError) */
+  TTK_ERR_SINGULAR = 4,     /* LU / triangular: exact zero pivot (scipy LinAlgError) */
+  TTK_ERR_NOT_CONVERGED = 5 /* iterative kernel hit its sweep cap */
+};
+
+const char *ttk_last_error(void);
+int ttk_version(void);
+/* number of kernel launches issued since load (profiling / launch-count tests) */
+long long ttk_launch_count(void);
+
+/* ---------------------------------------------------------------------------------------
+ * Contractions.  One pairwise step of a planned einsum:
+ *   C[b,m,n] = alpha * sum_k A[b,m,k] * B[b,k,n] + beta * C[b,m,n]
+ * with A[b,m,k] = A[a_b[b] + a_m[m] + a_k[k]] etc.  `offs` (device, int64) holds the nine
+ * offset tables back to back: a_b(nb) a_m(M) a_k(K) b_b(nb) b_k(K) b_n(N) c_b(nb) c_m(M) c_n(N).
+ * fp64 MFMA (v_mfma_f64_16x16x4_f64), 32x32 output tile per 256-thread workgroup, K staged
+ * through LDS.  Replaces every `cached_einsum` / `np.tensordot` step on the path
+ * (`src/tt_ops.py:26-28`, `src/tt_als.py:190-265`, `cy_src/tt_ops_cy.pyx:399,413,441,458`)
+ * and the dgemm chain of `MatVecWrapper` (`cy_src/lgmres_cy.pyx:36-49,126-153`).
+ * ------------------------------------------------------------------------------------- */
+int ttk_gemm_offs(void *stream, const double *A, const double *B, double *C, const int64_t *offs,
+                  int nb, int M, int N, int K, double alpha, double beta);
+
+/* Grouped variant: `ngroups` independent GEMMs of identical (nb,M,N,K) in one launch; operand
+ * base pointers are device arrays of pointers (group g uses Aptr[g], Bptr[g], Cptr[g]). */
+int ttk_gemm_offs_grouped(void *stream, const double *const *Aptr, const double *const *Bptr,
+                          double *const *Cptr, const int64_t *offs, int ngroups, int nb, int M,
+                          int N, int K, double alpha, double beta);
+
+/* ---------------------------------------------------------------------------------------
+ * Strided element-wise kernels (up to 6-D).  `shape`, `sstride`, `dstride` are host arrays.
+ * copy:  dst = alpha * src + beta * dst     (tt_add block-diagonal assembly
+ *        `cy_src/tt_ops_cy.pyx:228-258`, transposes/permute copies, tt_scale `:94-114`)
+ * mul:   dst = alpha * src * src2 + beta*dst (inv_I o v, `cy_src/lgmres_cy.pyx:107-120`)
+ * recip: dst = 1 / src                        (`np.divide(1, ...)`, `src/tt_ipm.py:191`)
+ * ------------------------------------------------------------------------------------- */
+int ttk_copy_nd(void *stream, const double *src, double *dst, int ndim, const int64_t *shape,
+                const int64_t *sstride, const int64_t *dstride, double alpha, double beta);
+int ttk_mul_nd(void *stream, const double *src, const double *src2, double *dst, int ndim,
+               const int64_t *shape, const int64_t *sstride, const int64_t *s2stride,
+               const int64_t *dstride, double alpha, double beta);
+int ttk_recip(void *stream, const double *src, double *dst, int64_t n);
+int ttk_fill(void *stream, double *dst, int64_t n, double value);
+int ttk_add_diag(void *stream, double *A, int n, int lda, double value);
+
+/* Reductions (strided up to 6-D), result copied to the host: sum(x*y), sum(x*x). */
+int ttk_dot_nd_sync(void *stream, const double *x, const double *y, int ndim, const int64_t *shape,
+                    const int64_t *xstride, const int64_t *ystride, double *result);
+/* batched sums of squares over `nb` contiguous slices of length n with stride `bstride`;
+ * `out` is a device array of nb doubles (no sync). */
+int ttk_sumsq_batched(void *stream, const double *x, int64_t n, int nb, int64_t bstride, double *out);
+/* copy `n` device doubles to the host (blocking) */
+int ttk_read_sync(void *stream, const double *src, double *host_dst, int64_t n);
+
+/* ---------------------------------------------------------------------------------------
+ * Small dense factorisations, one 256..1024-thread workgroup each (matrices staged in LDS
+ * when they fit, L2-resident global scratch otherwise).  Row-major, leading dimension = cols.
+ * ------------------------------------------------------------------------------------- */
+/* thin SVD A(m,n) = U(m,k) diag(S) Vt(k,n), k = min(m,n), S descending; one-sided Jacobi.
+ * Replaces scipy.linalg.svd(gesvd/gesdd) in `cy_src/tt_ops_cy.pyx:205-211,404,418`,
+ * `src/tt_als.py:269-274,331,457,1024,1171` and friends. `work` >= ttk_svd_work(m,n) doubles. */
+int64_t ttk_svd_work(int m, int n);
+int ttk_svd(void *stream, const double *A, int m, int n, double *U, double *S, double *Vt,
+            double *work);
+/* economic Householder QR A(m,n) = Q(m,k) R(k,n), k=min(m,n)  (scipy.linalg.qr economic,
+ * `cy_src/tt_ops_cy.pyx:147-151`, `src/tt_als.py:358,482`). */
+int64_t ttk_qr_work(int m, int n);
+int ttk_qr(void *stream, const double *A, int m, int n, double *Q, double *R, double *work);
+/* Cholesky (lower) in place on A(n,n); status TTK_ERR_NOT_PD like LAPACK potrf info>0
+ * (`src/tt_ipm.py:204-207,300-303`). Blocks on the stream to return the status. */
+int ttk_cholesky_sync(void *stream, double *A, int n);
+/* triangular solve with matrix RHS B(n,nrhs) in place: op(L) X = B, L lower (trans=0) or
+ * L^T (trans=1) (`forward_backward_sub`, `src/tt_ipm.py:178-181`). */
+int ttk_trsm_lower(void *stream, const double *L, int n, double *B, int nrhs, int ldb, int trans);
+/* LU with partial pivoting in place (getrf) + rcond estimate (gecon, 1-norm, Hager/Higham);
+ * `piv` device int[n]; returns TTK_ERR_SINGULAR on an exact zero pivot.  `rcond_out` host.
+ * (`scipy.linalg.solve(assume_a='gen')` / `lu_factor`, `src/tt_ipm.py:215,320,323`) */
+int ttk_lu_sync(void *stream, double *A, int n, int *piv, double *work, double *rcond_out);
+/* solve with LU factors, B(n,nrhs) in place (getrs) */
+int ttk_lu_solve(void *stream, const double *LU, int n, const int *piv, double *B, int nrhs, int ldb);
+/* symmetric eigen-decomposition A(n,n) = W diag(ev) W^T, cyclic Jacobi, ev ascending,
+ * W columns = eigenvectors (replaces ARPACK eigsh / lobpcg on the step-size local problems,
+ * `src/tt_als.py:963-993,1069-1098,1308`). */
+int64_t ttk_syev_work(int n);
+int ttk_syev(void *stream, double *A, int n, double *ev, double *W, double *work);
+
+/* ---------------------------------------------------------------------------------------
+ * LGMRES building blocks (PETSc KSPLGMRES semantics, see oracle/petsc_lgmres.py):
+ * one Arnoldi orthogonalisation + Hessenberg/Givens update per call.  V is (ldv x n)
+ * row-major (vector j at V + j*n); `hh` (HH|HES|GRS|CC|SS packed, see ttk_lgmres.hip) lives
+ * on the device; the new residual estimate and the breakdown flags are returned to the host
+ * (blocking).  Replaces PETSc KSP lgmres (`src/tt_ipm.py:101-154`). */
+/* res_out[2] = {new residual estimate |GRS(it+1)|, HH(it,it) after rotation};
+ * flags_out[2] = {happy breakdown, DIVERGED_NULL (zero rotation norm)} */
+int ttk_lgmres_arnoldi_sync(void *stream, double *V, int n, int it, double *hh, int max_k,
+                            double haptol, double *res_out, int *flags_out);
+/* Build the correction y = HH \ GRS (in place in GRS), temp = sum_j y_j basis_j where the
+ * basis list is given as a device pointer array of `nvec` vectors; x += temp; aug_temp = temp. */
+int ttk_lgmres_build(void *stream, double *hh, int max_k, int it, const double *const *basis,
+                     int nvec, int n, double *x, double *aug_temp);
+/* A*aug = V (HES y) / nrm over it_total+1 basis vectors (LGMRES augmentation bookkeeping). */
+int ttk_lgmres_aug(void *stream, const double *hh, int max_k, int it_total, const double *V,
+                   int n, double unused, const double *aug_temp, double *augvec, double *a_augvec);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TTK_H */

@@ -1,0 +1,85 @@
+"""ctypes binding of libttk.so (the HIP C ABI, include/ttk.h).
+
+The product path has no CPU fallback: importing this module on a machine without the built
+library raises immediately, and every wrapper raises on a non-zero status."""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libttk.so")
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(f"libttk.so not found at {LIB_PATH}: run `python __graft_entry__.py build` "
+                      "(hipcc --offload-arch=gfx950); the MI355X path has no CPU fallback")
+
+lib = ctypes.CDLL(LIB_PATH)
+
+c_dp = ctypes.POINTER(ctypes.c_double)
+c_i64p = ctypes.POINTER(ctypes.c_int64)
+c_ip = ctypes.POINTER(ctypes.c_int)
+vp = ctypes.c_void_p
+i32 = ctypes.c_int
+i64 = ctypes.c_int64
+f64 = ctypes.c_double
+
+_SIGS = {
+    "ttk_last_error": (ctypes.c_char_p, []),
+    "ttk_version": (i32, []),
+    "ttk_launch_count": (ctypes.c_longlong, []),
+    "ttk_gemm_offs": (i32, [vp, vp, vp, vp, vp, i32, i32, i32, i32, f64, f64]),
+    "ttk_gemm_offs_grouped": (i32, [vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, f64, f64]),
+    "ttk_copy_nd": (i32, [vp, vp, vp, i32, c_i64p, c_i64p, c_i64p, f64, f64]),
+    "ttk_mul_nd": (i32, [vp, vp, vp, vp, i32, c_i64p, c_i64p, c_i64p, c_i64p, f64, f64]),
+    "ttk_recip": (i32, [vp, vp, vp, i64]),
+    "ttk_fill": (i32, [vp, vp, i64, f64]),
+    "ttk_add_diag": (i32, [vp, vp, i32, i32, f64]),
+    "ttk_dot_nd_sync": (i32, [vp, vp, vp, i32, c_i64p, c_i64p, c_i64p, c_dp]),
+    "ttk_sumsq_batched": (i32, [vp, vp, i64, i32, i64, vp]),
+    "ttk_read_sync": (i32, [vp, vp, c_dp, i64]),
+    "ttk_svd_work": (i64, [i32, i32]),
+    "ttk_svd": (i32, [vp, vp, i32, i32, vp, vp, vp, vp]),
+    "ttk_qr_work": (i64, [i32, i32]),
+    "ttk_qr": (i32, [vp, vp, i32, i32, vp, vp, vp]),
+    "ttk_cholesky_sync": (i32, [vp, vp, i32]),
+    "ttk_trsm_lower": (i32, [vp, vp, i32, vp, i32, i32, i32]),
+    "ttk_lu_sync": (i32, [vp, vp, i32, vp, vp, c_dp]),
+    "ttk_lu_solve": (i32, [vp, vp, i32, vp, vp, i32, i32]),
+    "ttk_syev_work": (i64, [i32]),
+    "ttk_syev": (i32, [vp, vp, i32, vp, vp, vp]),
+    "ttk_lgmres_arnoldi_sync": (i32, [vp, vp, i32, i32, vp, i32, f64, c_dp, c_ip]),
+    "ttk_lgmres_build": (i32, [vp, vp, i32, i32, ctypes.POINTER(vp), i32, i32, vp, vp]),
+    "ttk_lgmres_aug": (i32, [vp, vp, i32, i32, vp, i32, f64, vp, vp, vp]),
+}
+
+for _name, (_res, _args) in _SIGS.items():
+    _f = getattr(lib, _name)
+    _f.restype = _res
+    _f.argtypes = _args
+
+EXPORTED = tuple(_SIGS)
+
+TTK_OK, TTK_ERR_ARG, TTK_ERR_HIP, TTK_ERR_NOT_PD, TTK_ERR_SINGULAR, TTK_ERR_NOT_CONVERGED = range(6)
+
+
+class TTKError(RuntimeError):
+    pass
+
+
+class LinAlgError(ValueError):
+    """Raised where LAPACK/SciPy would raise scipy.linalg.LinAlgError (potrf/getrf failure)."""
+
+
+class LinAlgWarning(RuntimeWarning):
+    """Raised (as an exception, like the reference's warnings-as-errors, src/tt_ipm.py:16) where
+    scipy.linalg.solve would warn about an ill-conditioned matrix."""
+
+
+def check(status, what=""):
+    if status == TTK_OK:
+        return
+    msg = lib.ttk_last_error().decode(errors="replace")
+    if status == TTK_ERR_NOT_PD:
+        raise LinAlgError(msg)
+    if status == TTK_ERR_SINGULAR:
+        raise LinAlgError(msg)
+    raise TTKError(f"{what}: status {status}: {msg}")

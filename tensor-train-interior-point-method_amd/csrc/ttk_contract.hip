@@ -1,0 +1,308 @@
+// Core-contraction kernel: one pairwise step of a planned einsum as an offset-table GEMM on
+// fp64 MFMA (v_mfma_f64_16x16x4_f64).
+//
+//   C[b,m,n] = alpha * sum_k A[a_b[b]+a_m[m]+a_k[k]] * B[b_b[b]+b_k[k]+b_n[n]] + beta * C[...]
+//
+// Offset tables (int64, device) make any strided / permuted operand layout free: the TT-core
+// contractions of the hot path ('lsr,lML,sMNS,rNR->LSR', 'lsr,smnS,LSR,rnR->lmL', ...) are
+// executed as 2-3 of these steps with no transpose copies (the reference pays explicit
+// transpose-copies between its dgemms, cy_src/lgmres_cy.pyx:56-120).
+//
+// Tile: 32x32 outputs per 256-thread workgroup = 2x2 waves, each wave one 16x16 MFMA tile.
+// K is staged through LDS 16 at a time (4 MFMAs per wave per stage).  f64 MFMA lane maps
+// (MI355X guide §3): A[i=l&15][k=l>>4], B[k=l>>4][j=l&15], D: col=l&15, row=(l>>4)+4*r.
+#include "ttk_common.h"
+
+namespace {
+
+constexpr int TM = 32, TN = 32, TK = 16;
+
+struct GemmArgs {
+  const double *A;
+  const double *B;
+  double *C;
+  const int64_t *offs;
+  int nb, M, N, K;
+  double alpha, beta;
+};
+
+struct GroupPtrs {
+  const double *const *A;
+  const double *const *B;
+  double *const *C;
+};
+
+typedef double double4_t __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void gemm_tile(const double *__restrict__ A, const double *__restrict__ B,
+                                          double *__restrict__ C, const int64_t *__restrict__ offs,
+                                          int nb, int M, int N, int K, double alpha, double beta,
+                                          int b, int m0, int n0) {
+  __shared__ double As[TK][TM + 1];
+  __shared__ double Bs[TK][TN + 1];
+  const int64_t *a_b = offs;
+  const int64_t *a_m = a_b + nb;
+  const int64_t *a_k = a_m + M;
+  const int64_t *b_b = a_k + K;
+  const int64_t *b_k = b_b + nb;
+  const int64_t *b_n = b_k + K;
+  const int64_t *c_b = b_n + N;
+  const int64_t *c_m = c_b + nb;
+  const int64_t *c_n = c_m + M;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1;
+  const int64_t abase = a_b[b], bbase = b_b[b];
+  // each thread stages 2 A and 2 B elements per K stage
+  const int la_m0 = tid & 31, la_k0 = tid >> 5;  // (m, k) and (m, k+8)
+  const int lb_n0 = tid & 31, lb_k0 = tid >> 5;
+  const bool am_ok = (m0 + la_m0) < M;
+  const bool bn_ok = (n0 + lb_n0) < N;
+  const int64_t aoff_m = am_ok ? a_m[m0 + la_m0] : 0;
+  const int64_t boff_n = bn_ok ? b_n[n0 + lb_n0] : 0;
+  double4_t acc = {0.0, 0.0, 0.0, 0.0};
+  for (int k0 = 0; k0 < K; k0 += TK) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int kk = la_k0 + 8 * h;
+      const int k = k0 + kk;
+      As[kk][la_m0] = (am_ok && k < K) ? A[abase + aoff_m + a_k[k]] : 0.0;
+      Bs[kk][lb_n0] = (bn_ok && k < K) ? B[bbase + b_k[k] + boff_n] : 0.0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < TK / 4; ++s) {
+      const double a = As[s * 4 + (lane >> 4)][wr * 16 + (lane & 15)];
+      const double bv = Bs[s * 4 + (lane >> 4)][wc * 16 + (lane & 15)];
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bv, acc, 0, 0, 0);
+    }
+    __syncthreads();
+  }
+  const int col = n0 + wc * 16 + (lane & 15);
+  if (col >= N) return;
+  const int64_t cb = c_b[b] + c_n[col];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int row = m0 + wr * 16 + (lane >> 4) + 4 * r;
+    if (row < M) {
+      double *p = C + cb + c_m[row];
+      const double v = alpha * acc[r];
+      *p = (beta == 0.0) ? v : v + beta * (*p);
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void gemm_offs_kernel(GemmArgs g) {
+  const int n0 = blockIdx.x * TN, m0 = blockIdx.y * TM, b = blockIdx.z;
+  gemm_tile(g.A, g.B, g.C, g.offs, g.nb, g.M, g.N, g.K, g.alpha, g.beta, b, m0, n0);
+}
+
+__global__ __launch_bounds__(256) void gemm_offs_grouped_kernel(GemmArgs g, GroupPtrs p) {
+  const int n0 = blockIdx.x * TN, m0 = blockIdx.y * TM;
+  const int grp = blockIdx.z / g.nb, b = blockIdx.z % g.nb;
+  gemm_tile(p.A[grp], p.B[grp], p.C[grp], g.offs, g.nb, g.M, g.N, g.K, g.alpha, g.beta, b, m0, n0);
+}
+
+// ------------------------------------------------------------------ element-wise (N-D strided)
+__device__ __forceinline__ void nd_offsets(const ttk::NdDesc &d, int64_t lin, int64_t &o0,
+                                           int64_t &o1, int64_t &o2) {
+  o0 = o1 = o2 = 0;
+  for (int i = d.ndim - 1; i >= 0; --i) {
+    const int64_t e = d.shape[i];
+    const int64_t q = lin / e;
+    const int64_t r = lin - q * e;
+    lin = q;
+    o0 += r * d.s0[i];
+    o1 += r * d.s1[i];
+    o2 += r * d.s2[i];
+  }
+}
+
+__global__ void copy_nd_kernel(const double *__restrict__ src, double *__restrict__ dst,
+                               ttk::NdDesc d, double alpha, double beta) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < d.total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t os, od, unused;
+    nd_offsets(d, i, os, od, unused);
+    const double v = alpha * src[os];
+    dst[od] = (beta == 0.0) ? v : v + beta * dst[od];
+  }
+}
+
+__global__ void mul_nd_kernel(const double *__restrict__ s1, const double *__restrict__ s2,
+                              double *__restrict__ dst, ttk::NdDesc d, double alpha, double beta) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < d.total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t o1, o2, od;
+    nd_offsets(d, i, o1, o2, od);
+    const double v = alpha * s1[o1] * s2[o2];
+    dst[od] = (beta == 0.0) ? v : v + beta * dst[od];
+  }
+}
+
+__global__ void recip_kernel(const double *__restrict__ src, double *__restrict__ dst, int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    dst[i] = 1.0 / src[i];
+}
+
+__global__ void fill_kernel(double *dst, int64_t n, double v) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    dst[i] = v;
+}
+
+__global__ void add_diag_kernel(double *A, int n, int lda, double v) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) A[(int64_t)i * lda + i] += v;
+}
+
+__global__ void dot_nd_kernel(const double *__restrict__ x, const double *__restrict__ y, ttk::NdDesc d,
+                              double *out) {
+  __shared__ double red[16];
+  double acc = 0.0;
+  for (int64_t i = threadIdx.x; i < d.total; i += blockDim.x) {
+    int64_t ox, oy, unused;
+    nd_offsets(d, i, ox, oy, unused);
+    acc += x[ox] * y[oy];
+  }
+  acc = ttk::block_sum(acc, red);
+  if (threadIdx.x == 0) out[0] = acc;
+}
+
+__global__ void sumsq_batched_kernel(const double *__restrict__ x, int64_t n, int64_t bstride, double *out) {
+  __shared__ double red[16];
+  const double *xb = x + blockIdx.x * bstride;
+  double acc = 0.0;
+  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) acc += xb[i] * xb[i];
+  acc = ttk::block_sum(acc, red);
+  if (threadIdx.x == 0) out[blockIdx.x] = acc;
+}
+
+int make_nd(ttk::NdDesc &d, int ndim, const int64_t *shape, const int64_t *s0, const int64_t *s1,
+            const int64_t *s2) {
+  if (ndim < 0 || ndim > ttk::MAXD) {
+    ttk::set_error("ndim %d out of range (max %d)", ndim, ttk::MAXD);
+    return TTK_ERR_ARG;
+  }
+  d.ndim = ndim;
+  d.total = 1;
+  for (int i = 0; i < ndim; ++i) {
+    d.shape[i] = shape[i];
+    d.s0[i] = s0 ? s0[i] : 0;
+    d.s1[i] = s1 ? s1[i] : 0;
+    d.s2[i] = s2 ? s2[i] : 0;
+    d.total *= shape[i];
+  }
+  return TTK_OK;
+}
+
+inline int grid_for(int64_t n, int block) {
+  int64_t g = (n + block - 1) / block;
+  if (g < 1) g = 1;
+  if (g > 4096) g = 4096;
+  return static_cast<int>(g);
+}
+
+double *g_dev_scalar = nullptr;
+
+}  // namespace
+
+extern "C" {
+
+int ttk_gemm_offs(void *stream, const double *A, const double *B, double *C, const int64_t *offs,
+                  int nb, int M, int N, int K, double alpha, double beta) {
+  if (nb <= 0 || M <= 0 || N <= 0) return TTK_OK;
+  if (K <= 0 || nb > 65535) {
+    ttk::set_error("ttk_gemm_offs: bad shape nb=%d M=%d N=%d K=%d", nb, M, N, K);
+    return TTK_ERR_ARG;
+  }
+  GemmArgs g{A, B, C, offs, nb, M, N, K, alpha, beta};
+  dim3 grid((N + TN - 1) / TN, (M + TM - 1) / TM, nb);
+  hipLaunchKernelGGL(gemm_offs_kernel, grid, dim3(256), 0, TTK_STREAM(stream), g);
+  TTK_LAUNCH_CHECK();
+  return TTK_OK;
+}
+
+int ttk_gemm_offs_grouped(void *stream, const double *const *Aptr, const double *const *Bptr,
+                          double *const *Cptr, const int64_t *offs, int ngroups, int nb, int M,
+                          int N, int K, double alpha, double beta) {
+  if (ngroups <= 0 || nb <= 0 || M <= 0 || N <= 0) return TTK_OK;
+  if (K <= 0 || (int64_t)nb * ngroups > 65535) {
+    ttk::set_error("ttk_gemm_offs_grouped: bad shape");
+    return TTK_ERR_ARG;
+  }
+  GemmArgs g{nullptr, nullptr, nullptr, offs, nb, M, N, K, alpha, beta};
+  GroupPtrs p{Aptr, Bptr, Cptr};
+  dim3 grid((N + TN - 1) / TN, (M + TM - 1) / TM, nb * ngroups);
+  hipLaunchKernelGGL(gemm_offs_grouped_kernel, grid, dim3(256), 0, TTK_STREAM(stream), g, p);
+  TTK_LAUNCH_CHECK();
+  return TTK_OK;
+}
+
+int ttk_copy_nd(void *stream, const double *src, double *dst, int ndim, const int64_t *shape,
+                const int64_t *sstride, const int64_t *dstride, double alpha, double beta) {
+  ttk::NdDesc d;
+  int st = make_nd(d, ndim, shape, sstride, dstride, nullptr);
+  if (st) return st;
+  if (d.total == 0) return TTK_OK;
+  hipLaunchKernelGGL(copy_nd_kernel, dim3(grid_for(d.total, 256)), dim3(256), 0, TTK_STREAM(stream), src,
+                     dst, d, alpha, beta);
+  TTK_LAUNCH_CHECK();
+  return TTK_OK;
+}
+
+int ttk_mul_nd(void *stream, const double *src, const double *src2, double *dst, int ndim,
+               const int64_t *shape, const int64_t *sstride, const int64_t *s2stride,
+               const int64_t *dstride, double alpha, double beta) {
+  ttk::NdDesc d;
+  int st = make_nd(d, ndim, shape, sstride, s2stride, dstride);
+  if (st) return st;
+  if (d.total == 0) return TTK_OK;
+  hipLaunchKernelGGL(mul_nd_kernel, dim3(grid_for(d.total, 256)), dim3(256), 0, TTK_STREAM(stream), src,
+                     src2, dst, d, alpha, beta);
+  TTK_LAUNCH_CHECK();
+  return TTK_OK;
+}
+
+int ttk_recip(void *stream, const double *src, double *dst, int64_t n) {
+  if (n <= 0) return TTK_OK;
+  hipLaunchKernelGGL(recip_kernel, dim3(grid_for(n, 256)), dim3(256), 0, TTK_STREAM(stream), src, dst, n);
+  TTK_LAUNCH_CHECK();
+  return TTK_OK;
+}
+
+int ttk_fill(void *stream, double *dst, int64_t n, double value) {
+  if (n <= 0) return TTK_OK;
+  hipLaunchKernelGGL(fill_kernel, dim3(grid_for(n, 256)), dim3(256), 0, TTK_STREAM(stream), dst, n, value);
+  TTK_LAUNCH_CHECK();
+  return TTK_OK;
+}
+
+int ttk_add_diag(void *stream, double *A, int n, int lda, double value) {
+  if (n <= 0) return TTK_OK;
+  hipLaunchKernelGGL(add_diag_kernel, dim3(grid_for(n, 256)), dim3(256), 0, TTK_STREAM(stream), A, n, lda, value);
+  TTK_LAUNCH_CHECK();
+  return TTK_OK;
+}
+
+int ttk_dot_nd_sync(void *stream, const double *x, const double *y, int ndim, const int64_t *shape,
+                    const int64_t *xstride, const int64_t *ystride, double *result) {
+  ttk::NdDesc d;
+  int st = make_nd(d, ndim, shape, xstride, ystride, nullptr);
+  if (st) return st;
+  if (!g_dev_scalar) TTK_HIP(hipMalloc(reinterpret_cast<void **>(&g_dev_scalar), 64 * sizeof(double)));
+  if (d.total == 0) {
+    *result = 0.0;
+    return TTK_OK;
+  }
+  hipLaunchKernelGGL(dot_nd_kernel, dim3(1), dim3(1024), 0, TTK_STREAM(stream), x, y, d, g_dev_scalar);
+  TTK_LAUNCH_CHECK();
+  return ttk_read_sync(stream, g_dev_scalar, result, 1);
+}
+
+int ttk_sumsq_batched(void *stream, const double *x, int64_t n, int nb, int64_t bstride, double *out) {
+  if (nb <= 0) return TTK_OK;
+  hipLaunchKernelGGL(sumsq_batched_kernel, dim3(nb), dim3(256), 0, TTK_STREAM(stream), x, n, bstride, out);
+  TTK_LAUNCH_CHECK();
+  return TTK_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,210 @@
+// LGMRES (PETSc KSPLGMRES semantics) building blocks on the device.
+//
+// The Krylov basis V, the Hessenberg matrices and the Givens rotations stay in HBM/L2; the host
+// only runs the integer bookkeeping of the restart/augmentation loop and reads ONE scalar
+// (the new residual estimate) per Arnoldi step for the convergence test -- the same decision
+// PETSc's KSPConvergedDefault takes (oracle/petsc_lgmres.py restates the algorithm).
+//
+// hh layout (doubles, ld = max_k+1):  HH[(max_k+2) x ld] | HES[(max_k+2) x ld] | GRS[max_k+2]
+//                                     | CC[ld] | SS[ld] | status[8]
+#include <math.h>
+
+#include "ttk_common.h"
+
+namespace {
+
+struct HH {
+  double *hh, *hes, *grs, *cc, *ss, *st;
+  int ld;
+  __device__ HH(double *base, int max_k) {
+    ld = max_k + 1;
+    hh = base;
+    hes = hh + (max_k + 2) * ld;
+    grs = hes + (max_k + 2) * ld;
+    cc = grs + (max_k + 2);
+    ss = cc + ld;
+    st = ss + ld;
+  }
+};
+
+constexpr int MAXV = 128;
+struct PtrList {
+  const double *p[MAXV];
+};
+
+// KSPGMRESClassicalGramSchmidtOrthogonalization (REFINE_NEVER) + new HH/HES column +
+// happy-breakdown test + KSPLGMRESUpdateHessenberg.  st[0]=res, st[1]=hapend, st[2]=null,
+// st[3]=HH(it,it) after rotation.
+__global__ __launch_bounds__(1024) void arnoldi_kernel(double *V, int n, int it, double *base, int max_k,
+                                                       double haptol) {
+  __shared__ double h[MAXV + 2];
+  __shared__ double red[16];
+  HH H(base, max_k);
+  const int tid = threadIdx.x, nt = blockDim.x;
+  const int lane = tid & 63, wid = tid >> 6, nw = nt >> 6;
+  double *w = V + (int64_t)(it + 1) * n;
+  // h_j = <V_j, w>, j = 0..it (one wave per j)
+  for (int j = wid; j <= it; j += nw) {
+    const double *vj = V + (int64_t)j * n;
+    double s = 0.0;
+    for (int i = lane; i < n; i += 64) s += vj[i] * w[i];
+    s = ttk::wave_sum(s);
+    if (lane == 0) h[j] = s;
+  }
+  __syncthreads();
+  // w -= sum_j h_j V_j
+  for (int i = tid; i < n; i += nt) {
+    double acc = w[i];
+    for (int j = 0; j <= it; ++j) acc -= h[j] * V[(int64_t)j * n + i];
+    w[i] = acc;
+  }
+  __syncthreads();
+  double s2 = 0.0;
+  for (int i = tid; i < n; i += nt) s2 += w[i] * w[i];
+  s2 = ttk::block_sum(s2, red);
+  const double tt = sqrt(s2);
+  const int ld = H.ld;
+  for (int j = tid; j <= it; j += nt) {
+    H.hh[j * ld + it] = h[j];
+    H.hes[j * ld + it] = h[j];
+  }
+  double hapbnd = fabs(tt / H.grs[it]);
+  if (hapbnd > haptol) hapbnd = haptol;
+  const bool hapend = !(tt > hapbnd);
+  if (!hapend) {
+    const double inv = 1.0 / tt;
+    for (int i = tid; i < n; i += nt) w[i] *= inv;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    H.hh[(it + 1) * ld + it] = tt;
+    H.hes[(it + 1) * ld + it] = tt;
+    for (int j = 1; j <= it; ++j) {
+      const double t0 = H.hh[(j - 1) * ld + it];
+      const double t1 = H.hh[j * ld + it];
+      H.hh[(j - 1) * ld + it] = H.cc[j - 1] * t0 + H.ss[j - 1] * t1;
+      H.hh[j * ld + it] = H.cc[j - 1] * t1 - H.ss[j - 1] * t0;
+    }
+    double res = 0.0, null_flag = 0.0;
+    if (!hapend) {
+      const double hv = H.hh[it * ld + it], hv1 = H.hh[(it + 1) * ld + it];
+      const double tr = sqrt(hv * hv + hv1 * hv1);
+      if (tr == 0.0) {
+        null_flag = 1.0;
+      } else {
+        H.cc[it] = hv / tr;
+        H.ss[it] = hv1 / tr;
+        H.grs[it + 1] = -(H.ss[it] * H.grs[it]);
+        H.grs[it] = H.cc[it] * H.grs[it];
+        H.hh[it * ld + it] = H.cc[it] * hv + H.ss[it] * hv1;
+        res = fabs(H.grs[it + 1]);
+      }
+    }
+    H.st[0] = res;
+    H.st[1] = hapend ? 1.0 : 0.0;
+    H.st[2] = null_flag;
+    H.st[3] = H.hh[it * ld + it];
+  }
+}
+
+// KSPLGMRESBuildSoln: back substitution in place in GRS, temp = sum y_j basis_j, x += temp.
+__global__ __launch_bounds__(1024) void build_kernel(double *base, int max_k, int it, PtrList basis, int nvec,
+                                                     int n, double *x, double *aug_temp) {
+  __shared__ double y[MAXV + 2];
+  HH H(base, max_k);
+  const int ld = H.ld;
+  const int tid = threadIdx.x, nt = blockDim.x;
+  if (tid == 0) {
+    H.grs[it] = H.grs[it] / H.hh[it * ld + it];
+    for (int k = it - 1; k >= 0; --k) {
+      double t0 = H.grs[k];
+      for (int j = k + 1; j <= it; ++j) t0 -= H.hh[k * ld + j] * H.grs[j];
+      H.grs[k] = t0 / H.hh[k * ld + k];
+    }
+    for (int j = 0; j <= it; ++j) y[j] = H.grs[j];
+  }
+  __syncthreads();
+  for (int i = tid; i < n; i += nt) {
+    double t = 0.0;
+    for (int j = 0; j < nvec; ++j) t += y[j] * basis.p[j][i];
+    aug_temp[i] = t;
+    x[i] += t;
+  }
+}
+
+// A*aug = V (HES y) / ||aug_temp||, augvec = aug_temp / ||aug_temp||
+__global__ __launch_bounds__(1024) void aug_kernel(const double *base_c, int max_k, int it_total, const double *V,
+                                                   int n, const double *aug_temp, double *augvec, double *a_augvec) {
+  __shared__ double avec[MAXV + 2];
+  __shared__ double red[16];
+  HH H(const_cast<double *>(base_c), max_k);
+  const int ld = H.ld;
+  const int tid = threadIdx.x, nt = blockDim.x;
+  if (tid == 0) {
+    for (int j = 0; j <= it_total; ++j) avec[j] = 0.0;
+    for (int ii = 0; ii <= it_total; ++ii)
+      for (int jj = 0; jj <= ii + 1 && jj <= it_total; ++jj) avec[jj] += H.hes[jj * ld + ii] * H.grs[ii];
+  }
+  double s2 = 0.0;
+  for (int i = tid; i < n; i += nt) s2 += aug_temp[i] * aug_temp[i];
+  s2 = ttk::block_sum(s2, red);
+  const double inv = 1.0 / sqrt(s2);
+  for (int i = tid; i < n; i += nt) {
+    augvec[i] = aug_temp[i] * inv;
+    double t = 0.0;
+    for (int j = 0; j <= it_total; ++j) t += avec[j] * V[(int64_t)j * n + i];
+    a_augvec[i] = t * inv;
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int ttk_lgmres_arnoldi_sync(void *stream, double *V, int n, int it, double *hh, int max_k, double haptol,
+                            double *res_out, int *hapend_out) {
+  if (it + 1 > MAXV || max_k + 2 > MAXV + 2) {
+    ttk::set_error("ttk_lgmres_arnoldi_sync: restart %d too large (max %d)", max_k, MAXV);
+    return TTK_ERR_ARG;
+  }
+  hipLaunchKernelGGL(arnoldi_kernel, dim3(1), dim3(1024), 0, TTK_STREAM(stream), V, n, it, hh, max_k, haptol);
+  TTK_LAUNCH_CHECK();
+  const int ld = max_k + 1;
+  const int64_t st_off = 2 * (int64_t)(max_k + 2) * ld + (max_k + 2) + 2 * ld;
+  double st[4];
+  int rc = ttk_read_sync(stream, hh + st_off, st, 4);
+  if (rc) return rc;
+  res_out[0] = st[0];
+  res_out[1] = st[3];
+  hapend_out[0] = (int)st[1];
+  hapend_out[1] = (int)st[2];
+  return TTK_OK;
+}
+
+int ttk_lgmres_build(void *stream, double *hh, int max_k, int it, const double *const *basis, int nvec, int n,
+                     double *x, double *aug_temp) {
+  if (nvec > MAXV || it + 1 > MAXV) {
+    ttk::set_error("ttk_lgmres_build: too many basis vectors %d", nvec);
+    return TTK_ERR_ARG;
+  }
+  PtrList pl;
+  for (int j = 0; j < nvec; ++j) pl.p[j] = basis[j];
+  hipLaunchKernelGGL(build_kernel, dim3(1), dim3(1024), 0, TTK_STREAM(stream), hh, max_k, it, pl, nvec, n, x, aug_temp);
+  TTK_LAUNCH_CHECK();
+  return TTK_OK;
+}
+
+int ttk_lgmres_aug(void *stream, const double *hh, int max_k, int it_total, const double *V, int n,
+                   double inv_nrm_unused, const double *aug_temp, double *augvec, double *a_augvec) {
+  (void)inv_nrm_unused;
+  if (it_total + 1 > MAXV) {
+    ttk::set_error("ttk_lgmres_aug: it_total %d too large", it_total);
+    return TTK_ERR_ARG;
+  }
+  hipLaunchKernelGGL(aug_kernel, dim3(1), dim3(1024), 0, TTK_STREAM(stream), hh, max_k, it_total, V, n, aug_temp,
+                     augvec, a_augvec);
+  TTK_LAUNCH_CHECK();
+  return TTK_OK;
+}
+
+}  // extern "C"

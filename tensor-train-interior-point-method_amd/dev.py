@@ -1,0 +1,423 @@
+"""Device op layer: fp64 tensors on the MI355X, every arithmetic op through libttk (HIP).
+
+PyTorch is used only as the allocator / container (torch.empty, views, H2D of host-generated
+random numbers); all arithmetic goes through the C ABI in `include/ttk.h`.
+
+* `einsum(eq, *ops)`: greedy pairwise plan (the reference plans with opt_einsum greedy and
+  caches the expression per (equation, shapes), `src/tt_ops.py:22-28`); each pairwise step is
+  ONE launch of the offset-table MFMA GEMM (`ttk_gemm_offs`), operands addressed through their
+  strides, so transposed/permuted views cost nothing.  Plans (offset tables in HBM, intermediate
+  buffers) are cached per (equation, shapes, strides).
+* small dense factorisations (`svd`, `qr`, `rq`, `cholesky_`, `lu_`, `syev`), reductions and
+  strided element-wise kernels.
+"""
+import ctypes
+import os
+from functools import lru_cache
+
+import numpy as np
+import torch
+
+from ._lib import LinAlgError, LinAlgWarning, c_dp, c_i64p, check, lib
+
+DEV = torch.device(os.environ.get("TTIPM_DEVICE", "cuda"))
+F64 = torch.float64
+_vp = ctypes.c_void_p
+
+
+def _stream():
+    return torch.cuda.current_stream().cuda_stream if DEV.type == "cuda" else None
+
+
+def _p(t):
+    return t.data_ptr()
+
+
+def empty(*shape):
+    return torch.empty(shape, dtype=F64, device=DEV)
+
+
+def zeros(*shape):
+    return torch.zeros(shape, dtype=F64, device=DEV)
+
+
+def from_numpy(a):
+    return torch.from_numpy(np.array(a, dtype=np.float64, order="C", copy=True)).to(DEV)
+
+
+def contig(t):
+    """t if contiguous, else a contiguous copy made by the HIP copy kernel (never torch)."""
+    return t if t.is_contiguous() else clone(t)
+
+
+def to_numpy(t):
+    return t.detach().to("cpu").numpy()
+
+
+def _arr(vals):
+    a = (ctypes.c_int64 * len(vals))(*vals)
+    return a
+
+
+# ------------------------------------------------------------------------ element-wise
+def copy_(dst, src, alpha=1.0, beta=0.0):
+    """dst = alpha * src + beta * dst (shapes must match; any strides)."""
+    assert tuple(dst.shape) == tuple(src.shape), (dst.shape, src.shape)
+    nd = dst.dim()
+    if nd == 0:
+        dst = dst.reshape(1)
+        src = src.reshape(1)
+        nd = 1
+    shp = _arr(dst.shape)
+    check(lib.ttk_copy_nd(_stream(), _p(src), _p(dst), nd, shp, _arr(src.stride()), _arr(dst.stride()),
+                          float(alpha), float(beta)), "copy_nd")
+    return dst
+
+
+def scaled(src, alpha):
+    out = empty(*src.shape)
+    return copy_(out, src, alpha, 0.0)
+
+
+def clone(src):
+    out = empty(*src.shape)
+    return copy_(out, src)
+
+
+def mul_(dst, a, b, alpha=1.0, beta=0.0):
+    """dst = alpha * a * b + beta * dst (element-wise, same shapes, any strides)."""
+    nd = dst.dim()
+    check(lib.ttk_mul_nd(_stream(), _p(a), _p(b), _p(dst), nd, _arr(dst.shape), _arr(a.stride()),
+                         _arr(b.stride()), _arr(dst.stride()), float(alpha), float(beta)), "mul_nd")
+    return dst
+
+
+def recip(src):
+    src = src.contiguous()
+    out = empty(*src.shape)
+    check(lib.ttk_recip(_stream(), _p(src), _p(out), src.numel()), "recip")
+    return out
+
+
+def fill_(dst, v):
+    assert dst.is_contiguous()
+    check(lib.ttk_fill(_stream(), _p(dst), dst.numel(), float(v)), "fill")
+    return dst
+
+
+def add_diag_(A, v):
+    check(lib.ttk_add_diag(_stream(), _p(A), A.shape[0], A.stride(0), float(v)), "add_diag")
+    return A
+
+
+def dot(x, y):
+    """sum(x*y) over all elements (same shapes), returned to the host."""
+    assert tuple(x.shape) == tuple(y.shape)
+    nd = x.dim()
+    out = ctypes.c_double(0.0)
+    if nd == 0:
+        x, y, nd = x.reshape(1), y.reshape(1), 1
+    check(lib.ttk_dot_nd_sync(_stream(), _p(x), _p(y), nd, _arr(x.shape), _arr(x.stride()), _arr(y.stride()),
+                              ctypes.byref(out)), "dot")
+    return out.value
+
+
+def norm(x):
+    return float(np.sqrt(max(dot(x, x), 0.0)))
+
+
+def read(t):
+    """Copy a (small) device tensor to a host numpy array (blocking)."""
+    t = t.contiguous()
+    out = np.empty(t.shape, dtype=np.float64)
+    if t.numel():
+        check(lib.ttk_read_sync(_stream(), _p(t), out.ctypes.data_as(c_dp), t.numel()), "read")
+    return out
+
+
+# ------------------------------------------------------------------------ einsum planner
+_ONES = {}
+
+
+def _ones_buf():
+    t = _ONES.get("o")
+    if t is None:
+        t = torch.ones(1, dtype=F64, device=DEV)
+        _ONES["o"] = t
+    return t
+
+
+def _parse(eq):
+    eq = eq.replace(" ", "")
+    lhs, out = eq.split("->")
+    return lhs.split(","), out
+
+
+def _group_offsets(group, ext, strides):
+    """Mixed-radix (row-major) enumeration of index group -> summed offsets (int64 array)."""
+    off = np.zeros(1, dtype=np.int64)
+    for c in group:
+        e = ext[c]
+        s = strides.get(c, 0)
+        off = (off[:, None] + np.arange(e, dtype=np.int64)[None, :] * s).reshape(-1)
+    return off
+
+
+def _greedy_path(ins, out, ext):
+    """Pairwise greedy order (min FLOPs of the pair, ties -> smaller result), opt_einsum-style.
+    Returns a list of position tuples in np.einsum_path's contraction-list convention."""
+    live = [set(i) for i in ins]
+    path = []
+    if len(live) == 1:
+        return [(0,)]
+    while len(live) > 1:
+        best = None
+        for i in range(len(live)):
+            for j in range(i + 1, len(live)):
+                keep = set(out)
+                for k, o in enumerate(live):
+                    if k != i and k != j:
+                        keep |= o
+                un = live[i] | live[j]
+                res = un & keep
+                flops = int(np.prod([ext[c] for c in un])) if un else 1
+                size = int(np.prod([ext[c] for c in res])) if res else 1
+                key = (flops, size, i, j)
+                if best is None or key < best[0]:
+                    best = (key, i, j, res)
+        _, i, j, res = best
+        path.append((i, j))
+        live = [o for k, o in enumerate(live) if k not in (i, j)] + [res]
+    return path
+
+
+class _Step:
+    __slots__ = ("a", "b", "out", "nb", "M", "N", "K", "offs", "tmp_shape")
+
+
+class _Plan:
+    __slots__ = ("steps", "out_shape", "tmp")
+
+
+def _contig_strides(idx, ext):
+    st = {}
+    acc = 1
+    for c in reversed(idx):
+        st[c] = acc
+        acc *= ext[c]
+    return st
+
+
+@lru_cache(maxsize=8192)
+def _plan(eq, shapes, strides, out_strides):
+    ins, out = _parse(eq)
+    ext = {}
+    for idx, shp in zip(ins, shapes):
+        for c, e in zip(idx, shp):
+            ext[c] = e
+    out_shape = tuple(ext[c] for c in out)
+    if out_strides is None:
+        out_strides = tuple(_contig_strides(out, ext)[c] for c in out) if out else ()
+    path = _greedy_path(ins, out, ext)
+    # live operands: (idx, strides-dict, slot) ; slot >= 0 input index, < 0 intermediate -(k+1)
+    live = [(idx, dict(zip(idx, st)), i) for i, (idx, st) in enumerate(zip(ins, strides))]
+    steps = []
+    ntmp = 0
+    for si, pair in enumerate(path):
+        last = si == len(path) - 1
+        pair = tuple(sorted(pair, reverse=True))
+        taken = [live.pop(p) for p in pair]
+        taken.reverse()
+        if len(taken) == 1:
+            X, Y = taken[0], ("", {}, "ones")
+        else:
+            X, Y = taken
+        rest = set(out)
+        for o in live:
+            rest |= set(o[0])
+        xs, ys = set(X[0]), set(Y[0])
+        allidx = []
+        for c in X[0] + Y[0]:
+            if c not in allidx:
+                allidx.append(c)
+        if last:
+            order = list(out)
+        else:
+            order = [c for c in allidx if c in rest]
+        batch = [c for c in order if c in xs and c in ys]
+        mgrp = [c for c in order if c in xs and c not in ys]
+        ngrp = [c for c in order if c in ys and c not in xs]
+        kgrp = [c for c in allidx if c not in rest]
+        if last:
+            cst = dict(zip(out, out_strides))
+            res_idx = out
+        else:
+            res_idx = "".join(batch + mgrp + ngrp)
+            cst = _contig_strides(res_idx, ext)
+        tabs = [_group_offsets(batch, ext, X[1]), _group_offsets(mgrp, ext, X[1]), _group_offsets(kgrp, ext, X[1]),
+                _group_offsets(batch, ext, Y[1]), _group_offsets(kgrp, ext, Y[1]), _group_offsets(ngrp, ext, Y[1]),
+                _group_offsets(batch, ext, cst), _group_offsets(mgrp, ext, cst), _group_offsets(ngrp, ext, cst)]
+        st = _Step()
+        st.a, st.b = X[2], Y[2]
+        st.nb, st.M, st.K, st.N = len(tabs[0]), len(tabs[1]), len(tabs[2]), len(tabs[5])
+        st.offs = torch.from_numpy(np.concatenate(tabs)).to(DEV)
+        if last:
+            st.out = "final"
+            st.tmp_shape = None
+        else:
+            st.out = -(ntmp + 1)
+            st.tmp_shape = tuple(ext[c] for c in res_idx)
+            ntmp += 1
+            live.append((res_idx, cst, st.out))
+        steps.append(st)
+    pl = _Plan()
+    pl.steps = steps
+    pl.out_shape = out_shape
+    pl.tmp = [empty(*s.tmp_shape) if s.tmp_shape is not None else None for s in steps]
+    return pl
+
+
+def einsum(eq, *ops, out=None, alpha=1.0, beta=0.0):
+    """out = alpha * einsum(eq, *ops) + beta * out, on the device (fp64 MFMA GEMM steps)."""
+    shapes = tuple(tuple(o.shape) for o in ops)
+    strides = tuple(tuple(o.stride()) for o in ops)
+    pl = _plan(eq, shapes, strides, None if out is None else tuple(out.stride()))
+    if out is None:
+        out = empty(*pl.out_shape)
+        beta = 0.0
+    s = _stream()
+    tmp_by_slot = {}
+    ones = None
+    for st, tmp in zip(pl.steps, pl.tmp):
+        A = ops[st.a] if st.a >= 0 else tmp_by_slot[st.a]
+        if st.b == "ones":
+            if ones is None:
+                ones = _ones_buf()
+            B = ones
+        elif st.b >= 0:
+            B = ops[st.b]
+        else:
+            B = tmp_by_slot[st.b]
+        if st.out == "final":
+            C, al, be = out, alpha, beta
+        else:
+            C, al, be = tmp, 1.0, 0.0
+            tmp_by_slot[st.out] = tmp
+        check(lib.ttk_gemm_offs(s, _p(A), _p(B), _p(C), _p(st.offs), st.nb, st.M, st.N, st.K, float(al), float(be)),
+              "gemm")
+    return out
+
+
+def tensordot(a, b, axes):
+    """numpy-style tensordot via the einsum executor."""
+    ax_a, ax_b = axes
+    letters = "abcdefghijklmnopqrstuvwxyzABCDEFGHIJKLMNOPQRSTUVWXYZ"
+    ia = list(letters[:a.dim()])
+    ib = list(letters[a.dim():a.dim() + b.dim()])
+    for x, y in zip(ax_a, ax_b):
+        ib[y] = ia[x]
+    outi = [c for i, c in enumerate(ia) if i not in ax_a] + [c for i, c in enumerate(ib) if i not in ax_b]
+    return einsum("".join(ia) + "," + "".join(ib) + "->" + "".join(outi), a, b)
+
+
+def matmul(a, b, out=None, alpha=1.0, beta=0.0):
+    return einsum("ik,kj->ij", a, b, out=out, alpha=alpha, beta=beta)
+
+
+# ------------------------------------------------------------------------ factorisations
+def svd(A):
+    """Thin SVD of a 2-D device matrix.  Returns (U, S, Vt, s_host)."""
+    A = A.contiguous()
+    m, n = A.shape
+    k = min(m, n)
+    U, S, Vt = empty(m, k), empty(k), empty(k, n)
+    work = empty(int(lib.ttk_svd_work(m, n)))
+    check(lib.ttk_svd(_stream(), _p(A), m, n, _p(U), _p(S), _p(Vt), _p(work)), "svd")
+    return U, S, Vt, read(S)
+
+
+def qr(A):
+    """Economic Householder QR: A (m,n) = Q (m,k) R (k,n)."""
+    A = A.contiguous()
+    m, n = A.shape
+    k = min(m, n)
+    Q, R = empty(m, k), empty(k, n)
+    work = empty(int(lib.ttk_qr_work(m, n)))
+    check(lib.ttk_qr(_stream(), _p(A), m, n, _p(Q), _p(R), _p(work)), "qr")
+    return Q, R
+
+
+_ANTI = {}
+
+
+def _anti_identity(n):
+    t = _ANTI.get(n)
+    if t is None:
+        t = from_numpy(np.eye(n)[::-1])
+        _ANTI[n] = t
+    return t
+
+
+def rq(M):
+    """Economic RQ (scipy.linalg.rq mode='economic') via QR of the row-reversed transpose:
+    M = R Q with Q orthonormal rows; J = anti-identity, M^T J = Qt Rt  =>  R = J Rt^T J, Q = J Qt^T."""
+    p, q = M.shape
+    k = min(p, q)
+    Jp, Jk = _anti_identity(p), _anti_identity(k)
+    Qt, Rt = qr(einsum("ji,jk->ik", M, Jp))
+    R = einsum("ij,lj,lk->ik", Jp, Rt, Jk)
+    Q = einsum("ij,lj->il", Jk, Qt)
+    return R, Q
+
+
+def cholesky_(A):
+    """In-place lower Cholesky; raises LinAlgError if not positive definite."""
+    assert A.is_contiguous()
+    check(lib.ttk_cholesky_sync(_stream(), _p(A), A.shape[0]), "cholesky")
+    return A
+
+
+def trsm_(L, B, trans=False):
+    """B <- op(L)^{-1} B in place (L lower, row-major contiguous); B (n, nrhs) row-major."""
+    assert L.is_contiguous() and B.stride(1) == 1
+    check(lib.ttk_trsm_lower(_stream(), _p(L), L.shape[0], _p(B), B.shape[1], B.stride(0), int(trans)), "trsm")
+    return B
+
+
+_EPS_E = float(np.finfo(np.float64).eps) / 2  # LAPACK dlamch('E')
+
+
+def lu_(A, check_rcond=True):
+    """In-place getrf; returns pivots.  Raises LinAlgError on an exact zero pivot and, like
+    scipy.linalg.solve under warnings-as-errors, LinAlgWarning when rcond < eps."""
+    assert A.is_contiguous()
+    n = A.shape[0]
+    piv = torch.empty(n, dtype=torch.int32, device=DEV)
+    work = empty(2 * n + 16)
+    rc = ctypes.c_double(0.0)
+    check(lib.ttk_lu_sync(_stream(), _p(A), n, _p(piv), _p(work), ctypes.byref(rc)), "lu")
+    if check_rcond and rc.value < _EPS_E:
+        raise LinAlgWarning(f"Ill-conditioned matrix (rcond={rc.value:.5g}): result may not be accurate.")
+    return piv
+
+
+def lu_solve_(LU, piv, B):
+    assert B.stride(-1) == 1
+    B2 = B.reshape(B.shape[0], -1)
+    check(lib.ttk_lu_solve(_stream(), _p(LU), LU.shape[0], _p(piv), _p(B2), B2.shape[1], B2.stride(0)), "lu_solve")
+    return B
+
+
+def syev(A):
+    """Symmetric eigen-decomposition (Jacobi).  Returns (ev device, W device, ev_host)."""
+    A = clone(A) if not A.is_contiguous() else A.clone()
+    n = A.shape[0]
+    ev, W = empty(n), empty(n, n)
+    work = empty(int(lib.ttk_syev_work(n)))
+    check(lib.ttk_syev(_stream(), _p(A), n, _p(ev), _p(W), _p(work)), "syev")
+    return ev, W, read(ev)
+
+
+__all__ = ["einsum", "tensordot", "matmul", "copy_", "scaled", "clone", "mul_", "recip", "fill_", "add_diag_",
+           "dot", "norm", "read", "svd", "qr", "rq", "cholesky_", "trsm_", "lu_", "lu_solve_", "syev", "empty",
+           "zeros", "from_numpy", "to_numpy", "LinAlgError", "LinAlgWarning"]

@@ -1,0 +1,401 @@
+"""Step-size ALS eigen-solvers on the MI355X -- drop-in for `tt_max_generalised_eigen`
+(`src/tt_als.py:1132-1283`) and `tt_min_eig` (`:1392-1499`).
+
+Environments and two-site local matrices are device contractions (MFMA GEMM steps).  The local
+eigenproblems, which the reference sends to ARPACK `eigsh` (with an `splu` shift-invert polish)
+or `lobpcg`, are solved exactly with the device cyclic-Jacobi eigensolver (`ttk_syev`); the
+generalised problem `-D v = lambda A v` goes through a device Cholesky of A.  The converged
+eigenpair is the same to the reference's tolerance (tol = 1e-8); ARPACK's failure branches
+(exceptions) map to the same fallbacks."""
+import time
+
+import numpy as np
+
+from . import dev as D
+from . import tt_ops as T
+from .dev import einsum
+from .tt_als import compute_phi_bck_A, compute_phi_fwd_A
+
+TWO_SITE = "lsr,smnk,kptS,LSR->lmpLrntR"
+ONE_SITE = "lsr,smnS,LSR->lmLrnR"
+MAX_DENSE = 4096
+
+
+def _sym(Mt, m):
+    M = Mt.view(m, m)
+    S = D.clone(M)
+    D.copy_(S, M.t(), 0.5, 0.5)
+    return S
+
+
+def _min_eigpair(M):
+    ev, W, evh = D.syev(M)
+    return float(evh[0]), D.clone(W[:, 0])
+
+
+def _gen_max_eig(Dm, Am):
+    """largest lambda of -D v = lambda A v (eigsh(-D, M=A, which='LA')); raises if A not PD."""
+    m = Am.shape[0]
+    L = D.clone(Am)
+    D.cholesky_(L)
+    C = D.scaled(Dm, -1.0)
+    D.trsm_(L, C)  # L^-1 (-D)
+    Ct = D.clone(C.t())
+    D.trsm_(L, Ct)  # L^-1 (L^-1 (-D))^T = L^-1 (-D) L^-T
+    S = D.clone(Ct)
+    D.copy_(S, Ct.t(), 0.5, 0.5)
+    ev, W, evh = D.syev(S)
+    y = D.clone(W[:, m - 1:m])
+    D.trsm_(L, y, trans=True)
+    return float(evh[-1]), y.view(-1)
+
+
+def _rayleigh(Am, Dm, step, v):
+    """eig = v^T M v, res = ||M v - eig v|| for M = A/step + D."""
+    M = D.scaled(Am, 1.0 / step)
+    D.copy_(M, Dm, 1.0, 1.0)
+    Mv = D.matmul(M, v.view(-1, 1)).view(-1)
+    ev = D.dot(v, Mv)
+    D.copy_(Mv, v, -ev, 1.0)
+    return ev, D.norm(Mv)
+
+
+def _normalise(v):
+    return D.scaled(v, 1.0 / D.norm(v))
+
+
+def _kick(u, v, r_add):
+    """`_add_kick_rank` (`src/tt_als.py:1041-1046`)."""
+    old = u.shape[-1]
+    uk = D.from_numpy(np.random.randn(u.shape[0], r_add))
+    cat = D.empty(u.shape[0], old + r_add)
+    D.copy_(cat[:, :old], u)
+    D.copy_(cat[:, old:], uk)
+    q, Rm = D.qr(cat)
+    return q, D.matmul(Rm[:, :old], v), q.shape[-1]
+
+
+def _kick_rev(u, v, r_add):
+    """`_add_kick_rank_rev` (`src/tt_als.py:1048-1053`)."""
+    old = v.shape[0]
+    uk = D.from_numpy(np.random.randn(r_add, v.shape[-1]))
+    cat = D.empty(old + r_add, v.shape[-1])
+    D.copy_(cat[:old], v)
+    D.copy_(cat[old:], uk)
+    Rm, q = D.rq(cat)
+    return D.matmul(u, Rm[:old]), q, q.shape[0]
+
+
+def _split(sol, sh, trunc_tol, max_rank, bwd):
+    a, b = sh[0] * sh[1], sh[2] * sh[3]
+    if bwd:
+        U, S, Vt, s = D.svd(D.clone(sol.view(a, b).t()))
+        v = einsum("r,rj->rj", S, Vt)
+        r = min(T.prune_singular_vals(s, trunc_tol), max_rank)
+        s1, s2, r = _kick_rev(D.clone(v[:r].t()), D.clone(U[:, :r].t()), 4)
+        return D.contig(s1).view(sh[0], sh[1], r), D.contig(s2).view(r, sh[2], sh[3])
+    U, S, Vt, s = D.svd(sol.view(a, b))
+    r = min(T.prune_singular_vals(s, trunc_tol), max_rank)
+    s1 = D.clone(U[:, :r])
+    s2 = einsum("r,rj->rj", S[:r], Vt[:r])
+    s1, s2, r = _kick(s1, s2, 4)
+    return D.contig(s1).view(sh[0], sh[1], r), D.contig(s2).view(r, sh[2], sh[3])
+
+
+def _check_dense(m):
+    if m > MAX_DENSE:
+        raise NotImplementedError(f"local eigenproblem of size {m} exceeds the dense device solver cap {MAX_DENSE}")
+
+
+def _step_size_local_solve(p1, p2, XAX_k, A_k, A_kp1, XAX_k2, XDX_k, D_k, D_kp1, XDX_k2, step, size_limit,
+                           trunc_tol, eps, max_rank, bwd=True):
+    """`_step_size_local_solve` (`src/tt_als.py:931-1038`)."""
+    if (not np.isfinite(step)) or step <= 0:
+        return p1, p2, 0.0, np.inf
+    prev = einsum("rny,ytR->rntR", p1, p2)
+    sh = tuple(prev.shape)
+    m = int(np.prod(sh))
+    _check_dense(m)
+    prev = prev.view(-1)
+    Dm = _sym(einsum(TWO_SITE, XDX_k, D_k, D_kp1, XDX_k2), m)
+    Am = _sym(einsum(TWO_SITE, XAX_k, A_k, A_kp1, XAX_k2), m)
+    M = D.scaled(Am, 1.0 / step)
+    D.copy_(M, Dm, 1.0, 1.0)
+    ev, sol = _min_eigpair(M)
+    sol = _normalise(sol)
+    if ev < 0:
+        try:
+            lam, sol = _gen_max_eig(Dm, Am)
+            step = max(0, min(step, 1 / lam))
+        except Exception:
+            sol = prev
+            step *= (1 - eps)
+    _, old_res = _rayleigh(Am, Dm, step, prev)  # 1/step raises ZeroDivisionError at step 0, as in the reference
+    sol = _normalise(sol)
+    s1, s2 = _split(sol, sh, trunc_tol, max_rank, bwd)
+    return s1, s2, step, old_res
+
+
+def _step_size_local_solve_last(prev, XDX_k, Dk, XDX_k1, XAX_k, Ak, XAX_k1, step, eps):
+    """`_step_size_local_solve_last` (`src/tt_als.py:1056-1129`)."""
+    if (not np.isfinite(step)) or step <= 0:
+        return prev.reshape(-1) if prev.is_contiguous() else D.clone(prev).view(-1), 0.0, np.inf
+    m = int(np.prod(prev.shape))
+    _check_dense(m)
+    prev = D.contig(prev).view(-1)
+    Dm = _sym(einsum(ONE_SITE, XDX_k, Dk, XDX_k1), m)
+    Am = _sym(einsum(ONE_SITE, XAX_k, Ak, XAX_k1), m)
+    M = D.scaled(Am, 1.0 / step)
+    D.copy_(M, Dm, 1.0, 1.0)
+    ev, sol = _min_eigpair(M)
+    if ev < 0:
+        try:
+            lam, sol = _gen_max_eig(Dm, Am)
+            step = max(0, min(step, 1 / lam))
+        except Exception:
+            sol = prev
+            step *= (1 - eps)
+    old_res = _rayleigh(Am, Dm, step, prev)[1]
+    return sol, step, old_res
+
+
+def _res_stalled(prev, res, tol):
+    return np.isfinite(prev) and np.isfinite(res) and res <= 50 * tol and res >= 0.8 * prev
+
+
+def _step_stalled(prev_step, step, prev_res, res, tol):
+    if prev_step is None:
+        return False
+    sc = max(abs(step), abs(prev_step), 1.0)
+    return abs(step - prev_step) <= max(10 * tol, 1e-12) * sc and _res_stalled(prev_res, res, tol)
+
+
+def _svd_left(x, k, rx, N, trunc_tol, max_rank):
+    """bck truncation of core k: returns (new core k, factor for core k-1 (R, rnew))."""
+    mat = D.clone(D.contig(x[k]).view(rx[k], N[k] * rx[k + 1]).t())
+    U, S, Vt, s = D.svd(mat)
+    v = einsum("r,rj->rj", S, Vt)
+    r = min(T.prune_singular_vals(s, trunc_tol), max_rank)
+    return D.clone(U[:, :r].t()).view(r, N[k], rx[k + 1]), v[:r], r
+
+
+def tt_max_generalised_eigen(A, Delta, x0=None, nswp=10, tol=1e-8, size_limit=256, verbose=False):
+    """`src/tt_als.py:1132-1283`: largest alpha with A + alpha*Delta >= 0 (two-site ALS)."""
+    if verbose:
+        print(f"\nStarting Eigen solve with:\n \t {tol} \n \t sweeps: {nswp}")
+        t0 = time.time()
+    x = T.tt_random_gaussian([2] * (len(A) - 1), (A[0].shape[2],)) if x0 is None else x0
+    d = len(x)
+    rx = np.array([1] + T.tt_ranks(x) + [1])
+    N = np.array([c.shape[1] for c in x])
+    o3 = T._const("one111", np.ones((1, 1, 1)))
+    XAX = [o3] + [None] * (d - 1) + [o3]
+    XDX = [o3] + [None] * (d - 1) + [o3]
+    step = 1
+    local_res = np.inf * np.ones((2, d - 1))
+    max_rank = int(np.floor(2 ** (d / 2)))
+    trunc_tol = tol / np.sqrt(d)
+    prev_step = None
+    prev_res = np.inf
+    swp = 0
+
+    def finish_fwd():
+        nonlocal step
+        for k in range(d):
+            sol, step, _ = _step_size_local_solve_last(x[k], XDX[k], Delta[k], XDX[k + 1], XAX[k], A[k], XAX[k + 1],
+                                                       step, tol)
+            sol = sol.view(rx[k] * N[k], rx[k + 1])
+            if k < d - 1:
+                U, S, Vt, s = D.svd(sol)
+                v = einsum("r,rj->rj", S, Vt)
+                r = min(T.prune_singular_vals(s, trunc_tol), max_rank)
+                x[k] = D.clone(U[:, :r]).view(rx[k], N[k], r)
+                x[k + 1] = einsum("ij,jkl->ikl", v[:r], x[k + 1])
+                rx[k + 1] = r
+                XAX[k + 1] = compute_phi_fwd_A(XAX[k], x[k], A[k], x[k])
+                XDX[k + 1] = compute_phi_fwd_A(XDX[k], x[k], Delta[k], x[k])
+            else:
+                x[k] = D.contig(sol).view(rx[k], N[k], rx[k + 1])
+
+    def finish_bck():
+        nonlocal step
+        for k in range(d - 1, -1, -1):
+            sol, step, _ = _step_size_local_solve_last(x[k], XDX[k], Delta[k], XDX[k + 1], XAX[k], A[k], XAX[k + 1],
+                                                       step, tol)
+            if k > 0:
+                mat = D.clone(sol.view(rx[k], N[k] * rx[k + 1]).t())
+                U, S, Vt, s = D.svd(mat)
+                v = einsum("r,rj->rj", S, Vt)
+                r = min(T.prune_singular_vals(s, trunc_tol), max_rank)
+                x[k] = D.clone(U[:, :r].t()).view(r, N[k], rx[k + 1])
+                x[k - 1] = einsum("rdc,Rc->rdR", x[k - 1], v[:r])
+                rx[k] = r
+                XAX[k] = compute_phi_bck_A(XAX[k + 1], x[k], A[k], x[k])
+                XDX[k] = compute_phi_bck_A(XDX[k + 1], x[k], Delta[k], x[k])
+            else:
+                x[k] = D.contig(sol).view(rx[k], N[k], rx[k + 1])
+
+    for swp in range(nswp):
+        zero = False
+        for k in range(d - 1, 0, -1):
+            if swp > 0:
+                x[k - 1], x[k], step, res = _step_size_local_solve(
+                    x[k - 1], x[k], XAX[k - 1], A[k - 1], A[k], XAX[k + 1], XDX[k - 1], Delta[k - 1], Delta[k],
+                    XDX[k + 1], step, size_limit, trunc_tol, tol, max_rank, bwd=True)
+                local_res[0, k - 1] = res
+                if step <= 0:
+                    zero = True
+                    break
+            else:
+                x[k], vr, r = _svd_left(x, k, rx, N, trunc_tol, max_rank)
+                x[k - 1] = einsum("rdc,Rc->rdR", x[k - 1], vr)
+            rx[k] = x[k].shape[0]
+            XAX[k] = compute_phi_bck_A(XAX[k + 1], x[k], A[k], x[k])
+            XDX[k] = compute_phi_bck_A(XDX[k + 1], x[k], Delta[k], x[k])
+        if zero:
+            if verbose:
+                print("\tStep size reached zero; stopping eigen sweeps.", flush=True)
+            break
+        if np.max(local_res) < tol or swp == nswp - 1:
+            finish_fwd()
+            break
+        if verbose:
+            print('\tStarting Sweep: %d' % swp)
+            print('\tStep size: %f' % step)
+            print(f'\tResidual {np.max(local_res[0])}')
+        for k in range(d - 1):
+            x[k], x[k + 1], step, res = _step_size_local_solve(
+                x[k], x[k + 1], XAX[k], A[k], A[k + 1], XAX[k + 2], XDX[k], Delta[k], Delta[k + 1], XDX[k + 2],
+                step, size_limit, trunc_tol, tol, max_rank, bwd=False)
+            local_res[1, k] = res
+            if step <= 0:
+                zero = True
+                break
+            rx[k + 1] = x[k + 1].shape[0]
+            XAX[k + 1] = compute_phi_fwd_A(XAX[k], x[k], A[k], x[k])
+            XDX[k + 1] = compute_phi_fwd_A(XDX[k], x[k], Delta[k], x[k])
+        if zero:
+            if verbose:
+                print("\tStep size reached zero; stopping eigen sweeps.", flush=True)
+            break
+        if np.max(local_res) < tol:
+            finish_bck()
+            break
+        sres = np.max(local_res)
+        if swp >= 2 and _step_stalled(prev_step, step, prev_res, sres, tol):
+            if verbose:
+                print("\tEigen sweep stalled; stopping early.", flush=True)
+            break
+        prev_step = step
+        prev_res = sres
+    max_res = np.max(local_res)
+    x = T.tt_normalise(x)
+    if verbose:
+        print(f"\t Solution rank is {rx[1:-1]}\n\t Step size: {step:f}\n\t Residual {max_res}")
+        print('\t Number of sweeps', swp + 1, '\n\t Time: ', time.time() - t0, flush=True)
+    if max_res > tol:
+        print('\t Target Residual not reached!', flush=True)
+        step *= (tol / max_res)
+    return step, x
+
+
+def _eigen_local_solve(p1, p2, XAX_k, A_k, A_kp1, XAX_k2, trunc_tol, max_rank, bwd=True):
+    """`_eigen_local_solve` (`src/tt_als.py:1286-1343`) with a dense device eigensolve."""
+    prev = einsum("rny,ytR->rntR", p1, p2)
+    sh = tuple(prev.shape)
+    m = int(np.prod(sh))
+    _check_dense(m)
+    prev = prev.view(-1)
+    Am = _sym(einsum(TWO_SITE, XAX_k, A_k, A_kp1, XAX_k2), m)
+    ev, sol = _min_eigpair(Am)
+    Ap = D.matmul(Am, prev.view(-1, 1)).view(-1)
+    D.copy_(Ap, prev, ev, -1.0)  # ev*prev - A prev
+    old_res = D.norm(Ap)
+    s1, s2 = _split(sol, sh, trunc_tol, max_rank, bwd)
+    return s1, s2, old_res
+
+
+def _eigen_local_solve_last(prev, XAX_k, A_k, XAX_k1, m):
+    """`_eigen_local_solve_last` (`src/tt_als.py:1346-1389`)."""
+    _check_dense(m)
+    prev = D.contig(prev).view(-1)
+    Am = _sym(einsum(ONE_SITE, XAX_k, A_k, XAX_k1), m)
+    ev, sol = _min_eigpair(Am)
+    return sol
+
+
+def tt_min_eig(A, x0=None, nswp=10, tol=1e-8, size_limit=64, return_eig_val=False, verbose=False):
+    """`tt_min_eig` (`src/tt_als.py:1392-1499`)."""
+    x = T.tt_random_gaussian([2] * (len(A) - 1), (A[0].shape[2],)) if x0 is None else x0
+    d = len(x)
+    rx = np.array([1] + T.tt_ranks(x) + [1])
+    N = np.array([c.shape[1] for c in x])
+    o3 = T._const("one111", np.ones((1, 1, 1)))
+    XAX = [o3] + [None] * (d - 1) + [o3]
+    max_rank = int(np.floor(2 ** (d / 2)))
+    trunc_tol = 0.1 * tol / np.sqrt(d)
+    prev_res = np.inf
+
+    def finish_fwd():
+        for k in range(d):
+            sol = _eigen_local_solve_last(x[k], XAX[k], A[k], XAX[k + 1], int(rx[k] * N[k] * rx[k + 1]))
+            sol = sol.view(rx[k] * N[k], rx[k + 1])
+            if k < d - 1:
+                U, S, Vt, s = D.svd(sol)
+                v = einsum("r,rj->rj", S, Vt)
+                r = min(T.prune_singular_vals(s, trunc_tol), max_rank)
+                x[k] = D.clone(U[:, :r]).view(rx[k], N[k], r)
+                x[k + 1] = einsum("ij,jkl->ikl", v[:r], x[k + 1])
+                rx[k + 1] = r
+                XAX[k + 1] = compute_phi_fwd_A(XAX[k], x[k], A[k], x[k])
+            else:
+                x[k] = D.contig(sol).view(rx[k], N[k], rx[k + 1])
+
+    def finish_bck():
+        for k in range(d - 1, -1, -1):
+            sol = _eigen_local_solve_last(x[k], XAX[k], A[k], XAX[k + 1], int(rx[k] * N[k] * rx[k + 1]))
+            if k > 0:
+                mat = D.clone(sol.view(rx[k], N[k] * rx[k + 1]).t())
+                U, S, Vt, s = D.svd(mat)
+                v = einsum("r,rj->rj", S, Vt)
+                r = min(T.prune_singular_vals(s, trunc_tol), max_rank)
+                x[k] = D.clone(U[:, :r].t()).view(r, N[k], rx[k + 1])
+                x[k - 1] = einsum("rdc,Rc->rdR", x[k - 1], v[:r])
+                rx[k] = r
+                XAX[k] = compute_phi_bck_A(XAX[k + 1], x[k], A[k], x[k])
+            else:
+                x[k] = D.contig(sol).view(rx[k], N[k], rx[k + 1])
+
+    for swp in range(nswp):
+        max_res = np.inf if swp == 0 else 0
+        for k in range(d - 1, 0, -1):
+            if swp > 0:
+                x[k - 1], x[k], lr = _eigen_local_solve(x[k - 1], x[k], XAX[k - 1], A[k - 1], A[k], XAX[k + 1],
+                                                        trunc_tol, max_rank, bwd=True)
+                max_res = max(max_res, lr)
+            else:
+                x[k], vr, r = _svd_left(x, k, rx, N, trunc_tol, max_rank)
+                x[k - 1] = einsum("rdc,Rc->rdR", x[k - 1], vr)
+            rx[k] = x[k].shape[0]
+            XAX[k] = compute_phi_bck_A(XAX[k + 1], x[k], A[k], x[k])
+        if max_res < tol or swp == nswp - 1:
+            finish_fwd()
+            break
+        max_res = 0
+        for k in range(d - 1):
+            x[k], x[k + 1], lr = _eigen_local_solve(x[k], x[k + 1], XAX[k], A[k], A[k + 1], XAX[k + 2],
+                                                    trunc_tol, max_rank, bwd=False)
+            max_res = max(max_res, lr)
+            rx[k + 1] = x[k + 1].shape[0]
+            XAX[k + 1] = compute_phi_fwd_A(XAX[k], x[k], A[k], x[k])
+        if max_res < tol:
+            finish_bck()
+            break
+        if swp >= 2 and _res_stalled(prev_res, max_res, tol):
+            break
+        prev_res = max_res
+    x = T.tt_normalise(x)
+    mev = None
+    if return_eig_val:
+        mev = T.tt_inner_prod(x, T.tt_fast_matrix_vec_mul(A, x, 1e-12))
+    return x, mev

@@ -1,0 +1,840 @@
+"""TT-IPM on the MI355X -- drop-in for `src/tt_ipm.py` (same entry point `tt_ipm`, same
+control flow and status fields).  The Newton/KKT hot path underneath (local KKT solves, AMEn,
+rounding, zip-up products, step-size eigen solves) runs in libttk HIP kernels; this module keeps
+the reference's host-side decisions.
+
+Local KKT solvers (`_ipm_local_solver`, `src/tt_ipm.py:183-282`; `_ipm_local_solver_ineq`,
+`:284-401`): dense Schur path = device assembly (MFMA GEMM), Cholesky, triangular solves, GEMMs
+and LU with the scipy rcond warning rule; iterative path = device LGMRES (PETSc semantics) on
+the Schur-reduced operator of `MatVecWrapper` (`cy_src/lgmres_cy.pyx:291-331`)."""
+import sys
+import traceback
+from dataclasses import dataclass
+from enum import Enum
+
+import numpy as np
+
+from . import dev as D
+from . import tt_ops as T
+from .dev import einsum
+from .lgmres import lgmres
+from .tt_als import (TTBlockMatrix, TTBlockVector, _tt_get_block, tt_mat_mat_mul, tt_mat_vec_mul,
+                     tt_restarted_block_amen)
+from .tt_eig import tt_max_generalised_eigen, tt_min_eig
+
+APPLY = "lsr,smnS,LSR,rnR->lmL"
+APPLY_T = "lsr,smnS,LSR,lmL->rnR"
+ASSEMBLE = "lsr,smnS,LSR->lmLrnR"
+DIAG = "lsr,smnS,LSR->lmL"
+RHS = "br,bmB,BR->rmR"
+
+# True reproduces the shipped reference bug (cy_src/lgmres_cy.pyx:510): the first iterative
+# inequality local solve raises.  Default: fixed (SURVEY.md §7 hard part 6).
+INEQ_MATVEC_BUG = False
+
+
+class IneqMatvecBug(TypeError):
+    pass
+
+
+class MatVecWrapper:
+    """Schur-reduced local KKT operator on [y; x] (`cy_src/lgmres_cy.pyx:203-331`):
+    [B00 y + B01 x ; B21 x - B22 (invI o B01^T y)]."""
+
+    keys = ((0, 0), (0, 1), (2, 1), (2, 2))
+
+    def __init__(self, L, A, R, inv_I, shape):
+        self.L = {k: L[k] for k in self.keys}
+        self.A = {k: A[k] for k in self.keys}
+        self.R = {k: R[k] for k in self.keys}
+        self.inv_I = inv_I
+        self.shape = shape
+        r, n, RR = shape
+        self.m = r * n * RR
+        self.tmp = D.empty(r, n, RR)
+
+    def _parts(self, v, nb):
+        r, n, R = self.shape
+        return [v[i * self.m:(i + 1) * self.m].view(r, n, R) for i in range(nb)]
+
+    def _op(self, key, v, out, alpha=1.0, beta=0.0):
+        einsum(APPLY, self.L[key], self.A[key], self.R[key], v, out=out, alpha=alpha, beta=beta)
+
+    def _schur_x(self, y):
+        einsum(APPLY_T, self.L[0, 1], self.A[0, 1], self.R[0, 1], y, out=self.tmp)
+        D.mul_(self.tmp, self.tmp, self.inv_I)
+        return self.tmp
+
+    def matvec_into(self, v, out):
+        y, x = self._parts(v, 2)
+        o0, o1 = self._parts(out, 2)
+        self._op((0, 0), y, o0)
+        self._op((0, 1), x, o0, beta=1.0)
+        self._op((2, 1), x, o1)
+        self._op((2, 2), self._schur_x(y), o1, alpha=-1.0, beta=1.0)
+        return out
+
+    def matvec(self, v):
+        out = D.empty(v.numel())
+        return self.matvec_into(v, out)
+
+
+class IneqMatVecWrapper(MatVecWrapper):
+    """`cy_src/lgmres_cy.pyx:379-510` on [y; x; t] (with the :510 bug fixed unless INEQ_MATVEC_BUG)."""
+
+    keys = ((0, 0), (0, 1), (2, 1), (2, 2), (3, 1), (3, 3))
+
+    def matvec_into(self, v, out):
+        if INEQ_MATVEC_BUG:
+            raise IneqMatvecBug("reference bug: IneqMatVecWrapper.matvec returns a memoryview")
+        y, x, t = self._parts(v, 3)
+        o0, o1, o2 = self._parts(out, 3)
+        self._op((0, 0), y, o0)
+        self._op((0, 1), x, o0, beta=1.0)
+        self._op((2, 1), x, o1)
+        w = self._schur_x(y)
+        D.copy_(w, t, 1.0, 1.0)
+        self._op((2, 2), w, o1, alpha=-1.0, beta=1.0)
+        self._op((3, 1), x, o2)
+        self._op((3, 3), t, o2, beta=1.0)
+        return out
+
+
+def _report(e):
+    tb = traceback.extract_tb(e.__traceback__)
+    last = tb[-1] if tb else None
+    if last is None:
+        print(f"\t⚠️ {type(e).__name__}: {e}")
+    else:
+        print(f"\t⚠️ {type(e).__name__} in {last.filename},\n\tline {last.lineno}: {last.line.strip()}")
+
+
+def _local_rhs(Xb_k, b_k, Xb_k1, shape, nb):
+    rhs = D.zeros(*shape)
+    for i in range(nb):
+        if i in b_k:
+            einsum(RHS, Xb_k[i], b_k[i], Xb_k1[i], out=rhs[:, i])
+    return rhs
+
+
+def _residual_norm(A_k, XAX_k, XAX_k1, x, rhs, nrhs):
+    res = D.scaled(rhs, -1.0)
+    A_k.block_local_product(XAX_k, XAX_k1, x, out=res)
+    return D.norm(res) / nrhs
+
+
+def _assemble(XAX_k, A_k, XAX_k1, key, m):
+    return einsum(ASSEMBLE, XAX_k[key], A_k[key], XAX_k1[key]).view(m, m)
+
+
+def _fbsub_(LZ, B):
+    """forward_backward_sub (`src/tt_ipm.py:178-181`) in place on B (n, k)."""
+    D.trsm_(LZ, B, trans=False)
+    D.trsm_(LZ, B, trans=True)
+    return B
+
+
+def _run_lgmres(op, rhs_flat, m, rtol):
+    restart = min(m, 100)
+    aug = max(restart // 10, 3)
+    return lgmres(op.matvec_into, rhs_flat, rtol=rtol, max_it=300, restart=restart, augment=aug)
+
+
+def _ipm_local_solver(XAX_k, A_k, XAX_k1, Xb_k, b_k, Xb_k1, prev, size_limit, dense_solve=True, rtol=1e-5):
+    """`_ipm_local_solver` (`src/tt_ipm.py:183-282`) on the device."""
+    xs = tuple(prev.shape)
+    r, n, R = xs[0], xs[2], xs[3]
+    m = r * n * R
+    rhs = _local_rhs(Xb_k, b_k, Xb_k1, xs, 3)
+    nrhs = max(D.norm(rhs), 1e-10)
+    inv_I = D.recip(einsum(DIAG, XAX_k[1, 2], A_k[1, 2], XAX_k1[1, 2]))
+    res_old = _residual_norm(A_k, XAX_k, XAX_k1, prev, rhs, nrhs)
+    dense_solve = (np.sqrt(r * R) <= size_limit) and dense_solve and (res_old >= rtol)
+    failed = not dense_solve
+    sol = None
+    if dense_solve:
+        try:
+            rp = rhs[:, 0].reshape(m, 1) if rhs[:, 0].is_contiguous() else D.clone(rhs[:, 0]).view(m, 1)
+            rd = D.clone(rhs[:, 1]).view(m, 1)
+            rc = D.clone(rhs[:, 2]).view(m, 1)
+            rp = D.clone(rhs[:, 0]).view(m, 1)
+            LXI = _assemble(XAX_k, A_k, XAX_k1, (2, 2), m)
+            D.mul_(LXI, LXI, inv_I.view(1, m).expand(m, m))
+            Leq = _assemble(XAX_k, A_k, XAX_k1, (0, 1), m)
+            LZ = _assemble(XAX_k, A_k, XAX_k1, (2, 1), m)
+            D.cholesky_(LZ)
+            t = D.clone(rc)
+            D.matmul(LXI, rd, out=t, alpha=-1.0, beta=1.0)
+            _fbsub_(LZ, t)
+            bvec = D.clone(rp)
+            D.matmul(Leq, t, out=bvec, alpha=-1.0, beta=1.0)
+            _fbsub_(LZ, LXI)
+            T1 = D.matmul(LXI, Leq.t())
+            Am = D.matmul(Leq, T1)
+            einsum(ASSEMBLE, XAX_k[0, 0], A_k[0, 0], XAX_k1[0, 0], out=Am.view(r, n, R, r, n, R), beta=1.0)
+            D.add_diag_(Am, 1e-11)
+            piv = D.lu_(Am)
+            D.lu_solve_(Am, piv, bvec)
+            sol = D.empty(*xs)
+            D.copy_(sol[:, 0], bvec.view(r, n, R))
+            t2 = D.clone(rd).view(r, n, R)
+            einsum(APPLY_T, XAX_k[0, 1], A_k[0, 1], XAX_k1[0, 1], sol[:, 0], out=t2, alpha=-1.0, beta=1.0)
+            D.mul_(sol[:, 2], t2, inv_I)
+            t3 = D.clone(rc).view(r, n, R)
+            einsum(APPLY, XAX_k[2, 2], A_k[2, 2], XAX_k1[2, 2], sol[:, 2], out=t3, alpha=-1.0, beta=1.0)
+            _fbsub_(LZ, t3.view(m, 1))
+            D.copy_(sol[:, 1], t3)
+        except Exception as e:
+            print(e)
+            _report(e)
+            failed = True
+    if not dense_solve or failed:
+        op = MatVecWrapper(XAX_k, A_k, XAX_k1, inv_I, (r, n, R))
+        lrhs = D.empty(2 * m)
+        l0, l1 = lrhs[:m].view(r, n, R), lrhs[m:].view(r, n, R)
+        D.copy_(l0, rhs[:, 0])
+        D.copy_(l1, rhs[:, 2])
+        w = D.empty(r, n, R)
+        D.mul_(w, inv_I, rhs[:, 1])
+        einsum(APPLY, XAX_k[2, 2], A_k[2, 2], XAX_k1[2, 2], w, out=l1, alpha=-1.0, beta=1.0)
+        lnorm = D.norm(lrhs)
+        pv = D.empty(2 * m)
+        D.copy_(pv.view(2, r, n, R), prev[:, :2].permute(1, 0, 2, 3))
+        lvec = op.matvec(pv)
+        diff = D.clone(lrhs)
+        D.copy_(diff, lvec, -1.0, 1.0)
+        use_prev = D.norm(diff) < lnorm
+        if use_prev:
+            lrhs = diff
+        it_fail = False
+        try:
+            lsol = _run_lgmres(op, lrhs, m, rtol)
+        except Exception as e:
+            _report(e)
+            it_fail = True
+            failed = True
+            sol = prev
+        if not it_fail:
+            sol = D.empty(*xs)
+            D.copy_(sol[:, :2], lsol.view(2, r, n, R).permute(1, 0, 2, 3))
+            if use_prev:
+                D.copy_(sol[:, :2], prev[:, :2], 1.0, 1.0)
+            zt = D.clone(rhs[:, 1])
+            einsum(APPLY_T, XAX_k[0, 1], A_k[0, 1], XAX_k1[0, 1], sol[:, 0], out=zt, alpha=-1.0, beta=1.0)
+            D.mul_(sol[:, 2], inv_I, zt)
+    res_new = _residual_norm(A_k, XAX_k, XAX_k1, sol, rhs, nrhs)
+    if res_old < res_new:
+        sol = prev
+    return sol, res_old, min(res_old, res_new), rhs, nrhs, failed
+
+
+def _ipm_local_solver_ineq(XAX_k, A_k, XAX_k1, Xb_k, b_k, Xb_k1, prev, size_limit, dense_solve=True, rtol=1e-5):
+    """`_ipm_local_solver_ineq` (`src/tt_ipm.py:284-401`) on the device."""
+    xs = tuple(prev.shape)
+    r, n, R = xs[0], xs[2], xs[3]
+    m = r * n * R
+    rhs = _local_rhs(Xb_k, b_k, Xb_k1, xs, 4)
+    inv_I = D.recip(einsum(DIAG, XAX_k[1, 2], A_k[1, 2], XAX_k1[1, 2]))
+    nrhs = max(D.norm(rhs), 1e-10)
+    res_old = _residual_norm(A_k, XAX_k, XAX_k1, prev, rhs, nrhs)
+    dense_solve = (np.sqrt(r * R) <= 0.95 * size_limit) and dense_solve and (res_old >= rtol)
+    failed = not dense_solve
+    sol = None
+    if dense_solve:
+        try:
+            LZ = _assemble(XAX_k, A_k, XAX_k1, (2, 1), m)
+            D.cholesky_(LZ)
+            rp, rd, rc, rt = (D.clone(rhs[:, i]).view(m, 1) for i in range(4))
+            LZ_rc = _fbsub_(LZ, D.clone(rc))
+            LZ_LX = _fbsub_(LZ, _assemble(XAX_k, A_k, XAX_k1, (2, 2), m))
+            Leq = _assemble(XAX_k, A_k, XAX_k1, (0, 1), m)
+            Top = _assemble(XAX_k, A_k, XAX_k1, (3, 1), m)
+            LZ_LXI = D.empty(m, m)
+            D.mul_(LZ_LXI, LZ_LX, inv_I.view(1, m).expand(m, m))
+            w = D.clone(LZ_rc)
+            D.matmul(LZ_LXI, rd, out=w, alpha=-1.0, beta=1.0)
+            u = D.clone(rp)
+            D.matmul(Leq, w, out=u, alpha=-1.0, beta=1.0)
+            v = D.clone(rt)
+            D.matmul(Top, w, out=v, alpha=-1.0, beta=1.0)
+            Am = _assemble(XAX_k, A_k, XAX_k1, (0, 0), m)
+            D.matmul(Leq, D.matmul(LZ_LXI, Leq.t()), out=Am, beta=1.0)
+            Dm = _assemble(XAX_k, A_k, XAX_k1, (3, 3), m)
+            D.matmul(Top, LZ_LX, out=Dm, beta=1.0)
+            D.add_diag_(Dm, 1e-11)
+            Top2 = D.matmul(D.matmul(Top, LZ_LXI), Leq.t())
+            Leq2 = D.matmul(Leq, LZ_LX)
+            dpiv = D.lu_(Dm, check_rcond=False)
+            Dv = D.clone(v)
+            D.lu_solve_(Dm, dpiv, Dv)
+            D.matmul(Leq2, Dv, out=u, alpha=-1.0, beta=1.0)
+            DT = D.clone(Top2)
+            D.lu_solve_(Dm, dpiv, DT)
+            D.matmul(Leq2, DT, out=Am, alpha=-1.0, beta=1.0)
+            piv = D.lu_(Am, check_rcond=False)
+            y = D.clone(u)
+            D.lu_solve_(Am, piv, y)
+            sol = D.empty(*xs)
+            D.copy_(sol[:, 0], y.view(r, n, R))
+            D.matmul(Top2, y, out=v, alpha=-1.0, beta=1.0)
+            D.lu_solve_(Dm, dpiv, v)
+            D.copy_(sol[:, 3], v.view(r, n, R))
+            t2 = D.clone(rd).view(r, n, R)
+            einsum(APPLY_T, XAX_k[0, 1], A_k[0, 1], XAX_k1[0, 1], sol[:, 0], out=t2, alpha=-1.0, beta=1.0)
+            D.mul_(sol[:, 2], t2, inv_I)
+            D.copy_(sol[:, 2], sol[:, 3], -1.0, 1.0)
+            t3 = D.clone(rc).view(r, n, R)
+            einsum(APPLY, XAX_k[2, 2], A_k[2, 2], XAX_k1[2, 2], sol[:, 2], out=t3, alpha=-1.0, beta=1.0)
+            _fbsub_(LZ, t3.view(m, 1))
+            D.copy_(sol[:, 1], t3)
+        except Exception as e:
+            _report(e)
+            failed = True
+    if not dense_solve or failed:
+        op = IneqMatVecWrapper(XAX_k, A_k, XAX_k1, inv_I, (r, n, R))
+        lrhs = D.empty(3 * m)
+        l0, l1, l2 = (lrhs[i * m:(i + 1) * m].view(r, n, R) for i in range(3))
+        D.copy_(l0, rhs[:, 0])
+        D.copy_(l1, rhs[:, 2])
+        w = D.empty(r, n, R)
+        D.mul_(w, inv_I, rhs[:, 1])
+        einsum(APPLY, XAX_k[2, 2], A_k[2, 2], XAX_k1[2, 2], w, out=l1, alpha=-1.0, beta=1.0)
+        D.copy_(l2, rhs[:, 3])
+        lnorm = D.norm(lrhs)
+        pv = D.empty(3 * m)
+        pv3 = pv.view(3, r, n, R)
+        D.copy_(pv3[0], prev[:, 0])
+        D.copy_(pv3[1], prev[:, 1])
+        D.copy_(pv3[2], prev[:, 3])
+        lvec = op.matvec(pv)  # raises like the reference when INEQ_MATVEC_BUG (outside any try)
+        diff = D.clone(lrhs)
+        D.copy_(diff, lvec, -1.0, 1.0)
+        use_prev = D.norm(diff) < lnorm
+        if use_prev:
+            lrhs = diff
+        it_fail = False
+        try:
+            lsol = _run_lgmres(op, lrhs, m, rtol)
+        except Exception as e:
+            _report(e)
+            it_fail = True
+            failed = True
+            sol = prev
+        if not it_fail:
+            l3 = lsol.view(3, r, n, R)
+            if use_prev:
+                D.copy_(l3[0], prev[:, 0], 1.0, 1.0)
+                D.copy_(l3[1], prev[:, 1], 1.0, 1.0)
+                D.copy_(l3[2], prev[:, 3], 1.0, 1.0)
+            zt = D.clone(rhs[:, 1])
+            einsum(APPLY_T, XAX_k[0, 1], A_k[0, 1], XAX_k1[0, 1], l3[0], out=zt, alpha=-1.0, beta=1.0)
+            sol = D.empty(*xs)
+            D.mul_(sol[:, 2], inv_I, zt)
+            D.copy_(sol[:, 2], l3[2], -1.0, 1.0)
+            D.copy_(sol[:, 0], l3[0])
+            D.copy_(sol[:, 1], l3[1])
+            D.copy_(sol[:, 3], l3[2])
+    res_new = _residual_norm(A_k, XAX_k, XAX_k1, sol, rhs, nrhs)
+    if res_old < res_new:
+        sol = prev
+    return sol, res_old, min(res_old, res_new), rhs, nrhs, failed
+
+
+# ------------------------------------------------------------------ IPM driver (`:404-1099`)
+class IneqStatus(Enum):
+    ACTIVE = 0
+    SETTING_ACTIVE = 1
+    SETTING_INACTIVE = 2
+    INACTIVE = 3
+    NOT_IN_USE = 4
+
+    def __str__(self):
+        return self.name.lower().replace('_', ' ')
+
+
+@dataclass
+class IPMStatus:
+    dim: int
+    feasibility_tol: float
+    centrality_tol: float
+    op_tol: float
+    eps: float
+    aho_direction: bool
+    is_primal_feasible: bool
+    primal_error: float
+    is_dual_feasible: bool
+    dual_error: float
+    is_central: bool
+    centrality_error: float
+    mu: float
+    is_last_iter: bool
+    ineq_status: IneqStatus
+    verbose: bool
+    primal_error_normalisation: float
+    dual_error_normalisation: float
+    mals_rank_restriction: int
+    boundary_val: float = 1e-10
+    ineq_boundary_val: float = 0.01
+    sigma: float = 0.5
+    num_ineq_constraints: float = 0
+    lag_map_t = None
+    lag_map_y = None
+    compl_ineq_mask = None
+    mals_delta0 = None
+    eigen_x0 = None
+    eigen_z0 = None
+    eigen_xt0 = None
+    eigen_zt0 = None
+    kkt_iterations = 7
+    centrl_error_normalisation: float = 1.0
+    eta = 1e-3
+
+
+def tt_compute_primal_feasibility(L, b, X, st):
+    """`src/tt_ipm.py:404-407`"""
+    e = 0.01 * st.eta * st.primal_error_normalisation
+    return T.tt_rank_reduce(T.tt_sub(tt_mat_vec_mul(L, T.tt_reshape(X, (4,)), e, st.eps), b), e)
+
+
+def tt_compute_dual_feasibility(C, Ladj, Z, Y, Tt, st):
+    """`src/tt_ipm.py:410-417`"""
+    act = st.ineq_status is IneqStatus.ACTIVE
+    df = T.tt_rank_reduce(T.tt_sub(T.tt_fast_matrix_vec_mul(Ladj, Y, st.eps),
+                                   T.tt_rank_reduce(T.tt_add(T.tt_reshape(Z, (4,)), C), st.eps)),
+                          st.eps if act else 0.01 * st.eta * st.dual_error_normalisation)
+    if act and Tt is not None:
+        df = T.tt_rank_reduce(T.tt_sub(df, T.tt_reshape(Tt, (4,))), 0.01 * st.eta * st.dual_error_normalisation)
+    return df
+
+
+def tt_compute_centrality(X, Z, st):
+    """`src/tt_ipm.py:420-426`"""
+    e = 0.01 * st.eta * st.centrl_error_normalisation
+    if st.aho_direction:
+        return T.tt_reshape(T.tt_scale(-1, _tt_symmetrise(tt_mat_mat_mul(X, Z, e, st.eps), e)), (4,))
+    return T.tt_reshape(T.tt_scale(-1, tt_mat_mat_mul(Z, X, e, st.eps)), (4,))
+
+
+def tt_infeasible_newton_system(lhs, C, X, Y, Z, Tt, L, Ladj, b, mask, st):
+    """`src/tt_ipm.py:429-475`"""
+    rhs = TTBlockVector()
+    pf = tt_compute_primal_feasibility(L, b, X, st)
+    st.primal_error = np.divide(T.tt_norm(pf), st.primal_error_normalisation)
+    st.is_primal_feasible = np.less(st.primal_error, st.feasibility_tol)
+    df = tt_compute_dual_feasibility(C, Ladj, Z, Y, Tt, st)
+    st.dual_error = np.divide(T.tt_norm(df), st.dual_error_normalisation)
+    st.is_dual_feasible = np.less(st.dual_error, (1 + (st.ineq_status is IneqStatus.ACTIVE)) * st.feasibility_tol)
+    st.is_last_iter = st.is_last_iter or (st.is_primal_feasible and st.is_dual_feasible and st.is_central)
+    if st.aho_direction:
+        lhs[2, 1] = T.tt_psd_rank_reduce(T.tt_scale(0.5, T.tt_add(T.tt_IkronM(Z), T.tt_MkronI(Z))),
+                                         eps=0.1 * st.eta * st.dual_error_normalisation)
+        lhs[2, 2] = T.tt_psd_rank_reduce(T.tt_scale(0.5, T.tt_add(T.tt_MkronI(X), T.tt_IkronM(X))),
+                                         eps=0.1 * st.eta * st.primal_error_normalisation)
+    else:
+        lhs[2, 1] = T.tt_psd_rank_reduce(T.tt_MkronI(Z), eps=0.1 * st.eta * st.dual_error_normalisation)
+        lhs[2, 2] = T.tt_psd_rank_reduce(T.tt_IkronM(X), eps=0.1 * st.eta * st.primal_error_normalisation)
+    if not st.is_primal_feasible or st.is_last_iter:
+        rhs[0] = pf
+    if not st.is_dual_feasible or st.is_last_iter:
+        rhs[1] = df
+    if not st.is_central or st.is_last_iter:
+        rhs[2] = tt_compute_centrality(X, Z, st)
+    if st.ineq_status is IneqStatus.ACTIVE:
+        lhs[3, 1] = T.tt_diag_op(Tt, 0.1 * st.eta * st.dual_error_normalisation)
+        mX = T.tt_rank_reduce(T.tt_add(T.tt_scale(st.ineq_boundary_val, mask), T.tt_fast_hadamard(mask, X, st.eps)),
+                              eps=st.eps)
+        lhs[3, 3] = T.tt_rank_reduce(T.tt_add(st.lag_map_t, T.tt_diag_op(mX, st.eps)),
+                                     eps=0.1 * st.eta * st.dual_error_normalisation)
+        if not st.is_central or st.is_last_iter:
+            rhs[3] = T.tt_rank_reduce(T.tt_reshape(T.tt_scale(-1, T.tt_fast_hadamard(mX, Tt, st.eps)), (4,)),
+                                      eps=0.01 * st.eta * st.centrl_error_normalisation)
+    return lhs, rhs, st
+
+
+def _tt_symmetrise(M, e):
+    return T.tt_rank_reduce(T.tt_scale(0.5, T.tt_add(M, T.tt_transpose(M))), eps=e)
+
+
+def _tt_psd_symmetrise(M, e):
+    return T.tt_psd_rank_reduce(T.tt_scale(0.5, T.tt_add(M, T.tt_transpose(M))), eps=e)
+
+
+def _tt_mask_symmetrise(M, mask, e):
+    return T.tt_mask_rank_reduce(T.tt_scale(0.5, T.tt_add(M, T.tt_transpose(M))), mask, eps=e)
+
+
+def _tt_copy(tt):
+    return [D.clone(c) for c in tt]
+
+
+def _tt_scale_nondestructive(tt, s):
+    if tt is None or np.isclose(s, 1.0):
+        return tt
+    return T.tt_scale(s, _tt_copy(tt))
+
+
+def _tt_rhs_row_norm(rhs, i):
+    row = rhs.get_row(i)
+    if row is None:
+        return 0.0
+    n = T.tt_norm(row)
+    return float(n) if np.isfinite(n) else 0.0
+
+
+def _tt_kkt_row_scales(rhs, st):
+    """`src/tt_ipm.py:510-528`"""
+    eps = max(st.op_tol, 1e-12)
+    fn = max(_tt_rhs_row_norm(rhs, 0), _tt_rhs_row_norm(rhs, 1))
+    cn = max(_tt_rhs_row_norm(rhs, 2), _tt_rhs_row_norm(rhs, 3))
+    sc = {}
+    if fn > eps:
+        fs = float(np.clip(1.0 / max(fn, eps), 1e-6, 1e6))
+        sc[0] = fs
+        sc[1] = fs
+    if cn > eps:
+        cs = float(np.clip(1.0 / max(cn, eps), 1e-6, 1e6))
+        if 0 in sc:
+            cs = min(cs, sc[0])
+        sc[2] = cs
+        sc[3] = cs
+    return sc
+
+
+def _tt_effective_row_scale(lhs, key, sc):
+    s = sc.get(key[0], 1.0)
+    if key in lhs._transposes:
+        cr, _ = lhs._transposes[key]
+        if cr in sc:
+            s = np.sqrt(s * sc[cr])
+    if key in lhs._aliases:
+        cr, _ = lhs._aliases[key]
+        if cr in sc:
+            s = np.sqrt(s * sc[cr])
+    return float(s)
+
+
+def _tt_build_row_scaled_kkt(lhs, rhs, st, row_scales=None):
+    """`src/tt_ipm.py:545-568`"""
+    sc = _tt_kkt_row_scales(rhs, st) if row_scales is None else row_scales
+    if not sc:
+        return lhs, rhs
+    L = TTBlockMatrix()
+    L._aliases = dict(lhs._aliases)
+    L._transposes = dict(lhs._transposes)
+    for key, blk in lhs._data.items():
+        L[key] = _tt_scale_nondestructive(blk, _tt_effective_row_scale(lhs, key, sc))
+    R = TTBlockVector()
+    for i in rhs.keys():
+        R[i] = _tt_scale_nondestructive(rhs.get_row(i), sc.get(i, 1.0))
+    if st.verbose:
+        print(f"KKT row scaling: feas={sc.get(0, sc.get(1, 1.0)):.2e}, cent={sc.get(2, sc.get(3, 1.0)):.2e}", flush=True)
+    return L, R
+
+
+def _ineq_step_size(Att, Dtt, e_tt, st):
+    """`src/tt_ipm.py:730-747`"""
+    s = T.tt_add(Att, Dtt)
+    if st.compl_ineq_mask:
+        s = T.tt_add(s, st.compl_ineq_mask)
+    s = T.tt_rank_reduce(s, st.eps)
+    e_tt, _ = tt_min_eig(T.tt_diag_op(s, st.eps), x0=e_tt, tol=1e-8, verbose=st.verbose)
+    esq = T.tt_reshape(e_tt, (2, 2))
+    if np.abs(T.tt_inner_prod(s, esq)) > st.eps:
+        esq = T.tt_normalise(T.tt_fast_hadamard(esq, esq, st.eps))
+        mA = np.abs(T.tt_inner_prod(Att, esq))
+        mD = T.tt_inner_prod(Dtt, esq)
+        step = 1 if mD >= -st.eps else np.clip(-mA / mD, a_min=0, a_max=1)
+    else:
+        step = 1
+    return step, e_tt
+
+
+def _tt_get_ineq_step_sizes(xs, zs, X, Tt, DX, DT, mask, st):
+    """`src/tt_ipm.py:750-779`"""
+    if xs > 0:
+        mX = T.tt_fast_hadamard(mask, X, st.eps)
+        mDX = T.tt_fast_hadamard(mask, DX, st.eps)
+        xis, st.eigen_xt0 = _ineq_step_size(T.tt_add(mX, T.tt_scale(st.ineq_boundary_val, mask)),
+                                            T.tt_scale(xs, mDX), st.eigen_xt0, st)
+        if not st.is_last_iter:
+            if 1 - xis < st.op_tol and T.tt_norm(Tt) < st.op_tol:
+                if st.ineq_status is IneqStatus.ACTIVE:
+                    st.ineq_status = IneqStatus.SETTING_INACTIVE
+            else:
+                if st.ineq_status is IneqStatus.INACTIVE:
+                    st.ineq_status = IneqStatus.SETTING_ACTIVE
+        xs *= xis
+    if zs > 0 and st.ineq_status is IneqStatus.ACTIVE:
+        ts, st.eigen_zt0 = _ineq_step_size(Tt, T.tt_scale(zs, DT), st.eigen_zt0, st)
+        zs *= ts
+    return xs, zs
+
+
+def _tt_get_step_sizes(X, Z, Tt, DX, DZ, DT, mask, st):
+    """`src/tt_ipm.py:700-727`"""
+    if st.is_last_iter:
+        X = T.tt_add(X, T.tt_scale(st.boundary_val, T.tt_identity(len(X))))
+        Z = T.tt_add(Z, T.tt_scale(st.boundary_val, T.tt_identity(len(Z))))
+    xs, st.eigen_x0 = tt_max_generalised_eigen(X, DX, x0=st.eigen_x0, tol=1e-8, verbose=st.verbose)
+    zs, st.eigen_z0 = tt_max_generalised_eigen(Z, DZ, x0=st.eigen_z0, tol=1e-8, verbose=st.verbose)
+    if st.ineq_status is not IneqStatus.NOT_IN_USE:
+        if st.is_last_iter:
+            X = T.tt_add(X, T.tt_scale(st.ineq_boundary_val + st.boundary_val, mask))
+            Tt = T.tt_add(Tt, T.tt_scale(st.ineq_boundary_val + st.boundary_val, mask))
+        xs, zs = _tt_get_ineq_step_sizes(xs, zs, X, Tt, DX, DT, mask, st)
+    tau = 0.9 + 0.05 * min(xs, zs)
+    if st.verbose:
+        print("Step search concluded.")
+        print(f"Step sizes: a_p:{xs:.2e}, a_d:{zs:.2e}", flush=True)
+    return tau * xs, tau * zs
+
+
+def _tt_ipm_newton_step(lhs, rhs, mask, X, Z, Tt, ZX, TX, st, solver):
+    """`_tt_ipm_newton_step` (`src/tt_ipm.py:571-697`)."""
+    try:
+        if st.verbose:
+            print("\n--- Predictor  step ---", flush=True)
+        sc = _tt_kkt_row_scales(rhs, st)
+        Lp, Rp = _tt_build_row_scaled_kkt(lhs, rhs, st, sc)
+        Dl, _ = solver(Lp, Rp, st.mals_delta0, st.kkt_iterations + st.is_last_iter, st.mals_rank_restriction, st.eta)
+        st.mals_delta0 = Dl
+        DX = _tt_symmetrise(T.tt_reshape(_tt_get_block(1, Dl), (2, 2)), st.eps)
+        DZ = _tt_symmetrise(T.tt_reshape(_tt_get_block(2, Dl), (2, 2)), st.eps)
+        DY = T.tt_rank_reduce(_tt_get_block(0, Dl), eps=st.eps)
+        DT = None
+        if st.ineq_status is IneqStatus.ACTIVE:
+            DT = T.tt_rank_reduce(_tt_get_block(3, Dl), eps=st.eps)
+            DT = T.tt_fast_hadamard(mask, T.tt_reshape(DT, (2, 2)), st.eps)
+        xs, zs = _tt_get_step_sizes(X, Z, Tt, DX, DZ, DT, mask, st)
+        if not st.is_central and not st.is_last_iter:
+            DXZ = T.tt_inner_prod(DX, DZ)
+            if st.verbose:
+                print("\n--- Centering-Corrector  step ---", flush=True)
+            if st.ineq_status is IneqStatus.ACTIVE:
+                mu_aff = (ZX + xs * zs * DXZ + zs * T.tt_inner_prod(X, DZ) + xs * T.tt_inner_prod(DX, Z)
+                          + TX + xs * zs * T.tt_inner_prod(DT, DX)
+                          + zs * (T.tt_inner_prod(X, DT) + st.ineq_boundary_val * T.tt_entrywise_sum(DT))
+                          + xs * T.tt_inner_prod(DX, Tt))
+                e = max(1, 3 * min(xs, zs) ** 2)
+                st.sigma = min(0.99, max(mu_aff / (ZX + TX), 0) ** e)
+                if st.sigma > 1e-4:
+                    rhs[3] = T.tt_rank_reduce(T.tt_add(T.tt_scale(st.sigma * st.mu, T.tt_reshape(mask, (4,))),
+                                                       rhs.get_row(3)), 0.1 * st.eta * st.centrl_error_normalisation)
+            else:
+                mu_aff = ZX + xs * zs * DXZ + zs * T.tt_inner_prod(X, DZ) + xs * T.tt_inner_prod(DX, Z)
+                e = max(1, 3 * min(xs, zs) ** 2)
+                st.sigma = min(0.99, max(mu_aff / ZX, 0) ** e)
+            ce = 0.1 * st.eta * st.centrl_error_normalisation
+            if DXZ > 0.1 * st.centrality_tol:
+                term = tt_compute_centrality(DX, DZ, st)
+                if st.sigma > 1e-4:
+                    rhs[2] = T.tt_rank_reduce(T.tt_add(T.tt_scale(st.sigma * st.mu, T.tt_reshape(T.tt_identity(len(X)), (4,))),
+                                                       T.tt_add(rhs.get_row(2), term)), ce)
+                else:
+                    rhs[2] = T.tt_rank_reduce(T.tt_add(rhs.get_row(2), term), ce)
+            else:
+                if st.sigma > 1e-4:
+                    rhs[2] = T.tt_rank_reduce(T.tt_add(T.tt_scale(st.sigma * st.mu, T.tt_reshape(T.tt_identity(len(X)), (4,))),
+                                                       rhs.get_row(2)), ce)
+                else:
+                    rhs[2] = rhs.get_row(2)
+            Lc, Rc = _tt_build_row_scaled_kkt(lhs, rhs, st, sc)
+            Dc, _ = solver(Lc, Rc, st.mals_delta0, st.kkt_iterations + st.is_last_iter, st.mals_rank_restriction, st.eta)
+            st.mals_delta0 = Dc
+            DXc = _tt_symmetrise(T.tt_reshape(_tt_get_block(1, Dc), (2, 2)), st.eps)
+            DZc = _tt_symmetrise(T.tt_reshape(_tt_get_block(2, Dc), (2, 2)), st.eps)
+            DYc = T.tt_rank_reduce(_tt_get_block(0, Dc), eps=st.eps)
+            DX = T.tt_rank_reduce(T.tt_add(DXc, DX), eps=st.eps)
+            DY = T.tt_rank_reduce(T.tt_add(DYc, DY), eps=st.eps)
+            DZ = T.tt_rank_reduce(T.tt_add(DZc, DZ), eps=st.eps)
+            if st.ineq_status is IneqStatus.ACTIVE:
+                DTc = T.tt_rank_reduce(_tt_get_block(3, Dc), eps=st.eps)
+                DTc = T.tt_fast_hadamard(mask, T.tt_reshape(DTc, (2, 2)), st.eps)
+                DT = T.tt_rank_reduce(T.tt_add(DTc, DT), eps=st.eps)
+            xs, zs = _tt_get_step_sizes(X, Z, Tt, DX, DZ, DT, mask, st)
+        else:
+            st.sigma = 0
+    except Exception as e:
+        print(f"\n\t⚠️ Attention: {e}")
+        print("\n\t==> Full traceback (most recent call last):")
+        traceback.print_exc(file=sys.stdout)
+        return 0, 0, None, None, None, None, st
+    return xs, zs, DX, DY, DZ, DT, st
+
+
+def _initialise(mask, st, dim, lam, lam_ineq):
+    """`src/tt_ipm.py:782-794`"""
+    X = T.tt_scale(lam, T.tt_identity(dim))
+    Z = T.tt_scale(lam, T.tt_identity(dim))
+    Y = T.tt_reshape(T.tt_zero_matrix(dim), (4,))
+    Tt = None
+    if st.ineq_status is IneqStatus.ACTIVE:
+        Tt = T.tt_scale(lam_ineq, mask)
+        xs, _ = tt_max_generalised_eigen(X, mask, tol=1e-7, verbose=st.verbose)
+        X = T.tt_rank_reduce(T.tt_add(X, T.tt_scale(0.1 * xs, mask)), 0.1 * st.eta * st.primal_error_normalisation)
+    return X, Y, Z, Tt
+
+
+def _ipm_check_for_stalled_progress(prev, st, gap_tol):
+    """`src/tt_ipm.py:853-866`"""
+    if st.is_last_iter:
+        return False
+    if (abs(prev['primal'] - st.primal_error) < 0.04 * gap_tol and abs(prev['dual'] - st.dual_error) < 0.04 * gap_tol
+            and abs(prev['centrality'] - st.centrality_error) < 0.02 * gap_tol):
+        if st.verbose:
+            print("============================================\n Progress stalled! Entering finishing phase.\n"
+                  "============================================")
+        return True
+    return False
+
+
+def _ipm_check_convergence(st, fin, ZX, TX, abs_tol, max_ref):
+    """`src/tt_ipm.py:869-888`"""
+    if not st.is_last_iter:
+        return st, fin
+    if abs(ZX) + abs(TX) < abs_tol and st.primal_error < abs_tol and st.dual_error < abs_tol:
+        if st.verbose:
+            print("Absolute tolerance reached!")
+        fin = 0
+    else:
+        fin -= 1
+        st.boundary_val = 0.001 * (1 - (fin / max_ref))
+        if fin == 1:
+            st.kkt_iterations += 1
+    return st, fin
+
+
+def _ipm_log_iteration(it, st, X, Y, Z, Tt):
+    """`src/tt_ipm.py:891-898`"""
+    print(f"\n--- Iteration {it - 1} ---")
+    print(f"Status: Finishing up={st.is_last_iter}, Ineq={str(st.ineq_status)}")
+    print(f"Feasibility: Central={st.is_central}, Primal={st.is_primal_feasible}, Dual={st.is_dual_feasible}")
+    print(f"Direction: {'AHO' if st.aho_direction else 'XZ'}, Sigma: {st.sigma:.2e}")
+    print(f"Errors: Centrality={st.centrality_error:.4e}, Primal={st.primal_error:.4e}, Dual={st.dual_error:.4e}")
+    print(f"Ranks: X={T.tt_ranks(X)}, Z={T.tt_ranks(Z)}, Y={T.tt_ranks(Y)}, T={T.tt_ranks(Tt) if Tt else 'N/A'}",
+          flush=True)
+
+
+def tt_ipm(lag_maps, obj_tt, lin_op_tt, bias_tt, ineq_mask=None, max_iter=100, max_refinement=5, warm_up=3,
+           gap_tol=1e-4, aho_direction=True, op_tol=1e-5, abs_tol=8e-4, eps=1e-12, mals_restarts=3, r_max=1000,
+           lambdaStar=1, lambdaStarIneq=1, epsilonDash=None, epsilonDashineq=None, verbose=False, trace=None,
+           iter_callback=None):
+    """`tt_ipm` (`src/tt_ipm.py:901-1099`).  `trace` (list) collects one record per Newton-system
+    assembly; `iter_callback(iteration)` is invoked after each completed IPM iteration (bench)."""
+    C, L, b, mask = obj_tt, lin_op_tt, bias_tt, ineq_mask
+    dim = len(C)
+    st = IPMStatus(len(C), 2 * gap_tol, gap_tol / np.sqrt(dim), op_tol, eps, aho_direction, False, np.inf, False,
+                   np.inf, False, np.inf, np.inf, False,
+                   IneqStatus.NOT_IN_USE if mask is None else IneqStatus.ACTIVE, verbose, 1, 1, r_max)
+    lag_maps = {k: T.tt_rank_reduce(v, eps=eps) for k, v in lag_maps.items()}
+    C = T.tt_rank_reduce(C, eps=eps)
+    L = T.tt_rank_reduce(L, eps=eps)
+    b = T.tt_rank_reduce(b, eps=eps)
+    st.primal_error_normalisation = 1 + T.tt_norm(b)
+    st.dual_error_normalisation = 1 + T.tt_norm(C)
+    skel = TTBlockMatrix()
+    skel[1, 2] = T.tt_reshape(T.tt_identity(2 * dim), (4, 4))
+
+    def make_solver(ls):
+        return lambda lhs, rhs, x0, nswp, restr, tol: tt_restarted_block_amen(
+            lhs, rhs, rank_restriction=restr, x0=x0, local_solver=ls, op_tol=op_tol, termination_tol=tol,
+            num_restarts=mals_restarts, inner_m=nswp, verbose=verbose)
+
+    solver_ineq = make_solver(_ipm_local_solver_ineq)
+    solver_eq = make_solver(_ipm_local_solver)
+    if st.ineq_status is IneqStatus.ACTIVE:
+        solver = solver_ineq
+        st.num_ineq_constraints = T.tt_inner_prod(mask, mask)
+        st.compl_ineq_mask = T.tt_rank_reduce(T.tt_sub(T.tt_one_matrix(dim), mask), eps=eps)
+        st.lag_map_t = lag_maps["t"]
+        skel.add_alias((1, 2), (1, 3))
+    else:
+        solver = solver_eq
+        st.num_ineq_constraints = 0
+    Ladj = T.tt_transpose(L)
+    skel[0, 1] = T.tt_scale(-1, L)
+    skel.add_alias((0, 1), (1, 0), is_transpose=True)
+    skel[0, 0] = lag_maps["y"]
+    st.lag_map_y = lag_maps["y"]
+    X, Y, Z, Tt = _initialise(mask, st, dim, lambdaStar, lambdaStarIneq)
+    it = 0
+    fin = max_refinement
+    prev = {'primal': np.inf, 'dual': np.inf, 'centrality': np.inf}
+    lhs = skel
+    while fin > 0:
+        it += 1
+        st.aho_direction = (it > warm_up)
+        if max_iter - max_refinement == it - 1 and not st.is_last_iter:
+            print("============================================\n Maximum #iterations reached!\n"
+                  "============================================")
+            st.is_last_iter = True
+        ZX = T.tt_inner_prod(Z, X)
+        TX = (T.tt_inner_prod(X, Tt) + st.ineq_boundary_val * T.tt_entrywise_sum(Tt)) \
+            if st.ineq_status is IneqStatus.ACTIVE else 0
+        st.mu = np.divide(abs(ZX) + abs(TX), (2 ** dim + (st.ineq_status is IneqStatus.ACTIVE) * st.num_ineq_constraints))
+        st.centrl_error_normalisation = 1 + abs(T.tt_inner_prod(C, T.tt_reshape(X, (4,))))
+        st.centrality_error = st.mu / st.centrl_error_normalisation
+        st.is_central = np.less(st.centrality_error, st.centrality_tol)
+        st.eta = max(min(st.eta, 2 * st.mu), st.op_tol)
+        lhs_m, rhs_v, st = tt_infeasible_newton_system(lhs, C, X, Y, Z, Tt, L, Ladj, b, mask, st)
+        if trace is not None:
+            trace.append({"iter": it, "mu": float(st.mu), "primal_error": float(st.primal_error),
+                          "dual_error": float(st.dual_error), "centrality_error": float(st.centrality_error),
+                          "sigma": float(st.sigma), "ranksX": T.tt_ranks(X), "ranksZ": T.tt_ranks(Z),
+                          "ranksY": T.tt_ranks(Y), "is_last_iter": bool(st.is_last_iter)})
+        if verbose:
+            _ipm_log_iteration(it, st, X, Y, Z, Tt)
+        st, fin = _ipm_check_convergence(st, fin, ZX, TX, abs_tol, max_refinement)
+        if fin == 0:
+            it -= 1
+            break
+        xs, zs, DX, DY, DZ, DT, st = _tt_ipm_newton_step(lhs_m, rhs_v, mask, X, Z, Tt, ZX, TX, st, solver)
+        if (DX is None and DZ is None) or (xs < 1e-5 and zs < 1e-5):
+            if st.is_last_iter:
+                break
+            print("============================================\n Hit PSD boundary! Entering finishing phase.\n"
+                  "============================================")
+            st.is_last_iter = True
+        else:
+            e_p = 0.1 * st.eta * st.primal_error_normalisation
+            e_d = 0.1 * st.eta * st.dual_error_normalisation
+            if fin <= 1:
+                X = _tt_symmetrise(T.tt_add(X, T.tt_scale(xs, DX)), e_p)
+            else:
+                X = _tt_psd_symmetrise(T.tt_add(X, T.tt_scale(xs, DX)), e_p)
+            if fin <= 1:
+                Z = _tt_symmetrise(T.tt_add(Z, T.tt_scale(zs, DZ)), e_d)
+            else:
+                Z = _tt_psd_symmetrise(T.tt_add(Z, T.tt_scale(zs, DZ)), e_d)
+            Y = T.tt_rank_reduce(T.tt_add(Y, T.tt_scale(zs, DY)), st.eps)
+            Y = T.tt_reshape(_tt_symmetrise(T.tt_reshape(T.tt_sub(Y, T.tt_fast_matrix_vec_mul(st.lag_map_y, Y, st.eps)),
+                                                         (2, 2)), e_d), (4,))
+            if st.ineq_status is IneqStatus.ACTIVE:
+                if fin <= 1:
+                    Tt = _tt_symmetrise(T.tt_add(Tt, T.tt_scale(zs, DT)), e_d)
+                else:
+                    Tt = _tt_mask_symmetrise(T.tt_add(Tt, T.tt_scale(zs, DT)), mask, e_d)
+            elif st.ineq_status is IneqStatus.SETTING_INACTIVE:
+                solver = solver_eq
+                lhs = skel.get_submatrix(2, 2)
+                st.mals_delta0 = None
+                st.ineq_status = IneqStatus.INACTIVE
+            elif st.ineq_status is IneqStatus.SETTING_ACTIVE:
+                solver = solver_ineq
+                lhs = skel
+                st.mals_delta0 = None
+                st.ineq_status = IneqStatus.ACTIVE
+        if _ipm_check_for_stalled_progress(prev, st, gap_tol):
+            st.is_last_iter = True
+        prev['primal'] = st.primal_error
+        prev['dual'] = st.dual_error
+        prev['centrality'] = st.centrality_error
+        if iter_callback is not None:
+            iter_callback(it)
+    rX, rZ, rY = T.tt_ranks(X), T.tt_ranks(Z), T.tt_ranks(Y)
+    rT = T.tt_ranks(Tt) if Tt else [0] * (st.dim - 1)
+    print("---Terminated---")
+    print(f"Converged in {it} iterations.")
+    print(f"Ranks: X={rX}, Z={rZ}, Y={rY}, T={rT}")
+    info = {"num_iters": it, "ranksX": rX, "ranksY": rY, "ranksZ": rZ, "ranksT": rT, "status": st}
+    return X, Y, Tt, Z, info

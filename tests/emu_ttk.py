@@ -1,0 +1,298 @@
+"""NumPy emulation of the libttk C ABI -- TEST INFRASTRUCTURE for CPU-only tests.
+
+Lets the `-m "not gpu"` suite exercise the product's HOST logic (einsum planner, TT algebra,
+AMEn / IPM control flow, LGMRES bookkeeping) on CPU tensors, by swapping `ttipm_amd._lib.lib`
+for this object before `ttipm_amd.dev` is imported (see `emulated_ttipm()` below).  It is
+never used by the product, by `smoke()` or by `bench.py`; the GPU tests run the real HIP
+library and fail if it is missing."""
+import ctypes
+import importlib
+import os
+import sys
+
+import numpy as np
+import scipy.linalg as sla
+
+
+def _dv(ptr, n):
+    if n <= 0:
+        return np.zeros(0)
+    return np.ctypeslib.as_array((ctypes.c_double * int(n)).from_address(int(ptr)))
+
+
+def _iv(ptr, n):
+    return np.ctypeslib.as_array((ctypes.c_int64 * int(n)).from_address(int(ptr)))
+
+
+def _i32(ptr, n):
+    return np.ctypeslib.as_array((ctypes.c_int32 * int(n)).from_address(int(ptr)))
+
+
+def _nd_index(ndim, shape, strides):
+    shape = [int(shape[i]) for i in range(ndim)]
+    idx = np.zeros(shape, dtype=np.int64)
+    for i in range(ndim):
+        sh = [1] * ndim
+        sh[i] = shape[i]
+        idx = idx + (np.arange(shape[i], dtype=np.int64) * int(strides[i])).reshape(sh)
+    return idx.reshape(-1)
+
+
+class EmuLib:
+    def __init__(self):
+        self.err = b""
+        self.launches = 0
+
+    # --- bookkeeping
+    def ttk_last_error(self):
+        return self.err
+
+    def ttk_version(self):
+        return 1
+
+    def ttk_launch_count(self):
+        return self.launches
+
+    # --- contractions
+    def ttk_gemm_offs(self, s, A, B, C, offs, nb, M, N, K, alpha, beta):
+        self.launches += 1
+        o = _iv(offs, 3 * nb + 2 * M + 2 * N + 2 * K)
+        a_b, a_m, a_k = o[:nb], o[nb:nb + M], o[nb + M:nb + M + K]
+        p = nb + M + K
+        b_b, b_k, b_n = o[p:p + nb], o[p + nb:p + nb + K], o[p + nb + K:p + nb + K + N]
+        p += nb + K + N
+        c_b, c_m, c_n = o[p:p + nb], o[p + nb:p + nb + M], o[p + nb + M:p + nb + M + N]
+        ia = a_b[:, None, None] + a_m[None, :, None] + a_k[None, None, :]
+        ib = b_b[:, None, None] + b_k[None, :, None] + b_n[None, None, :]
+        ic = c_b[:, None, None] + c_m[None, :, None] + c_n[None, None, :]
+        Av = _dv(A, ia.max() + 1)[ia]
+        Bv = _dv(B, ib.max() + 1)[ib]
+        Cm = _dv(C, ic.max() + 1)
+        res = alpha * np.einsum("bmk,bkn->bmn", Av, Bv)
+        if beta != 0.0:
+            res = res + beta * Cm[ic]
+        Cm[ic] = res
+        return 0
+
+    # --- element-wise
+    def ttk_copy_nd(self, s, src, dst, nd, shape, ss, ds, alpha, beta):
+        self.launches += 1
+        i_s, i_d = _nd_index(nd, shape, ss), _nd_index(nd, shape, ds)
+        if i_s.size == 0:
+            return 0
+        S = _dv(src, i_s.max() + 1)[i_s].copy()
+        Dm = _dv(dst, i_d.max() + 1)
+        v = alpha * S
+        if beta != 0.0:
+            v = v + beta * Dm[i_d]
+        Dm[i_d] = v
+        return 0
+
+    def ttk_mul_nd(self, s, a, b, dst, nd, shape, sa, sb, ds, alpha, beta):
+        self.launches += 1
+        ia, ib, idd = _nd_index(nd, shape, sa), _nd_index(nd, shape, sb), _nd_index(nd, shape, ds)
+        if ia.size == 0:
+            return 0
+        v = alpha * _dv(a, ia.max() + 1)[ia] * _dv(b, ib.max() + 1)[ib]
+        Dm = _dv(dst, idd.max() + 1)
+        if beta != 0.0:
+            v = v + beta * Dm[idd]
+        Dm[idd] = v
+        return 0
+
+    def ttk_recip(self, s, src, dst, n):
+        _dv(dst, n)[:] = 1.0 / _dv(src, n)
+        return 0
+
+    def ttk_fill(self, s, dst, n, v):
+        _dv(dst, n)[:] = v
+        return 0
+
+    def ttk_add_diag(self, s, A, n, lda, v):
+        a = _dv(A, (n - 1) * lda + n)
+        a[np.arange(n) * lda + np.arange(n)] += v
+        return 0
+
+    def ttk_dot_nd_sync(self, s, x, y, nd, shape, xs, ys, out):
+        ix, iy = _nd_index(nd, shape, xs), _nd_index(nd, shape, ys)
+        val = float(np.dot(_dv(x, ix.max() + 1)[ix], _dv(y, iy.max() + 1)[iy])) if ix.size else 0.0
+        out._obj.value = val
+        return 0
+
+    def ttk_sumsq_batched(self, s, x, n, nb, bstride, out):
+        xv = _dv(x, (nb - 1) * bstride + n)
+        o = _dv(out, nb)
+        for b in range(nb):
+            seg = xv[b * bstride:b * bstride + n]
+            o[b] = np.dot(seg, seg)
+        return 0
+
+    def ttk_read_sync(self, s, src, dst, n):
+        ctypes.memmove(dst, int(src), int(n) * 8)
+        return 0
+
+    # --- factorisations
+    def ttk_svd_work(self, m, n):
+        return 16
+
+    def ttk_svd(self, s, A, m, n, U, S, Vt, work):
+        a = _dv(A, m * n).reshape(m, n)
+        u, sv, vt = np.linalg.svd(a, full_matrices=False)
+        k = min(m, n)
+        _dv(U, m * k)[:] = u.ravel()
+        _dv(S, k)[:] = sv
+        _dv(Vt, k * n)[:] = vt.ravel()
+        return 0
+
+    def ttk_qr_work(self, m, n):
+        return 16
+
+    def ttk_qr(self, s, A, m, n, Q, R, work):
+        a = _dv(A, m * n).reshape(m, n)
+        q, r = np.linalg.qr(a, mode="reduced")
+        k = min(m, n)
+        _dv(Q, m * k)[:] = q.ravel()
+        _dv(R, k * n)[:] = r.ravel()
+        return 0
+
+    def ttk_cholesky_sync(self, s, A, n):
+        a = _dv(A, n * n).reshape(n, n)
+        try:
+            L = np.linalg.cholesky(a)
+        except np.linalg.LinAlgError:
+            self.err = b"not positive definite"
+            return 3
+        a[:] = L
+        return 0
+
+    def ttk_trsm_lower(self, s, L, n, B, nrhs, ldb, trans):
+        l = _dv(L, n * n).reshape(n, n)
+        b = np.lib.stride_tricks.as_strided(_dv(B, (n - 1) * ldb + nrhs), shape=(n, nrhs), strides=(ldb * 8, 8))
+        b[:] = sla.solve_triangular(l.T if trans else l, b.copy(), lower=not trans)
+        return 0
+
+    def ttk_lu_sync(self, s, A, n, piv, work, rcond):
+        a = _dv(A, n * n).reshape(n, n)
+        anorm = np.abs(a).sum(axis=0).max()
+        lu, p = sla.lu_factor(a.copy(), check_finite=False)
+        if np.any(np.diag(lu) == 0):
+            self.err = b"singular"
+            return 4
+        a[:] = lu
+        _i32(piv, n)[:] = p
+        inv1 = np.abs(sla.lu_solve((lu, p), np.eye(n))).sum(axis=0).max()
+        rcond._obj.value = 1.0 / (anorm * inv1) if anorm > 0 else 0.0
+        return 0
+
+    def ttk_lu_solve(self, s, LU, n, piv, B, nrhs, ldb):
+        lu = _dv(LU, n * n).reshape(n, n)
+        p = _i32(piv, n).copy()
+        b = np.lib.stride_tricks.as_strided(_dv(B, (n - 1) * ldb + nrhs), shape=(n, nrhs), strides=(ldb * 8, 8))
+        b[:] = sla.lu_solve((lu, p), b.copy())
+        return 0
+
+    def ttk_syev_work(self, n):
+        return 16
+
+    def ttk_syev(self, s, A, n, ev, W, work):
+        a = _dv(A, n * n).reshape(n, n)
+        w, v = np.linalg.eigh(a)
+        _dv(ev, n)[:] = w
+        _dv(W, n * n)[:] = v.ravel()
+        return 0
+
+    # --- LGMRES (same semantics as csrc/ttk_lgmres.hip)
+    @staticmethod
+    def _hh(base, max_k):
+        ld = max_k + 1
+        tot = 2 * (max_k + 2) * ld + (max_k + 2) + 2 * ld + 8
+        h = _dv(base, tot)
+        HH = h[:(max_k + 2) * ld].reshape(max_k + 2, ld)
+        HES = h[(max_k + 2) * ld:2 * (max_k + 2) * ld].reshape(max_k + 2, ld)
+        o = 2 * (max_k + 2) * ld
+        GRS = h[o:o + max_k + 2]
+        CC = h[o + max_k + 2:o + max_k + 2 + ld]
+        SS = h[o + max_k + 2 + ld:o + max_k + 2 + 2 * ld]
+        return HH, HES, GRS, CC, SS
+
+    def ttk_lgmres_arnoldi_sync(self, s, V, n, it, hh, max_k, haptol, res_out, flags):
+        Vm = _dv(V, (it + 2) * n).reshape(it + 2, n)
+        HH, HES, GRS, CC, SS = self._hh(hh, max_k)
+        w = Vm[it + 1]
+        h = Vm[:it + 1] @ w
+        w -= h @ Vm[:it + 1]
+        tt = float(np.sqrt(w @ w))
+        HH[:it + 1, it] = h
+        HES[:it + 1, it] = h
+        HH[it + 1, it] = tt
+        HES[it + 1, it] = tt
+        hapbnd = min(abs(tt / GRS[it]), haptol)
+        hapend = not (tt > hapbnd)
+        if not hapend:
+            w *= 1.0 / tt
+        for j in range(1, it + 1):
+            t0 = HH[j - 1, it]
+            HH[j - 1, it] = CC[j - 1] * t0 + SS[j - 1] * HH[j, it]
+            HH[j, it] = CC[j - 1] * HH[j, it] - SS[j - 1] * t0
+        res, null = 0.0, 0
+        if not hapend:
+            hv, hv1 = HH[it, it], HH[it + 1, it]
+            tr = np.sqrt(hv * hv + hv1 * hv1)
+            if tr == 0.0:
+                null = 1
+            else:
+                CC[it], SS[it] = hv / tr, hv1 / tr
+                GRS[it + 1] = -(SS[it] * GRS[it])
+                GRS[it] = CC[it] * GRS[it]
+                HH[it, it] = CC[it] * hv + SS[it] * hv1
+                res = abs(GRS[it + 1])
+        res_out[0] = res
+        res_out[1] = HH[it, it]
+        flags[0] = int(hapend)
+        flags[1] = null
+        return 0
+
+    def ttk_lgmres_build(self, s, hh, max_k, it, basis, nvec, n, x, aug_temp):
+        HH, HES, GRS, CC, SS = self._hh(hh, max_k)
+        GRS[it] = GRS[it] / HH[it, it]
+        for k in range(it - 1, -1, -1):
+            t0 = GRS[k]
+            for j in range(k + 1, it + 1):
+                t0 -= HH[k, j] * GRS[j]
+            GRS[k] = t0 / HH[k, k]
+        t = np.zeros(n)
+        for j in range(nvec):
+            t += GRS[j] * _dv(basis[j], n)
+        _dv(aug_temp, n)[:] = t
+        _dv(x, n)[:] += t
+        return 0
+
+    def ttk_lgmres_aug(self, s, hh, max_k, it_total, V, n, unused, aug_temp, augvec, a_augvec):
+        HH, HES, GRS, CC, SS = self._hh(hh, max_k)
+        avec = np.zeros(it_total + 1)
+        for ii in range(it_total + 1):
+            for jj in range(0, min(ii + 2, it_total + 1)):
+                avec[jj] += HES[jj, ii] * GRS[ii]
+        at = _dv(aug_temp, n)
+        inv = 1.0 / np.sqrt(at @ at)
+        _dv(augvec, n)[:] = at * inv
+        Vm = _dv(V, (it_total + 1) * n).reshape(it_total + 1, n)
+        _dv(a_augvec, n)[:] = (avec @ Vm) * inv
+        return 0
+
+
+def emulated_ttipm():
+    """Import `ttipm_amd` with CPU tensors and the NumPy emulator in place of libttk.so."""
+    os.environ["TTIPM_DEVICE"] = "cpu"
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    if root not in sys.path:
+        sys.path.insert(0, root)
+    for k in [k for k in sys.modules if k == "ttipm_amd" or k.startswith("ttipm_amd.")]:
+        del sys.modules[k]
+    import ttipm_amd  # noqa: F401
+    lib_mod = importlib.import_module("ttipm_amd._lib")
+    lib_mod.lib = EmuLib()
+    for name in ("dev", "lgmres"):
+        m = importlib.import_module("ttipm_amd." + name)
+        m.lib = lib_mod.lib
+    return ttipm_amd

@@ -1,0 +1,181 @@
+"""Numerics of the hand-written HIP kernels (libttk) against NumPy/SciPy fp64 references.
+All tests need an MI355X."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from ttipm_amd import dev as D
+    return D
+
+
+def _rng(seed=0):
+    return np.random.default_rng(seed)
+
+
+EQS = [
+    ("lsr,lML,sMNS,rNR->LSR", [(3, 2, 3), (3, 4, 5), (2, 4, 4, 3), (3, 4, 5)]),
+    ("LSR,lML,sMNS,rNR->lsr", [(5, 3, 5), (4, 2, 5), (6, 2, 2, 3), (4, 2, 5)]),
+    ("lsr,smnS,LSR,rnR->lmL", [(13, 10, 13), (10, 4, 4, 10), (13, 10, 13), (13, 4, 13)]),
+    ("lsr,smnS,LSR,lmL->rnR", [(7, 5, 6), (5, 4, 4, 3), (9, 3, 8), (7, 4, 9)]),
+    ("lsr,smnS,LSR->lmLrnR", [(3, 2, 4), (2, 4, 4, 3), (5, 3, 2)]),
+    ("lsr,smnS,LSR->lmL", [(3, 2, 4), (2, 4, 4, 3), (5, 3, 2)]),
+    ("br,bmB,BR->rmR", [(4, 3), (4, 4, 6), (6, 5)]),
+    ("ab,aijm,bijn->mn", [(3, 4), (3, 2, 2, 5), (4, 2, 2, 1)]),
+    ("ij,rjR->rijR", [(4, 4), (3, 4, 5)]),
+    ("rmnR,lijL->rlminjRL", [(1, 2, 2, 1), (3, 2, 2, 4)]),
+    ("ik,kj->ij", [(70, 45), (45, 33)]),
+    ("ik,kj->ij", [(1, 300), (300, 1)]),
+]
+
+
+@pytest.mark.parametrize("eq,shapes", EQS)
+def test_einsum_matches_numpy(dev, eq, shapes):
+    rng = _rng(1)
+    ops = [rng.standard_normal(s) for s in shapes]
+    ref = np.einsum(eq, *ops)
+    got = dev.read(dev.einsum(eq, *[dev.from_numpy(o) for o in ops]))
+    assert got.shape == ref.shape
+    assert np.max(np.abs(got - ref)) <= 1e-13 * max(1.0, np.max(np.abs(ref)))
+
+
+def test_einsum_strided_views_and_accumulate(dev):
+    rng = _rng(2)
+    A = rng.standard_normal((5, 4, 4, 6))
+    x = rng.standard_normal((6, 4, 5))
+    tA = dev.from_numpy(A).transpose(1, 2)  # (5,4,4,6) swapped axes view
+    tx = dev.from_numpy(x).permute(2, 1, 0)  # (5,4,6) view
+    out = dev.from_numpy(np.ones((5, 4, 5)))
+    dev.einsum("smnS,rnS->smr", tA, tx, out=out, alpha=2.0, beta=-1.0)
+    ref = 2.0 * np.einsum("smnS,rnS->smr", np.swapaxes(A, 1, 2), np.transpose(x, (2, 1, 0))) - 1.0
+    assert np.allclose(dev.read(out), ref, rtol=1e-13, atol=1e-13)
+    # accumulate into a strided slice of a larger tensor
+    big = dev.zeros(5, 3, 4, 5)
+    dev.einsum("smnS,rnS->smr", tA, tx, out=big[:, 1], beta=1.0)
+    assert np.allclose(dev.read(big)[:, 1], ref / 2 + 0.5, rtol=1e-13, atol=1e-13)
+
+
+def test_mfma_layout_asymmetric(dev):
+    """A = I with an asymmetric B catches transposed C/D fragment maps."""
+    B = np.arange(32 * 32, dtype=np.float64).reshape(32, 32)
+    got = dev.read(dev.matmul(dev.from_numpy(np.eye(32)), dev.from_numpy(B)))
+    assert np.array_equal(got, B)
+
+
+@pytest.mark.parametrize("m,n", [(1, 1), (4, 4), (12, 3), (3, 12), (39, 52), (52, 39), (64, 7), (130, 40), (17, 1), (1, 9)])
+def test_svd(dev, m, n):
+    rng = _rng(m * 100 + n)
+    A = rng.standard_normal((m, n))
+    if min(m, n) > 3:
+        A[:, 2] = A[:, 0] * 1e-9  # near rank deficiency
+    U, S, Vt, s = dev.svd(dev.from_numpy(A))
+    U, Vt = dev.read(U), dev.read(Vt)
+    ref = np.linalg.svd(A, compute_uv=False)
+    assert np.allclose(s, ref, rtol=1e-12, atol=1e-14 * ref[0])
+    assert np.all(np.diff(s) <= 0)
+    assert np.allclose((U * s) @ Vt, A, atol=1e-13 * np.abs(A).max())
+    k = min(m, n)
+    assert np.allclose(U.T @ U, np.eye(k), atol=1e-12)
+    assert np.allclose(Vt @ Vt.T, np.eye(k), atol=1e-12)
+
+
+def test_svd_zero_and_rank_one(dev):
+    U, S, Vt, s = dev.svd(dev.zeros(6, 4))
+    assert np.all(s == 0)
+    U = dev.read(U)
+    assert np.allclose(U.T @ U, np.eye(4), atol=1e-12)
+    a = np.outer(np.arange(1, 7.0), np.arange(1, 5.0))
+    U, S, Vt, s = dev.svd(dev.from_numpy(a))
+    assert np.allclose(s[0], np.linalg.norm(a)) and np.all(np.abs(s[1:]) < 1e-12)
+
+
+@pytest.mark.parametrize("m,n", [(4, 4), (13, 4), (4, 13), (60, 20), (200, 30), (1, 5), (5, 1)])
+def test_qr_and_rq(dev, m, n):
+    rng = _rng(7 + m + n)
+    A = rng.standard_normal((m, n))
+    Q, R = dev.qr(dev.from_numpy(A))
+    Q, R = dev.read(Q), dev.read(R)
+    k = min(m, n)
+    assert np.allclose(Q @ R, A, atol=1e-13 * np.abs(A).max())
+    assert np.allclose(Q.T @ Q, np.eye(k), atol=1e-13)
+    assert np.allclose(np.tril(R, -1), 0)
+    Rr, Qr = dev.rq(dev.from_numpy(A))
+    Rr, Qr = dev.read(Rr), dev.read(Qr)
+    assert np.allclose(Rr @ Qr, A, atol=1e-12 * np.abs(A).max())
+    assert np.allclose(Qr @ Qr.T, np.eye(k), atol=1e-12)
+
+
+@pytest.mark.parametrize("n", [1, 5, 40, 130])
+def test_cholesky_trsm(dev, n):
+    rng = _rng(n)
+    M = rng.standard_normal((n, n))
+    A = M @ M.T + n * np.eye(n)
+    L = dev.from_numpy(A)
+    dev.cholesky_(L)
+    Lh = dev.read(L)
+    assert np.allclose(Lh, np.linalg.cholesky(A), rtol=1e-12, atol=1e-12)
+    B = rng.standard_normal((n, 7))
+    X = dev.from_numpy(B)
+    dev.trsm_(L, X)
+    assert np.allclose(Lh @ dev.read(X), B, atol=1e-10)
+    X2 = dev.from_numpy(B)
+    dev.trsm_(L, X2, trans=True)
+    assert np.allclose(Lh.T @ dev.read(X2), B, atol=1e-10)
+
+
+def test_cholesky_not_pd_raises(dev):
+    A = dev.from_numpy(np.array([[1.0, 2.0], [2.0, 1.0]]))
+    with pytest.raises(dev.LinAlgError):
+        dev.cholesky_(A)
+
+
+@pytest.mark.parametrize("n", [1, 6, 50, 200])
+def test_lu_solve_rcond(dev, n):
+    rng = _rng(3 * n)
+    A = rng.standard_normal((n, n)) + 0.1 * np.eye(n)
+    b = rng.standard_normal((n, 3))
+    LU = dev.from_numpy(A)
+    piv = dev.lu_(LU)
+    X = dev.from_numpy(b)
+    dev.lu_solve_(LU, piv, X)
+    assert np.allclose(A @ dev.read(X), b, atol=1e-8 * np.linalg.cond(A))
+
+
+def test_lu_ill_conditioned_raises_warning(dev):
+    A = np.array([[1.0, 1.0], [1.0, 1.0 + 1e-17]])
+    A[1, 1] = 1.0 + 2 ** -52
+    with pytest.raises((dev.LinAlgWarning, dev.LinAlgError)):
+        dev.lu_(dev.from_numpy(A))
+
+
+@pytest.mark.parametrize("n", [1, 2, 9, 64, 150])
+def test_syev(dev, n):
+    rng = _rng(11 * n)
+    M = rng.standard_normal((n, n))
+    A = M + M.T
+    ev, W, evh = dev.syev(dev.from_numpy(A))
+    W = dev.read(W)
+    assert np.allclose(evh, np.linalg.eigvalsh(A), atol=1e-12 * max(1, np.abs(evh).max()))
+    assert np.allclose(A @ W, W * evh, atol=1e-11 * max(1, np.abs(evh).max()))
+
+
+def test_elementwise_and_reductions(dev):
+    rng = _rng(5)
+    a = rng.standard_normal((3, 4, 5))
+    b = rng.standard_normal((3, 4, 5))
+    ta, tb = dev.from_numpy(a), dev.from_numpy(b)
+    assert np.isclose(dev.dot(ta, tb), np.sum(a * b), rtol=1e-13)
+    assert np.isclose(dev.dot(ta.transpose(0, 2), tb.transpose(0, 2)), np.sum(a * b), rtol=1e-13)
+    out = dev.zeros(3, 5, 4)
+    dev.copy_(out, ta.transpose(1, 2), 2.0)
+    assert np.allclose(dev.read(out), 2 * np.swapaxes(a, 1, 2))
+    dev.mul_(out, ta.transpose(1, 2), tb.transpose(1, 2), 1.0, 1.0)
+    assert np.allclose(dev.read(out), 2 * np.swapaxes(a, 1, 2) + np.swapaxes(a * b, 1, 2))
+    r = dev.recip(dev.from_numpy(np.array([2.0, 4.0])))
+    assert np.allclose(dev.read(r), [0.5, 0.25])

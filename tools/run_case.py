@@ -1,0 +1,25 @@
+"""Run one (problem, config, seed, rank) through the MI355X path and compare with the golden run."""
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import yaml  # noqa: E402
+
+from ttipm_amd.utils import run_and_record  # noqa: E402
+
+prob, cfg_name, seed, rank = sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4])
+key = sys.argv[5] if len(sys.argv) > 5 else f"{cfg_name}_r{rank}_s{seed}"
+cfg = yaml.safe_load(open(os.path.join("configs", cfg_name + ".yaml")))
+trace = []
+t = time.time()
+r = run_and_record(prob, cfg, seed, rank, trace=trace, verbose=False)
+print("wall", time.time() - t)
+g = json.load(open("tests/golden/runs.json")).get(key)
+if g:
+    for k in ("num_iters", "gap", "feas", "dual_feas", "ranksX", "ranksZ"):
+        print(f"{k:10s} gpu={r[k]} ref={g[k]}")
+    for a, b in zip(trace, g["trace"]):
+        print(f"mu {a['mu']:.6e} {b['mu']:.6e}  primal {a['primal_error']:.6e} {b['primal_error']:.6e}  ranks {a['ranksX']} {b['ranksX']}")
+json.dump({"result": r, "trace": trace}, open(f"gpurun_out/run_{key}.json", "w"), indent=1)
