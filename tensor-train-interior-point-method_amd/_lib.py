@@ -5,6 +5,8 @@ library raises immediately, and every wrapper raises on a non-zero status."""
 import ctypes
 import os
 
+import torch  # noqa: F401  -- load PyTorch's HIP runtime first so libttk binds to the same one
+
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libttk.so")
 

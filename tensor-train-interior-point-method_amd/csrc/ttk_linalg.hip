@@ -22,7 +22,7 @@
 namespace {
 
 constexpr double EPS = 2.220446049250313e-16;
-constexpr int LDS_DOUBLES = 8000;  // 64000 B of dynamic LDS
+constexpr int LDS_DOUBLES = 20000;  // 160000 B of dynamic LDS (gfx950: 160 KiB per workgroup)
 
 // round-robin (circle method) pair k of round r over P (even) items
 __device__ __forceinline__ void rr_pair(int P, int r, int k, int &p, int &q) {
@@ -66,7 +66,10 @@ __global__ __launch_bounds__(1024) void svd_kernel(const double *__restrict__ A,
   for (int64_t e = tid; e < (int64_t)p * p; e += nt) V[e] = ((e / p) == (e % p)) ? 1.0 : 0.0;
   __syncthreads();
   const int P = (p % 2) ? p + 1 : p;
-  for (int sweep = 0; sweep < 60; ++sweep) {
+  // rotate only when the columns are not orthogonal to working precision (LAPACK gesvj uses
+  // sqrt(m)*eps; q*eps is the safe side that still converges quadratically)
+  const double tol = EPS * (q > 16 ? (double)q : 16.0);
+  for (int sweep = 0; sweep < 40; ++sweep) {
     if (tid == 0) any_rot = 0;
     __syncthreads();
     for (int r = 0; r < P - 1; ++r) {
@@ -85,8 +88,8 @@ __global__ __launch_bounds__(1024) void svd_kernel(const double *__restrict__ A,
         al = ttk::wave_sum(al);
         be = ttk::wave_sum(be);
         ga = ttk::wave_sum(ga);
-        if (al == 0.0 || be == 0.0) continue;
-        if (fabs(ga) <= EPS * sqrt(al) * sqrt(be)) continue;
+        if (al < 1e-300 || be < 1e-300) continue;
+        if (fabs(ga) <= tol * sqrt(al) * sqrt(be)) continue;
         const double zeta = (be - al) / (2.0 * ga);
         double t;
         if (fabs(zeta) > 1e150)
@@ -603,8 +606,12 @@ __global__ __launch_bounds__(1024) void syev_kernel(double *__restrict__ Ain, in
   }
   __syncthreads();
   const int P = (n % 2) ? n + 1 : n;
+  __shared__ double red[16];
   double fro = 0.0;
-  for (int sweep = 0; sweep < 60 && n > 1; ++sweep) {
+  for (int64_t e = tid; e < (int64_t)n * n; e += nt) fro += A[e] * A[e];
+  fro = sqrt(ttk::block_sum(fro, red));
+  const double abs_floor = EPS * fro / (n > 1 ? n : 1);
+  for (int sweep = 0; sweep < 40 && n > 1; ++sweep) {
     if (tid == 0) any_rot = 0;
     __syncthreads();
     for (int r = 0; r < P - 1; ++r) {
@@ -616,7 +623,7 @@ __global__ __launch_bounds__(1024) void syev_kernel(double *__restrict__ Ain, in
         if (q < n) {
           const double apq = A[(int64_t)p * n + q];
           const double app = A[(int64_t)p * n + p], aqq = A[(int64_t)q * n + q];
-          if (apq != 0.0 && fabs(apq) > EPS * sqrt(fabs(app) * fabs(aqq)) && fabs(apq) > 1e-300) {
+          if (fabs(apq) > EPS * sqrt(fabs(app) * fabs(aqq)) && fabs(apq) > abs_floor && fabs(apq) > 1e-300) {
             const double th = (aqq - app) / (2.0 * apq);
             double t;
             if (fabs(th) > 1e150)
@@ -666,7 +673,6 @@ __global__ __launch_bounds__(1024) void syev_kernel(double *__restrict__ Ain, in
     if (!any_rot) break;
     __syncthreads();
   }
-  (void)fro;
   for (int i = tid; i < n; i += nt) d[i] = A[(int64_t)i * n + i];
   __syncthreads();
   for (int j = tid; j < n; j += nt) {
@@ -681,6 +687,12 @@ __global__ __launch_bounds__(1024) void syev_kernel(double *__restrict__ Ain, in
     const int i = (int)(e / n), j = (int)(e % n);
     Wout[(int64_t)i * n + rank[j]] = V[e];
   }
+}
+
+template <typename K>
+void allow_big_lds(K kernel, size_t bytes) {
+  if (bytes > 65536) (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kernel),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
 }
 
 int *g_status = nullptr;
@@ -711,6 +723,7 @@ int ttk_svd(void *stream, const double *A, int m, int n, double *U, double *S, d
   const int64_t need = ttk_svd_work(m, n);
   const int use_lds = need <= LDS_DOUBLES;
   const size_t shm = use_lds ? need * sizeof(double) : 0;
+  allow_big_lds(svd_kernel, shm);
   hipLaunchKernelGGL(svd_kernel, dim3(1), dim3(1024), shm, TTK_STREAM(stream), A, m, n, U, S, Vt, work, use_lds);
   TTK_LAUNCH_CHECK();
   return TTK_OK;
@@ -729,6 +742,7 @@ int ttk_qr(void *stream, const double *A, int m, int n, double *Q, double *R, do
   const int64_t need = ttk_qr_work(m, n);
   const int use_lds = need <= LDS_DOUBLES;
   const size_t shm = use_lds ? need * sizeof(double) : 0;
+  allow_big_lds(qr_kernel, shm);
   hipLaunchKernelGGL(qr_kernel, dim3(1), dim3(1024), shm, TTK_STREAM(stream), A, m, n, Q, R, work, use_lds);
   TTK_LAUNCH_CHECK();
   return TTK_OK;
@@ -793,6 +807,7 @@ int ttk_syev(void *stream, double *A, int n, double *ev, double *W, double *work
   const int64_t need = ttk_syev_work(n);
   const int use_lds = need <= LDS_DOUBLES;
   const size_t shm = use_lds ? need * sizeof(double) : 0;
+  allow_big_lds(syev_kernel, shm);
   hipLaunchKernelGGL(syev_kernel, dim3(1), dim3(1024), shm, TTK_STREAM(stream), A, n, ev, W, work, use_lds);
   TTK_LAUNCH_CHECK();
   return TTK_OK;

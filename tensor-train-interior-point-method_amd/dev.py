@@ -54,6 +54,26 @@ def to_numpy(t):
     return t.detach().to("cpu").numpy()
 
 
+# optional op statistics (TTIPM_OPSTATS=1): name -> {shape: [count, seconds]} (synchronised timing)
+OPSTATS = {} if os.environ.get("TTIPM_OPSTATS") else None
+
+
+def _stat(name, shape, t0):
+    import time as _t
+    torch.cuda.synchronize()
+    d = OPSTATS.setdefault(name, {})
+    e = d.setdefault(shape, [0, 0.0])
+    e[0] += 1
+    e[1] += _t.perf_counter() - t0
+
+
+def _tic():
+    import time as _t
+    if OPSTATS is not None:
+        torch.cuda.synchronize()
+    return _t.perf_counter()
+
+
 def _arr(vals):
     a = (ctypes.c_int64 * len(vals))(*vals)
     return a
@@ -327,13 +347,17 @@ def matmul(a, b, out=None, alpha=1.0, beta=0.0):
 # ------------------------------------------------------------------------ factorisations
 def svd(A):
     """Thin SVD of a 2-D device matrix.  Returns (U, S, Vt, s_host)."""
+    t0 = _tic() if OPSTATS is not None else 0
     A = A.contiguous()
     m, n = A.shape
     k = min(m, n)
     U, S, Vt = empty(m, k), empty(k), empty(k, n)
     work = empty(int(lib.ttk_svd_work(m, n)))
     check(lib.ttk_svd(_stream(), _p(A), m, n, _p(U), _p(S), _p(Vt), _p(work)), "svd")
-    return U, S, Vt, read(S)
+    sh = read(S)
+    if OPSTATS is not None:
+        _stat("svd", (m, n), t0)
+    return U, S, Vt, sh
 
 
 def qr(A):
@@ -410,12 +434,16 @@ def lu_solve_(LU, piv, B):
 
 def syev(A):
     """Symmetric eigen-decomposition (Jacobi).  Returns (ev device, W device, ev_host)."""
-    A = clone(A) if not A.is_contiguous() else A.clone()
+    t0 = _tic() if OPSTATS is not None else 0
+    A = clone(A)
     n = A.shape[0]
     ev, W = empty(n), empty(n, n)
     work = empty(int(lib.ttk_syev_work(n)))
     check(lib.ttk_syev(_stream(), _p(A), n, _p(ev), _p(W), _p(work)), "syev")
-    return ev, W, read(ev)
+    evh = read(ev)
+    if OPSTATS is not None:
+        _stat("syev", n, t0)
+    return ev, W, evh
 
 
 __all__ = ["einsum", "tensordot", "matmul", "copy_", "scaled", "clone", "mul_", "recip", "fill_", "add_diag_",

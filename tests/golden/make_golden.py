@@ -8,7 +8,8 @@
   (opt_einsum -> numpy.einsum greedy; petsc4py KSPLGMRES -> oracle/petsc_lgmres.py restatement;
   scikit-sparse / memory_profiler -> unused stubs);
 * the reference's `IneqMatVecWrapper.matvec` returns a memoryview (`cy_src/lgmres_cy.pyx:510`);
-  the "fixed" inequality runs wrap it in `np.asarray` (SURVEY.md §0.5), the "shipped" runs do not;
+  "fixed" runs load the variant built by oracle/build_ref.py with that one line corrected
+  (SURVEY.md §0.5), "shipped" runs load the module as written; each run is its own process;
 * writes `tests/golden/runs.json` (per-seed final metrics + per-Newton-system trace) and
   `tests/golden/prims.npz` (primitive-level input/output pairs).
 
@@ -32,22 +33,15 @@ import yaml  # noqa: E402
 
 
 def _import_reference(fixed_ineq=True):
-    sys.path[:0] = [os.path.join(HERE, "refshim"), os.path.join(REPO, "oracle", "_ref"), REF]
     from oracle.build_ref import build
     build()
+    cy = os.path.join(REPO, "oracle", "_ref", "fixed") if fixed_ineq else os.path.join(REPO, "oracle", "_ref")
+    sys.path[:0] = [os.path.join(HERE, "refshim"), cy, REF]
     import src.tt_ops as rops  # noqa
     import src.tt_als as rals  # noqa
     import src.tt_ipm as ripm  # noqa
     import warnings
     warnings.simplefilter("default")  # tt_ipm sets "error" at import; re-enabled around runs
-    if fixed_ineq:
-        base = ripm.IneqMatVecWrapper
-
-        class FixedIneqMatVec(base):
-            def matvec(self, x):
-                return np.asarray(base.matvec(self, x))
-
-        ripm.IneqMatVecWrapper = FixedIneqMatVec
     return rops, rals, ripm
 
 
@@ -131,7 +125,10 @@ def make_runs(only=None):
         if only and cfg not in only and key not in only:
             continue
         print("running reference", key, flush=True)
-        res = run_reference(prob, cfg, seed, rank, fixed)
+        import subprocess
+        tmp = os.path.join("/tmp", f"golden_{key}.json")
+        subprocess.check_call([sys.executable, __file__, "one", prob, cfg, str(seed), str(rank), str(int(fixed)), tmp])
+        res = json.load(open(tmp))
         print(key, {k: res[k] for k in ("num_iters", "gap", "feas", "dual_feas", "sec_per_iter")}, flush=True)
         out[key] = res
         with open(path, "w") as f:
@@ -139,6 +136,10 @@ def make_runs(only=None):
 
 
 if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "one":
+        _, _, prob, cfg, seed, rank, fixed, tmp = sys.argv
+        json.dump(run_reference(prob, cfg, int(seed), int(rank), bool(int(fixed))), open(tmp, "w"))
+        sys.exit(0)
     what = sys.argv[1] if len(sys.argv) > 1 else "all"
     rest = sys.argv[2:]
     if what in ("runs", "all"):
