@@ -95,10 +95,16 @@ int ttk_read_sync(void *stream, const double *src, double *host_dst, int64_t n);
 int64_t ttk_svd_work(int m, int n);
 int ttk_svd(void *stream, const double *A, int m, int n, double *U, double *S, double *Vt,
             double *work);
+/* SVDs with min(m,n) >= p whose working set exceeds LDS take the multi-workgroup Jacobi path
+ * (default 64); p <= 2 forces it for every size (tests).  Returns the previous threshold. */
+int ttk_svd_set_big_threshold(int p);
 /* economic Householder QR A(m,n) = Q(m,k) R(k,n), k=min(m,n)  (scipy.linalg.qr economic,
  * `cy_src/tt_ops_cy.pyx:147-151`, `src/tt_als.py:358,482`). */
 int64_t ttk_qr_work(int m, int n);
 int ttk_qr(void *stream, const double *A, int m, int n, double *Q, double *R, double *work);
+/* QRs with min(m,n) >= k whose working set exceeds LDS take the blocked multi-workgroup
+ * Householder path (default 48); k <= 2 forces it (tests).  Returns the previous threshold. */
+int ttk_qr_set_big_threshold(int k);
 /* Cholesky (lower) in place on A(n,n); status TTK_ERR_NOT_PD like LAPACK potrf info>0
  * (`src/tt_ipm.py:204-207,300-303`). Blocks on the stream to return the status. */
 int ttk_cholesky_sync(void *stream, double *A, int n);
@@ -116,6 +122,16 @@ int ttk_lu_solve(void *stream, const double *LU, int n, const int *piv, double *
  * `src/tt_als.py:963-993,1069-1098,1308`). */
 int64_t ttk_syev_work(int n);
 int ttk_syev(void *stream, double *A, int n, double *ev, double *W, double *work);
+/* one extreme eigenpair of a symmetric A(n,n) (which = 0: smallest, 1: largest): Householder
+ * tridiagonalisation + Sturm multisection + inverse iteration, one launch.  ev: 1 device double,
+ * vec: n device doubles (unit 2-norm).  A is not modified.  Replaces the `eigsh(which='SA'|'LA')`
+ * calls of the step-size ALS (`src/tt_als.py:963-993` (_step_size_local_solve),
+ * `:1069-1098`, `:1308` (_eigen_local_solve)). */
+int64_t ttk_syev_extreme_work(int n);
+/* diagnostic counters of the factorisation kernels (8 x u64: svd calls, svd sweeps, eig calls,
+ * multisection rounds, ...); synchronous; reset != 0 zeroes them */
+int ttk_debug_counters(unsigned long long *out, int reset);
+int ttk_syev_extreme(void *stream, const double *A, int n, int which, double *ev, double *vec, double *work);
 
 /* ---------------------------------------------------------------------------------------
  * LGMRES building blocks (PETSc KSPLGMRES semantics, see oracle/petsc_lgmres.py):

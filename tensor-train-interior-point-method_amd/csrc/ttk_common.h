@@ -23,10 +23,47 @@ struct NdDesc {
   int64_t s2[MAXD];
 };
 
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+// Cross-lane moves through DPP (ALU latency) instead of ds_bpermute (LDS round trip).
+template <int CTRL>
+__device__ __forceinline__ double dpp_mov(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xf, 0xf, false);
+  return __hiloint2double(hi, lo);
+}
+
+// all-reduce over aligned groups of G lanes (G = 1, 2, 4, 8, 16); every lane of a group ends
+// with the bitwise-same value (each stage adds two equal partial sums in swapped order)
+template <int G>
+__device__ __forceinline__ double group_sum(double v) {
+  if (G >= 2) v += dpp_mov<0xB1>(v);   // quad_perm [1,0,3,2]
+  if (G >= 4) v += dpp_mov<0x4E>(v);   // quad_perm [2,3,0,1]
+  if (G >= 8) v += dpp_mov<0x141>(v);  // row_half_mirror
+  if (G >= 16) v += dpp_mov<0x140>(v); // row_mirror
   return v;
+}
+
+__device__ __forceinline__ double readlane_d(double v, int l) {
+  return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l),
+                          __builtin_amdgcn_readlane(__double2loint(v), l));
+}
+
+// wave-wide sum, uniform result; the whole wave must be active
+__device__ __forceinline__ double wave_sum(double v) {
+  v = group_sum<16>(v);
+  return (readlane_d(v, 0) + readlane_d(v, 16)) + (readlane_d(v, 32) + readlane_d(v, 48));
+}
+
+// all-reduce over aligned groups of g lanes, g a power of two <= 64 (uniform within a group)
+__device__ __forceinline__ double group_sum_rt(double v, int g) {
+  switch (g) {
+    case 1: return v;
+    case 2: return group_sum<2>(v);
+    case 4: return group_sum<4>(v);
+    case 8: return group_sum<8>(v);
+    case 16: return group_sum<16>(v);
+    case 32: v = group_sum<16>(v); return v + __shfl_xor(v, 16, 64);
+    default: return wave_sum(v);
+  }
 }
 
 // block-wide sum; `red` must hold blockDim.x/64 doubles; result valid on all threads

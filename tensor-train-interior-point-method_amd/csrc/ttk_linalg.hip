@@ -22,6 +22,9 @@
 namespace {
 
 constexpr double EPS = 2.220446049250313e-16;
+// diagnostic counters: [0] svd calls, [1] svd sweeps, [2] eig calls, [3] multisection rounds
+__device__ unsigned long long g_dbg[8];
+
 constexpr int LDS_DOUBLES = 20000;  // 160000 B of dynamic LDS (gfx950: 160 KiB per workgroup)
 
 // round-robin (circle method) pair k of round r over P (even) items
@@ -42,79 +45,14 @@ __device__ __forceinline__ void rr_pair(int P, int r, int k, int &p, int &q) {
 
 // ------------------------------------------------------------------------------ SVD
 // W: q x p column-major (column j at W + j*q), V: p x p column-major.
-__global__ __launch_bounds__(1024) void svd_kernel(const double *__restrict__ A, int m, int n,
-                                                   double *__restrict__ U, double *__restrict__ S,
-                                                   double *__restrict__ Vt, double *__restrict__ gwork,
-                                                   int use_lds) {
-  extern __shared__ double lds[];
-  __shared__ int any_rot;
+// Shared epilogue of both SVD paths (one workgroup): singular values = column norms of the
+// converged W, descending order, unit left vectors (exact-zero columns completed), outputs.
+__device__ void svd_epilogue(double *W, double *V, double *sig, int *rank, int m, int n, bool tall,
+                             double *__restrict__ U, double *__restrict__ S, double *__restrict__ Vt) {
   __shared__ double red[16];
-  const bool tall = m >= n;
-  const int p = tall ? n : m;  // columns to orthogonalise
-  const int q = tall ? m : n;  // column length
-  double *base = use_lds ? lds : gwork;
-  double *W = base;
-  double *V = W + (int64_t)q * p;
-  double *sig = V + (int64_t)p * p;
-  int *rank = reinterpret_cast<int *>(sig + p);
+  const int p = tall ? n : m, q = tall ? m : n;
   const int tid = threadIdx.x, nt = blockDim.x;
   const int lane = tid & 63, wid = tid >> 6, nw = nt >> 6;
-  for (int64_t e = tid; e < (int64_t)q * p; e += nt) {
-    const int j = (int)(e / q), i = (int)(e % q);
-    W[e] = tall ? A[(int64_t)i * n + j] : A[(int64_t)j * n + i];
-  }
-  for (int64_t e = tid; e < (int64_t)p * p; e += nt) V[e] = ((e / p) == (e % p)) ? 1.0 : 0.0;
-  __syncthreads();
-  const int P = (p % 2) ? p + 1 : p;
-  // rotate only when the columns are not orthogonal to working precision (LAPACK gesvj uses
-  // sqrt(m)*eps; q*eps is the safe side that still converges quadratically)
-  const double tol = EPS * (q > 16 ? (double)q : 16.0);
-  for (int sweep = 0; sweep < 40; ++sweep) {
-    if (tid == 0) any_rot = 0;
-    __syncthreads();
-    for (int r = 0; r < P - 1; ++r) {
-      for (int k = wid; k < P / 2; k += nw) {
-        int a, b;
-        rr_pair(P, r, k, a, b);
-        if (b >= p) continue;  // dummy partner
-        double *wa = W + (int64_t)a * q, *wb = W + (int64_t)b * q;
-        double al = 0.0, be = 0.0, ga = 0.0;
-        for (int i = lane; i < q; i += 64) {
-          const double x = wa[i], y = wb[i];
-          al += x * x;
-          be += y * y;
-          ga += x * y;
-        }
-        al = ttk::wave_sum(al);
-        be = ttk::wave_sum(be);
-        ga = ttk::wave_sum(ga);
-        if (al < 1e-300 || be < 1e-300) continue;
-        if (fabs(ga) <= tol * sqrt(al) * sqrt(be)) continue;
-        const double zeta = (be - al) / (2.0 * ga);
-        double t;
-        if (fabs(zeta) > 1e150)
-          t = 0.5 / zeta;
-        else
-          t = (zeta >= 0.0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
-        const double c = 1.0 / sqrt(1.0 + t * t), s = c * t;
-        for (int i = lane; i < q; i += 64) {
-          const double x = wa[i], y = wb[i];
-          wa[i] = c * x - s * y;
-          wb[i] = s * x + c * y;
-        }
-        double *va = V + (int64_t)a * p, *vb = V + (int64_t)b * p;
-        for (int i = lane; i < p; i += 64) {
-          const double x = va[i], y = vb[i];
-          va[i] = c * x - s * y;
-          vb[i] = s * x + c * y;
-        }
-        if (lane == 0) any_rot = 1;
-      }
-      __syncthreads();
-    }
-    if (!any_rot) break;
-    __syncthreads();
-  }
   // singular values = column norms
   for (int j = wid; j < p; j += nw) {
     const double *wj = W + (int64_t)j * q;
@@ -194,6 +132,139 @@ __global__ __launch_bounds__(1024) void svd_kernel(const double *__restrict__ A,
       Vt[(int64_t)rank[j] * n + i] = W[(int64_t)j * q + i];
     }
   }
+}
+
+__global__ __launch_bounds__(1024) void svd_kernel(const double *__restrict__ A, int m, int n,
+                                                   double *__restrict__ U, double *__restrict__ S,
+                                                   double *__restrict__ Vt, double *__restrict__ gwork,
+                                                   int use_lds, int g) {
+  extern __shared__ double lds[];
+  __shared__ int any_rot;
+  const bool tall = m >= n;
+  const int p = tall ? n : m;  // columns to orthogonalise
+  const int q = tall ? m : n;  // column length
+  double *base = use_lds ? lds : gwork;
+  double *W = base;
+  double *V = W + (int64_t)q * p;
+  double *sig = V + (int64_t)p * p;
+  int *rank = reinterpret_cast<int *>(sig + p);
+  const int tid = threadIdx.x, nt = blockDim.x;
+  const int lane = tid & 63, wid = tid >> 6, nw = nt >> 6;
+  for (int e = tid; e < q * p; e += nt) {
+    const int j = e / q, i = e - j * q;
+    W[e] = tall ? A[(int64_t)i * n + j] : A[(int64_t)j * n + i];
+  }
+  for (int e = tid; e < p * p; e += nt) V[e] = ((e / p) == (e % p)) ? 1.0 : 0.0;
+  __syncthreads();
+  const int P = (p % 2) ? p + 1 : p;
+  // g lanes per column pair (host picks g ~ q/4, bounded by the block); group reductions are DPP
+  const int gl = tid & (g - 1), gid = tid / g, ng = nt / g;
+  // rotate only when the columns are not orthogonal to working precision (LAPACK gesvj uses
+  // sqrt(m)*eps; q*eps is the safe side that still converges quadratically)
+  const double tol = EPS * (q > 16 ? (double)q : 16.0);
+  for (int sweep = 0; sweep < 40; ++sweep) {
+    if (tid == 0) any_rot = 0;
+    __syncthreads();
+    for (int r = 0; r < P - 1; ++r) {
+      for (int k = gid; k < P / 2; k += ng) {
+        int a, b;
+        rr_pair(P, r, k, a, b);
+        if (b >= p) continue;  // dummy partner (uniform within the group)
+        double *wa = W + (int64_t)a * q, *wb = W + (int64_t)b * q;
+        double al = 0.0, be = 0.0, ga = 0.0;
+        for (int i = gl; i < q; i += g) {
+          const double x = wa[i], y = wb[i];
+          al += x * x;
+          be += y * y;
+          ga += x * y;
+        }
+        al = ttk::group_sum_rt(al, g);
+        be = ttk::group_sum_rt(be, g);
+        ga = ttk::group_sum_rt(ga, g);
+        if (al < 1e-300 || be < 1e-300) continue;
+        if (fabs(ga) <= tol * sqrt(al) * sqrt(be)) continue;
+        const double zeta = (be - al) / (2.0 * ga);
+        double t;
+        if (fabs(zeta) > 1e150)
+          t = 0.5 / zeta;
+        else
+          t = (zeta >= 0.0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
+        const double c = 1.0 / sqrt(1.0 + t * t), s = c * t;
+        for (int i = gl; i < q; i += g) {
+          const double x = wa[i], y = wb[i];
+          wa[i] = c * x - s * y;
+          wb[i] = s * x + c * y;
+        }
+        double *va = V + (int64_t)a * p, *vb = V + (int64_t)b * p;
+        for (int i = gl; i < p; i += g) {
+          const double x = va[i], y = vb[i];
+          va[i] = c * x - s * y;
+          vb[i] = s * x + c * y;
+        }
+        if (gl == 0) any_rot = 1;
+      }
+      __syncthreads();
+    }
+    if (tid == 0) atomicAdd(&g_dbg[1], 1ull);
+    if (!any_rot) break;
+    __syncthreads();
+  }
+  if (tid == 0) atomicAdd(&g_dbg[0], 1ull);
+  svd_epilogue(W, V, sig, rank, m, n, tall, U, S, Vt);
+}
+
+// Multi-workgroup one-sided Jacobi for large unfoldings (the 1e-12 rank reductions at the end of
+// a solve produce ~1000 x 1000 swap/rounding unfoldings), run on X = R^T after a blocked QR
+// (svd_big below).  One wave per column pair, one launch per round-robin round (all P/2 pairs in
+// flight across the chip); X and V stay L2/MALL resident.  The host drives sweeps and reads one
+// convergence flag per sweep.
+__global__ __launch_bounds__(256) void svd_big_round_kernel(double *__restrict__ W, double *__restrict__ V, int p,
+                                                            int q, int r, double tol, int *__restrict__ flag) {
+  const int P = (p % 2) ? p + 1 : p;
+  const int k = (int)((blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6);
+  const int lane = threadIdx.x & 63;
+  if (k >= P / 2) return;  // whole wave exits together
+  int a, b;
+  rr_pair(P, r, k, a, b);
+  if (b >= p) return;
+  double *wa = W + (int64_t)a * q, *wb = W + (int64_t)b * q;
+  double al = 0.0, be = 0.0, ga = 0.0;
+  for (int i = lane; i < q; i += 64) {
+    const double x = wa[i], y = wb[i];
+    al += x * x;
+    be += y * y;
+    ga += x * y;
+  }
+  al = ttk::wave_sum(al);
+  be = ttk::wave_sum(be);
+  ga = ttk::wave_sum(ga);
+  if (al < 1e-300 || be < 1e-300) return;
+  if (fabs(ga) <= tol * sqrt(al) * sqrt(be)) return;
+  const double zeta = (be - al) / (2.0 * ga);
+  double t;
+  if (fabs(zeta) > 1e150)
+    t = 0.5 / zeta;
+  else
+    t = (zeta >= 0.0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
+  const double c = 1.0 / sqrt(1.0 + t * t), s = c * t;
+  for (int i = lane; i < q; i += 64) {
+    const double x = wa[i], y = wb[i];
+    wa[i] = c * x - s * y;
+    wb[i] = s * x + c * y;
+  }
+  double *va = V + (int64_t)a * p, *vb = V + (int64_t)b * p;
+  for (int i = lane; i < p; i += 64) {
+    const double x = va[i], y = vb[i];
+    va[i] = c * x - s * y;
+    vb[i] = s * x + c * y;
+  }
+  if (lane == 0) *flag = 1;
+}
+
+__global__ __launch_bounds__(1024) void svd_big_finish_kernel(double *W, double *V, double *sig, int *rank, int m,
+                                                              int n, double *__restrict__ U, double *__restrict__ S,
+                                                              double *__restrict__ Vt) {
+  svd_epilogue(W, V, sig, rank, m, n, m >= n, U, S, Vt);
 }
 
 // ------------------------------------------------------------------------------ QR
@@ -610,7 +681,7 @@ __global__ __launch_bounds__(1024) void syev_kernel(double *__restrict__ Ain, in
   double fro = 0.0;
   for (int64_t e = tid; e < (int64_t)n * n; e += nt) fro += A[e] * A[e];
   fro = sqrt(ttk::block_sum(fro, red));
-  const double abs_floor = EPS * fro / (n > 1 ? n : 1);
+  const double abs_floor = EPS * fro;
   for (int sweep = 0; sweep < 40 && n > 1; ++sweep) {
     if (tid == 0) any_rot = 0;
     __syncthreads();
@@ -689,10 +760,475 @@ __global__ __launch_bounds__(1024) void syev_kernel(double *__restrict__ Ain, in
   }
 }
 
+// ------------------------------------------------------------------ extreme eigenpair
+// One eigenpair (the smallest, which=0, or the largest, which=1) of a symmetric n x n matrix:
+//   1. Householder tridiagonalisation Q^T A Q = T (row-oriented dsytd2; reflector k is kept in
+//      row k right of the diagonal, its tau in tv[k]),
+//   2. Sturm-count multisection on T: every thread evaluates one shift, so each round shrinks
+//      the bracket ~1000x (about 6 rounds reach working precision),
+//   3. inverse iteration on T (tridiagonal LU with partial pivoting as dgttrf/dgtts2, thread 0),
+//   4. back-transform y = H_0 ... H_{n-3} z by one wave.
+// ~4/3 n^3 flops once, against ~10 sweeps x 4 n^3 for cyclic Jacobi; only the extreme pair is
+// used on the path (`_min_eigpair` / `_gen_max_eig` in tt_eig.py).
+int64_t syev_extreme_need(int n) { return (int64_t)n * n + 12 * (int64_t)n + 16; }
+
+__global__ __launch_bounds__(1024) void syev_extreme_kernel(const double *__restrict__ Ain, int n, int which,
+                                                            double *__restrict__ ev_out,
+                                                            double *__restrict__ vec_out,
+                                                            double *__restrict__ gwork, int use_lds) {
+  extern __shared__ double lds[];
+  __shared__ double red[16];
+  __shared__ double sh_a, sh_b;
+  __shared__ int sh_first;
+  double *A = use_lds ? lds : gwork;
+  double *dv = A + (int64_t)n * n;  // diag(T)
+  double *ov = dv + n;              // offdiag(T)
+  double *ev2 = ov + n;             // offdiag^2
+  double *tv = ev2 + n;             // tau per reflector
+  double *pv = tv + n;              // matvec scratch
+  double *z = pv + n;               // eigenvector (T basis, then A basis)
+  double *fd = z + n, *fdu = fd + n, *fdu2 = fdu + n, *fdl = fdu2 + n, *fpiv = fdl + n;
+  const int tid = threadIdx.x, nt = blockDim.x;
+  const int lane = tid & 63, wid = tid >> 6, nw = nt >> 6;
+  for (int e = tid; e < n * n; e += nt) A[e] = Ain[e];
+  __syncthreads();
+  // ---- 1. tridiagonalisation (3 barriers per reflector)
+  for (int k = 0; k + 2 < n; ++k) {
+    double *v = A + (int64_t)k * n + k + 1;  // x = A[k, k+1:], becomes the reflector
+    const int m = n - k - 1;
+    if (wid == 0) {  // reflector by wave 0
+      double part = 0.0;
+      for (int i = 1 + lane; i < m; i += 64) part += v[i] * v[i];
+      const double sigma = ttk::wave_sum(part);
+      const double alpha = v[0];
+      double tau = 0.0, beta = alpha;
+      if (sigma > 0.0) {
+        beta = -copysign(sqrt(alpha * alpha + sigma), alpha);
+        tau = (beta - alpha) / beta;
+        const double sc = 1.0 / (alpha - beta);
+        for (int i = 1 + lane; i < m; i += 64) v[i] *= sc;
+      }
+      if (lane == 0) {
+        v[0] = 1.0;
+        tv[k] = tau;
+        ov[k] = beta;
+        dv[k] = A[(int64_t)k * n + k];
+      }
+    }
+    __syncthreads();
+    const double tau = tv[k];
+    if (tau == 0.0) continue;
+    // p = tau * A22 v with g lanes per row
+    int g = 1;
+    while (g < 16 && 2 * g * m <= nt) g *= 2;
+    const int gl = tid & (g - 1), ng = nt / g;
+    for (int i = tid / g; i < m; i += ng) {
+      const double *ai = A + (int64_t)(k + 1 + i) * n + k + 1;
+      double acc = 0.0;
+      for (int j = gl; j < m; j += g) acc += ai[j] * v[j];
+      acc = ttk::group_sum_rt(acc, g);
+      if (gl == 0) pv[i] = tau * acc;
+    }
+    __syncthreads();
+    double part = 0.0;  // every wave forms K = tau/2 p^T v itself (no barrier)
+    for (int i = lane; i < m; i += 64) part += pv[i] * v[i];
+    const double K = 0.5 * tau * ttk::wave_sum(part);
+    for (int i = wid; i < m; i += nw) {  // A22 -= v w^T + w v^T, w = p - K v
+      const double vi = v[i], wi = pv[i] - K * vi;
+      double *ai = A + (int64_t)(k + 1 + i) * n + k + 1;
+      for (int j = lane; j < m; j += 64) {
+        const double vj = v[j];
+        ai[j] -= vi * (pv[j] - K * vj) + wi * vj;
+      }
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    if (n >= 2) {
+      dv[n - 2] = A[(int64_t)(n - 2) * n + n - 2];
+      ov[n - 2] = A[(int64_t)(n - 2) * n + n - 1];
+      tv[n - 2] = 0.0;
+    }
+    dv[n - 1] = A[(int64_t)(n - 1) * n + n - 1];
+  }
+  __syncthreads();
+  for (int i = tid; i + 1 < n; i += nt) ev2[i] = ov[i] * ov[i];
+  __syncthreads();
+  // Gershgorin bracket
+  double lo = 1e308, hi = -1e308, emax2 = 0.0;
+  for (int i = 0; i < n; ++i) {
+    const double r = (i > 0 ? fabs(ov[i - 1]) : 0.0) + (i + 1 < n ? fabs(ov[i]) : 0.0);
+    lo = fmin(lo, dv[i] - r);
+    hi = fmax(hi, dv[i] + r);
+    if (i + 1 < n) emax2 = fmax(emax2, ev2[i]);
+  }
+  const double tnorm = fmax(fmax(fabs(lo), fabs(hi)), 1e-300);
+  const double pivmin = fmax(2.2250738585072014e-308 * fmax(emax2, 1.0), 1e-290);
+  const double pad = 2.0 * EPS * tnorm + 4.0 * pivmin;
+  lo -= pad;
+  hi += pad;
+  const int target = which ? n : 1;  // smallest x with #{eig < x} >= target
+  if (tid == 0) {
+    sh_a = lo;
+    sh_b = hi;
+  }
+  __syncthreads();
+  // ---- 2. multisection
+  for (int round = 0; round < 16; ++round) {
+    const double a = sh_a, b = sh_b;
+    if (b - a <= 2.0 * EPS * fmax(fabs(a), fabs(b)) + 2.0 * pivmin) break;
+    if (tid == 0) atomicAdd(&g_dbg[3], 1ull);
+    const double x = a + (b - a) * (double)(tid + 1) / (double)(nt + 1);
+    int cnt = 0;
+    double q = dv[0] - x;
+    if (fabs(q) < pivmin) q = -pivmin;
+    cnt += q < 0.0;
+    for (int i = 1; i < n; ++i) {
+      q = dv[i] - x - ev2[i - 1] / q;
+      if (fabs(q) < pivmin) q = -pivmin;
+      cnt += q < 0.0;
+    }
+    if (tid == 0) sh_first = nt;
+    __syncthreads();
+    if (cnt >= target) atomicMin(&sh_first, tid);
+    __syncthreads();
+    if (tid == 0) {
+      const int f = sh_first;
+      sh_a = (f == 0) ? a : a + (b - a) * (double)f / (double)(nt + 1);
+      sh_b = (f >= nt) ? b : a + (b - a) * (double)(f + 1) / (double)(nt + 1);
+    }
+    __syncthreads();
+  }
+  const double lam = 0.5 * (sh_a + sh_b);
+  if (tid == 0) atomicAdd(&g_dbg[2], 1ull);
+  // ---- 3. inverse iteration on T (thread 0, O(n) per solve)
+  if (tid == 0) {
+    for (int i = 0; i < n; ++i) {
+      fd[i] = dv[i] - lam;
+      fdu[i] = (i + 1 < n) ? ov[i] : 0.0;
+      fdl[i] = fdu[i];
+      fdu2[i] = 0.0;
+      fpiv[i] = 0.0;
+    }
+    for (int i = 0; i + 1 < n; ++i) {  // dgttrf
+      if (fabs(fd[i]) >= fabs(fdl[i])) {
+        if (fd[i] != 0.0) {
+          const double f = fdl[i] / fd[i];
+          fdl[i] = f;
+          fd[i + 1] -= f * fdu[i];
+        }
+      } else {
+        const double f = fd[i] / fdl[i];
+        fd[i] = fdl[i];
+        fdl[i] = f;
+        const double t = fdu[i];
+        fdu[i] = fd[i + 1];
+        fd[i + 1] = t - f * fd[i + 1];
+        if (i + 2 < n) {
+          fdu2[i] = fdu[i + 1];
+          fdu[i + 1] = -f * fdu[i + 1];
+        }
+        fpiv[i] = 1.0;
+      }
+    }
+    const double tiny = EPS * tnorm;
+    for (int i = 0; i < n; ++i)
+      if (fabs(fd[i]) < tiny) fd[i] = copysign(tiny, fd[i] == 0.0 ? 1.0 : fd[i]);
+    uint32_t h = 0x9e3779b9u;  // fixed pseudo-random start (dstein uses a random start)
+    for (int i = 0; i < n; ++i) {
+      h ^= h << 13;
+      h ^= h >> 17;
+      h ^= h << 5;
+      z[i] = 0.5 + (double)(h & 0xffffff) / 16777216.0;
+    }
+    for (int it = 0; it < 3; ++it) {
+      for (int i = 0; i + 1 < n; ++i) {  // dgtts2 forward
+        if (fpiv[i] == 0.0) {
+          z[i + 1] -= fdl[i] * z[i];
+        } else {
+          const double t = z[i];
+          z[i] = z[i + 1];
+          z[i + 1] = t - fdl[i] * z[i];
+        }
+      }
+      z[n - 1] /= fd[n - 1];
+      if (n > 1) z[n - 2] = (z[n - 2] - fdu[n - 2] * z[n - 1]) / fd[n - 2];
+      for (int i = n - 3; i >= 0; --i) z[i] = (z[i] - fdu[i] * z[i + 1] - fdu2[i] * z[i + 2]) / fd[i];
+      double mx = 0.0;
+      for (int i = 0; i < n; ++i) mx = fmax(mx, fabs(z[i]));
+      const double sc = mx > 0.0 ? 1.0 / mx : 1.0;
+      for (int i = 0; i < n; ++i) z[i] *= sc;
+    }
+    double nn = 0.0;
+    for (int i = 0; i < n; ++i) nn += z[i] * z[i];
+    const double sc = 1.0 / sqrt(nn);
+    for (int i = 0; i < n; ++i) z[i] *= sc;
+    ev_out[0] = lam;
+  }
+  __syncthreads();
+  // ---- 4. back-transform by wave 0 (no block barriers inside)
+  if (wid == 0) {
+    for (int k = n - 3; k >= 0; --k) {
+      const double tau = tv[k];
+      if (tau == 0.0) continue;
+      const double *v = A + (int64_t)k * n + k + 1;
+      double *zk = z + k + 1;
+      const int m = n - k - 1;
+      double acc = 0.0;
+      for (int j = lane; j < m; j += 64) acc += v[j] * zk[j];
+      acc = tau * ttk::wave_sum(acc);
+      for (int j = lane; j < m; j += 64) zk[j] -= acc * v[j];
+      __threadfence_block();
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < n; i += nt) vec_out[i] = z[i];
+}
+
 template <typename K>
 void allow_big_lds(K kernel, size_t bytes) {
   if (bytes > 65536) (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kernel),
                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+}
+
+// ---------------------------------------------------------------- blocked Householder QR
+// Multi-workgroup QR for large matrices (LAPACK dgeqrf + dorgqr structure):
+//   panel  : one workgroup factors nb columns (dgeqr2) and forms the nb x nb triangular factor T
+//            of the compact-WY form H_j0 ... H_j0+nb-1 = I - Y T Y^T (dlarft, forward/columnwise),
+//   apply  : C <- (I - Y op(T) Y^T) C over the chip in two launches: Z = op(T) (Y^T C) (one
+//            workgroup per 16 columns, reduction over rows staged through LDS), then C -= Y Z
+//            (64 x 16 tiles).  op = T^T applies Q^T (trailing update), op = T applies Q.
+// Matrices are column-major with leading dimension ld (column j at base + j*ld).  Y_k is column
+// j0+k of the factored matrix with an implicit 1 at row j0+k and zeros above.
+constexpr int QB = 32;  // panel width
+
+__device__ __forceinline__ double ycoef(const double *Wf, int ld, int j0, int k, int row) {
+  const int d = j0 + k;
+  return row < d ? 0.0 : (row == d ? 1.0 : Wf[(int64_t)d * ld + row]);
+}
+
+__global__ __launch_bounds__(1024) void qrb_panel_kernel(double *W, int m, int ld, int j0, int nbe,
+                                                         double *__restrict__ tau, double *__restrict__ T) {
+  __shared__ double red[16];
+  __shared__ double ytv[QB];
+  const int tid = threadIdx.x, nt = blockDim.x;
+  const int lane = tid & 63, wid = tid >> 6, nw = nt >> 6;
+  for (int e = tid; e < QB * QB; e += nt) T[e] = 0.0;
+  for (int jj = 0; jj < nbe; ++jj) {
+    const int c = j0 + jj;
+    double *x = W + (int64_t)c * ld;
+    double part = 0.0;
+    for (int i = c + 1 + tid; i < m; i += nt) part += x[i] * x[i];
+    const double sigma = ttk::block_sum(part, red);
+    const double alpha = x[c];
+    double t = 0.0, beta = alpha;
+    if (sigma > 0.0) {
+      beta = -copysign(sqrt(alpha * alpha + sigma), alpha);
+      t = (beta - alpha) / beta;
+      const double sc = 1.0 / (alpha - beta);
+      for (int i = c + 1 + tid; i < m; i += nt) x[i] *= sc;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      x[c] = beta;
+      tau[c] = t;
+    }
+    // apply H_c to the remaining panel columns (one wave per column); v = [1; x[c+1:]]
+    for (int c2 = c + 1 + wid; c2 < j0 + nbe; c2 += nw) {
+      double *y = W + (int64_t)c2 * ld;
+      double acc = 0.0;
+      for (int i = c + 1 + lane; i < m; i += 64) acc += x[i] * y[i];
+      const double w = t * (ttk::wave_sum(acc) + y[c]);
+      for (int i = c + 1 + lane; i < m; i += 64) y[i] -= w * x[i];
+      if (lane == 0) y[c] -= w;
+    }
+    // T(0:jj, jj) = -t T(0:jj, 0:jj) (Y(:, 0:jj)^T v)
+    for (int k = wid; k < jj; k += nw) {
+      const double *yk = W + (int64_t)(j0 + k) * ld;
+      double acc = 0.0;
+      for (int i = c + 1 + lane; i < m; i += 64) acc += yk[i] * x[i];
+      acc = ttk::wave_sum(acc) + yk[c];
+      if (lane == 0) ytv[k] = acc;
+    }
+    __syncthreads();
+    if (tid < jj) {
+      double acc = 0.0;
+      for (int k = tid; k < jj; ++k) acc += T[tid + k * QB] * ytv[k];
+      T[tid + jj * QB] = -t * acc;
+    }
+    if (tid == 0) T[jj + jj * QB] = t;
+    __syncthreads();
+  }
+}
+
+// Z(0:nbe, 0:ncols) = op(T) Y^T C(:, c0:c0+ncols), rows j0..m-1
+__global__ __launch_bounds__(256) void qrb_ytc_kernel(const double *__restrict__ Wf, int m, int ldw, int j0, int nbe,
+                                                      const double *__restrict__ C, int ldc, int c0, int ncols,
+                                                      const double *__restrict__ T, int transT,
+                                                      double *__restrict__ Z) {
+  __shared__ double ys[64][QB + 1];
+  __shared__ double cs[64][17];
+  __shared__ double zs[QB][17];
+  __shared__ double ts[QB][QB + 1];
+  const int tid = threadIdx.x;
+  const int colb = blockIdx.x * 16;
+  const int k = tid >> 3, cl = (tid & 7) * 2;  // 32 x 8 threads, 2 columns each
+  double acc0 = 0.0, acc1 = 0.0;
+  for (int r0 = j0; r0 < m; r0 += 64) {
+    for (int e = tid; e < 64 * QB; e += 256) {
+      const int rr = e & 63, kk = e >> 6, row = r0 + rr;
+      ys[rr][kk] = (row < m && kk < nbe) ? ycoef(Wf, ldw, j0, kk, row) : 0.0;
+    }
+    for (int e = tid; e < 64 * 16; e += 256) {
+      const int rr = e & 63, cc = e >> 6, row = r0 + rr, col = colb + cc;
+      cs[rr][cc] = (row < m && col < ncols) ? C[(int64_t)(c0 + col) * ldc + row] : 0.0;
+    }
+    __syncthreads();
+#pragma unroll 8
+    for (int rr = 0; rr < 64; ++rr) {
+      const double y = ys[rr][k];
+      acc0 += y * cs[rr][cl];
+      acc1 += y * cs[rr][cl + 1];
+    }
+    __syncthreads();
+  }
+  zs[k][cl] = acc0;
+  zs[k][cl + 1] = acc1;
+  for (int e = tid; e < QB * QB; e += 256) {
+    const int i = e & (QB - 1), j = e / QB;
+    ts[i][j] = transT ? T[j + i * QB] : T[i + j * QB];  // op(T)(i, j)
+  }
+  __syncthreads();
+  double o0 = 0.0, o1 = 0.0;
+  for (int j = 0; j < nbe; ++j) {
+    const double tij = ts[k][j];
+    o0 += tij * zs[j][cl];
+    o1 += tij * zs[j][cl + 1];
+  }
+  if (k < nbe) {
+    if (colb + cl < ncols) Z[(int64_t)(colb + cl) * QB + k] = o0;
+    if (colb + cl + 1 < ncols) Z[(int64_t)(colb + cl + 1) * QB + k] = o1;
+  }
+}
+
+// C(j0:m, c0:c0+ncols) -= Y Z
+__global__ __launch_bounds__(256) void qrb_update_kernel(const double *__restrict__ Wf, int m, int ldw, int j0,
+                                                         int nbe, double *__restrict__ C, int ldc, int c0, int ncols,
+                                                         const double *__restrict__ Z) {
+  __shared__ double ys[64][QB + 1];
+  __shared__ double zs[QB][17];
+  const int tid = threadIdx.x;
+  const int r0 = j0 + blockIdx.x * 64, colb = blockIdx.y * 16;
+  for (int e = tid; e < 64 * QB; e += 256) {
+    const int rr = e & 63, kk = e >> 6, row = r0 + rr;
+    ys[rr][kk] = (row < m && kk < nbe) ? ycoef(Wf, ldw, j0, kk, row) : 0.0;
+  }
+  for (int e = tid; e < QB * 16; e += 256) {
+    const int kk = e & (QB - 1), cc = e / QB, col = colb + cc;
+    zs[kk][cc] = (kk < nbe && col < ncols) ? Z[(int64_t)col * QB + kk] : 0.0;
+  }
+  __syncthreads();
+  const int cc = tid & 15, rb = (tid >> 4) * 4;
+  const int col = colb + cc;
+  if (col >= ncols) return;
+  double *cp = C + (int64_t)(c0 + col) * ldc;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int rr = rb + i, row = r0 + rr;
+    if (row >= m) break;
+    double acc = 0.0;
+    for (int kk = 0; kk < nbe; ++kk) acc += ys[rr][kk] * zs[kk][cc];
+    cp[row] -= acc;
+  }
+}
+
+// dst(rows x cols, row-major ldd) = src viewed column-major (ld lds) [transposed read] or copy
+__global__ void cm_to_rm_kernel(const double *__restrict__ src, int lds, double *__restrict__ dst, int rows,
+                                int cols) {
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < (int64_t)rows * cols;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int i = (int)(e / cols), j = (int)(e - (int64_t)i * cols);
+    dst[e] = src[(int64_t)j * lds + i];
+  }
+}
+
+// A (m x n row-major) -> W (column-major, ld = m)
+__global__ void rm_to_cm_kernel(const double *__restrict__ A, int m, int n, double *__restrict__ W) {
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < (int64_t)m * n;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int j = (int)(e / m), i = (int)(e - (int64_t)j * m);
+    W[e] = A[(int64_t)i * n + j];
+  }
+}
+
+// M (column-major q x p, ld q) = [Vt^T ; 0] where Vt is p x p row-major (column j of M = row j of Vt)
+// or [I; 0] when Vt == nullptr
+__global__ void qpad_kernel(const double *__restrict__ Vt, int p, int q, int k, double *__restrict__ M) {
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < (int64_t)q * k;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int j = (int)(e / q), i = (int)(e - (int64_t)j * q);
+    M[e] = Vt ? (i < p ? Vt[(int64_t)j * p + i] : 0.0) : (i == j ? 1.0 : 0.0);
+  }
+}
+
+// X (p x p column-major) = R^T where R = upper triangle of W's first p rows; V = I
+__global__ void rt_build_kernel(const double *__restrict__ W, int ld, int p, double *__restrict__ X,
+                                double *__restrict__ V) {
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < (int64_t)p * p;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int j = (int)(e / p), k = (int)(e - (int64_t)j * p);  // X(k, j) = R(j, k)
+    X[e] = (k >= j) ? W[(int64_t)k * ld + j] : 0.0;
+    V[e] = (j == k) ? 1.0 : 0.0;
+  }
+}
+
+// R (k x n row-major) = upper triangle of W (col-major, ld m)
+__global__ void r_extract_kernel(const double *__restrict__ W, int ld, int k, int n, double *__restrict__ R) {
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < (int64_t)k * n;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int i = (int)(e / n), j = (int)(e - (int64_t)i * n);
+    R[e] = (j >= i) ? W[(int64_t)j * ld + i] : 0.0;
+  }
+}
+
+inline int grid_for(int64_t n) {
+  const int64_t g = (n + 255) / 256;
+  return (int)(g < 4096 ? (g > 0 ? g : 1) : 4096);
+}
+
+// factor W (m x n col-major, ld m) in place: R in the upper triangle, reflectors below, tau (k),
+// T factors (QB x QB each) per panel
+int qrb_factor(hipStream_t st, double *W, int m, int n, double *tau, double *Tall, double *Z) {
+  const int k = m < n ? m : n;
+  for (int j0 = 0; j0 < k; j0 += QB) {
+    const int nbe = (k - j0) < QB ? (k - j0) : QB;
+    double *T = Tall + (int64_t)(j0 / QB) * QB * QB;
+    hipLaunchKernelGGL(qrb_panel_kernel, dim3(1), dim3(1024), 0, st, W, m, m, j0, nbe, tau, T);
+    TTK_LAUNCH_CHECK();
+    const int c0 = j0 + nbe, nc = n - c0;
+    if (nc > 0) {
+      hipLaunchKernelGGL(qrb_ytc_kernel, dim3((nc + 15) / 16), dim3(256), 0, st, W, m, m, j0, nbe, W, m, c0, nc, T, 1,
+                         Z);
+      hipLaunchKernelGGL(qrb_update_kernel, dim3((m - j0 + 63) / 64, (nc + 15) / 16), dim3(256), 0, st, W, m, m, j0,
+                         nbe, W, m, c0, nc, Z);
+      TTK_LAUNCH_CHECK();
+    }
+  }
+  return TTK_OK;
+}
+
+// M (m x nc col-major, ld m) <- Q M with Q = H_0 ... H_{k-1} from qrb_factor
+int qrb_apply_q(hipStream_t st, const double *W, int m, int k, const double *Tall, double *M, int nc, double *Z) {
+  const int npan = (k + QB - 1) / QB;
+  for (int pi = npan - 1; pi >= 0; --pi) {
+    const int j0 = pi * QB, nbe = (k - j0) < QB ? (k - j0) : QB;
+    const double *T = Tall + (int64_t)pi * QB * QB;
+    hipLaunchKernelGGL(qrb_ytc_kernel, dim3((nc + 15) / 16), dim3(256), 0, st, W, m, m, j0, nbe, M, m, 0, nc, T, 0, Z);
+    hipLaunchKernelGGL(qrb_update_kernel, dim3((m - j0 + 63) / 64, (nc + 15) / 16), dim3(256), 0, st, W, m, m, j0, nbe,
+                       M, m, 0, nc, Z);
+    TTK_LAUNCH_CHECK();
+  }
+  return TTK_OK;
 }
 
 int *g_status = nullptr;
@@ -710,9 +1246,108 @@ int ensure_status() {
 
 extern "C" {
 
+static int g_svd_big_p = 64;  // smallest p that takes the multi-workgroup path (when W does not fit LDS)
+
+static int64_t svd_big_work(int m, int n) {
+  const int64_t p = m < n ? m : n, q = m < n ? n : m, npan = (p + QB - 1) / QB;
+  return 2 * q * p + 4 * p * p + p + npan * QB * QB + QB * p + 2 * p + 64;
+}
+
+// Large SVD: W = Q R (blocked Householder), one-sided Jacobi on X = R^T (p x p; QR preconditioning
+// cuts the sweep count ~4x on graded spectra), then U_W = Q V_X.  W = A (tall) or A^T (wide).
+static int svd_big(void *stream, const double *A, int m, int n, double *U, double *S, double *Vt, double *work) {
+  int rc = ensure_status();
+  if (rc != TTK_OK) return rc;
+  const bool tall = m >= n;
+  const int p = tall ? n : m, q = tall ? m : n, P = (p % 2) ? p + 1 : p;
+  const int npan = (p + QB - 1) / QB;
+  double *W = work;                                  // q x p col-major
+  double *M = W + (int64_t)q * p;                    // q x p col-major
+  double *X = M + (int64_t)q * p;                    // p x p col-major
+  double *V = X + (int64_t)p * p;                    // p x p col-major
+  double *Ux = V + (int64_t)p * p;                   // p x p row-major
+  double *VtX = Ux + (int64_t)p * p;                 // p x p row-major
+  double *tau = VtX + (int64_t)p * p;                // p
+  double *Tall = tau + p;                            // npan * QB * QB
+  double *Z = Tall + (int64_t)npan * QB * QB;        // QB * p
+  double *sig = Z + (int64_t)QB * p;                 // p
+  int *rank = reinterpret_cast<int *>(sig + p);      // p ints
+  int *flag = g_status + 8;
+  hipStream_t st = TTK_STREAM(stream);
+  if (tall)
+    hipLaunchKernelGGL(rm_to_cm_kernel, dim3(grid_for((int64_t)q * p)), dim3(256), 0, st, A, m, n, W);
+  else  // W = A^T: column j of W = row j of A -> a plain copy
+    TTK_HIP(hipMemcpyAsync(W, A, sizeof(double) * (size_t)q * p, hipMemcpyDeviceToDevice, st));
+  TTK_LAUNCH_CHECK();
+  rc = qrb_factor(st, W, q, p, tau, Tall, Z);
+  if (rc != TTK_OK) return rc;
+  hipLaunchKernelGGL(rt_build_kernel, dim3(grid_for((int64_t)p * p)), dim3(256), 0, st, W, q, p, X, V);
+  TTK_LAUNCH_CHECK();
+  const double tol = EPS * (p > 16 ? (double)p : 16.0);
+  const int grid = (P / 2 * 64 + 255) / 256;
+  for (int sweep = 0; sweep < 60; ++sweep) {
+    TTK_HIP(hipMemsetAsync(flag, 0, sizeof(int), st));
+    for (int r = 0; r < P - 1; ++r)
+      hipLaunchKernelGGL(svd_big_round_kernel, dim3(grid), dim3(256), 0, st, X, V, p, p, r, tol, flag);
+    TTK_LAUNCH_CHECK();
+    int h = 0;
+    TTK_HIP(hipMemcpyAsync(&h, flag, sizeof(int), hipMemcpyDeviceToHost, st));
+    TTK_HIP(hipStreamSynchronize(st));
+    if (!h) break;
+  }
+  // X = U_X S V_X^T (epilogue sorts): Ux (p x p row-major), VtX = V_X^T (row-major)
+  hipLaunchKernelGGL(svd_big_finish_kernel, dim3(1), dim3(1024), 0, st, X, V, sig, rank, p, p, Ux, S, VtX);
+  TTK_LAUNCH_CHECK();
+  // M = Q [V_X; 0]
+  hipLaunchKernelGGL(qpad_kernel, dim3(grid_for((int64_t)q * p)), dim3(256), 0, st, VtX, p, q, p, M);
+  TTK_LAUNCH_CHECK();
+  rc = qrb_apply_q(st, W, q, p, Tall, M, p, Z);
+  if (rc != TTK_OK) return rc;
+  if (tall) {  // A = W = (Q V_X) S U_X^T
+    hipLaunchKernelGGL(cm_to_rm_kernel, dim3(grid_for((int64_t)q * p)), dim3(256), 0, st, M, q, U, q, p);
+    hipLaunchKernelGGL(cm_to_rm_kernel, dim3(grid_for((int64_t)p * p)), dim3(256), 0, st, Ux, p, Vt, p, p);
+  } else {  // A = W^T = U_X S (Q V_X)^T
+    TTK_HIP(hipMemcpyAsync(U, Ux, sizeof(double) * (size_t)p * p, hipMemcpyDeviceToDevice, st));
+    TTK_HIP(hipMemcpyAsync(Vt, M, sizeof(double) * (size_t)q * p, hipMemcpyDeviceToDevice, st));
+  }
+  TTK_LAUNCH_CHECK();
+  return TTK_OK;
+}
+
+static int64_t qr_big_work(int m, int n) {
+  const int64_t k = m < n ? m : n, npan = (k + QB - 1) / QB, mx = m > n ? m : n;
+  return (int64_t)m * n + (int64_t)m * k + k + npan * QB * QB + QB * mx + 64;
+}
+
+static int qr_big(void *stream, const double *A, int m, int n, double *Q, double *R, double *work) {
+  const int k = m < n ? m : n, npan = (k + QB - 1) / QB;
+  double *W = work, *M = W + (int64_t)m * n, *tau = M + (int64_t)m * k, *Tall = tau + k;
+  double *Z = Tall + (int64_t)npan * QB * QB;
+  hipStream_t st = TTK_STREAM(stream);
+  hipLaunchKernelGGL(rm_to_cm_kernel, dim3(grid_for((int64_t)m * n)), dim3(256), 0, st, A, m, n, W);
+  TTK_LAUNCH_CHECK();
+  int rc = qrb_factor(st, W, m, n, tau, Tall, Z);
+  if (rc != TTK_OK) return rc;
+  hipLaunchKernelGGL(qpad_kernel, dim3(grid_for((int64_t)m * k)), dim3(256), 0, st, nullptr, k, m, k, M);
+  TTK_LAUNCH_CHECK();
+  rc = qrb_apply_q(st, W, m, k, Tall, M, k, Z);
+  if (rc != TTK_OK) return rc;
+  hipLaunchKernelGGL(cm_to_rm_kernel, dim3(grid_for((int64_t)m * k)), dim3(256), 0, st, M, m, Q, m, k);
+  hipLaunchKernelGGL(r_extract_kernel, dim3(grid_for((int64_t)k * n)), dim3(256), 0, st, W, m, k, n, R);
+  TTK_LAUNCH_CHECK();
+  return TTK_OK;
+}
+
+int ttk_svd_set_big_threshold(int p) {
+  const int old = g_svd_big_p;
+  if (p > 0) g_svd_big_p = p;
+  return old;
+}
+
 int64_t ttk_svd_work(int m, int n) {
   const int64_t p = m < n ? m : n, q = m < n ? n : m;
-  return q * p + p * p + 2 * p + 16;
+  const int64_t small = q * p + p * p + 2 * p + 16, big = svd_big_work(m, n);
+  return small > big ? small : big;
 }
 
 int ttk_svd(void *stream, const double *A, int m, int n, double *U, double *S, double *Vt, double *work) {
@@ -720,18 +1355,34 @@ int ttk_svd(void *stream, const double *A, int m, int n, double *U, double *S, d
     ttk::set_error("ttk_svd: empty matrix %dx%d", m, n);
     return TTK_ERR_ARG;
   }
-  const int64_t need = ttk_svd_work(m, n);
+  const int p = m < n ? m : n, q = m < n ? n : m, pairs = (p + 1) / 2;
+  const int64_t need = (int64_t)q * p + (int64_t)p * p + 2 * p + 16;
   const int use_lds = need <= LDS_DOUBLES;
+  if (p >= g_svd_big_p && (!use_lds || g_svd_big_p <= 2)) return svd_big(stream, A, m, n, U, S, Vt, work);
   const size_t shm = use_lds ? need * sizeof(double) : 0;
   allow_big_lds(svd_kernel, shm);
-  hipLaunchKernelGGL(svd_kernel, dim3(1), dim3(1024), shm, TTK_STREAM(stream), A, m, n, U, S, Vt, work, use_lds);
+  int g = 1;
+  while (g < 64 && g * 4 < q) g *= 2;           // ~4 elements per lane
+  while (g > 1 && pairs * g > 1024) g /= 2;     // all pairs of a round in flight
+  int nt = pairs * g;
+  nt = nt < 64 ? 64 : (nt > 1024 ? 1024 : (nt + 63) / 64 * 64);
+  hipLaunchKernelGGL(svd_kernel, dim3(1), dim3(nt), shm, TTK_STREAM(stream), A, m, n, U, S, Vt, work, use_lds, g);
   TTK_LAUNCH_CHECK();
   return TTK_OK;
 }
 
+static int g_qr_big_k = 48;  // smallest min(m,n) that takes the blocked path (when it does not fit LDS)
+
+int ttk_qr_set_big_threshold(int k) {
+  const int old = g_qr_big_k;
+  if (k > 0) g_qr_big_k = k;
+  return old;
+}
+
 int64_t ttk_qr_work(int m, int n) {
   const int64_t k = m < n ? m : n;
-  return (int64_t)m * n + k + (int64_t)m * k + 16;
+  const int64_t small = (int64_t)m * n + k + (int64_t)m * k + 16, big = qr_big_work(m, n);
+  return small > big ? small : big;
 }
 
 int ttk_qr(void *stream, const double *A, int m, int n, double *Q, double *R, double *work) {
@@ -739,8 +1390,10 @@ int ttk_qr(void *stream, const double *A, int m, int n, double *Q, double *R, do
     ttk::set_error("ttk_qr: empty matrix %dx%d", m, n);
     return TTK_ERR_ARG;
   }
-  const int64_t need = ttk_qr_work(m, n);
+  const int64_t k = m < n ? m : n;
+  const int64_t need = (int64_t)m * n + k + (int64_t)m * k + 16;
   const int use_lds = need <= LDS_DOUBLES;
+  if (k >= g_qr_big_k && (!use_lds || g_qr_big_k <= 2)) return qr_big(stream, A, m, n, Q, R, work);
   const size_t shm = use_lds ? need * sizeof(double) : 0;
   allow_big_lds(qr_kernel, shm);
   hipLaunchKernelGGL(qr_kernel, dim3(1), dim3(1024), shm, TTK_STREAM(stream), A, m, n, Q, R, work, use_lds);
@@ -809,6 +1462,34 @@ int ttk_syev(void *stream, double *A, int n, double *ev, double *W, double *work
   const size_t shm = use_lds ? need * sizeof(double) : 0;
   allow_big_lds(syev_kernel, shm);
   hipLaunchKernelGGL(syev_kernel, dim3(1), dim3(1024), shm, TTK_STREAM(stream), A, n, ev, W, work, use_lds);
+  TTK_LAUNCH_CHECK();
+  return TTK_OK;
+}
+
+int ttk_debug_counters(unsigned long long *out, int reset) {
+  TTK_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dbg), sizeof(g_dbg)));
+  if (reset) {
+    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    TTK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_dbg), z, sizeof(z)));
+  }
+  return TTK_OK;
+}
+
+int64_t ttk_syev_extreme_work(int n) { return n > 0 ? syev_extreme_need(n) : 0; }
+
+int ttk_syev_extreme(void *stream, const double *A, int n, int which, double *ev, double *vec, double *work) {
+  if (n <= 0 || (which != 0 && which != 1)) {
+    ttk::set_error("ttk_syev_extreme: bad arguments");
+    return TTK_ERR_ARG;
+  }
+  const int64_t need = syev_extreme_need(n);
+  const int use_lds = need <= LDS_DOUBLES;
+  const size_t shm = use_lds ? need * sizeof(double) : 0;
+  allow_big_lds(syev_extreme_kernel, shm);
+  int nt = 4 * n;
+  nt = nt < 64 ? 64 : (nt > 1024 ? 1024 : (nt + 63) / 64 * 64);
+  hipLaunchKernelGGL(syev_extreme_kernel, dim3(1), dim3(nt), shm, TTK_STREAM(stream), A, n, which, ev, vec, work,
+                     use_lds);
   TTK_LAUNCH_CHECK();
   return TTK_OK;
 }

@@ -446,6 +446,22 @@ def syev(A):
     return ev, W, evh
 
 
-__all__ = ["einsum", "tensordot", "matmul", "copy_", "scaled", "clone", "mul_", "recip", "fill_", "add_diag_",
+def syev_extreme(A, largest=False):
+    """One extreme eigenpair of a symmetric device matrix (Householder tridiagonalisation +
+    multisection + inverse iteration, one launch).  Returns (eigenvalue float, unit vector)."""
+    t0 = _tic() if OPSTATS is not None else 0
+    A = A.contiguous()
+    n = A.shape[0]
+    buf = empty(n + 1)
+    work = empty(int(lib.ttk_syev_extreme_work(n)))
+    check(lib.ttk_syev_extreme(_stream(), _p(A), n, 1 if largest else 0, _p(buf), _p(buf[1:]), _p(work)),
+          "syev_extreme")
+    lam = float(read(buf[:1])[0])
+    if OPSTATS is not None:
+        _stat("syev_extreme", n, t0)
+    return lam, buf[1:]
+
+
+__all__ = ["syev_extreme", "einsum", "tensordot", "matmul", "copy_", "scaled", "clone", "mul_", "recip", "fill_", "add_diag_",
            "dot", "norm", "read", "svd", "qr", "rq", "cholesky_", "trsm_", "lu_", "lu_solve_", "syev", "empty",
            "zeros", "from_numpy", "to_numpy", "LinAlgError", "LinAlgWarning"]

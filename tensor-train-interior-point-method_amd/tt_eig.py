@@ -3,7 +3,7 @@
 
 Environments and two-site local matrices are device contractions (MFMA GEMM steps).  The local
 eigenproblems, which the reference sends to ARPACK `eigsh` (with an `splu` shift-invert polish)
-or `lobpcg`, are solved exactly with the device cyclic-Jacobi eigensolver (`ttk_syev`); the
+or `lobpcg`, are solved exactly with the device extreme-eigenpair solver (`ttk_syev_extreme`); the
 generalised problem `-D v = lambda A v` goes through a device Cholesky of A.  The converged
 eigenpair is the same to the reference's tolerance (tol = 1e-8); ARPACK's failure branches
 (exceptions) map to the same fallbacks."""
@@ -29,8 +29,7 @@ def _sym(Mt, m):
 
 
 def _min_eigpair(M):
-    ev, W, evh = D.syev(M)
-    return float(evh[0]), D.clone(W[:, 0])
+    return D.syev_extreme(M, largest=False)
 
 
 def _gen_max_eig(Dm, Am):
@@ -44,10 +43,10 @@ def _gen_max_eig(Dm, Am):
     D.trsm_(L, Ct)  # L^-1 (L^-1 (-D))^T = L^-1 (-D) L^-T
     S = D.clone(Ct)
     D.copy_(S, Ct.t(), 0.5, 0.5)
-    ev, W, evh = D.syev(S)
-    y = D.clone(W[:, m - 1:m])
+    lam, w = D.syev_extreme(S, largest=True)
+    y = w.view(m, 1)
     D.trsm_(L, y, trans=True)
-    return float(evh[-1]), y.view(-1)
+    return lam, y.view(-1)
 
 
 def _rayleigh(Am, Dm, step, v):

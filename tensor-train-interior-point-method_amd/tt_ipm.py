@@ -12,6 +12,8 @@ import traceback
 from dataclasses import dataclass
 from enum import Enum
 
+import time
+
 import numpy as np
 
 from . import dev as D
@@ -781,7 +783,8 @@ def tt_ipm(lag_maps, obj_tt, lin_op_tt, bias_tt, ineq_mask=None, max_iter=100, m
             trace.append({"iter": it, "mu": float(st.mu), "primal_error": float(st.primal_error),
                           "dual_error": float(st.dual_error), "centrality_error": float(st.centrality_error),
                           "sigma": float(st.sigma), "ranksX": T.tt_ranks(X), "ranksZ": T.tt_ranks(Z),
-                          "ranksY": T.tt_ranks(Y), "is_last_iter": bool(st.is_last_iter)})
+                          "ranksY": T.tt_ranks(Y), "is_last_iter": bool(st.is_last_iter),
+                          "t": time.time()})
         if verbose:
             _ipm_log_iteration(it, st, X, Y, Z, Tt)
         st, fin = _ipm_check_convergence(st, fin, ZX, TX, abs_tol, max_refinement)

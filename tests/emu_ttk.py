@@ -201,6 +201,26 @@ class EmuLib:
         _dv(W, n * n)[:] = v.ravel()
         return 0
 
+    def ttk_qr_set_big_threshold(self, k):
+        return 48
+
+    def ttk_svd_set_big_threshold(self, p):
+        return 64
+
+    def ttk_debug_counters(self, out, reset):
+        return 0
+
+    def ttk_syev_extreme_work(self, n):
+        return 16
+
+    def ttk_syev_extreme(self, s, A, n, which, ev, vec, work):
+        a = _dv(A, n * n).reshape(n, n)
+        w, v = np.linalg.eigh(0.5 * (a + a.T))
+        j = n - 1 if which else 0
+        _dv(ev, 1)[0] = w[j]
+        _dv(vec, n)[:] = v[:, j]
+        return 0
+
     # --- LGMRES (same semantics as csrc/ttk_lgmres.hip)
     @staticmethod
     def _hh(base, max_k):

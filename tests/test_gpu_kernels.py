@@ -85,6 +85,70 @@ def test_svd(dev, m, n):
     assert np.allclose(Vt @ Vt.T, np.eye(k), atol=1e-12)
 
 
+def _check_svd(dev, A, rtol=1e-12):
+    m, n = A.shape
+    U, S, Vt, s = dev.svd(dev.from_numpy(A))
+    U, Vt = dev.read(U), dev.read(Vt)
+    ref = np.linalg.svd(A, compute_uv=False)
+    assert np.allclose(s, ref, rtol=rtol, atol=1e-14 * ref[0])
+    assert np.all(np.diff(s) <= 0)
+    assert np.allclose((U * s) @ Vt, A, atol=1e-13 * np.abs(A).max() * max(1, np.sqrt(min(m, n)) / 4))
+    k = min(m, n)
+    assert np.allclose(U.T @ U, np.eye(k), atol=1e-12)
+    assert np.allclose(Vt @ Vt.T, np.eye(k), atol=1e-12)
+
+
+@pytest.mark.parametrize("m,n", [(5, 4), (39, 52), (52, 39), (3, 1), (1, 3)])
+def test_svd_multi_workgroup_forced(dev, m, n):
+    from ttipm_amd._lib import lib
+    rng = _rng(m + 3 * n)
+    A = rng.standard_normal((m, n))
+    old = lib.ttk_svd_set_big_threshold(1)
+    try:
+        _check_svd(dev, A)
+    finally:
+        lib.ttk_svd_set_big_threshold(old)
+
+
+@pytest.mark.parametrize("m,n", [(70, 40), (40, 70), (33, 33), (130, 64), (5, 3), (3, 5)])
+def test_qr_blocked_forced(dev, m, n):
+    from ttipm_amd._lib import lib
+    rng = _rng(m * 7 + n)
+    A = rng.standard_normal((m, n))
+    old = lib.ttk_qr_set_big_threshold(1)
+    try:
+        Q, R = dev.qr(dev.from_numpy(A))
+    finally:
+        lib.ttk_qr_set_big_threshold(old)
+    Q, R = dev.read(Q), dev.read(R)
+    Qr, Rr = np.linalg.qr(A)
+    k = min(m, n)
+    assert np.allclose(Q @ R, A, atol=1e-13 * np.abs(A).max() * np.sqrt(k))
+    assert np.allclose(Q.T @ Q, np.eye(k), atol=1e-13)
+    assert np.allclose(np.tril(R, -1), 0)
+    # LAPACK sign convention (beta = -sign(alpha)||x||) -> same factors as numpy/LAPACK
+    assert np.allclose(R, Rr, atol=1e-11 * np.abs(A).max())
+
+
+@pytest.mark.parametrize("m,n", [(1400, 256), (256, 900), (700, 500)])
+def test_qr_large(dev, m, n):
+    rng = _rng(m + n)
+    A = rng.standard_normal((m, n))
+    Q, R = dev.qr(dev.from_numpy(A))
+    Q, R = dev.read(Q), dev.read(R)
+    k = min(m, n)
+    assert np.allclose(Q @ R, A, atol=1e-12 * np.abs(A).max() * np.sqrt(k))
+    assert np.allclose(Q.T @ Q, np.eye(k), atol=1e-12)
+
+
+@pytest.mark.parametrize("m,n,r", [(300, 420, 300), (520, 260, 60), (868, 1024, 217), (1400, 256, 256)])
+def test_svd_large_rank_deficient(dev, m, n, r):
+    """Sizes and rank structure of the 1e-12 roundings at the end of a solve."""
+    rng = _rng(m + n)
+    A = rng.standard_normal((m, r)) @ (rng.standard_normal((r, n)) * np.logspace(0, -13, r)[:, None])
+    _check_svd(dev, A)
+
+
 def test_svd_zero_and_rank_one(dev):
     U, S, Vt, s = dev.svd(dev.zeros(6, 4))
     assert np.all(s == 0)
@@ -163,6 +227,35 @@ def test_syev(dev, n):
     W = dev.read(W)
     assert np.allclose(evh, np.linalg.eigvalsh(A), atol=1e-12 * max(1, np.abs(evh).max()))
     assert np.allclose(A @ W, W * evh, atol=1e-11 * max(1, np.abs(evh).max()))
+
+
+def _sym_cases(n, rng):
+    M = rng.standard_normal((n, n))
+    yield "gauss", M + M.T
+    Q, _ = np.linalg.qr(rng.standard_normal((n, n)))
+    d = np.sort(rng.standard_normal(n))
+    if n > 2:
+        d[:2] = d[0]  # degenerate extreme eigenvalue
+        d[-2:] = d[-1]
+    yield "degenerate", (Q * d) @ Q.T
+    B = rng.standard_normal((n, max(1, n // 3)))
+    yield "psd_rank_deficient", B @ B.T
+    yield "scaled", 1e-6 * (M + M.T) + np.diag(np.arange(n, dtype=float))
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 10, 100, 139, 140, 288])
+@pytest.mark.parametrize("largest", [False, True])
+def test_syev_extreme(dev, n, largest):
+    rng = _rng(7 * n + largest)
+    for name, A in _sym_cases(n, rng):
+        lam, v = dev.syev_extreme(dev.from_numpy(A), largest=largest)
+        v = dev.read(v)
+        w = np.linalg.eigvalsh(A)
+        ref = w[-1] if largest else w[0]
+        scale = max(1.0, np.abs(w).max())
+        assert abs(lam - ref) <= 1e-12 * scale, (name, lam, ref)
+        assert abs(np.linalg.norm(v) - 1.0) < 1e-12, name
+        assert np.linalg.norm(A @ v - lam * v) <= 1e-10 * scale, name
 
 
 def test_elementwise_and_reductions(dev):
