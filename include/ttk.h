@@ -59,6 +59,12 @@ int ttk_gemm_offs(void *stream, const double *A, const double *B, double *C, con
 int ttk_gemm_offs_grouped(void *stream, const double *const *Aptr, const double *const *Bptr,
                           double *const *Cptr, const int64_t *offs, int ngroups, int nb, int M,
                           int N, int K, double alpha, double beta);
+/* contraction-kernel accounting for the roofline report: on != 0 brackets every ttk_gemm_offs*
+ * launch with two HIP events on its stream (returns the previous setting) */
+int ttk_contract_timing(int on);
+/* out[5] = {algorithmic FLOPs (2*M*N*K*batch per GEMM step), launches, timed FLOPs,
+ * timed launches, summed kernel ms of the timed launches}; synchronises pending events */
+int ttk_contract_stats(double *out, int reset);
 
 /* ---------------------------------------------------------------------------------------
  * Strided element-wise kernels (up to 6-D).  `shape`, `sstride`, `dstride` are host arrays.

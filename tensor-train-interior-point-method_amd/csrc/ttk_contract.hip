@@ -11,6 +11,10 @@
 // Tile: 32x32 outputs per 256-thread workgroup = 2x2 waves, each wave one 16x16 MFMA tile.
 // K is staged through LDS 16 at a time (4 MFMAs per wave per stage).  f64 MFMA lane maps
 // (MI355X guide §3): A[i=l&15][k=l>>4], B[k=l>>4][j=l&15], D: col=l&15, row=(l>>4)+4*r.
+#include <hip/hip_ext.h>
+
+#include <vector>
+
 #include "ttk_common.h"
 
 namespace {
@@ -203,6 +207,62 @@ inline int grid_for(int64_t n, int block) {
 
 double *g_dev_scalar = nullptr;
 
+// Contraction-kernel accounting (bench.py roofline): algorithmic FLOPs (2*M*N*K per GEMM step,
+// the opt_einsum convention of SURVEY.md 8(d)) are always counted; with timing on, every
+// contraction launch is bracketed by two HIP events on its own stream and the durations are
+// summed at harvest (auto-harvest every EV_CHUNK events keeps the pool bounded).  The events are
+// handed to hipExtLaunchKernelGGL, so they time the dispatch itself (no marker packets between).
+struct ContractStats {
+  double flops = 0.0, timed_flops = 0.0, timed_ms = 0.0;
+  long long launches = 0, timed_launches = 0;
+  bool timing = false;
+  std::vector<hipEvent_t> ev;
+  size_t used = 0;
+};
+ContractStats g_cs;
+constexpr size_t EV_CHUNK = 8192;
+
+int harvest_events() {
+  if (g_cs.used == 0) return TTK_OK;
+  TTK_HIP(hipEventSynchronize(g_cs.ev[g_cs.used - 1]));
+  for (size_t i = 0; i + 1 < g_cs.used; i += 2) {
+    float ms = 0.0f;
+    TTK_HIP(hipEventElapsedTime(&ms, g_cs.ev[i], g_cs.ev[i + 1]));
+    g_cs.timed_ms += ms;
+  }
+  g_cs.used = 0;
+  return TTK_OK;
+}
+
+// start/stop events for the next contraction launch (nullptr when timing is off); they are
+// passed to hipExtLaunchKernelGGL, which records them with the dispatch itself
+int contract_events(hipEvent_t *ev0, hipEvent_t *ev1) {
+  *ev0 = *ev1 = nullptr;
+  if (!g_cs.timing) return TTK_OK;
+  if (g_cs.used + 2 > EV_CHUNK) {
+    int rc = harvest_events();
+    if (rc != TTK_OK) return rc;
+  }
+  while (g_cs.ev.size() < g_cs.used + 2) {
+    hipEvent_t e;
+    TTK_HIP(hipEventCreate(&e));
+    g_cs.ev.push_back(e);
+  }
+  *ev0 = g_cs.ev[g_cs.used];
+  *ev1 = g_cs.ev[g_cs.used + 1];
+  g_cs.used += 2;
+  return TTK_OK;
+}
+
+void contract_count(double flops) {
+  g_cs.flops += flops;
+  g_cs.launches += 1;
+  if (g_cs.timing) {
+    g_cs.timed_flops += flops;
+    g_cs.timed_launches += 1;
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -216,8 +276,12 @@ int ttk_gemm_offs(void *stream, const double *A, const double *B, double *C, con
   }
   GemmArgs g{A, B, C, offs, nb, M, N, K, alpha, beta};
   dim3 grid((N + TN - 1) / TN, (M + TM - 1) / TM, nb);
-  hipLaunchKernelGGL(gemm_offs_kernel, grid, dim3(256), 0, TTK_STREAM(stream), g);
+  hipEvent_t e0, e1;
+  int rc = contract_events(&e0, &e1);
+  if (rc != TTK_OK) return rc;
+  hipExtLaunchKernelGGL(gemm_offs_kernel, grid, dim3(256), 0, TTK_STREAM(stream), e0, e1, 0, g);
   TTK_LAUNCH_CHECK();
+  contract_count(2.0 * M * N * (double)K * nb);
   return TTK_OK;
 }
 
@@ -232,8 +296,12 @@ int ttk_gemm_offs_grouped(void *stream, const double *const *Aptr, const double 
   GemmArgs g{nullptr, nullptr, nullptr, offs, nb, M, N, K, alpha, beta};
   GroupPtrs p{Aptr, Bptr, Cptr};
   dim3 grid((N + TN - 1) / TN, (M + TM - 1) / TM, nb * ngroups);
-  hipLaunchKernelGGL(gemm_offs_grouped_kernel, grid, dim3(256), 0, TTK_STREAM(stream), g, p);
+  hipEvent_t e0, e1;
+  int rc = contract_events(&e0, &e1);
+  if (rc != TTK_OK) return rc;
+  hipExtLaunchKernelGGL(gemm_offs_grouped_kernel, grid, dim3(256), 0, TTK_STREAM(stream), e0, e1, 0, g, p);
   TTK_LAUNCH_CHECK();
+  contract_count(2.0 * M * N * (double)K * nb * ngroups);
   return TTK_OK;
 }
 
@@ -302,6 +370,31 @@ int ttk_sumsq_batched(void *stream, const double *x, int64_t n, int nb, int64_t 
   if (nb <= 0) return TTK_OK;
   hipLaunchKernelGGL(sumsq_batched_kernel, dim3(nb), dim3(256), 0, TTK_STREAM(stream), x, n, bstride, out);
   TTK_LAUNCH_CHECK();
+  return TTK_OK;
+}
+
+int ttk_contract_timing(int on) {
+  const int old = g_cs.timing;
+  if (!on && g_cs.timing) {
+    int rc = harvest_events();
+    if (rc != TTK_OK) return rc;
+  }
+  g_cs.timing = on != 0;
+  return old;
+}
+
+int ttk_contract_stats(double *out, int reset) {
+  int rc = harvest_events();
+  if (rc != TTK_OK) return rc;
+  out[0] = g_cs.flops;
+  out[1] = (double)g_cs.launches;
+  out[2] = g_cs.timed_flops;
+  out[3] = (double)g_cs.timed_launches;
+  out[4] = g_cs.timed_ms;
+  if (reset) {
+    g_cs.flops = g_cs.timed_flops = g_cs.timed_ms = 0.0;
+    g_cs.launches = g_cs.timed_launches = 0;
+  }
   return TTK_OK;
 }
 

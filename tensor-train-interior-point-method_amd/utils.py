@@ -25,14 +25,15 @@ def _sync():
         torch.cuda.synchronize()
 
 
-def run_and_record(problem, config, seed, rank, trace=None, verbose=None, iter_callback=None):
-    """`run_and_record` (`src/utils.py:245-321`) for one seed; returns a dict of the recorded values."""
-    create = PROBLEMS[problem]
+def create(problem, config, seed, rank, verbose=None):
+    """Problem creation half of `run_and_record` (`src/utils.py:258-270`): seeds the global NumPy
+    RNG, builds the problem on the device and returns it with the RNG state the IPM continues
+    from (the IPM's own random draws follow creation in the same stream)."""
     verbose = config.get("verbose", False) if verbose is None else verbose
     np.random.seed(seed)
     _sync()
     t1 = time.time()
-    prob = create(config["dim"], rank, verbose=verbose)
+    prob = PROBLEMS[problem](config["dim"], rank, verbose=verbose)
     if len(prob) == 5:
         C, L, b, mask, lag = prob
     else:
@@ -42,6 +43,17 @@ def run_and_record(problem, config, seed, rank, trace=None, verbose=None, iter_c
     lag = {k: T.tt_reshape(v, (4, 4)) for k, v in lag.items()}
     C = T.tt_reshape(C, (4,))
     b = T.tt_reshape(b, (4,))
+    _sync()
+    return {"seed": seed, "C": C, "L": L, "b": b, "mask": mask, "lag": lag,
+            "rng_state": np.random.get_state(), "creation_time": time.time() - t1}
+
+
+def solve(prepared, config, trace=None, verbose=None, iter_callback=None, quiet=False):
+    """Timed half of `run_and_record` (`src/utils.py:272-321`): `tt_ipm` between t2 and t3, then
+    the recorded gap / primal / dual feasibility."""
+    verbose = config.get("verbose", False) if verbose is None else verbose
+    C, L, b, mask, lag = prepared["C"], prepared["L"], prepared["b"], prepared["mask"], prepared["lag"]
+    np.random.set_state(prepared["rng_state"])
     _sync()
     t2 = time.time()
     X, Y, Tt, Z, info = tt_ipm(lag, C, L, b, ineq_mask=mask, max_iter=config["max_iter"], verbose=verbose,
@@ -62,14 +74,21 @@ def run_and_record(problem, config, seed, rank, trace=None, verbose=None, iter_c
         dr = T.tt_rank_reduce(T.tt_sub(dr, T.tt_reshape(Tt, (4,))), eps=1e-12)
     dfeas = T.tt_inner_prod(dr, dr)
     n_it = int(info["num_iters"])
-    out = {"seed": seed, "creation_time": t2 - t1, "runtime": t3 - t2, "num_iters": n_it,
-           "sec_per_iter": (t3 - t2) / max(n_it, 1), "gap": float(gap), "feas": float(feas),
+    out = {"seed": prepared["seed"], "creation_time": prepared["creation_time"], "runtime": t3 - t2,
+           "num_iters": n_it, "sec_per_iter": (t3 - t2) / max(n_it, 1), "gap": float(gap), "feas": float(feas),
            "dual_feas": float(dfeas), "ranksX": info["ranksX"], "ranksY": info["ranksY"], "ranksZ": info["ranksZ"],
            "ranksT": info["ranksT"]}
-    print(f"Convergence after {n_it} iterations. Compl Slackness: {gap:.4e}. Feasibility error: {feas:.4e}. "
-          f"Dual Feasibility error: {dfeas:.4e}.")
-    print(f"Convergence in {t3 - t2:.2f}s ({out['sec_per_iter']:.3f} s/iter).", flush=True)
+    if not quiet:
+        print(f"Convergence after {n_it} iterations. Compl Slackness: {gap:.4e}. Feasibility error: {feas:.4e}. "
+              f"Dual Feasibility error: {dfeas:.4e}.")
+        print(f"Convergence in {t3 - t2:.2f}s ({out['sec_per_iter']:.3f} s/iter).", flush=True)
     return out
+
+
+def run_and_record(problem, config, seed, rank, trace=None, verbose=None, iter_callback=None):
+    """`run_and_record` (`src/utils.py:245-321`) for one seed; returns a dict of the recorded values."""
+    return solve(create(problem, config, seed, rank, verbose=verbose), config, trace=trace, verbose=verbose,
+                 iter_callback=iter_callback)
 
 
 def print_results_summary(config, results):

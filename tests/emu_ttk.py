@@ -201,6 +201,13 @@ class EmuLib:
         _dv(W, n * n)[:] = v.ravel()
         return 0
 
+    def ttk_contract_timing(self, on):
+        return 0
+
+    def ttk_contract_stats(self, out, reset):
+        _dv(out, 5)[:] = 0.0
+        return 0
+
     def ttk_qr_set_big_threshold(self, k):
         return 48
 
