@@ -21,6 +21,7 @@
   seed -- a bounded sample of the same workload.
 """
 import argparse
+import contextlib
 import ctypes
 import json
 import os
@@ -135,14 +136,16 @@ def main():
     from ttipm_amd.utils import solve as _solve
 
     def solve(prep, cfg, quiet=True):
-        return _solve(prep, cfg, quiet=quiet, verbose=False)
+        with contextlib.redirect_stdout(sys.stderr):  # stdout carries only the JSON line
+            return _solve(prep, cfg, quiet=quiet, verbose=False)
 
     with open(args.config) as f:
         config = yaml.safe_load(f)
     seeds = _seed_list(config, args.steps * world)
     step_seeds = [seeds[(i * world + p) % len(seeds)] for i in range(args.steps) for p in range(world)]
     sched = [step_seeds[i * world:(i + 1) * world] for i in range(args.steps)]
-    packed = shard.broadcast_problems(args.problem, config, step_seeds, args.rank)
+    with contextlib.redirect_stdout(sys.stderr):
+        packed = shard.broadcast_problems(args.problem, config, step_seeds, args.rank)
     mine = [packed[i * world + rank] for i in range(args.steps)]
 
     def sync():
@@ -191,7 +194,8 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args.problem, config, step_seeds[0], args.rank, args.cpu_iters)
+        with contextlib.redirect_stdout(sys.stderr):
+            cpu = cpu_baseline(args.problem, config, step_seeds[0], args.rank, args.cpu_iters)
 
     if rank == 0:
         out = {"metric": METRIC, "value": elapsed / max(iters, 1), "unit": "s/IPM-iter", "n_gpus": world,
