@@ -570,13 +570,13 @@ def tt_mat_mat_mul(m1, m2, op_tol, eps, verbose=False):
     """`src/tt_als.py:1631-1634`"""
     if np.max(np.array(T.tt_ranks(m1)) * np.array(T.tt_ranks(m2))) <= 40:
         return T.tt_rank_reduce(T.tt_fast_mat_mat_mul(m1, m2, eps), eps=op_tol)
-    from .tt_approx import tt_approx_mat_mat_mul
-    return tt_approx_mat_mat_mul(m1, m2, tol=op_tol)
+    raise NotImplementedError("tt_approx_mat_mat_mul (src/tt_als.py:1502-1634; SURVEY.md 8(f3)): rank product "
+                              "exceeds the exact zip-up limit 40")
 
 
 def tt_mat_vec_mul(mat, vec, op_tol, eps, verbose=False):
     """`src/tt_als.py:1765-1768`"""
     if np.max(np.array(T.tt_ranks(mat)) * np.array(T.tt_ranks(vec))) <= 80:
         return T.tt_rank_reduce(T.tt_fast_matrix_vec_mul(mat, vec, eps), op_tol)
-    from .tt_approx import tt_approx_mat_vec_mul
-    return tt_approx_mat_vec_mul(mat, vec, tol=op_tol)
+    raise NotImplementedError("tt_approx_mat_vec_mul (src/tt_als.py:1637-1768; SURVEY.md 8(f3)): rank product "
+                              "exceeds the exact zip-up limit 80")
