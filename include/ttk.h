@@ -101,6 +101,13 @@ int ttk_read_sync(void *stream, const double *src, double *host_dst, int64_t n);
 int64_t ttk_svd_work(int m, int n);
 int ttk_svd(void *stream, const double *A, int m, int n, double *U, double *S, double *Vt,
             double *work);
+/* ttk_svd with a deflation tolerance for large unfoldings: the column-pivoted QR that precedes
+ * the multi-workgroup Jacobi stops once the remaining Frobenius norm is <= defl; the deflated
+ * directions get S = 0 and zero vectors.  Callers pass 1e-3 x their truncation threshold, so
+ * the dropped energy (<= 1e-6 threshold^2) cannot change a `prune_singular_vals` decision
+ * (`cy_src/tt_ops_cy.pyx:161-177`).  defl = 0: exact. */
+int ttk_svd_tol(void *stream, const double *A, int m, int n, double *U, double *S, double *Vt,
+                double *work, double defl);
 /* SVDs with min(m,n) >= p whose working set exceeds LDS take the multi-workgroup Jacobi path
  * (default 64); p <= 2 forces it for every size (tests).  Returns the previous threshold. */
 int ttk_svd_set_big_threshold(int p);

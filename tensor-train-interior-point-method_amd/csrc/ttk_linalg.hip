@@ -1191,6 +1191,248 @@ __global__ void r_extract_kernel(const double *__restrict__ W, int ld, int k, in
   }
 }
 
+// ------------------------------------------------------ QR with column pivoting (dgeqp3)
+// Per column c: one workgroup picks the pivot (first max of the downdated norms, idamax), swaps
+// it in and forms the Householder reflector; then one launch applies the reflector to every
+// trailing column (one wave per column) and downdates its norm with LAPACK's dlaqp2 rule
+// (recompute when the downdate loses more than sqrt(eps)).  Column pivoting makes R's rows
+// graded, which is what lets the one-sided Jacobi on R^T converge in ~10 sweeps on the path's
+// unfoldings (41+ without it; Drmac-Veselic preconditioning).  Optional deflation: stop when the
+// remaining Frobenius norm is <= defl (the caller's truncation tolerance x 1e-3).
+// ctl[0] = effective rank, ctl[1] = stopped flag.
+__global__ __launch_bounds__(256) void qrcp_init_kernel(const double *__restrict__ W, int m, int n,
+                                                        double *__restrict__ vn1, double *__restrict__ vn2,
+                                                        int *__restrict__ perm, int *__restrict__ ctl, int k) {
+  const int j = (int)((blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6);
+  const int lane = threadIdx.x & 63;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    ctl[0] = k;
+    ctl[1] = 0;
+  }
+  if (j >= n) return;
+  const double *w = W + (int64_t)j * m;
+  double acc = 0.0;
+  for (int i = lane; i < m; i += 64) acc += w[i] * w[i];
+  acc = sqrt(ttk::wave_sum(acc));
+  if (lane == 0) {
+    vn1[j] = acc;
+    vn2[j] = acc;
+    perm[j] = j;
+  }
+}
+
+__global__ __launch_bounds__(1024) void qrcp_pivot_kernel(double *W, int m, int n, int c, double *vn1, double *vn2,
+                                                          int *perm, double *__restrict__ tau, int *ctl, double defl2) {
+  __shared__ double smax[16], ssum[16], red[16];
+  __shared__ int sidx[16];
+  __shared__ int s_piv, s_stop;
+  if (ctl[1]) return;
+  const int tid = threadIdx.x, nt = blockDim.x;
+  const int lane = tid & 63, wid = tid >> 6, nw = nt >> 6;
+  double bm = -1.0, sum = 0.0;
+  int bi = n;
+  for (int j = c + tid; j < n; j += nt) {
+    const double v = vn1[j];
+    sum += v * v;
+    if (v > bm) {  // strided scan: first max within this thread's subsequence
+      bm = v;
+      bi = j;
+    }
+  }
+  // wave reduction of (max, first index) and the sum
+  for (int off = 32; off > 0; off >>= 1) {
+    const double om = __shfl_xor(bm, off, 64);
+    const int oi = __shfl_xor(bi, off, 64);
+    if (om > bm || (om == bm && oi < bi)) {
+      bm = om;
+      bi = oi;
+    }
+  }
+  sum = ttk::wave_sum(sum);
+  if (lane == 0) {
+    smax[wid] = bm;
+    sidx[wid] = bi;
+    ssum[wid] = sum;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    double m0 = -1.0, s0 = 0.0;
+    int i0 = n;
+    for (int w = 0; w < nw; ++w) {
+      s0 += ssum[w];
+      if (smax[w] > m0 || (smax[w] == m0 && sidx[w] < i0)) {
+        m0 = smax[w];
+        i0 = sidx[w];
+      }
+    }
+    s_stop = (defl2 > 0.0 && s0 <= defl2) || s0 == 0.0;
+    s_piv = i0;
+    if (s_stop) {
+      ctl[0] = c;
+      ctl[1] = 1;
+    }
+  }
+  __syncthreads();
+  if (s_stop) return;
+  const int piv = s_piv;
+  if (piv != c) {
+    double *a = W + (int64_t)c * m, *b = W + (int64_t)piv * m;
+    for (int i = tid; i < m; i += nt) {
+      const double t = a[i];
+      a[i] = b[i];
+      b[i] = t;
+    }
+    if (tid == 0) {
+      double t = vn1[c];
+      vn1[c] = vn1[piv];
+      vn1[piv] = t;
+      t = vn2[c];
+      vn2[c] = vn2[piv];
+      vn2[piv] = t;
+      const int pi = perm[c];
+      perm[c] = perm[piv];
+      perm[piv] = pi;
+    }
+    __syncthreads();
+  }
+  double *x = W + (int64_t)c * m;
+  double part = 0.0;
+  for (int i = c + 1 + tid; i < m; i += nt) part += x[i] * x[i];
+  const double sigma = ttk::block_sum(part, red);
+  const double alpha = x[c];
+  double t = 0.0, beta = alpha;
+  if (sigma > 0.0) {
+    beta = -copysign(sqrt(alpha * alpha + sigma), alpha);
+    t = (beta - alpha) / beta;
+    const double sc = 1.0 / (alpha - beta);
+    for (int i = c + 1 + tid; i < m; i += nt) x[i] *= sc;
+  }
+  __syncthreads();  // every thread has read alpha = x[c] before it is overwritten
+  if (tid == 0) {
+    x[c] = beta;
+    tau[c] = t;
+  }
+  (void)wid;
+}
+
+__global__ __launch_bounds__(256) void qrcp_update_kernel(double *__restrict__ W, int m, int n, int c,
+                                                          double *__restrict__ vn1, double *__restrict__ vn2,
+                                                          const double *__restrict__ tau, const int *__restrict__ ctl) {
+  if (ctl[1]) return;
+  const int j = c + 1 + (int)((blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6);
+  const int lane = threadIdx.x & 63;
+  if (j >= n) return;
+  const double t = tau[c];
+  const double *v = W + (int64_t)c * m;
+  double *y = W + (int64_t)j * m;
+  double yc = y[c];
+  if (t != 0.0) {
+    double acc = 0.0;
+    for (int i = c + 1 + lane; i < m; i += 64) acc += v[i] * y[i];
+    const double w = t * (ttk::wave_sum(acc) + yc);
+    for (int i = c + 1 + lane; i < m; i += 64) y[i] -= w * v[i];
+    yc -= w;
+    if (lane == 0) y[c] = yc;
+  }
+  const double a = vn1[j];
+  if (a != 0.0) {  // dlaqp2 norm downdate
+    double temp = fabs(yc) / a;
+    temp = fmax(1.0 - temp * temp, 0.0);
+    const double r = a / vn2[j];
+    if (temp * r * r <= 1.4901161193847656e-08) {
+      double acc = 0.0;
+      for (int i = c + 1 + lane; i < m; i += 64) acc += y[i] * y[i];
+      acc = sqrt(ttk::wave_sum(acc));
+      if (lane == 0) {
+        vn1[j] = acc;
+        vn2[j] = acc;
+      }
+    } else if (lane == 0) {
+      vn1[j] = a * sqrt(temp);
+    }
+  }
+}
+
+// T factors (dlarft, forward/columnwise) of every QB-panel of reflectors 0..kk-1 stored in W
+__global__ __launch_bounds__(256) void tfactor_kernel(const double *__restrict__ W, int m, int kk,
+                                                      const double *__restrict__ tau, double *__restrict__ Tall) {
+  __shared__ double ytv[QB];
+  const int pi = blockIdx.x, j0 = pi * QB;
+  const int nbe = (kk - j0) < QB ? (kk - j0) : QB;
+  double *T = Tall + (int64_t)pi * QB * QB;
+  const int tid = threadIdx.x, nt = blockDim.x;
+  const int lane = tid & 63, wid = tid >> 6, nw = nt >> 6;
+  for (int e = tid; e < QB * QB; e += nt) T[e] = 0.0;
+  __syncthreads();
+  for (int jj = 0; jj < nbe; ++jj) {
+    const int c = j0 + jj;
+    const double t = tau[c];
+    const double *x = W + (int64_t)c * m;
+    for (int k = wid; k < jj; k += nw) {
+      const double *yk = W + (int64_t)(j0 + k) * m;
+      double acc = 0.0;
+      for (int i = c + 1 + lane; i < m; i += 64) acc += yk[i] * x[i];
+      acc = ttk::wave_sum(acc) + yk[c];
+      if (lane == 0) ytv[k] = acc;
+    }
+    __syncthreads();
+    if (tid < jj) {
+      double acc = 0.0;
+      for (int k = tid; k < jj; ++k) acc += T[tid + k * QB] * ytv[k];
+      T[tid + jj * QB] = -t * acc;
+    }
+    if (tid == 0) T[jj + jj * QB] = t;
+    __syncthreads();
+  }
+}
+
+// X (col-major, column length p, kk columns) = R1^T, R1 = first kk rows of the upper triangle of
+// W (col-major, ld m); V = I (kk x kk)
+__global__ void rt_build2_kernel(const double *__restrict__ W, int ld, int p, int kk, double *__restrict__ X,
+                                 double *__restrict__ V) {
+  const int64_t tx = (int64_t)kk * p, tv = (int64_t)kk * kk;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < tx + tv; e += (int64_t)gridDim.x * blockDim.x) {
+    if (e < tx) {
+      const int i = (int)(e / p), j = (int)(e - (int64_t)i * p);  // X(j, i) = R(i, j)
+      X[e] = (j >= i) ? W[(int64_t)j * ld + i] : 0.0;
+    } else {
+      const int64_t f = e - tx;
+      V[f] = ((f / kk) == (f % kk)) ? 1.0 : 0.0;
+    }
+  }
+}
+
+// final assembly: Lw = M (col-major q x kk), Rw = P Ux (Ux row-major p x kk, perm[i] = original
+// column of pivoted column i); tall: U = Lw, Vt = Rw^T; wide: U = Rw, Vt = Lw^T; rank >= kk zero
+__global__ void svd_big_out_kernel(const double *__restrict__ M, const double *__restrict__ Ux,
+                                   const int *__restrict__ perm, int q, int p, int kk, int tall,
+                                   double *__restrict__ U, double *__restrict__ Vt, double *__restrict__ S) {
+  const int64_t nl = (int64_t)q * p, nr = (int64_t)p * p;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < nl + nr + p;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    if (e < nl) {  // left factor of W: element (i, r), i < q, r < p
+      const int i = (int)(e / p), r = (int)(e - (int64_t)i * p);
+      const double v = r < kk ? M[(int64_t)r * q + i] : 0.0;
+      if (tall)
+        U[(int64_t)i * p + r] = v;        // U (q x p)
+      else
+        Vt[(int64_t)r * q + i] = v;       // Vt (p x q)
+    } else if (e < nl + nr) {  // right factor of W: element (perm[i], r)
+      const int64_t f = e - nl;
+      const int i = (int)(f / p), r = (int)(f - (int64_t)i * p);
+      const double v = r < kk ? Ux[(int64_t)i * kk + r] : 0.0;
+      const int oi = perm[i];
+      if (tall)
+        Vt[(int64_t)r * p + oi] = v;      // Vt (p x p)
+      else
+        U[(int64_t)oi * p + r] = v;       // U (p x p)
+    } else {
+      const int r = (int)(e - nl - nr);
+      if (r >= kk) S[r] = 0.0;
+    }
+  }
+}
+
 inline int grid_for(int64_t n) {
   const int64_t g = (n + 255) / 256;
   return (int)(g < 4096 ? (g > 0 ? g : 1) : 4096);
@@ -1250,28 +1492,33 @@ static int g_svd_big_p = 64;  // smallest p that takes the multi-workgroup path 
 
 static int64_t svd_big_work(int m, int n) {
   const int64_t p = m < n ? m : n, q = m < n ? n : m, npan = (p + QB - 1) / QB;
-  return 2 * q * p + 4 * p * p + p + npan * QB * QB + QB * p + 2 * p + 64;
+  return 2 * q * p + 4 * p * p + 6 * p + npan * QB * QB + QB * p + 64;
 }
 
-// Large SVD: W = Q R (blocked Householder), one-sided Jacobi on X = R^T (p x p; QR preconditioning
-// cuts the sweep count ~4x on graded spectra), then U_W = Q V_X.  W = A (tall) or A^T (wide).
-static int svd_big(void *stream, const double *A, int m, int n, double *U, double *S, double *Vt, double *work) {
+// Large SVD: W P = Q R by column-pivoted Householder QR (optionally deflated at `defl`), one-sided
+// Jacobi on X = R1^T (p x k_eff; QRCP makes it converge in ~10 sweeps), then the left vectors
+// Q [V_X; 0] and the right vectors P U_X.  W = A (tall) or A^T (wide).
+static int svd_big(void *stream, const double *A, int m, int n, double *U, double *S, double *Vt, double *work,
+                   double defl) {
   int rc = ensure_status();
   if (rc != TTK_OK) return rc;
   const bool tall = m >= n;
-  const int p = tall ? n : m, q = tall ? m : n, P = (p % 2) ? p + 1 : p;
+  const int p = tall ? n : m, q = tall ? m : n;
   const int npan = (p + QB - 1) / QB;
   double *W = work;                                  // q x p col-major
   double *M = W + (int64_t)q * p;                    // q x p col-major
-  double *X = M + (int64_t)q * p;                    // p x p col-major
-  double *V = X + (int64_t)p * p;                    // p x p col-major
-  double *Ux = V + (int64_t)p * p;                   // p x p row-major
-  double *VtX = Ux + (int64_t)p * p;                 // p x p row-major
+  double *X = M + (int64_t)q * p;                    // p x p col-major (k_eff columns used)
+  double *V = X + (int64_t)p * p;                    // k_eff x k_eff
+  double *Ux = V + (int64_t)p * p;                   // p x k_eff row-major
+  double *VtX = Ux + (int64_t)p * p;                 // k_eff x k_eff row-major
   double *tau = VtX + (int64_t)p * p;                // p
-  double *Tall = tau + p;                            // npan * QB * QB
-  double *Z = Tall + (int64_t)npan * QB * QB;        // QB * p
-  double *sig = Z + (int64_t)QB * p;                 // p
+  double *vn1 = tau + p, *vn2 = vn1 + p;             // p, p
+  double *sig = vn2 + p;                             // p
   int *rank = reinterpret_cast<int *>(sig + p);      // p ints
+  int *perm = reinterpret_cast<int *>(sig + 2 * p);  // p ints
+  double *Tall = sig + 3 * p;                        // npan * QB * QB
+  double *Z = Tall + (int64_t)npan * QB * QB;        // QB * p
+  int *ctl = g_status + 10;                          // [0] k_eff, [1] stopped
   int *flag = g_status + 8;
   hipStream_t st = TTK_STREAM(stream);
   if (tall)
@@ -1279,37 +1526,53 @@ static int svd_big(void *stream, const double *A, int m, int n, double *U, doubl
   else  // W = A^T: column j of W = row j of A -> a plain copy
     TTK_HIP(hipMemcpyAsync(W, A, sizeof(double) * (size_t)q * p, hipMemcpyDeviceToDevice, st));
   TTK_LAUNCH_CHECK();
-  rc = qrb_factor(st, W, q, p, tau, Tall, Z);
-  if (rc != TTK_OK) return rc;
-  hipLaunchKernelGGL(rt_build_kernel, dim3(grid_for((int64_t)p * p)), dim3(256), 0, st, W, q, p, X, V);
+  const double defl2 = defl > 0.0 ? defl * defl : 0.0;
+  hipLaunchKernelGGL(qrcp_init_kernel, dim3((p * 64 + 255) / 256), dim3(256), 0, st, W, q, p, vn1, vn2, perm, ctl, p);
+  TTK_LAUNCH_CHECK();
+  for (int c = 0; c < p; ++c) {
+    hipLaunchKernelGGL(qrcp_pivot_kernel, dim3(1), dim3(1024), 0, st, W, q, p, c, vn1, vn2, perm, tau, ctl, defl2);
+    if (c + 1 < p)
+      hipLaunchKernelGGL(qrcp_update_kernel, dim3(((p - c - 1) * 64 + 255) / 256), dim3(256), 0, st, W, q, p, c, vn1,
+                         vn2, tau, ctl);
+    TTK_LAUNCH_CHECK();
+    if ((c & 63) == 63 && c + 1 < p) {  // early-exit check for deflated solves
+      int h = 0;
+      TTK_HIP(hipMemcpyAsync(&h, ctl + 1, sizeof(int), hipMemcpyDeviceToHost, st));
+      TTK_HIP(hipStreamSynchronize(st));
+      if (h) break;
+    }
+  }
+  int hk[2] = {p, 0};
+  TTK_HIP(hipMemcpyAsync(hk, ctl, 2 * sizeof(int), hipMemcpyDeviceToHost, st));
+  TTK_HIP(hipStreamSynchronize(st));
+  const int kk = hk[0] < 1 ? 1 : hk[0];  // keep one direction so the epilogue is well defined
+  const int nkp = (kk + QB - 1) / QB;
+  hipLaunchKernelGGL(tfactor_kernel, dim3(nkp), dim3(256), 0, st, W, q, kk, tau, Tall);
+  hipLaunchKernelGGL(rt_build2_kernel, dim3(grid_for((int64_t)kk * (p + kk))), dim3(256), 0, st, W, q, p, kk, X, V);
   TTK_LAUNCH_CHECK();
   const double tol = EPS * (p > 16 ? (double)p : 16.0);
+  const int P = (kk % 2) ? kk + 1 : kk;
   const int grid = (P / 2 * 64 + 255) / 256;
-  for (int sweep = 0; sweep < 60; ++sweep) {
+  for (int sweep = 0; sweep < 60 && kk > 1; ++sweep) {
     TTK_HIP(hipMemsetAsync(flag, 0, sizeof(int), st));
     for (int r = 0; r < P - 1; ++r)
-      hipLaunchKernelGGL(svd_big_round_kernel, dim3(grid), dim3(256), 0, st, X, V, p, p, r, tol, flag);
+      hipLaunchKernelGGL(svd_big_round_kernel, dim3(grid), dim3(256), 0, st, X, V, kk, p, r, tol, flag);
     TTK_LAUNCH_CHECK();
     int h = 0;
     TTK_HIP(hipMemcpyAsync(&h, flag, sizeof(int), hipMemcpyDeviceToHost, st));
     TTK_HIP(hipStreamSynchronize(st));
     if (!h) break;
   }
-  // X = U_X S V_X^T (epilogue sorts): Ux (p x p row-major), VtX = V_X^T (row-major)
-  hipLaunchKernelGGL(svd_big_finish_kernel, dim3(1), dim3(1024), 0, st, X, V, sig, rank, p, p, Ux, S, VtX);
+  // X (p x kk) = U_X S V_X^T: Ux (p x kk row-major), S[0:kk], VtX (kk x kk row-major)
+  hipLaunchKernelGGL(svd_big_finish_kernel, dim3(1), dim3(1024), 0, st, X, V, sig, rank, p, kk, Ux, S, VtX);
   TTK_LAUNCH_CHECK();
-  // M = Q [V_X; 0]
-  hipLaunchKernelGGL(qpad_kernel, dim3(grid_for((int64_t)q * p)), dim3(256), 0, st, VtX, p, q, p, M);
+  // M = Q [V_X; 0]  (q x kk)
+  hipLaunchKernelGGL(qpad_kernel, dim3(grid_for((int64_t)q * kk)), dim3(256), 0, st, VtX, kk, q, kk, M);
   TTK_LAUNCH_CHECK();
-  rc = qrb_apply_q(st, W, q, p, Tall, M, p, Z);
+  rc = qrb_apply_q(st, W, q, kk, Tall, M, kk, Z);
   if (rc != TTK_OK) return rc;
-  if (tall) {  // A = W = (Q V_X) S U_X^T
-    hipLaunchKernelGGL(cm_to_rm_kernel, dim3(grid_for((int64_t)q * p)), dim3(256), 0, st, M, q, U, q, p);
-    hipLaunchKernelGGL(cm_to_rm_kernel, dim3(grid_for((int64_t)p * p)), dim3(256), 0, st, Ux, p, Vt, p, p);
-  } else {  // A = W^T = U_X S (Q V_X)^T
-    TTK_HIP(hipMemcpyAsync(U, Ux, sizeof(double) * (size_t)p * p, hipMemcpyDeviceToDevice, st));
-    TTK_HIP(hipMemcpyAsync(Vt, M, sizeof(double) * (size_t)q * p, hipMemcpyDeviceToDevice, st));
-  }
+  hipLaunchKernelGGL(svd_big_out_kernel, dim3(grid_for((int64_t)q * p + (int64_t)p * p + p)), dim3(256), 0, st, M, Ux,
+                     perm, q, p, kk, tall ? 1 : 0, U, Vt, S);
   TTK_LAUNCH_CHECK();
   return TTK_OK;
 }
@@ -1351,6 +1614,11 @@ int64_t ttk_svd_work(int m, int n) {
 }
 
 int ttk_svd(void *stream, const double *A, int m, int n, double *U, double *S, double *Vt, double *work) {
+  return ttk_svd_tol(stream, A, m, n, U, S, Vt, work, 0.0);
+}
+
+int ttk_svd_tol(void *stream, const double *A, int m, int n, double *U, double *S, double *Vt, double *work,
+                double defl) {
   if (m <= 0 || n <= 0) {
     ttk::set_error("ttk_svd: empty matrix %dx%d", m, n);
     return TTK_ERR_ARG;
@@ -1358,7 +1626,7 @@ int ttk_svd(void *stream, const double *A, int m, int n, double *U, double *S, d
   const int p = m < n ? m : n, q = m < n ? n : m, pairs = (p + 1) / 2;
   const int64_t need = (int64_t)q * p + (int64_t)p * p + 2 * p + 16;
   const int use_lds = need <= LDS_DOUBLES;
-  if (p >= g_svd_big_p && (!use_lds || g_svd_big_p <= 2)) return svd_big(stream, A, m, n, U, S, Vt, work);
+  if (p >= g_svd_big_p && (!use_lds || g_svd_big_p <= 2)) return svd_big(stream, A, m, n, U, S, Vt, work, defl);
   const size_t shm = use_lds ? need * sizeof(double) : 0;
   allow_big_lds(svd_kernel, shm);
   int g = 1;

@@ -58,13 +58,20 @@ def to_numpy(t):
 OPSTATS = {} if os.environ.get("TTIPM_OPSTATS") else None
 
 
-def _stat(name, shape, t0):
+def _stat(name, shape, t0, site_min=None):
     import time as _t
     torch.cuda.synchronize()
     d = OPSTATS.setdefault(name, {})
     e = d.setdefault(shape, [0, 0.0])
     e[0] += 1
-    e[1] += _t.perf_counter() - t0
+    dt = _t.perf_counter() - t0
+    e[1] += dt
+    if site_min is not None and site_min:  # record the Python call chain of large calls
+        import traceback
+        chain = " < ".join(f"{f.name}:{f.lineno}" for f in traceback.extract_stack()[-8:-2][::-1])
+        s = OPSTATS.setdefault(name + "@sites", {}).setdefault(chain, [0, 0.0])
+        s[0] += 1
+        s[1] += dt
 
 
 def _tic():
@@ -345,29 +352,40 @@ def matmul(a, b, out=None, alpha=1.0, beta=0.0):
 
 
 # ------------------------------------------------------------------------ factorisations
-def svd(A):
-    """Thin SVD of a 2-D device matrix.  Returns (U, S, Vt, s_host)."""
+_DUMP = {"min": int(os.environ.get("TTIPM_DUMP_SVD", "0")), "n": 0}
+
+
+def svd(A, defl=0.0):
+    """Thin SVD of a 2-D device matrix.  Returns (U, S, Vt, s_host).  `defl` > 0 lets the large-
+    matrix path deflate directions whose total Frobenius norm is <= defl (S = 0 there)."""
     t0 = _tic() if OPSTATS is not None else 0
     A = A.contiguous()
     m, n = A.shape
+    if _DUMP["min"] and min(m, n) >= _DUMP["min"] and _DUMP["n"] < 12:  # dev diagnostics only
+        os.makedirs("gpurun_out", exist_ok=True)
+        np.save(f"gpurun_out/svd_in_{_DUMP['n']}.npy", read(A))
+        _DUMP["n"] += 1
     k = min(m, n)
     U, S, Vt = empty(m, k), empty(k), empty(k, n)
     work = empty(int(lib.ttk_svd_work(m, n)))
-    check(lib.ttk_svd(_stream(), _p(A), m, n, _p(U), _p(S), _p(Vt), _p(work)), "svd")
+    check(lib.ttk_svd_tol(_stream(), _p(A), m, n, _p(U), _p(S), _p(Vt), _p(work), float(defl)), "svd")
     sh = read(S)
     if OPSTATS is not None:
-        _stat("svd", (m, n), t0)
+        _stat("svd", (m, n), t0, site_min=min(m, n) >= 64)
     return U, S, Vt, sh
 
 
 def qr(A):
     """Economic Householder QR: A (m,n) = Q (m,k) R (k,n)."""
+    t0 = _tic() if OPSTATS is not None else 0
     A = A.contiguous()
     m, n = A.shape
     k = min(m, n)
     Q, R = empty(m, k), empty(k, n)
     work = empty(int(lib.ttk_qr_work(m, n)))
     check(lib.ttk_qr(_stream(), _p(A), m, n, _p(Q), _p(R), _p(work)), "qr")
+    if OPSTATS is not None:
+        _stat("qr", (m, n), t0, site_min=min(m, n) >= 64)
     return Q, R
 
 
@@ -458,7 +476,7 @@ def syev_extreme(A, largest=False):
           "syev_extreme")
     lam = float(read(buf[:1])[0])
     if OPSTATS is not None:
-        _stat("syev_extreme", n, t0)
+        _stat("syev_extreme", n, t0, site_min=n >= 200)
     return lam, buf[1:]
 
 

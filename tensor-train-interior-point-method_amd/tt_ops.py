@@ -183,6 +183,9 @@ def add_kick_rank(u, v, r_add=2):
 
 
 # ------------------------------------------------------------------ rounding (`:130-388`)
+DEFL = 1e-3  # SVD deflation tolerance relative to a caller's truncation threshold
+
+
 def prune_singular_vals(s, eps):
     """`cy_src/tt_ops_cy.pyx:161-177` -- host decision on the copied-back singular values."""
     if np.linalg.norm(s) == 0.0:
@@ -236,7 +239,9 @@ def _svd_step(tt, idx, rank, eps, track):
     ish = tt[idx].shape
     nsh = tt[idx + 1].shape
     mat = D.contig(tt[idx]).view(rank * int(np.prod(ish[1:-1])), -1)
-    U, S, Vt, s = D.svd(mat)
+    # deflation below 1e-3 x the truncation threshold cannot change the rank decision; the PSD /
+    # mask variants (track) feed the discarded energy back, so they stay exact
+    U, S, Vt, s = D.svd(mat, defl=0.0 if track else DEFL * eps)
     tail = 0.0
     if track:
         sc = np.cumsum(np.abs(s[::-1]) ** 2)[::-1]
@@ -334,13 +339,13 @@ def swap_cores(a, b, eps):
     """`cy_src/tt_ops_cy.pyx:393-426`"""
     if a.dim() == 3:
         m = D.einsum("ijr,rkl->ikjl", a, b).view(a.shape[0] * b.shape[1], -1)
-        U, S, Vt, s = D.svd(m)
+        U, S, Vt, s = D.svd(m, defl=DEFL * eps)
         r = prune_singular_vals(s, eps)
         na = D.einsum("ij,j->ij", U[:, :r], S[:r]).view(a.shape[0], b.shape[1], r)
         nb = D.clone(Vt[:r]).view(r, a.shape[1], b.shape[2])
         return na, nb
     m = D.einsum("ijkr,rlmn->ilmjkn", a, b).view(a.shape[0] * b.shape[1] * b.shape[2], -1)
-    U, S, Vt, s = D.svd(m)
+    U, S, Vt, s = D.svd(m, defl=DEFL * eps)
     r = prune_singular_vals(s, eps)
     na = D.einsum("ij,j->ij", U[:, :r], S[:r]).view(a.shape[0], b.shape[1], b.shape[2], r)
     nb = D.clone(Vt[:r]).view(r, a.shape[1], a.shape[2], b.shape[3])

@@ -211,6 +211,9 @@ class EmuLib:
     def ttk_qr_set_big_threshold(self, k):
         return 48
 
+    def ttk_svd_tol(self, s, A, m, n, U, S, Vt, work, defl):
+        return self.ttk_svd(s, A, m, n, U, S, Vt, work)
+
     def ttk_svd_set_big_threshold(self, p):
         return 64
 

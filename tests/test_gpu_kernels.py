@@ -149,6 +149,31 @@ def test_svd_large_rank_deficient(dev, m, n, r):
     _check_svd(dev, A)
 
 
+@pytest.mark.parametrize("case", ["graded", "clustered"])
+def test_svd_large_deflated(dev, case):
+    """Deflated large SVD: singular values above the deflation level are exact, the deflated
+    ones are zero, and the kept triplets reconstruct A to the dropped energy."""
+    rng = _rng(5)
+    m, n, r = 500, 700, 240
+    if case == "graded":
+        s = np.logspace(0, -15, r)
+    else:
+        s = np.concatenate([np.full(40, np.sqrt(2.0)), np.logspace(-1, -15, r - 40)])
+    Ql, _ = np.linalg.qr(rng.standard_normal((m, r)))
+    Qr, _ = np.linalg.qr(rng.standard_normal((n, r)))
+    A = (Ql * s) @ Qr.T
+    defl = 1e-3 * 1e-12
+    U, S, Vt, sv = dev.svd(dev.from_numpy(A), defl=defl)
+    U, Vt = dev.read(U), dev.read(Vt)
+    ref = np.linalg.svd(A, compute_uv=False)
+    assert np.all(np.diff(sv) <= 0)
+    k = int(np.sum(sv > 0))
+    assert np.sum(ref[k:] ** 2) <= defl ** 2 * 1.01 + 1e-30
+    assert np.allclose(sv[:k], ref[:k], rtol=0, atol=5e-14 * ref[0])
+    assert np.abs((U[:, :k] * sv[:k]) @ Vt[:k] - A).max() <= 1e-13 * np.abs(A).max() + defl
+    assert np.allclose(U[:, :k].T @ U[:, :k], np.eye(k), atol=1e-12)
+
+
 def test_svd_zero_and_rank_one(dev):
     U, S, Vt, s = dev.svd(dev.zeros(6, 4))
     assert np.all(s == 0)

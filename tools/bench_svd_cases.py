@@ -1,0 +1,26 @@
+"""Time the device SVD on dumped real unfoldings (.svd_cases/*.npy; dev tool)."""
+import glob
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from ttipm_amd import dev as D  # noqa: E402
+
+for f in sorted(glob.glob(".svd_cases/*.npy")):
+    A = np.load(f)
+    dA = D.from_numpy(A)
+    D.svd(dA)
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    U, S, Vt, s = D.svd(dA)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t
+    ref = np.linalg.svd(A, compute_uv=False)
+    U, Vt = D.read(U), D.read(Vt)
+    err = np.abs((U * s) @ Vt - A).max() / np.abs(A).max()
+    print(f"{f} {A.shape} {dt * 1e3:8.1f} ms  sv err {np.max(np.abs(s - ref)) / ref[0]:.2e}  recon {err:.2e}  "
+          f"orthU {np.abs(U.T @ U - np.eye(U.shape[1])).max():.2e}", flush=True)
