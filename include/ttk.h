@@ -59,6 +59,15 @@ int ttk_gemm_offs(void *stream, const double *A, const double *B, double *C, con
 int ttk_gemm_offs_grouped(void *stream, const double *const *Aptr, const double *const *Bptr,
                           double *const *Cptr, const int64_t *offs, int ngroups, int nb, int M,
                           int N, int K, double alpha, double beta);
+/* Native einsum engine (replaces `cached_einsum`, src/tt_ops.py:22-28, and the tensordot chains
+ * of cy_src/tt_ops_cy.pyx): out = alpha * einsum(eq, ops) + beta * out on device fp64 data.
+ * desc = [nops, {ptr, ndim, shape[ndim], stride[ndim]} x nops, has_out_strides, (ndim,
+ * out_stride[ndim])], strides in elements (views need not be contiguous).  Plans (greedy
+ * pairwise order + offset tables) are cached per (eq, shapes, strides); each pairwise step is one
+ * ttk_gemm_offs launch. */
+int ttk_einsum(void *stream, const char *eq, const int64_t *desc, double *out, double alpha, double beta);
+/* out[3] = {plan hits, plan misses, cached plans} */
+int ttk_einsum_stats(long long *out);
 /* contraction-kernel accounting for the roofline report: on != 0 brackets every ttk_gemm_offs*
  * launch with two HIP events on its stream (returns the previous setting) */
 int ttk_contract_timing(int on);
@@ -108,8 +117,10 @@ int ttk_svd(void *stream, const double *A, int m, int n, double *U, double *S, d
  * (`cy_src/tt_ops_cy.pyx:161-177`).  defl = 0: exact. */
 int ttk_svd_tol(void *stream, const double *A, int m, int n, double *U, double *S, double *Vt,
                 double *work, double defl);
-/* SVDs with min(m,n) >= p whose working set exceeds LDS take the multi-workgroup Jacobi path
- * (default 64); p <= 2 forces it for every size (tests).  Returns the previous threshold. */
+/* min(m,n) <= 96: one-workgroup kernel (column-pivoted QR + one-sided Jacobi on R^T in LDS);
+ * larger: the multi-workgroup path (pivoted QR launches + one launch per Jacobi round).
+ * ttk_svd_set_big_threshold(p <= 2) forces the multi-workgroup path for every size (tests);
+ * returns the previous setting. */
 int ttk_svd_set_big_threshold(int p);
 /* economic Householder QR A(m,n) = Q(m,k) R(k,n), k=min(m,n)  (scipy.linalg.qr economic,
  * `cy_src/tt_ops_cy.pyx:147-151`, `src/tt_als.py:358,482`). */

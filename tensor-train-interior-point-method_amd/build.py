@@ -6,7 +6,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libttk.so")
-SOURCES = ["ttk_runtime.hip", "ttk_contract.hip", "ttk_linalg.hip", "ttk_lgmres.hip"]
+SOURCES = ["ttk_runtime.hip", "ttk_contract.hip", "ttk_einsum.hip", "ttk_linalg.hip", "ttk_lgmres.hip"]
 HEADERS = ["ttk_common.h", os.path.join("..", "..", "include", "ttk.h")]
 
 

@@ -1,0 +1,420 @@
+// Native einsum engine: plan cache + executor for every small TT contraction on the path
+// (`cached_einsum` / `get_contract_expr_cached`, src/tt_ops.py:22-28, and the pairwise
+// `tensordot` chains of cy_src/tt_ops_cy.pyx).
+//
+// A plan is built once per (equation, operand shapes, operand strides, output strides):
+//   * pairwise greedy contraction order (opt_einsum "greedy": minimise the pair's FLOPs, ties by
+//     result size, then position), the same order the Python planner used;
+//   * per pairwise step: batch / M / N / K index groups and five int64 offset tables (batch, m, k
+//     for A; batch, k, n for B; batch, m, n for C) that address the operands through their
+//     strides, so permuted/transposed views are never materialised;
+//   * the tables of all steps live in one device allocation (bump arena).
+// Executing a plan is one `gemm_offs` launch per step (fp64 MFMA, ttk_contract.hip).
+// Intermediates go to a single stream-ordered scratch buffer shared by all calls: every call is
+// on the same in-order stream, so the next call's kernels cannot overtake this call's.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstring>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "ttk_common.h"
+
+extern "C" int ttk_gemm_offs(void *stream, const double *A, const double *B, double *C, const int64_t *offs, int nb,
+                             int M, int N, int K, double alpha, double beta);
+
+namespace {
+
+constexpr int SLOT_ONES = -1000000;
+constexpr int SLOT_FINAL = -2000000;
+constexpr int MAX_IDX = 52;
+
+struct Step {
+  int a, b, out;  // operand slots: >= 0 input, < 0 intermediate -(k+1); b may be SLOT_ONES
+  int nb, M, N, K;
+  int64_t offs;  // element offset of this step's tables inside the plan's table block
+  int64_t tmp;   // element offset of this step's result inside the scratch (intermediates)
+};
+
+struct Plan {
+  std::vector<Step> steps;
+  int64_t *dtab = nullptr;  // device tables
+  int64_t scratch = 0;      // doubles of scratch needed
+};
+
+struct Arena {  // device bump allocator for offset tables (freed only on a full cache reset)
+  std::vector<void *> chunks;
+  char *cur = nullptr;
+  size_t left = 0;
+  void *take(size_t bytes) {
+    bytes = (bytes + 255) & ~size_t(255);
+    if (bytes > left) {
+      size_t sz = bytes > (size_t(16) << 20) ? bytes : (size_t(16) << 20);
+      void *p = nullptr;
+      if (hipMalloc(&p, sz) != hipSuccess) return nullptr;
+      chunks.push_back(p);
+      cur = static_cast<char *>(p);
+      left = sz;
+    }
+    void *r = cur;
+    cur += bytes;
+    left -= bytes;
+    return r;
+  }
+  void reset() {
+    for (void *p : chunks) (void)hipFree(p);
+    chunks.clear();
+    cur = nullptr;
+    left = 0;
+  }
+};
+
+struct Engine {
+  std::unordered_map<std::string, Plan> plans;
+  Arena arena;
+  double *scratch = nullptr;
+  int64_t scratch_n = 0;
+  double *ones = nullptr;
+  long long hits = 0, misses = 0;
+};
+Engine g_eng;
+
+struct Operand {
+  std::string idx;
+  int64_t st[128];  // stride per index char (by char code)
+  int slot;
+};
+
+inline int64_t extent_of(const int64_t *ext, const std::string &s) {
+  int64_t p = 1;
+  for (char c : s) p *= ext[(unsigned char)c];
+  return p;
+}
+
+void group_offsets(const std::string &grp, const int64_t *ext, const int64_t *st, std::vector<int64_t> &out) {
+  const size_t base = out.size();
+  out.push_back(0);
+  for (char c : grp) {
+    const int64_t e = ext[(unsigned char)c], s = st[(unsigned char)c];
+    const size_t n0 = out.size() - base;
+    std::vector<int64_t> nxt;
+    nxt.reserve(n0 * e);
+    for (size_t i = 0; i < n0; ++i)
+      for (int64_t k = 0; k < e; ++k) nxt.push_back(out[base + i] + k * s);
+    out.resize(base);
+    out.insert(out.end(), nxt.begin(), nxt.end());
+  }
+}
+
+bool contains(const std::string &s, char c) { return s.find(c) != std::string::npos; }
+
+// build a plan; returns false with ttk error set
+bool build_plan(const std::string &eq, int nops, const int *ndims, const int64_t *shapes, const int64_t *strides,
+                int out_nd, const int64_t *out_strides, Plan &pl) {
+  const size_t arrow = eq.find("->");
+  if (arrow == std::string::npos) {
+    ttk::set_error("einsum: equation needs '->': %s", eq.c_str());
+    return false;
+  }
+  std::vector<std::string> ins;
+  {
+    std::string lhs = eq.substr(0, arrow), cur;
+    for (char c : lhs) {
+      if (c == ',') {
+        ins.push_back(cur);
+        cur.clear();
+      } else if (c != ' ') {
+        cur.push_back(c);
+      }
+    }
+    ins.push_back(cur);
+  }
+  std::string out;
+  for (char c : eq.substr(arrow + 2))
+    if (c != ' ') out.push_back(c);
+  if ((int)ins.size() != nops) {
+    ttk::set_error("einsum: %d operands for %s", nops, eq.c_str());
+    return false;
+  }
+  int64_t ext[128];
+  for (int i = 0; i < 128; ++i) ext[i] = 1;
+  std::vector<Operand> live;
+  {
+    int64_t o = 0;
+    for (int i = 0; i < nops; ++i) {
+      if ((int)ins[i].size() != ndims[i]) {
+        ttk::set_error("einsum: operand %d has %d dims, equation %s", i, ndims[i], eq.c_str());
+        return false;
+      }
+      Operand op;
+      op.idx = ins[i];
+      op.slot = i;
+      std::memset(op.st, 0, sizeof(op.st));
+      for (int d = 0; d < ndims[i]; ++d) {  // a repeated index (diagonal) adds its strides
+        const unsigned char c = (unsigned char)ins[i][d];
+        ext[c] = shapes[o + d];
+        op.st[c] += strides[o + d];
+      }
+      std::string uniq;
+      for (char c : op.idx)
+        if (!contains(uniq, c)) uniq.push_back(c);
+      op.idx = uniq;
+      o += ndims[i];
+      live.push_back(op);
+    }
+  }
+  int64_t out_st[128];
+  std::memset(out_st, 0, sizeof(out_st));
+  if (out_strides && out_nd == (int)out.size()) {
+    for (int d = 0; d < out_nd; ++d) out_st[(unsigned char)out[d]] = out_strides[d];
+  } else {
+    int64_t acc = 1;
+    for (int d = (int)out.size() - 1; d >= 0; --d) {
+      out_st[(unsigned char)out[d]] = acc;
+      acc *= ext[(unsigned char)out[d]];
+    }
+  }
+  // greedy path over index sets (ordered strings used as sets)
+  std::vector<std::pair<int, int>> path;
+  {
+    std::vector<std::string> sets;
+    for (const Operand &o : live) sets.push_back(o.idx);
+    if (sets.size() == 1) path.push_back({0, -1});
+    while (sets.size() > 1) {
+      bool have = false;
+      int64_t bf = 0, bs = 0;
+      int bi = 0, bj = 0;
+      std::string bres;
+      for (size_t i = 0; i < sets.size(); ++i)
+        for (size_t j = i + 1; j < sets.size(); ++j) {
+          std::string un = sets[i];
+          for (char c : sets[j])
+            if (!contains(un, c)) un.push_back(c);
+          std::string res;
+          for (char c : un) {
+            bool keep = contains(out, c);
+            for (size_t k = 0; k < sets.size() && !keep; ++k)
+              if (k != i && k != j && contains(sets[k], c)) keep = true;
+            if (keep) res.push_back(c);
+          }
+          const int64_t fl = extent_of(ext, un), sz = extent_of(ext, res);
+          if (!have || fl < bf || (fl == bf && (sz < bs || (sz == bs && ((int)i < bi || ((int)i == bi && (int)j < bj)))))) {
+            have = true;
+            bf = fl;
+            bs = sz;
+            bi = (int)i;
+            bj = (int)j;
+            bres = res;
+          }
+        }
+      path.push_back({bi, bj});
+      std::vector<std::string> nxt;
+      for (size_t k = 0; k < sets.size(); ++k)
+        if ((int)k != bi && (int)k != bj) nxt.push_back(sets[k]);
+      nxt.push_back(bres);
+      sets.swap(nxt);
+    }
+  }
+  std::vector<int64_t> tabs;
+  int ntmp = 0;
+  int64_t scratch = 0;
+  for (size_t si = 0; si < path.size(); ++si) {
+    const bool last = si + 1 == path.size();
+    Operand X, Y;
+    bool ones = false;
+    if (path[si].second < 0) {
+      X = live[path[si].first];
+      live.erase(live.begin() + path[si].first);
+      ones = true;
+      Y.idx.clear();
+      std::memset(Y.st, 0, sizeof(Y.st));
+      Y.slot = SLOT_ONES;
+    } else {
+      const int i = path[si].first, j = path[si].second;  // i < j
+      X = live[i];
+      Y = live[j];
+      live.erase(live.begin() + j);
+      live.erase(live.begin() + i);
+    }
+    std::string rest = out;
+    for (const Operand &o : live)
+      for (char c : o.idx)
+        if (!contains(rest, c)) rest.push_back(c);
+    std::string allidx;
+    for (char c : X.idx + Y.idx)
+      if (!contains(allidx, c)) allidx.push_back(c);
+    std::string order;
+    if (last) {
+      order = out;
+    } else {
+      for (char c : allidx)
+        if (contains(rest, c)) order.push_back(c);
+    }
+    std::string batch, mg, ng, kg;
+    for (char c : order) {
+      const bool inx = contains(X.idx, c), iny = contains(Y.idx, c);
+      if (inx && iny)
+        batch.push_back(c);
+      else if (inx)
+        mg.push_back(c);
+      else if (iny)
+        ng.push_back(c);
+    }
+    for (char c : allidx)
+      if (!contains(rest, c)) kg.push_back(c);
+    Operand R;
+    std::memset(R.st, 0, sizeof(R.st));
+    if (last) {
+      R.idx = out;
+      std::memcpy(R.st, out_st, sizeof(out_st));
+    } else {
+      R.idx = batch + mg + ng;
+      int64_t acc = 1;
+      for (int d = (int)R.idx.size() - 1; d >= 0; --d) {
+        R.st[(unsigned char)R.idx[d]] = acc;
+        acc *= ext[(unsigned char)R.idx[d]];
+      }
+    }
+    Step st;
+    st.a = X.slot;
+    st.b = ones ? SLOT_ONES : Y.slot;
+    st.offs = (int64_t)tabs.size();
+    group_offsets(batch, ext, X.st, tabs);
+    group_offsets(mg, ext, X.st, tabs);
+    group_offsets(kg, ext, X.st, tabs);
+    group_offsets(batch, ext, Y.st, tabs);
+    group_offsets(kg, ext, Y.st, tabs);
+    group_offsets(ng, ext, Y.st, tabs);
+    group_offsets(batch, ext, R.st, tabs);
+    group_offsets(mg, ext, R.st, tabs);
+    group_offsets(ng, ext, R.st, tabs);
+    st.nb = (int)extent_of(ext, batch);
+    st.M = (int)extent_of(ext, mg);
+    st.K = (int)extent_of(ext, kg);
+    st.N = (int)extent_of(ext, ng);
+    if (last) {
+      st.out = SLOT_FINAL;
+      st.tmp = 0;
+    } else {
+      st.out = -(ntmp + 1);
+      ++ntmp;
+      st.tmp = scratch;
+      scratch += (extent_of(ext, R.idx) + 31) / 32 * 32;
+      R.slot = st.out;
+      live.push_back(R);
+    }
+    pl.steps.push_back(st);
+  }
+  pl.scratch = scratch;
+  pl.dtab = static_cast<int64_t *>(g_eng.arena.take(tabs.size() * sizeof(int64_t)));
+  if (!pl.dtab) {
+    ttk::set_error("einsum: table allocation failed");
+    return false;
+  }
+  if (hipMemcpy(pl.dtab, tabs.data(), tabs.size() * sizeof(int64_t), hipMemcpyHostToDevice) != hipSuccess) {
+    ttk::set_error("einsum: table upload failed");
+    return false;
+  }
+  return true;
+}
+
+}  // namespace
+
+extern "C" {
+
+// desc: [nops, then per operand: ptr, ndim, shape..., stride..., then has_out_strides, (out ndim,
+// out strides...)]
+int ttk_einsum(void *stream, const char *eq, const int64_t *desc, double *out, double alpha, double beta) {
+  const int nops = (int)desc[0];
+  if (nops < 1 || nops > 8) {
+    ttk::set_error("ttk_einsum: %d operands", nops);
+    return TTK_ERR_ARG;
+  }
+  const double *ptrs[8];
+  int ndims[8];
+  int64_t shapes[8 * 16], strides[8 * 16];
+  int64_t pos = 1, so = 0;
+  std::string key(eq);
+  key.push_back('|');
+  for (int i = 0; i < nops; ++i) {
+    ptrs[i] = reinterpret_cast<const double *>(desc[pos]);
+    const int nd = (int)desc[pos + 1];
+    if (nd > 16) {
+      ttk::set_error("ttk_einsum: operand rank %d", nd);
+      return TTK_ERR_ARG;
+    }
+    ndims[i] = nd;
+    std::memcpy(shapes + so, desc + pos + 2, nd * sizeof(int64_t));
+    std::memcpy(strides + so, desc + pos + 2 + nd, nd * sizeof(int64_t));
+    key.append(reinterpret_cast<const char *>(desc + pos + 1), (1 + 2 * nd) * sizeof(int64_t));
+    so += nd;
+    pos += 2 + 2 * nd;
+  }
+  const int has_out = (int)desc[pos];
+  int out_nd = 0;
+  const int64_t *out_st = nullptr;
+  if (has_out) {
+    out_nd = (int)desc[pos + 1];
+    out_st = desc + pos + 2;
+    key.append(reinterpret_cast<const char *>(desc + pos), (2 + out_nd) * sizeof(int64_t));
+  } else {
+    key.push_back('c');
+  }
+  auto it = g_eng.plans.find(key);
+  if (it == g_eng.plans.end()) {
+    if (g_eng.plans.size() >= 200000) {  // bounded cache: drain the stream, then start over
+      if (hipStreamSynchronize(TTK_STREAM(stream)) != hipSuccess) return TTK_ERR_HIP;
+      g_eng.plans.clear();
+      g_eng.arena.reset();
+    }
+    Plan pl;
+    if (!build_plan(eq, nops, ndims, shapes, strides, out_nd, out_st, pl)) return TTK_ERR_ARG;
+    it = g_eng.plans.emplace(std::move(key), std::move(pl)).first;
+    ++g_eng.misses;
+  } else {
+    ++g_eng.hits;
+  }
+  const Plan &pl = it->second;
+  if (pl.scratch > g_eng.scratch_n) {
+    // growing the shared scratch: earlier calls may still be using the old buffer on the stream
+    if (g_eng.scratch) {
+      TTK_HIP(hipStreamSynchronize(TTK_STREAM(stream)));
+      TTK_HIP(hipFree(g_eng.scratch));
+    }
+    int64_t want = pl.scratch * 2 > (1 << 20) ? pl.scratch * 2 : (1 << 20);
+    TTK_HIP(hipMalloc(reinterpret_cast<void **>(&g_eng.scratch), want * sizeof(double)));
+    g_eng.scratch_n = want;
+  }
+  if (!g_eng.ones) {
+    TTK_HIP(hipMalloc(reinterpret_cast<void **>(&g_eng.ones), 64 * sizeof(double)));
+    const double one[1] = {1.0};
+    TTK_HIP(hipMemcpy(g_eng.ones, one, sizeof(double), hipMemcpyHostToDevice));
+  }
+  for (const Step &st : pl.steps) {
+    const double *A = st.a >= 0 ? ptrs[st.a] : g_eng.scratch + pl.steps[-st.a - 1].tmp;
+    const double *B = st.b == SLOT_ONES ? g_eng.ones : (st.b >= 0 ? ptrs[st.b] : g_eng.scratch + pl.steps[-st.b - 1].tmp);
+    double *C;
+    double al = 1.0, be = 0.0;
+    if (st.out == SLOT_FINAL) {
+      C = out;
+      al = alpha;
+      be = beta;
+    } else {
+      C = g_eng.scratch + st.tmp;
+    }
+    int rc = ttk_gemm_offs(stream, A, B, C, pl.dtab + st.offs, st.nb, st.M, st.N, st.K, al, be);
+    if (rc != TTK_OK) return rc;
+  }
+  return TTK_OK;
+}
+
+int ttk_einsum_stats(long long *out) {
+  out[0] = g_eng.hits;
+  out[1] = g_eng.misses;
+  out[2] = (long long)g_eng.plans.size();
+  return TTK_OK;
+}
+
+}  // extern "C"

@@ -134,85 +134,6 @@ __device__ void svd_epilogue(double *W, double *V, double *sig, int *rank, int m
   }
 }
 
-__global__ __launch_bounds__(1024) void svd_kernel(const double *__restrict__ A, int m, int n,
-                                                   double *__restrict__ U, double *__restrict__ S,
-                                                   double *__restrict__ Vt, double *__restrict__ gwork,
-                                                   int use_lds, int g) {
-  extern __shared__ double lds[];
-  __shared__ int any_rot;
-  const bool tall = m >= n;
-  const int p = tall ? n : m;  // columns to orthogonalise
-  const int q = tall ? m : n;  // column length
-  double *base = use_lds ? lds : gwork;
-  double *W = base;
-  double *V = W + (int64_t)q * p;
-  double *sig = V + (int64_t)p * p;
-  int *rank = reinterpret_cast<int *>(sig + p);
-  const int tid = threadIdx.x, nt = blockDim.x;
-  const int lane = tid & 63, wid = tid >> 6, nw = nt >> 6;
-  for (int e = tid; e < q * p; e += nt) {
-    const int j = e / q, i = e - j * q;
-    W[e] = tall ? A[(int64_t)i * n + j] : A[(int64_t)j * n + i];
-  }
-  for (int e = tid; e < p * p; e += nt) V[e] = ((e / p) == (e % p)) ? 1.0 : 0.0;
-  __syncthreads();
-  const int P = (p % 2) ? p + 1 : p;
-  // g lanes per column pair (host picks g ~ q/4, bounded by the block); group reductions are DPP
-  const int gl = tid & (g - 1), gid = tid / g, ng = nt / g;
-  // rotate only when the columns are not orthogonal to working precision (LAPACK gesvj uses
-  // sqrt(m)*eps; q*eps is the safe side that still converges quadratically)
-  const double tol = EPS * (q > 16 ? (double)q : 16.0);
-  for (int sweep = 0; sweep < 40; ++sweep) {
-    if (tid == 0) any_rot = 0;
-    __syncthreads();
-    for (int r = 0; r < P - 1; ++r) {
-      for (int k = gid; k < P / 2; k += ng) {
-        int a, b;
-        rr_pair(P, r, k, a, b);
-        if (b >= p) continue;  // dummy partner (uniform within the group)
-        double *wa = W + (int64_t)a * q, *wb = W + (int64_t)b * q;
-        double al = 0.0, be = 0.0, ga = 0.0;
-        for (int i = gl; i < q; i += g) {
-          const double x = wa[i], y = wb[i];
-          al += x * x;
-          be += y * y;
-          ga += x * y;
-        }
-        al = ttk::group_sum_rt(al, g);
-        be = ttk::group_sum_rt(be, g);
-        ga = ttk::group_sum_rt(ga, g);
-        if (al < 1e-300 || be < 1e-300) continue;
-        if (fabs(ga) <= tol * sqrt(al) * sqrt(be)) continue;
-        const double zeta = (be - al) / (2.0 * ga);
-        double t;
-        if (fabs(zeta) > 1e150)
-          t = 0.5 / zeta;
-        else
-          t = (zeta >= 0.0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
-        const double c = 1.0 / sqrt(1.0 + t * t), s = c * t;
-        for (int i = gl; i < q; i += g) {
-          const double x = wa[i], y = wb[i];
-          wa[i] = c * x - s * y;
-          wb[i] = s * x + c * y;
-        }
-        double *va = V + (int64_t)a * p, *vb = V + (int64_t)b * p;
-        for (int i = gl; i < p; i += g) {
-          const double x = va[i], y = vb[i];
-          va[i] = c * x - s * y;
-          vb[i] = s * x + c * y;
-        }
-        if (gl == 0) any_rot = 1;
-      }
-      __syncthreads();
-    }
-    if (tid == 0) atomicAdd(&g_dbg[1], 1ull);
-    if (!any_rot) break;
-    __syncthreads();
-  }
-  if (tid == 0) atomicAdd(&g_dbg[0], 1ull);
-  svd_epilogue(W, V, sig, rank, m, n, tall, U, S, Vt);
-}
-
 // Multi-workgroup one-sided Jacobi for large unfoldings (the 1e-12 rank reductions at the end of
 // a solve produce ~1000 x 1000 swap/rounding unfoldings), run on X = R^T after a blocked QR
 // (svd_big below).  One wave per column pair, one launch per round-robin round (all P/2 pairs in
@@ -265,6 +186,299 @@ __global__ __launch_bounds__(1024) void svd_big_finish_kernel(double *W, double 
                                                               int n, double *__restrict__ U, double *__restrict__ S,
                                                               double *__restrict__ Vt) {
   svd_epilogue(W, V, sig, rank, m, n, m >= n, U, S, Vt);
+}
+
+// ------------------------------------------- one-workgroup SVD with QRCP preconditioning
+// For min(m,n) <= WG_P: W = A (tall) or A^T (wide), q x p column-major.  W P = Q R by column-
+// pivoted Householder QR inside the workgroup (pivot/reflector by wave 0, one wave per trailing
+// column with the dlaqp2 norm downdate), then one-sided Jacobi on X = R1^T (p x kk) with X and V
+// resident in LDS, then the left vectors Q [V_X; 0] (one wave per column through all
+// reflectors, no block barriers) and the right vectors P U_X.  QRCP grades the rows of R, which
+// cuts the Jacobi sweeps ~4x on the path's unfoldings and shrinks the column length from q to p.
+constexpr int WG_P = 96;
+
+__global__ __launch_bounds__(1024) void svd_wg_kernel(const double *__restrict__ A, int m, int n,
+                                                      double *__restrict__ U, double *__restrict__ S,
+                                                      double *__restrict__ Vt, double *__restrict__ gwork,
+                                                      int w_in_lds, int g, double defl2) {
+  extern __shared__ double lds[];
+  __shared__ int s_piv, s_stop, s_kk, any_rot;
+  __shared__ double red[16];
+  const bool tall = m >= n;
+  const int p = tall ? n : m, q = tall ? m : n;
+  const int tid = threadIdx.x, nt = blockDim.x;
+  const int lane = tid & 63, wid = tid >> 6, nw = nt >> 6;
+  // LDS: X (p*p) | V (p*p) | tau, vn1, vn2, sig (4p) | perm, rank (2p ints) | [W, M if w_in_lds]
+  double *X = lds, *V = X + p * p, *tau = V + p * p, *vn1 = tau + p, *vn2 = vn1 + p, *sig = vn2 + p;
+  int *perm = reinterpret_cast<int *>(sig + p), *rank = perm + p;
+  double *W = w_in_lds ? reinterpret_cast<double *>(rank + p + (p & 1)) : gwork;
+  double *M = W + (int64_t)q * p;
+  for (int e = tid; e < q * p; e += nt) {
+    const int j = e / q, i = e - j * q;
+    W[e] = tall ? A[(int64_t)i * n + j] : A[(int64_t)j * n + i];
+  }
+  __syncthreads();
+  for (int j = wid; j < p; j += nw) {
+    const double *w = W + (int64_t)j * q;
+    double acc = 0.0;
+    for (int i = lane; i < q; i += 64) acc += w[i] * w[i];
+    acc = sqrt(ttk::wave_sum(acc));
+    if (lane == 0) {
+      vn1[j] = acc;
+      vn2[j] = acc;
+      perm[j] = j;
+    }
+  }
+  if (tid == 0) s_kk = p;
+  __syncthreads();
+  // ---- QRCP
+  for (int c = 0; c < p; ++c) {
+    if (tid == 0) {
+      double bm = -1.0, sum = 0.0;
+      int bi = c;
+      for (int j = c; j < p; ++j) {
+        const double v = vn1[j];
+        sum += v * v;
+        if (v > bm) {
+          bm = v;
+          bi = j;
+        }
+      }
+      s_piv = bi;
+      s_stop = 0;  // no deflation on this path: every direction gets an orthonormal vector
+      (void)sum;
+      (void)defl2;
+    }
+    __syncthreads();
+    if (s_stop) break;
+    const int piv = s_piv;
+    if (piv != c) {
+      double *a = W + (int64_t)c * q, *b = W + (int64_t)piv * q;
+      for (int i = tid; i < q; i += nt) {
+        const double t = a[i];
+        a[i] = b[i];
+        b[i] = t;
+      }
+      if (tid == 0) {
+        double t = vn1[c];
+        vn1[c] = vn1[piv];
+        vn1[piv] = t;
+        t = vn2[c];
+        vn2[c] = vn2[piv];
+        vn2[piv] = t;
+        const int pi = perm[c];
+        perm[c] = perm[piv];
+        perm[piv] = pi;
+      }
+      __syncthreads();
+    }
+    double *x = W + (int64_t)c * q;
+    if (wid == 0) {  // reflector (dlarfg) by wave 0
+      double part = 0.0;
+      for (int i = c + 1 + lane; i < q; i += 64) part += x[i] * x[i];
+      const double sigma = ttk::wave_sum(part);
+      const double alpha = x[c];
+      double t = 0.0, beta = alpha;
+      if (sigma > 0.0) {
+        beta = -copysign(sqrt(alpha * alpha + sigma), alpha);
+        t = (beta - alpha) / beta;
+        const double sc = 1.0 / (alpha - beta);
+        for (int i = c + 1 + lane; i < q; i += 64) x[i] *= sc;
+      }
+      if (lane == 0) {
+        x[c] = beta;
+        tau[c] = t;
+      }
+    }
+    __syncthreads();
+    const double t = tau[c];
+    for (int j = c + 1 + wid; j < p; j += nw) {  // trailing update + norm downdate
+      double *y = W + (int64_t)j * q;
+      double yc = y[c];
+      if (t != 0.0) {
+        double acc = 0.0;
+        for (int i = c + 1 + lane; i < q; i += 64) acc += x[i] * y[i];
+        const double w = t * (ttk::wave_sum(acc) + yc);
+        for (int i = c + 1 + lane; i < q; i += 64) y[i] -= w * x[i];
+        yc -= w;
+        if (lane == 0) y[c] = yc;
+      }
+      const double a = vn1[j];
+      if (a != 0.0) {
+        double temp = fabs(yc) / a;
+        temp = fmax(1.0 - temp * temp, 0.0);
+        const double r = a / vn2[j];
+        if (temp * r * r <= 1.4901161193847656e-08) {
+          double acc = 0.0;
+          for (int i = c + 1 + lane; i < q; i += 64) acc += y[i] * y[i];
+          acc = sqrt(ttk::wave_sum(acc));
+          if (lane == 0) {
+            vn1[j] = acc;
+            vn2[j] = acc;
+          }
+        } else if (lane == 0) {
+          vn1[j] = a * sqrt(temp);
+        }
+      }
+    }
+    __syncthreads();
+  }
+  const int kk = s_kk < 1 ? 1 : s_kk;
+  // ---- X = R1^T (column length p, kk columns), V = I
+  for (int e = tid; e < kk * p; e += nt) {
+    const int i = e / p, j = e - i * p;
+    X[e] = (j >= i) ? W[(int64_t)j * q + i] : 0.0;
+  }
+  for (int e = tid; e < kk * kk; e += nt) V[e] = ((e / kk) == (e % kk)) ? 1.0 : 0.0;
+  __syncthreads();
+  // ---- one-sided Jacobi on X
+  const int P = (kk % 2) ? kk + 1 : kk;
+  const int gl = tid & (g - 1), gid = tid / g, ng = nt / g;
+  const double tol = EPS * (p > 16 ? (double)p : 16.0);
+  for (int sweep = 0; sweep < 60 && kk > 1; ++sweep) {
+    if (tid == 0) any_rot = 0;
+    __syncthreads();
+    for (int r = 0; r < P - 1; ++r) {
+      for (int k = gid; k < P / 2; k += ng) {
+        int a, b;
+        rr_pair(P, r, k, a, b);
+        if (b >= kk) continue;
+        double *wa = X + a * p, *wb = X + b * p;
+        double al = 0.0, be = 0.0, ga = 0.0;
+        for (int i = gl; i < p; i += g) {
+          const double xa = wa[i], xb = wb[i];
+          al += xa * xa;
+          be += xb * xb;
+          ga += xa * xb;
+        }
+        al = ttk::group_sum_rt(al, g);
+        be = ttk::group_sum_rt(be, g);
+        ga = ttk::group_sum_rt(ga, g);
+        if (al < 1e-300 || be < 1e-300) continue;
+        if (fabs(ga) <= tol * sqrt(al) * sqrt(be)) continue;
+        const double zeta = (be - al) / (2.0 * ga);
+        double tt;
+        if (fabs(zeta) > 1e150)
+          tt = 0.5 / zeta;
+        else
+          tt = (zeta >= 0.0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
+        const double cs = 1.0 / sqrt(1.0 + tt * tt), sn = cs * tt;
+        for (int i = gl; i < p; i += g) {
+          const double xa = wa[i], xb = wb[i];
+          wa[i] = cs * xa - sn * xb;
+          wb[i] = sn * xa + cs * xb;
+        }
+        double *va = V + a * kk, *vb = V + b * kk;
+        for (int i = gl; i < kk; i += g) {
+          const double xa = va[i], xb = vb[i];
+          va[i] = cs * xa - sn * xb;
+          vb[i] = sn * xa + cs * xb;
+        }
+        if (gl == 0) any_rot = 1;
+      }
+      __syncthreads();
+    }
+    if (!any_rot) break;
+    __syncthreads();
+  }
+  // ---- singular values, order, unit U_X columns
+  for (int j = wid; j < kk; j += nw) {
+    const double *xj = X + j * p;
+    double s2 = 0.0;
+    for (int i = lane; i < p; i += 64) s2 += xj[i] * xj[i];
+    s2 = ttk::wave_sum(s2);
+    if (lane == 0) sig[j] = sqrt(s2);
+  }
+  __syncthreads();
+  for (int j = tid; j < kk; j += nt) {
+    int rk = 0;
+    const double sj = sig[j];
+    for (int i = 0; i < kk; ++i) rk += (sig[i] > sj) || (sig[i] == sj && i < j);
+    rank[j] = rk;
+  }
+  __syncthreads();
+  for (int j = wid; j < kk; j += nw) {
+    double *xj = X + j * p;
+    const double sj = sig[j];
+    const double inv = sj > 0.0 ? 1.0 / sj : 0.0;
+    for (int i = lane; i < p; i += 64) xj[i] *= inv;
+  }
+  for (int r = tid; r < p; r += nt) S[r] = 0.0;
+  __syncthreads();
+  // exact-zero columns: complete U_X to an orthonormal set (rare; MGS against e_i candidates)
+  for (int j = 0; j < kk; ++j) {
+    if (sig[j] > 0.0) continue;
+    double *xj = X + j * p;
+    for (int cand = 0; cand < p; ++cand) {
+      for (int i = tid; i < p; i += nt) xj[i] = (i == cand) ? 1.0 : 0.0;
+      __syncthreads();
+      for (int o = 0; o < kk; ++o) {
+        if (o == j || (sig[o] == 0.0 && o > j)) continue;
+        const double *xo = X + o * p;
+        double d = 0.0;
+        for (int i = tid; i < p; i += nt) d += xo[i] * xj[i];
+        d = ttk::block_sum(d, red);
+        for (int i = tid; i < p; i += nt) xj[i] -= d * xo[i];
+        __syncthreads();
+      }
+      double nn = 0.0;
+      for (int i = tid; i < p; i += nt) nn += xj[i] * xj[i];
+      nn = ttk::block_sum(nn, red);
+      if (nn > 0.25) {
+        const double inv = 1.0 / sqrt(nn);
+        for (int i = tid; i < p; i += nt) xj[i] *= inv;
+        __syncthreads();
+        break;
+      }
+      __syncthreads();
+    }
+  }
+  __syncthreads();
+  for (int j = tid; j < kk; j += nt) S[rank[j]] = sig[j];
+  // ---- left factor of W: M(:, rank[j]) = Q [V_X(:, j); 0], one wave per column
+  for (int j = wid; j < kk; j += nw) {
+    double *mc = M + (int64_t)rank[j] * q;
+    const double *vj = V + j * kk;
+    for (int i = lane; i < q; i += 64) mc[i] = i < kk ? vj[i] : 0.0;
+    __threadfence_block();
+    for (int c = kk - 1; c >= 0; --c) {
+      const double t = tau[c];
+      if (t == 0.0) continue;
+      const double *v = W + (int64_t)c * q;
+      double acc = 0.0;
+      for (int i = c + 1 + lane; i < q; i += 64) acc += v[i] * mc[i];
+      const double w = t * (ttk::wave_sum(acc) + mc[c]);
+      for (int i = c + 1 + lane; i < q; i += 64) mc[i] -= w * v[i];
+      __threadfence_block();
+      if (lane == 0) mc[c] -= w;
+      __threadfence_block();
+    }
+  }
+  __syncthreads();
+  // ---- outputs: left factor Lw = M (q x kk), right factor Rw(perm[i], rank[j]) = U_X(i, j)
+  for (int e = tid; e < q * p; e += nt) {
+    const int i = e / p, r = e - i * p;
+    const double v = r < kk ? M[(int64_t)r * q + i] : 0.0;
+    if (tall)
+      U[(int64_t)i * p + r] = v;
+    else
+      Vt[(int64_t)r * q + i] = v;
+  }
+  for (int e = tid; e < p * p; e += nt) {
+    const int i = e / p, r = e - i * p;  // pivoted row i of R, output rank position r
+    double v = 0.0;
+    if (r < kk) {
+      int j = 0;
+      for (; j < kk; ++j)
+        if (rank[j] == r) break;
+      v = X[j * p + i];
+    }
+    const int oi = perm[i];
+    if (tall)
+      Vt[(int64_t)r * p + oi] = v;
+    else
+      U[(int64_t)oi * p + r] = v;
+  }
 }
 
 // ------------------------------------------------------------------------------ QR
@@ -1609,7 +1823,7 @@ int ttk_svd_set_big_threshold(int p) {
 
 int64_t ttk_svd_work(int m, int n) {
   const int64_t p = m < n ? m : n, q = m < n ? n : m;
-  const int64_t small = q * p + p * p + 2 * p + 16, big = svd_big_work(m, n);
+  const int64_t small = 2 * q * p + 16, big = svd_big_work(m, n);
   return small > big ? small : big;
 }
 
@@ -1623,18 +1837,24 @@ int ttk_svd_tol(void *stream, const double *A, int m, int n, double *U, double *
     ttk::set_error("ttk_svd: empty matrix %dx%d", m, n);
     return TTK_ERR_ARG;
   }
-  const int p = m < n ? m : n, q = m < n ? n : m, pairs = (p + 1) / 2;
-  const int64_t need = (int64_t)q * p + (int64_t)p * p + 2 * p + 16;
-  const int use_lds = need <= LDS_DOUBLES;
-  if (p >= g_svd_big_p && (!use_lds || g_svd_big_p <= 2)) return svd_big(stream, A, m, n, U, S, Vt, work, defl);
-  const size_t shm = use_lds ? need * sizeof(double) : 0;
-  allow_big_lds(svd_kernel, shm);
+  const int p = m < n ? m : n, q = m < n ? n : m;
+  const bool forced_big = g_svd_big_p <= 2;
+  if (p > WG_P || forced_big) return svd_big(stream, A, m, n, U, S, Vt, work, defl);
+  const int64_t fixed = 2 * (int64_t)p * p + 5 * (int64_t)p + 2;  // X, V, 4 vectors, 2 int vectors
+  const int64_t wm = 2 * (int64_t)q * p;                            // W and M
+  const int w_in_lds = fixed + wm <= LDS_DOUBLES;
+  const size_t shm = (size_t)(fixed + (w_in_lds ? wm : 0)) * sizeof(double);
+  allow_big_lds(svd_wg_kernel, shm);
+  const int pairs = (p + 1) / 2;
   int g = 1;
-  while (g < 64 && g * 4 < q) g *= 2;           // ~4 elements per lane
-  while (g > 1 && pairs * g > 1024) g /= 2;     // all pairs of a round in flight
-  int nt = pairs * g;
+  while (g < 64 && g * 4 < p) g *= 2;        // ~4 elements of an X column per lane
+  while (g > 1 && pairs * g > 1024) g /= 2;  // all pairs of a round in flight
+  int nt = pairs * g;  // the QRCP strides its trailing columns over however many waves this gives
+  if (q * p > 4096 && nt < 256) nt = 256;  // long columns: more waves for the QR phase
   nt = nt < 64 ? 64 : (nt > 1024 ? 1024 : (nt + 63) / 64 * 64);
-  hipLaunchKernelGGL(svd_kernel, dim3(1), dim3(nt), shm, TTK_STREAM(stream), A, m, n, U, S, Vt, work, use_lds, g);
+  const double defl2 = defl > 0.0 ? defl * defl : 0.0;
+  hipLaunchKernelGGL(svd_wg_kernel, dim3(1), dim3(nt), shm, TTK_STREAM(stream), A, m, n, U, S, Vt, work, w_in_lds, g,
+                     defl2);
   TTK_LAUNCH_CHECK();
   return TTK_OK;
 }

@@ -25,8 +25,15 @@ F64 = torch.float64
 _vp = ctypes.c_void_p
 
 
+_STREAM = []
+
+
 def _stream():
-    return torch.cuda.current_stream().cuda_stream if DEV.type == "cuda" else None
+    """The launch stream (the device's current stream when first used; the path never switches
+    streams, and torch.cuda.current_stream() costs ~10 us per call)."""
+    if not _STREAM:
+        _STREAM.append(torch.cuda.current_stream().cuda_stream if DEV.type == "cuda" else None)
+    return _STREAM[0]
 
 
 def _p(t):
@@ -180,158 +187,42 @@ def _parse(eq):
     return lhs.split(","), out
 
 
-def _group_offsets(group, ext, strides):
-    """Mixed-radix (row-major) enumeration of index group -> summed offsets (int64 array)."""
-    off = np.zeros(1, dtype=np.int64)
-    for c in group:
-        e = ext[c]
-        s = strides.get(c, 0)
-        off = (off[:, None] + np.arange(e, dtype=np.int64)[None, :] * s).reshape(-1)
-    return off
+@lru_cache(maxsize=None)
+def _eq_bytes(eq):
+    return eq.encode()
 
 
-def _greedy_path(ins, out, ext):
-    """Pairwise greedy order (min FLOPs of the pair, ties -> smaller result), opt_einsum-style.
-    Returns a list of position tuples in np.einsum_path's contraction-list convention."""
-    live = [set(i) for i in ins]
-    path = []
-    if len(live) == 1:
-        return [(0,)]
-    while len(live) > 1:
-        best = None
-        for i in range(len(live)):
-            for j in range(i + 1, len(live)):
-                keep = set(out)
-                for k, o in enumerate(live):
-                    if k != i and k != j:
-                        keep |= o
-                un = live[i] | live[j]
-                res = un & keep
-                flops = int(np.prod([ext[c] for c in un])) if un else 1
-                size = int(np.prod([ext[c] for c in res])) if res else 1
-                key = (flops, size, i, j)
-                if best is None or key < best[0]:
-                    best = (key, i, j, res)
-        _, i, j, res = best
-        path.append((i, j))
-        live = [o for k, o in enumerate(live) if k not in (i, j)] + [res]
-    return path
-
-
-class _Step:
-    __slots__ = ("a", "b", "out", "nb", "M", "N", "K", "offs", "tmp_shape")
-
-
-class _Plan:
-    __slots__ = ("steps", "out_shape", "tmp")
-
-
-def _contig_strides(idx, ext):
-    st = {}
-    acc = 1
-    for c in reversed(idx):
-        st[c] = acc
-        acc *= ext[c]
-    return st
-
-
-@lru_cache(maxsize=8192)
-def _plan(eq, shapes, strides, out_strides):
+@lru_cache(maxsize=65536)
+def _out_shape(eq, shapes):
     ins, out = _parse(eq)
     ext = {}
     for idx, shp in zip(ins, shapes):
         for c, e in zip(idx, shp):
             ext[c] = e
-    out_shape = tuple(ext[c] for c in out)
-    if out_strides is None:
-        out_strides = tuple(_contig_strides(out, ext)[c] for c in out) if out else ()
-    path = _greedy_path(ins, out, ext)
-    # live operands: (idx, strides-dict, slot) ; slot >= 0 input index, < 0 intermediate -(k+1)
-    live = [(idx, dict(zip(idx, st)), i) for i, (idx, st) in enumerate(zip(ins, strides))]
-    steps = []
-    ntmp = 0
-    for si, pair in enumerate(path):
-        last = si == len(path) - 1
-        pair = tuple(sorted(pair, reverse=True))
-        taken = [live.pop(p) for p in pair]
-        taken.reverse()
-        if len(taken) == 1:
-            X, Y = taken[0], ("", {}, "ones")
-        else:
-            X, Y = taken
-        rest = set(out)
-        for o in live:
-            rest |= set(o[0])
-        xs, ys = set(X[0]), set(Y[0])
-        allidx = []
-        for c in X[0] + Y[0]:
-            if c not in allidx:
-                allidx.append(c)
-        if last:
-            order = list(out)
-        else:
-            order = [c for c in allidx if c in rest]
-        batch = [c for c in order if c in xs and c in ys]
-        mgrp = [c for c in order if c in xs and c not in ys]
-        ngrp = [c for c in order if c in ys and c not in xs]
-        kgrp = [c for c in allidx if c not in rest]
-        if last:
-            cst = dict(zip(out, out_strides))
-            res_idx = out
-        else:
-            res_idx = "".join(batch + mgrp + ngrp)
-            cst = _contig_strides(res_idx, ext)
-        tabs = [_group_offsets(batch, ext, X[1]), _group_offsets(mgrp, ext, X[1]), _group_offsets(kgrp, ext, X[1]),
-                _group_offsets(batch, ext, Y[1]), _group_offsets(kgrp, ext, Y[1]), _group_offsets(ngrp, ext, Y[1]),
-                _group_offsets(batch, ext, cst), _group_offsets(mgrp, ext, cst), _group_offsets(ngrp, ext, cst)]
-        st = _Step()
-        st.a, st.b = X[2], Y[2]
-        st.nb, st.M, st.K, st.N = len(tabs[0]), len(tabs[1]), len(tabs[2]), len(tabs[5])
-        st.offs = torch.from_numpy(np.concatenate(tabs)).to(DEV)
-        if last:
-            st.out = "final"
-            st.tmp_shape = None
-        else:
-            st.out = -(ntmp + 1)
-            st.tmp_shape = tuple(ext[c] for c in res_idx)
-            ntmp += 1
-            live.append((res_idx, cst, st.out))
-        steps.append(st)
-    pl = _Plan()
-    pl.steps = steps
-    pl.out_shape = out_shape
-    pl.tmp = [empty(*s.tmp_shape) if s.tmp_shape is not None else None for s in steps]
-    return pl
+    return tuple(ext[c] for c in out)
 
 
 def einsum(eq, *ops, out=None, alpha=1.0, beta=0.0):
-    """out = alpha * einsum(eq, *ops) + beta * out, on the device (fp64 MFMA GEMM steps)."""
-    shapes = tuple(tuple(o.shape) for o in ops)
-    strides = tuple(tuple(o.stride()) for o in ops)
-    pl = _plan(eq, shapes, strides, None if out is None else tuple(out.stride()))
+    """out = alpha * einsum(eq, *ops) + beta * out, on the device.  Planning (greedy pairwise
+    order, offset tables) and execution (one fp64 MFMA GEMM launch per pairwise step) happen in
+    the native engine `ttk_einsum` (csrc/ttk_einsum.hip); this wrapper only packs pointers,
+    shapes and strides."""
+    desc = [len(ops)]
+    for o in ops:
+        desc.append(o.data_ptr())
+        desc.append(o.dim())
+        desc.extend(o.shape)
+        desc.extend(o.stride())
     if out is None:
-        out = empty(*pl.out_shape)
+        out = empty(*_out_shape(eq, tuple(tuple(o.shape) for o in ops)))
         beta = 0.0
-    s = _stream()
-    tmp_by_slot = {}
-    ones = None
-    for st, tmp in zip(pl.steps, pl.tmp):
-        A = ops[st.a] if st.a >= 0 else tmp_by_slot[st.a]
-        if st.b == "ones":
-            if ones is None:
-                ones = _ones_buf()
-            B = ones
-        elif st.b >= 0:
-            B = ops[st.b]
-        else:
-            B = tmp_by_slot[st.b]
-        if st.out == "final":
-            C, al, be = out, alpha, beta
-        else:
-            C, al, be = tmp, 1.0, 0.0
-            tmp_by_slot[st.out] = tmp
-        check(lib.ttk_gemm_offs(s, _p(A), _p(B), _p(C), _p(st.offs), st.nb, st.M, st.N, st.K, float(al), float(be)),
-              "gemm")
+        desc.append(0)
+    else:
+        desc.append(1)
+        desc.append(out.dim())
+        desc.extend(out.stride())
+    check(lib.ttk_einsum(_stream(), _eq_bytes(eq), (ctypes.c_int64 * len(desc))(*desc), out.data_ptr(),
+                         float(alpha), float(beta)), "einsum")
     return out
 
 

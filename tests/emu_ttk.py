@@ -54,6 +54,45 @@ class EmuLib:
         return self.launches
 
     # --- contractions
+    @staticmethod
+    def _strided(ptr, shape, strides):
+        n = 1 + sum((e - 1) * st for e, st in zip(shape, strides) if e > 0)
+        base = _dv(ptr, max(n, 1))
+        return np.lib.stride_tricks.as_strided(base, shape=tuple(shape), strides=tuple(8 * st for st in strides))
+
+    def ttk_einsum(self, s, eq, desc, out, alpha, beta):
+        self.launches += 1
+        eq = eq.decode() if isinstance(eq, bytes) else eq
+        d = [int(v) for v in desc[:4096]]
+        nops, pos, views, shapes = d[0], 1, [], []
+        for _ in range(nops):
+            ptr, nd = d[pos], d[pos + 1]
+            shp, st = d[pos + 2:pos + 2 + nd], d[pos + 2 + nd:pos + 2 + 2 * nd]
+            views.append(self._strided(ptr, shp, st))
+            shapes.append(shp)
+            pos += 2 + 2 * nd
+        lhs, rhs = eq.replace(" ", "").split("->")
+        ext = {}
+        for idx, shp in zip(lhs.split(","), shapes):
+            ext.update(zip(idx, shp))
+        oshape = [ext[c] for c in rhs]
+        if d[pos]:
+            ost = d[pos + 2:pos + 2 + d[pos + 1]]
+        else:
+            ost, acc = [], 1
+            for e in reversed(oshape):
+                ost.insert(0, acc)
+                acc *= e
+        ov = self._strided(out, oshape, ost)
+        res = alpha * np.einsum(eq, *views)
+        if beta != 0.0:
+            res = res + beta * ov
+        ov[...] = res
+        return 0
+
+    def ttk_einsum_stats(self, out):
+        return 0
+
     def ttk_gemm_offs(self, s, A, B, C, offs, nb, M, N, K, alpha, beta):
         self.launches += 1
         o = _iv(offs, 3 * nb + 2 * M + 2 * N + 2 * K)

@@ -49,6 +49,17 @@ if _D.OPSTATS is not None:
         ops += f"OP {name}: {cnt} calls {tot:.3f}s\n"
         for shp, (c, t) in sorted(d.items(), key=lambda kv: -kv[1][1])[:25]:
             ops += f"   {str(shp):14s} {c:6d} {t * 1e3:9.2f}ms {t / c * 1e6:9.1f}us\n"
+if _D.OPSTATS is not None and "svd" in _D.OPSTATS:
+    bk = {}
+    for (m, n), (c, t) in _D.OPSTATS["svd"].items():
+        p_, q_ = min(m, n), max(m, n)
+        key = next(f"p<={b}" for b in (4, 8, 16, 24, 32, 48, 64, 96, 128, 256, 10 ** 9) if p_ <= b)
+        e = bk.setdefault(key, [0, 0.0, 0])
+        e[0] += c
+        e[1] += t
+        e[2] = max(e[2], q_)
+    ops += "SVD buckets (p=min dim): " + " | ".join(f"{k}: {v[0]} calls {v[1] * 1e3:.1f} ms (max q {v[2]})"
+                                                   for k, v in bk.items()) + "\n"
 out = f"wall {wall:.2f}s launches {lib.ttk_launch_count() - l0}\n" + ops + s.getvalue()
 os.makedirs("gpurun_out", exist_ok=True)
 open(f"gpurun_out/prof_{cfg_name}_s{seed}.txt", "w").write(out)
