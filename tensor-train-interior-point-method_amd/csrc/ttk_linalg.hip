@@ -22,25 +22,62 @@
 namespace {
 
 constexpr double EPS = 2.220446049250313e-16;
-// diagnostic counters: [0] svd calls, [1] svd sweeps, [2] eig calls, [3] multisection rounds
+// diagnostic counters: [0] svd calls, [1] svd sweeps, [2] eig calls, [3] multisection rounds,
+// [4..7] one-workgroup SVD phase ticks (QRCP, Jacobi, vectors, output; 100 MHz)
 __device__ unsigned long long g_dbg[8];
 
 constexpr int LDS_DOUBLES = 20000;  // 160000 B of dynamic LDS (gfx950: 160 KiB per workgroup)
 
-// round-robin (circle method) pair k of round r over P (even) items
+// round-robin (circle method) pair k of round r over P (even) items; 0 <= r < P-1, 0 <= k < P/2,
+// so both residues need one conditional subtraction (a runtime-divisor `%` costs ~280 cycles)
 __device__ __forceinline__ void rr_pair(int P, int r, int k, int &p, int &q) {
+  const int P1 = P - 1;
   if (k == 0) {
     p = r;
-    q = P - 1;
+    q = P1;
   } else {
-    p = (r + k) % (P - 1);
-    q = (r - k + P - 1) % (P - 1);
+    p = r + k;
+    if (p >= P1) p -= P1;
+    q = r - k + P1;
+    if (q >= P1) q -= P1;
   }
   if (p > q) {
     int t = p;
     p = q;
     q = t;
   }
+}
+
+// 1/x and 1/sqrt(x) from the hardware estimates plus Newton steps (~1 ulp).  Rotation parameters
+// only need c^2 + s^2 = 1 to a few ulps; the IEEE div/sqrt expansions cost ~280 cycles each.
+__device__ __forceinline__ double fast_rcp(double x) {
+  double r = __builtin_amdgcn_rcp(x);
+  r = fma(fma(-x, r, 1.0), r, r);
+  r = fma(fma(-x, r, 1.0), r, r);
+  return r;
+}
+
+__device__ __forceinline__ double fast_rsqrt(double x) {
+  double r = __builtin_amdgcn_rsq(x);
+  double h = 0.5 * x * r;
+  double e = fma(-h, r, 0.5);
+  r = fma(r, e, r);
+  h = 0.5 * x * r;
+  e = fma(-h, r, 0.5);
+  return fma(r, e, r);
+}
+
+// Hestenes rotation zeroing the pair's inner product ga (column norms^2 al, be):
+// t = sign(d) 2 ga / (|d| + sqrt(d^2 + 4 ga^2)), d = be - al; c = 1/sqrt(1 + t^2), s = c t.
+// (Same t as Rutishauser's zeta form, without the zeta division and its overflow branch.)
+__device__ __forceinline__ void jacobi_rotation(double al, double be, double ga, double &c, double &s) {
+  const double d = be - al, g2 = 2.0 * ga;
+  const double hh = fma(d, d, g2 * g2);
+  const double h = hh * fast_rsqrt(hh);  // sqrt(d^2 + 4 ga^2) > 0 since ga != 0
+  double t = g2 * fast_rcp(fabs(d) + h);
+  if (d < 0.0) t = -t;
+  c = fast_rsqrt(fma(t, t, 1.0));
+  s = c * t;
 }
 
 // ------------------------------------------------------------------------------ SVD
@@ -160,14 +197,9 @@ __global__ __launch_bounds__(256) void svd_big_round_kernel(double *__restrict__
   be = ttk::wave_sum(be);
   ga = ttk::wave_sum(ga);
   if (al < 1e-300 || be < 1e-300) return;
-  if (fabs(ga) <= tol * sqrt(al) * sqrt(be)) return;
-  const double zeta = (be - al) / (2.0 * ga);
-  double t;
-  if (fabs(zeta) > 1e150)
-    t = 0.5 / zeta;
-  else
-    t = (zeta >= 0.0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
-  const double c = 1.0 / sqrt(1.0 + t * t), s = c * t;
+  if (ga * ga <= tol * tol * al * be) return;
+  double c, s;
+  jacobi_rotation(al, be, ga, c, s);
   for (int i = lane; i < q; i += 64) {
     const double x = wa[i], y = wb[i];
     wa[i] = c * x - s * y;
@@ -197,236 +229,264 @@ __global__ __launch_bounds__(1024) void svd_big_finish_kernel(double *W, double 
 // cuts the Jacobi sweeps ~4x on the path's unfoldings and shrinks the column length from q to p.
 constexpr int WG_P = 96;
 
+
+// One round-robin round of one-sided Jacobi with G lanes per column pair; each lane keeps its
+// <= VPL elements of both columns in registers for the whole round (one LDS load batch, one
+// store batch), so a round costs ~two LDS latencies plus the rotation instead of one LDS round
+// trip per element.
+constexpr int VPL = 8;
+
+template <int G>
+__device__ __forceinline__ void jacobi_round(double *X, double *V, int p, int L, int P, int r, double tol2,
+                                             int *any_rot) {
+  const int tid = threadIdx.x, gl = tid & (G - 1), gid = tid / G, ng = blockDim.x / G;
+  for (int k = gid; k < P / 2; k += ng) {
+    int a, b;
+    rr_pair(P, r, k, a, b);
+    if (b >= p) continue;
+    double *wa = X + a * L, *wb = X + b * L;
+    double xa[VPL], xb[VPL];
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) {
+      const int i = gl + v * G;
+      xa[v] = i < L ? wa[i] : 0.0;
+      xb[v] = i < L ? wb[i] : 0.0;
+    }
+    double al = 0.0, be = 0.0, ga = 0.0;
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) {
+      al = fma(xa[v], xa[v], al);
+      be = fma(xb[v], xb[v], be);
+      ga = fma(xa[v], xb[v], ga);
+    }
+    if (G > 1) {
+      al = ttk::group_sum_rt(al, G);
+      be = ttk::group_sum_rt(be, G);
+      ga = ttk::group_sum_rt(ga, G);
+    }
+    if (al < 1e-300 || be < 1e-300) continue;
+    if (ga * ga <= tol2 * al * be) continue;  // |ga| <= tol sqrt(al be)
+    double cs, sn;
+    jacobi_rotation(al, be, ga, cs, sn);
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) {
+      const int i = gl + v * G;
+      if (i < L) {
+        wa[i] = cs * xa[v] - sn * xb[v];
+        wb[i] = sn * xa[v] + cs * xb[v];
+      }
+    }
+    double *va = V + a * p, *vb = V + b * p;
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) {
+      const int i = gl + v * G;
+      if (i < p) {
+        const double ya = va[i], yb = vb[i];
+        va[i] = cs * ya - sn * yb;
+        vb[i] = sn * ya + cs * yb;
+      }
+    }
+    if (gl == 0) *any_rot = 1;
+  }
+}
+
+template <int G>
 __global__ __launch_bounds__(1024) void svd_wg_kernel(const double *__restrict__ A, int m, int n,
                                                       double *__restrict__ U, double *__restrict__ S,
                                                       double *__restrict__ Vt, double *__restrict__ gwork,
-                                                      int w_in_lds, int g, double defl2) {
+                                                      int w_in_lds, int use_qr) {
   extern __shared__ double lds[];
-  __shared__ int s_piv, s_stop, s_kk, any_rot;
+  __shared__ int s_piv, any_rot;
   __shared__ double red[16];
   const bool tall = m >= n;
   const int p = tall ? n : m, q = tall ? m : n;
+  const int L = use_qr ? p : q;  // Jacobi column length
   const int tid = threadIdx.x, nt = blockDim.x;
   const int lane = tid & 63, wid = tid >> 6, nw = nt >> 6;
-  // LDS: X (p*p) | V (p*p) | tau, vn1, vn2, sig (4p) | perm, rank (2p ints) | [W, M if w_in_lds]
-  double *X = lds, *V = X + p * p, *tau = V + p * p, *vn1 = tau + p, *vn2 = vn1 + p, *sig = vn2 + p;
+  // LDS: X (L*p) | V (p*p) | tau, vn1, vn2, sig (4p) | perm, rank (2p ints) | [W, M if w_in_lds]
+  double *X = lds, *V = X + L * p, *tau = V + p * p, *vn1 = tau + p, *vn2 = vn1 + p, *sig = vn2 + p;
   int *perm = reinterpret_cast<int *>(sig + p), *rank = perm + p;
-  double *W = w_in_lds ? reinterpret_cast<double *>(rank + p + (p & 1)) : gwork;
+  double *W = use_qr ? (w_in_lds ? reinterpret_cast<double *>(rank + p + (p & 1)) : gwork) : X;
   double *M = W + (int64_t)q * p;
   for (int e = tid; e < q * p; e += nt) {
     const int j = e / q, i = e - j * q;
     W[e] = tall ? A[(int64_t)i * n + j] : A[(int64_t)j * n + i];
   }
   __syncthreads();
-  for (int j = wid; j < p; j += nw) {
-    const double *w = W + (int64_t)j * q;
-    double acc = 0.0;
-    for (int i = lane; i < q; i += 64) acc += w[i] * w[i];
-    acc = sqrt(ttk::wave_sum(acc));
-    if (lane == 0) {
-      vn1[j] = acc;
-      vn2[j] = acc;
-      perm[j] = j;
-    }
-  }
-  if (tid == 0) s_kk = p;
-  __syncthreads();
-  // ---- QRCP
-  for (int c = 0; c < p; ++c) {
-    if (tid == 0) {
-      double bm = -1.0, sum = 0.0;
-      int bi = c;
-      for (int j = c; j < p; ++j) {
-        const double v = vn1[j];
-        sum += v * v;
-        if (v > bm) {
-          bm = v;
-          bi = j;
-        }
+  if (use_qr) {
+    for (int j = wid; j < p; j += nw) {
+      const double *w = W + (int64_t)j * q;
+      double acc = 0.0;
+      for (int i = lane; i < q; i += 64) acc += w[i] * w[i];
+      acc = sqrt(ttk::wave_sum(acc));
+      if (lane == 0) {
+        vn1[j] = acc;
+        vn2[j] = acc;
+        perm[j] = j;
       }
-      s_piv = bi;
-      s_stop = 0;  // no deflation on this path: every direction gets an orthonormal vector
-      (void)sum;
-      (void)defl2;
     }
     __syncthreads();
-    if (s_stop) break;
-    const int piv = s_piv;
-    if (piv != c) {
-      double *a = W + (int64_t)c * q, *b = W + (int64_t)piv * q;
-      for (int i = tid; i < q; i += nt) {
-        const double t = a[i];
-        a[i] = b[i];
-        b[i] = t;
+    // ---- QRCP (all p steps: zero columns get tau = 0, so every direction keeps a unit vector)
+    for (int c = 0; c < p; ++c) {
+      if (wid == 0) {  // first max of the downdated norms (idamax) over <= 96 columns, wave 0
+        double bm = -1.0;
+        int bi = p;
+        for (int j = c + lane; j < p; j += 64) {
+          const double v = vn1[j];
+          if (v > bm) {
+            bm = v;
+            bi = j;
+          }
+        }
+        for (int off = 32; off > 0; off >>= 1) {
+          const double om = __shfl_xor(bm, off, 64);
+          const int oi = __shfl_xor(bi, off, 64);
+          if (om > bm || (om == bm && oi < bi)) {
+            bm = om;
+            bi = oi;
+          }
+        }
+        if (lane == 0) s_piv = bi < p ? bi : c;
       }
-      if (tid == 0) {
-        double t = vn1[c];
-        vn1[c] = vn1[piv];
-        vn1[piv] = t;
-        t = vn2[c];
-        vn2[c] = vn2[piv];
-        vn2[piv] = t;
-        const int pi = perm[c];
-        perm[c] = perm[piv];
-        perm[piv] = pi;
+      __syncthreads();
+      const int piv = s_piv;
+      if (piv != c) {
+        double *a = W + (int64_t)c * q, *b = W + (int64_t)piv * q;
+        for (int i = tid; i < q; i += nt) {
+          const double t = a[i];
+          a[i] = b[i];
+          b[i] = t;
+        }
+        if (tid == 0) {
+          double t = vn1[c];
+          vn1[c] = vn1[piv];
+          vn1[piv] = t;
+          t = vn2[c];
+          vn2[c] = vn2[piv];
+          vn2[piv] = t;
+          const int pi = perm[c];
+          perm[c] = perm[piv];
+          perm[piv] = pi;
+        }
+        __syncthreads();
+      }
+      double *x = W + (int64_t)c * q;
+      if (wid == 0) {  // reflector (dlarfg) by wave 0
+        double part = 0.0;
+        for (int i = c + 1 + lane; i < q; i += 64) part += x[i] * x[i];
+        const double sigma = ttk::wave_sum(part);
+        const double alpha = x[c];
+        double t = 0.0, beta = alpha;
+        if (sigma > 0.0) {
+          beta = -copysign(sqrt(alpha * alpha + sigma), alpha);
+          t = (beta - alpha) / beta;
+          const double sc = 1.0 / (alpha - beta);
+          for (int i = c + 1 + lane; i < q; i += 64) x[i] *= sc;
+        }
+        if (lane == 0) {
+          x[c] = beta;
+          tau[c] = t;
+        }
+      }
+      __syncthreads();
+      const double t = tau[c];
+      for (int j = c + 1 + wid; j < p; j += nw) {  // trailing update + dlaqp2 norm downdate
+        double *y = W + (int64_t)j * q;
+        double yc = y[c];
+        if (t != 0.0) {
+          double acc = 0.0;
+          for (int i = c + 1 + lane; i < q; i += 64) acc += x[i] * y[i];
+          const double w = t * (ttk::wave_sum(acc) + yc);
+          for (int i = c + 1 + lane; i < q; i += 64) y[i] -= w * x[i];
+          yc -= w;
+          if (lane == 0) y[c] = yc;
+        }
+        const double a = vn1[j];
+        if (a != 0.0) {
+          double temp = fabs(yc) / a;
+          temp = fmax(1.0 - temp * temp, 0.0);
+          const double r = a / vn2[j];
+          if (temp * r * r <= 1.4901161193847656e-08) {
+            double acc = 0.0;
+            for (int i = c + 1 + lane; i < q; i += 64) acc += y[i] * y[i];
+            acc = sqrt(ttk::wave_sum(acc));
+            if (lane == 0) {
+              vn1[j] = acc;
+              vn2[j] = acc;
+            }
+          } else if (lane == 0) {
+            vn1[j] = a * sqrt(temp);
+          }
+        }
       }
       __syncthreads();
     }
-    double *x = W + (int64_t)c * q;
-    if (wid == 0) {  // reflector (dlarfg) by wave 0
-      double part = 0.0;
-      for (int i = c + 1 + lane; i < q; i += 64) part += x[i] * x[i];
-      const double sigma = ttk::wave_sum(part);
-      const double alpha = x[c];
-      double t = 0.0, beta = alpha;
-      if (sigma > 0.0) {
-        beta = -copysign(sqrt(alpha * alpha + sigma), alpha);
-        t = (beta - alpha) / beta;
-        const double sc = 1.0 / (alpha - beta);
-        for (int i = c + 1 + lane; i < q; i += 64) x[i] *= sc;
-      }
-      if (lane == 0) {
-        x[c] = beta;
-        tau[c] = t;
-      }
+    // X = R^T (column length p)
+    for (int e = tid; e < p * p; e += nt) {
+      const int i = e / p, j = e - i * p;
+      X[e] = (j >= i) ? W[(int64_t)j * q + i] : 0.0;
     }
-    __syncthreads();
-    const double t = tau[c];
-    for (int j = c + 1 + wid; j < p; j += nw) {  // trailing update + norm downdate
-      double *y = W + (int64_t)j * q;
-      double yc = y[c];
-      if (t != 0.0) {
-        double acc = 0.0;
-        for (int i = c + 1 + lane; i < q; i += 64) acc += x[i] * y[i];
-        const double w = t * (ttk::wave_sum(acc) + yc);
-        for (int i = c + 1 + lane; i < q; i += 64) y[i] -= w * x[i];
-        yc -= w;
-        if (lane == 0) y[c] = yc;
-      }
-      const double a = vn1[j];
-      if (a != 0.0) {
-        double temp = fabs(yc) / a;
-        temp = fmax(1.0 - temp * temp, 0.0);
-        const double r = a / vn2[j];
-        if (temp * r * r <= 1.4901161193847656e-08) {
-          double acc = 0.0;
-          for (int i = c + 1 + lane; i < q; i += 64) acc += y[i] * y[i];
-          acc = sqrt(ttk::wave_sum(acc));
-          if (lane == 0) {
-            vn1[j] = acc;
-            vn2[j] = acc;
-          }
-        } else if (lane == 0) {
-          vn1[j] = a * sqrt(temp);
-        }
-      }
-    }
-    __syncthreads();
   }
-  const int kk = s_kk < 1 ? 1 : s_kk;
-  // ---- X = R1^T (column length p, kk columns), V = I
-  for (int e = tid; e < kk * p; e += nt) {
-    const int i = e / p, j = e - i * p;
-    X[e] = (j >= i) ? W[(int64_t)j * q + i] : 0.0;
-  }
-  for (int e = tid; e < kk * kk; e += nt) V[e] = ((e / kk) == (e % kk)) ? 1.0 : 0.0;
+  for (int e = tid; e < p * p; e += nt) V[e] = ((e / p) == (e % p)) ? 1.0 : 0.0;
   __syncthreads();
-  // ---- one-sided Jacobi on X
-  const int P = (kk % 2) ? kk + 1 : kk;
-  const int gl = tid & (g - 1), gid = tid / g, ng = nt / g;
-  const double tol = EPS * (p > 16 ? (double)p : 16.0);
-  for (int sweep = 0; sweep < 60 && kk > 1; ++sweep) {
+  // ---- one-sided Jacobi on the p columns of X (length L)
+  const int P = (p % 2) ? p + 1 : p;
+  const double tol = EPS * (L > 16 ? (double)L : 16.0), tol2 = tol * tol;
+  for (int sweep = 0; sweep < 60 && p > 1; ++sweep) {
     if (tid == 0) any_rot = 0;
     __syncthreads();
     for (int r = 0; r < P - 1; ++r) {
-      for (int k = gid; k < P / 2; k += ng) {
-        int a, b;
-        rr_pair(P, r, k, a, b);
-        if (b >= kk) continue;
-        double *wa = X + a * p, *wb = X + b * p;
-        double al = 0.0, be = 0.0, ga = 0.0;
-        for (int i = gl; i < p; i += g) {
-          const double xa = wa[i], xb = wb[i];
-          al += xa * xa;
-          be += xb * xb;
-          ga += xa * xb;
-        }
-        al = ttk::group_sum_rt(al, g);
-        be = ttk::group_sum_rt(be, g);
-        ga = ttk::group_sum_rt(ga, g);
-        if (al < 1e-300 || be < 1e-300) continue;
-        if (fabs(ga) <= tol * sqrt(al) * sqrt(be)) continue;
-        const double zeta = (be - al) / (2.0 * ga);
-        double tt;
-        if (fabs(zeta) > 1e150)
-          tt = 0.5 / zeta;
-        else
-          tt = (zeta >= 0.0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
-        const double cs = 1.0 / sqrt(1.0 + tt * tt), sn = cs * tt;
-        for (int i = gl; i < p; i += g) {
-          const double xa = wa[i], xb = wb[i];
-          wa[i] = cs * xa - sn * xb;
-          wb[i] = sn * xa + cs * xb;
-        }
-        double *va = V + a * kk, *vb = V + b * kk;
-        for (int i = gl; i < kk; i += g) {
-          const double xa = va[i], xb = vb[i];
-          va[i] = cs * xa - sn * xb;
-          vb[i] = sn * xa + cs * xb;
-        }
-        if (gl == 0) any_rot = 1;
-      }
+      jacobi_round<G>(X, V, p, L, P, r, tol2, &any_rot);
       __syncthreads();
     }
     if (!any_rot) break;
     __syncthreads();
   }
-  // ---- singular values, order, unit U_X columns
-  for (int j = wid; j < kk; j += nw) {
-    const double *xj = X + j * p;
+  // ---- singular values, order, unit columns
+  for (int j = wid; j < p; j += nw) {
+    const double *xj = X + j * L;
     double s2 = 0.0;
-    for (int i = lane; i < p; i += 64) s2 += xj[i] * xj[i];
+    for (int i = lane; i < L; i += 64) s2 += xj[i] * xj[i];
     s2 = ttk::wave_sum(s2);
     if (lane == 0) sig[j] = sqrt(s2);
   }
   __syncthreads();
-  for (int j = tid; j < kk; j += nt) {
+  for (int j = tid; j < p; j += nt) {
     int rk = 0;
     const double sj = sig[j];
-    for (int i = 0; i < kk; ++i) rk += (sig[i] > sj) || (sig[i] == sj && i < j);
+    for (int i = 0; i < p; ++i) rk += (sig[i] > sj) || (sig[i] == sj && i < j);
     rank[j] = rk;
   }
   __syncthreads();
-  for (int j = wid; j < kk; j += nw) {
-    double *xj = X + j * p;
+  for (int j = wid; j < p; j += nw) {
+    double *xj = X + j * L;
     const double sj = sig[j];
     const double inv = sj > 0.0 ? 1.0 / sj : 0.0;
-    for (int i = lane; i < p; i += 64) xj[i] *= inv;
+    for (int i = lane; i < L; i += 64) xj[i] *= inv;
   }
-  for (int r = tid; r < p; r += nt) S[r] = 0.0;
   __syncthreads();
-  // exact-zero columns: complete U_X to an orthonormal set (rare; MGS against e_i candidates)
-  for (int j = 0; j < kk; ++j) {
+  // exact-zero columns: complete to an orthonormal set (rare; MGS against e_i candidates)
+  for (int j = 0; j < p; ++j) {
     if (sig[j] > 0.0) continue;
-    double *xj = X + j * p;
-    for (int cand = 0; cand < p; ++cand) {
-      for (int i = tid; i < p; i += nt) xj[i] = (i == cand) ? 1.0 : 0.0;
+    double *xj = X + j * L;
+    for (int cand = 0; cand < L; ++cand) {
+      for (int i = tid; i < L; i += nt) xj[i] = (i == cand) ? 1.0 : 0.0;
       __syncthreads();
-      for (int o = 0; o < kk; ++o) {
+      for (int o = 0; o < p; ++o) {
         if (o == j || (sig[o] == 0.0 && o > j)) continue;
-        const double *xo = X + o * p;
+        const double *xo = X + o * L;
         double d = 0.0;
-        for (int i = tid; i < p; i += nt) d += xo[i] * xj[i];
+        for (int i = tid; i < L; i += nt) d += xo[i] * xj[i];
         d = ttk::block_sum(d, red);
-        for (int i = tid; i < p; i += nt) xj[i] -= d * xo[i];
+        for (int i = tid; i < L; i += nt) xj[i] -= d * xo[i];
         __syncthreads();
       }
       double nn = 0.0;
-      for (int i = tid; i < p; i += nt) nn += xj[i] * xj[i];
+      for (int i = tid; i < L; i += nt) nn += xj[i] * xj[i];
       nn = ttk::block_sum(nn, red);
       if (nn > 0.25) {
         const double inv = 1.0 / sqrt(nn);
-        for (int i = tid; i < p; i += nt) xj[i] *= inv;
+        for (int i = tid; i < L; i += nt) xj[i] *= inv;
         __syncthreads();
         break;
       }
@@ -434,50 +494,65 @@ __global__ __launch_bounds__(1024) void svd_wg_kernel(const double *__restrict__
     }
   }
   __syncthreads();
-  for (int j = tid; j < kk; j += nt) S[rank[j]] = sig[j];
-  // ---- left factor of W: M(:, rank[j]) = Q [V_X(:, j); 0], one wave per column
-  for (int j = wid; j < kk; j += nw) {
-    double *mc = M + (int64_t)rank[j] * q;
-    const double *vj = V + j * kk;
-    for (int i = lane; i < q; i += 64) mc[i] = i < kk ? vj[i] : 0.0;
-    __threadfence_block();
-    for (int c = kk - 1; c >= 0; --c) {
-      const double t = tau[c];
-      if (t == 0.0) continue;
-      const double *v = W + (int64_t)c * q;
-      double acc = 0.0;
-      for (int i = c + 1 + lane; i < q; i += 64) acc += v[i] * mc[i];
-      const double w = t * (ttk::wave_sum(acc) + mc[c]);
-      for (int i = c + 1 + lane; i < q; i += 64) mc[i] -= w * v[i];
+  for (int j = tid; j < p; j += nt) S[rank[j]] = sig[j];
+  if (use_qr) {
+    // left factor of W: M(:, rank[j]) = Q [V(:, j); 0], one wave per column through all reflectors
+    for (int j = wid; j < p; j += nw) {
+      double *mc = M + (int64_t)rank[j] * q;
+      const double *vj = V + j * p;
+      for (int i = lane; i < q; i += 64) mc[i] = i < p ? vj[i] : 0.0;
       __threadfence_block();
-      if (lane == 0) mc[c] -= w;
-      __threadfence_block();
+      for (int c = p - 1; c >= 0; --c) {
+        const double t = tau[c];
+        if (t == 0.0) continue;
+        const double *v = W + (int64_t)c * q;
+        double acc = 0.0;
+        for (int i = c + 1 + lane; i < q; i += 64) acc += v[i] * mc[i];
+        const double w = t * (ttk::wave_sum(acc) + mc[c]);
+        for (int i = c + 1 + lane; i < q; i += 64) mc[i] -= w * v[i];
+        __threadfence_block();
+        if (lane == 0) mc[c] -= w;
+        __threadfence_block();
+      }
     }
   }
   __syncthreads();
-  // ---- outputs: left factor Lw = M (q x kk), right factor Rw(perm[i], rank[j]) = U_X(i, j)
-  for (int e = tid; e < q * p; e += nt) {
-    const int i = e / p, r = e - i * p;
-    const double v = r < kk ? M[(int64_t)r * q + i] : 0.0;
-    if (tall)
-      U[(int64_t)i * p + r] = v;
-    else
-      Vt[(int64_t)r * q + i] = v;
-  }
-  for (int e = tid; e < p * p; e += nt) {
-    const int i = e / p, r = e - i * p;  // pivoted row i of R, output rank position r
-    double v = 0.0;
-    if (r < kk) {
-      int j = 0;
-      for (; j < kk; ++j)
-        if (rank[j] == r) break;
-      v = X[j * p + i];
+  // ---- outputs
+  if (use_qr) {  // left = M (q x p), right(perm[i], rank[j]) = X(i, j)
+    for (int e = tid; e < q * p; e += nt) {
+      const int i = e / p, r = e - i * p;
+      const double v = M[(int64_t)r * q + i];
+      if (tall)
+        U[(int64_t)i * p + r] = v;
+      else
+        Vt[(int64_t)r * q + i] = v;
     }
-    const int oi = perm[i];
-    if (tall)
-      Vt[(int64_t)r * p + oi] = v;
-    else
-      U[(int64_t)oi * p + r] = v;
+    for (int e = tid; e < p * p; e += nt) {
+      const int j = e / p, i = e - j * p;  // X(i, j): pivoted row i, column j
+      const int r = rank[j], oi = perm[i];
+      const double v = X[j * p + i];
+      if (tall)
+        Vt[(int64_t)r * p + oi] = v;
+      else
+        U[(int64_t)oi * p + r] = v;
+    }
+  } else {  // left(i, rank[j]) = X(i, j) (length q), right(i, rank[j]) = V(i, j)
+    for (int e = tid; e < q * p; e += nt) {
+      const int j = e / q, i = e - j * q;
+      const double v = X[e];
+      if (tall)
+        U[(int64_t)i * p + rank[j]] = v;
+      else
+        Vt[(int64_t)rank[j] * q + i] = v;
+    }
+    for (int e = tid; e < p * p; e += nt) {
+      const int j = e / p, i = e - j * p;
+      const double v = V[e];
+      if (tall)
+        Vt[(int64_t)rank[j] * p + i] = v;
+      else
+        U[(int64_t)i * p + rank[j]] = v;
+    }
   }
 }
 
@@ -1840,21 +1915,41 @@ int ttk_svd_tol(void *stream, const double *A, int m, int n, double *U, double *
   const int p = m < n ? m : n, q = m < n ? n : m;
   const bool forced_big = g_svd_big_p <= 2;
   if (p > WG_P || forced_big) return svd_big(stream, A, m, n, U, S, Vt, work, defl);
-  const int64_t fixed = 2 * (int64_t)p * p + 5 * (int64_t)p + 2;  // X, V, 4 vectors, 2 int vectors
-  const int64_t wm = 2 * (int64_t)q * p;                            // W and M
+  // small near-square problems converge fast without QR preconditioning; otherwise QRCP first
+  const int use_qr = !(p <= 16 && q <= 2 * p);
+  const int L = use_qr ? p : q;
+  const int64_t fixed = (int64_t)L * p + (int64_t)p * p + 5 * (int64_t)p + 2;  // X, V, vectors
+  const int64_t wm = use_qr ? 2 * (int64_t)q * p : 0;                          // W and M
   const int w_in_lds = fixed + wm <= LDS_DOUBLES;
   const size_t shm = (size_t)(fixed + (w_in_lds ? wm : 0)) * sizeof(double);
-  allow_big_lds(svd_wg_kernel, shm);
+
   const int pairs = (p + 1) / 2;
   int g = 1;
-  while (g < 64 && g * 4 < p) g *= 2;        // ~4 elements of an X column per lane
-  while (g > 1 && pairs * g > 1024) g /= 2;  // all pairs of a round in flight
-  int nt = pairs * g;  // the QRCP strides its trailing columns over however many waves this gives
-  if (q * p > 4096 && nt < 256) nt = 256;  // long columns: more waves for the QR phase
+  while (g < 64 && g * VPL < L) g *= 2;  // <= VPL elements of a column per lane
+  int nt = pairs * g;
+  if (use_qr) {  // the QRCP phase runs one wave per trailing column
+    const int qr = 64 * (p - 1 < 16 ? p - 1 : 16);
+    if (qr > nt) nt = qr;
+  }
   nt = nt < 64 ? 64 : (nt > 1024 ? 1024 : (nt + 63) / 64 * 64);
-  const double defl2 = defl > 0.0 ? defl * defl : 0.0;
-  hipLaunchKernelGGL(svd_wg_kernel, dim3(1), dim3(nt), shm, TTK_STREAM(stream), A, m, n, U, S, Vt, work, w_in_lds, g,
-                     defl2);
+  (void)defl;  // no deflation on this path (every direction keeps an orthonormal vector)
+#define TTK_SVD_WG(GG)                                                                                    \
+  case GG:                                                                                                \
+    allow_big_lds(svd_wg_kernel<GG>, shm);                                                                \
+    hipLaunchKernelGGL(svd_wg_kernel<GG>, dim3(1), dim3(nt), shm, TTK_STREAM(stream), A, m, n, U, S, Vt, work, \
+                       w_in_lds, use_qr);                                                                 \
+    break;
+  switch (g) {
+    TTK_SVD_WG(1)
+    TTK_SVD_WG(2)
+    TTK_SVD_WG(4)
+    TTK_SVD_WG(8)
+    TTK_SVD_WG(16)
+    TTK_SVD_WG(32)
+    default:
+      TTK_SVD_WG(64)
+  }
+#undef TTK_SVD_WG
   TTK_LAUNCH_CHECK();
   return TTK_OK;
 }

@@ -60,7 +60,8 @@ def main():
         t_k = timed(lambda: lib.ttk_svd(st, D._p(A), m, n, D._p(U), D._p(S), D._p(Vt), D._p(work)))
         c = counters()
         print(f"     identity {t_i:8.1f}us sweeps/call {ci[1] / max(ci[0], 1):.1f};  random sweeps/call "
-              f"{c[1] / max(c[0], 1):.1f}")
+              f"{c[1] / max(c[0], 1):.1f}  phases us (qrcp, jacobi, vectors, out): "
+              f"{[round(c[k] / 100.0 / max(c[0], 1), 1) for k in (4, 5, 6, 7)]}")
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(20):
