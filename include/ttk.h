@@ -61,11 +61,15 @@ int ttk_gemm_offs_grouped(void *stream, const double *const *Aptr, const double 
                           int N, int K, double alpha, double beta);
 /* Native einsum engine (replaces `cached_einsum`, src/tt_ops.py:22-28, and the tensordot chains
  * of cy_src/tt_ops_cy.pyx): out = alpha * einsum(eq, ops) + beta * out on device fp64 data.
- * desc = [nops, {ptr, ndim, shape[ndim], stride[ndim]} x nops, has_out_strides, (ndim,
- * out_stride[ndim])], strides in elements (views need not be contiguous).  Plans (greedy
+ * desc = [nops | (allow_fused << 8), {ptr, ndim, shape[ndim], stride[ndim]} x nops, has_out_strides,
+ * (ndim, out_stride[ndim])], strides in elements (views need not be contiguous).  Plans (greedy
  * pairwise order + offset tables) are cached per (eq, shapes, strides); each pairwise step is one
  * ttk_gemm_offs launch. */
 int ttk_einsum(void *stream, const char *eq, const int64_t *desc, double *out, double alpha, double beta);
+/* calls that opt in (desc flag) route 'lsr,smnS,LSR,rnR->lmL' / 'lsr,smnS,LSR,lmL->rnR' (the local
+ * operator, src/tt_als.py:190-200, cy_src/lgmres_cy.pyx:126-153) to a one-launch fused kernel when
+ * its intermediates fit LDS; this switch disables it globally.  Returns the previous setting. */
+int ttk_einsum_set_fused(int on);
 /* out[3] = {plan hits, plan misses, cached plans} */
 int ttk_einsum_stats(long long *out);
 /* contraction-kernel accounting for the roofline report: on != 0 brackets every ttk_gemm_offs*
@@ -155,6 +159,8 @@ int64_t ttk_syev_extreme_work(int n);
 /* diagnostic counters of the factorisation kernels (8 x u64: svd calls, svd sweeps, eig calls,
  * multisection rounds, ...); synchronous; reset != 0 zeroes them */
 int ttk_debug_counters(unsigned long long *out, int reset);
+/* phase timers of the one-workgroup SVD into the debug counters [4..7] (diagnostics) */
+int ttk_svd_set_timing(int on);
 int ttk_syev_extreme(void *stream, const double *A, int n, int which, double *ev, double *vec, double *work);
 
 /* ---------------------------------------------------------------------------------------

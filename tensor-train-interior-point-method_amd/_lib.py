@@ -50,10 +50,12 @@ _SIGS = {
     "ttk_syev": (i32, [vp, vp, i32, vp, vp, vp]),
     "ttk_syev_extreme_work": (i64, [i32]),
     "ttk_debug_counters": (i32, [vp, i32]),
+    "ttk_svd_set_timing": (i32, [i32]),
     "ttk_svd_set_big_threshold": (i32, [i32]),
     "ttk_svd_tol": (i32, [vp, vp, i32, i32, vp, vp, vp, vp, f64]),
     "ttk_einsum": (i32, [vp, ctypes.c_char_p, vp, vp, f64, f64]),
     "ttk_einsum_stats": (i32, [vp]),
+    "ttk_einsum_set_fused": (i32, [i32]),
     "ttk_qr_set_big_threshold": (i32, [i32]),
     "ttk_contract_timing": (i32, [i32]),
     "ttk_contract_stats": (i32, [vp, i32]),

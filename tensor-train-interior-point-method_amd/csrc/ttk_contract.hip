@@ -265,6 +265,12 @@ void contract_count(double flops) {
 
 }  // namespace
 
+namespace ttk {
+// contraction accounting for kernels launched outside this file (fused local apply)
+int contract_events_ext(hipEvent_t *ev0, hipEvent_t *ev1) { return contract_events(ev0, ev1); }
+void contract_count_ext(double flops) { contract_count(flops); }
+}  // namespace ttk
+
 extern "C" {
 
 int ttk_gemm_offs(void *stream, const double *A, const double *B, double *C, const int64_t *offs,

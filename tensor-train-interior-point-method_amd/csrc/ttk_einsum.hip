@@ -12,9 +12,11 @@
 // Executing a plan is one `gemm_offs` launch per step (fp64 MFMA, ttk_contract.hip).
 // Intermediates go to a single stream-ordered scratch buffer shared by all calls: every call is
 // on the same in-order stream, so the next call's kernels cannot overtake this call's.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <unordered_map>
@@ -322,12 +324,25 @@ bool build_plan(const std::string &eq, int nops, const int *ndims, const int64_t
 
 }  // namespace
 
+int fused_apply_try(void *stream, const char *eq, const int64_t *desc, double *out, double alpha, double beta);
+static int g_fused_apply = 1;
+
 extern "C" {
+
+int ttk_einsum_set_fused(int on) {
+  const int old = g_fused_apply;
+  g_fused_apply = on;
+  return old;
+}
 
 // desc: [nops, then per operand: ptr, ndim, shape..., stride..., then has_out_strides, (out ndim,
 // out strides...)]
 int ttk_einsum(void *stream, const char *eq, const int64_t *desc, double *out, double alpha, double beta) {
-  const int nops = (int)desc[0];
+  if (g_fused_apply) {
+    const int rc = fused_apply_try(stream, eq, desc, out, alpha, beta);
+    if (rc != 0) return rc < 0 ? TTK_ERR_HIP : TTK_OK;
+  }
+  const int nops = (int)(desc[0] & 255);
   if (nops < 1 || nops > 8) {
     ttk::set_error("ttk_einsum: %d operands", nops);
     return TTK_ERR_ARG;
@@ -418,3 +433,172 @@ int ttk_einsum_stats(long long *out) {
 }
 
 }  // extern "C"
+
+// ------------------------------------------------------------ fused local operator apply
+// The AMEn / LGMRES local operator (`TTBlockMatrixView.block_local_product`,
+// src/tt_als.py:190-200; `MatVecWrapper` kernel einsum, cy_src/lgmres_cy.pyx:126-153):
+//     out[a, i, c] = alpha * sum_{s,b,j,S,d} P[a,s,b] A[s,i,j,S] Q[c,S,d] x[b,j,d] + beta * out
+// ('lsr,smnS,LSR,rnR->lmL'; the transposed 'lsr,smnS,LSR,lmL->rnR' is the same sum with the
+// roles of (l,r), (L,R), (m,n) exchanged, i.e. permuted strides).  One workgroup per output
+// index c: t1[b,j,S] = sum_d x[b,j,d] Q[c,S,d]; t2[b,s,i] = sum_{j,S} t1[b,j,S] A[s,i,j,S];
+// out[a,i,c] = sum_{s,b} P[a,s,b] t2[b,s,i].  x, the Q slice, A and both intermediates live in
+// LDS; one launch replaces the three pairwise GEMM launches of the greedy plan.
+namespace {
+
+struct ApplyArgs {
+  const double *P, *A, *Q, *x;
+  double *out;
+  int64_t ps[3], as[4], qs[3], xs[3], os[3];
+  int na, ns, nb, ni, nj, nS, nc, nd;
+  double alpha, beta;
+};
+
+// Association follows the greedy pairwise plan the reference's opt_einsum picks for these shapes
+// (t1 = P x over r, t2 = A t1 over (s,n), out = Q t2 over (S,R)), so intermediates and rounding
+// behave like the plan path's.  One workgroup per output index a.
+__global__ __launch_bounds__(256) void fused_apply_kernel(ApplyArgs g) {
+  extern __shared__ double sm[];
+  const int a = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
+  const int nb = g.nb, nj = g.nj, nd = g.nd, nS = g.nS, ns = g.ns, ni = g.ni, nc = g.nc;
+  double *X = sm;                       // nb*nj*nd     [b][j][d]
+  double *Pa = X + nb * nj * nd;        // ns*nb        [s][b]   (P[a, s, b])
+  double *As = Pa + ns * nb;            // ns*ni*nj*nS  [i][S][s][j]
+  double *T1 = As + ns * ni * nj * nS;  // ns*nj*nd     [s][j][d]
+  double *T2 = T1 + ns * nj * nd;       // ni*nS*nd     [i][S][d]
+  for (int e = tid; e < nb * nj * nd; e += nt) {
+    const int b = e / (nj * nd), r = e - b * nj * nd, j = r / nd, d = r - j * nd;
+    X[e] = g.x[b * g.xs[0] + j * g.xs[1] + d * g.xs[2]];
+  }
+  for (int e = tid; e < ns * nb; e += nt) {
+    const int s = e / nb, b = e - s * nb;
+    Pa[e] = g.P[a * g.ps[0] + s * g.ps[1] + b * g.ps[2]];
+  }
+  for (int e = tid; e < ns * ni * nj * nS; e += nt) {  // As[i][S][s][j] = A[s, i, j, S]
+    int r = e;
+    const int j = r % nj;
+    r /= nj;
+    const int s = r % ns;
+    r /= ns;
+    const int S = r % nS, i = r / nS;
+    As[e] = g.A[s * g.as[0] + i * g.as[1] + j * g.as[2] + S * g.as[3]];
+  }
+  __syncthreads();
+  for (int e = tid; e < ns * nj * nd; e += nt) {  // t1[s][j][d] = sum_b P[a,s,b] x[b,j,d]
+    const int s = e / (nj * nd), r = e - s * nj * nd;  // r = j*nd + d
+    const double *pr = Pa + s * nb;
+    double acc = 0.0;
+    for (int b = 0; b < nb; ++b) acc = fma(pr[b], X[b * nj * nd + r], acc);
+    T1[e] = acc;
+  }
+  __syncthreads();
+  const int sj = ns * nj;
+  for (int e = tid; e < ni * nS * nd; e += nt) {  // t2[i][S][d] = sum_{s,j} A[s,i,j,S] t1[s][j][d]
+    const int iS = e / nd, d = e - iS * nd;
+    const double *ar = As + iS * sj;
+    double acc = 0.0;
+    for (int k = 0; k < sj; ++k) acc = fma(ar[k], T1[k * nd + d], acc);
+    T2[e] = acc;
+  }
+  __syncthreads();
+  for (int e = tid; e < ni * nc; e += nt) {  // out[a][i][c] = sum_{S,d} Q[c,S,d] t2[i][S][d]
+    const int i = e / nc, c = e - i * nc;
+    const double *tr = T2 + i * nS * nd;
+    double acc = 0.0;
+    for (int S = 0; S < nS; ++S) {
+      const double *qr = g.Q + c * g.qs[0] + S * g.qs[1];
+      for (int d = 0; d < nd; ++d) acc = fma(qr[d * g.qs[2]], tr[S * nd + d], acc);
+    }
+    double *o = g.out + a * g.os[0] + i * g.os[1] + c * g.os[2];
+    *o = g.beta != 0.0 ? g.alpha * acc + g.beta * *o : g.alpha * acc;
+  }
+}
+
+constexpr int64_t APPLY_LDS_DOUBLES = 20000;
+
+int64_t apply_lds(int nb, int nj, int nd, int nS, int ns, int ni) {
+  return (int64_t)nb * nj * nd + (int64_t)ns * nb + (int64_t)ns * ni * nj * nS + (int64_t)ns * nj * nd +
+         (int64_t)ni * nS * nd;
+}
+
+}  // namespace
+
+// Try the fused kernel for the two local-apply equations; returns 1 if handled, 0 if the caller
+// should run the generic plan, <0 on error.  desc as in ttk_einsum.
+int fused_apply_try(void *stream, const char *eq, const int64_t *desc, double *out, double alpha, double beta) {
+  if (!(desc[0] & 256)) return 0;  // caller did not opt in
+  const bool fwd = std::strcmp(eq, "lsr,smnS,LSR,rnR->lmL") == 0;
+  const bool bwd = !fwd && std::strcmp(eq, "lsr,smnS,LSR,lmL->rnR") == 0;
+  if (!fwd && !bwd) return 0;
+  if ((desc[0] & 255) != 4) return 0;
+  const int64_t *o = desc + 1;
+  // operand records: ptr, ndim, shape..., stride...
+  const int64_t *rP = o, *rA = rP + 2 + 2 * 3, *rQ = rA + 2 + 2 * 4, *rx = rQ + 2 + 2 * 3, *ro = rx + 2 + 2 * 3;
+  if (rP[1] != 3 || rA[1] != 4 || rQ[1] != 3 || rx[1] != 3) return 0;
+  const int64_t *Psh = rP + 2, *Pst = rP + 5, *Ash = rA + 2, *Ast = rA + 6, *Qsh = rQ + 2, *Qst = rQ + 5;
+  const int64_t *xst = rx + 5;
+  ApplyArgs g;
+  g.P = reinterpret_cast<const double *>(rP[0]);
+  g.A = reinterpret_cast<const double *>(rA[0]);
+  g.Q = reinterpret_cast<const double *>(rQ[0]);
+  g.x = reinterpret_cast<const double *>(rx[0]);
+  g.out = out;
+  g.alpha = alpha;
+  g.beta = beta;
+  g.ns = (int)Psh[1];
+  g.nS = (int)Qsh[1];
+  if (fwd) {  // a=l, b=r, c=L, d=R, i=m, j=n
+    g.na = (int)Psh[0];
+    g.nb = (int)Psh[2];
+    g.nc = (int)Qsh[0];
+    g.nd = (int)Qsh[2];
+    g.ni = (int)Ash[1];
+    g.nj = (int)Ash[2];
+    for (int k = 0; k < 3; ++k) g.ps[k] = Pst[k];
+    for (int k = 0; k < 4; ++k) g.as[k] = Ast[k];
+    for (int k = 0; k < 3; ++k) g.qs[k] = Qst[k];
+    for (int k = 0; k < 3; ++k) g.xs[k] = xst[k];  // x[r][n][R] = x[b][j][d]
+  } else {  // a=r, b=l, c=R, d=L, i=n, j=m
+    g.na = (int)Psh[2];
+    g.nb = (int)Psh[0];
+    g.nc = (int)Qsh[2];
+    g.nd = (int)Qsh[0];
+    g.ni = (int)Ash[2];
+    g.nj = (int)Ash[1];
+    g.ps[0] = Pst[2];
+    g.ps[1] = Pst[1];
+    g.ps[2] = Pst[0];
+    g.as[0] = Ast[0];
+    g.as[1] = Ast[2];
+    g.as[2] = Ast[1];
+    g.as[3] = Ast[3];
+    g.qs[0] = Qst[2];
+    g.qs[1] = Qst[1];
+    g.qs[2] = Qst[0];
+    for (int k = 0; k < 3; ++k) g.xs[k] = xst[k];  // x[l][m][L] = x[b][j][d]
+  }
+  // output strides: out[a][i][c] (both equations write their natural output order)
+  if (ro[0]) {
+    if (ro[1] != 3) return 0;
+    for (int k = 0; k < 3; ++k) g.os[k] = ro[2 + k];
+  } else {
+    g.os[2] = 1;
+    g.os[1] = g.nc;
+    g.os[0] = (int64_t)g.ni * g.nc;
+  }
+  const int64_t need = apply_lds(g.nb, g.nj, g.nd, g.nS, g.ns, g.ni);
+  if (need > APPLY_LDS_DOUBLES || g.na < 1 || g.na > 65535) return 0;
+  const size_t shm = need * sizeof(double);
+  if (shm > 65536)
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(fused_apply_kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+  static const int dbg_sync = getenv("TTK_FUSED_SYNC") != nullptr;
+  if (dbg_sync) (void)hipStreamSynchronize(TTK_STREAM(stream));
+  hipEvent_t e0, e1;
+  if (ttk::contract_events_ext(&e0, &e1) != TTK_OK) return -1;
+  hipExtLaunchKernelGGL(fused_apply_kernel, dim3(g.na), dim3(256), shm, TTK_STREAM(stream), e0, e1, 0, g);
+  TTK_LAUNCH_CHECK();
+  ttk::contract_count_ext(2.0 * g.na *
+                          ((double)g.ns * g.nj * g.nd * g.nb + (double)g.ni * g.nS * g.nd * g.ns * g.nj +
+                           (double)g.ni * g.nc * g.nS * g.nd));
+  return 1;
+}

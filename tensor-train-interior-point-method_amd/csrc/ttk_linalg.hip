@@ -94,6 +94,7 @@ __device__ void svd_epilogue(double *W, double *V, double *sig, int *rank, int m
   for (int j = wid; j < p; j += nw) {
     const double *wj = W + (int64_t)j * q;
     double s2 = 0.0;
+    #pragma unroll 8
     for (int i = lane; i < q; i += 64) s2 += wj[i] * wj[i];
     s2 = ttk::wave_sum(s2);
     if (lane == 0) sig[j] = sqrt(s2);
@@ -115,6 +116,7 @@ __device__ void svd_epilogue(double *W, double *V, double *sig, int *rank, int m
     const double sj = sig[j];
     if (sj > 0.0) {
       const double inv = 1.0 / sj;
+      #pragma unroll 8
       for (int i = lane; i < q; i += 64) wj[i] *= inv;
     }
   }
@@ -187,6 +189,7 @@ __global__ __launch_bounds__(256) void svd_big_round_kernel(double *__restrict__
   if (b >= p) return;
   double *wa = W + (int64_t)a * q, *wb = W + (int64_t)b * q;
   double al = 0.0, be = 0.0, ga = 0.0;
+  #pragma unroll 8
   for (int i = lane; i < q; i += 64) {
     const double x = wa[i], y = wb[i];
     al += x * x;
@@ -200,12 +203,14 @@ __global__ __launch_bounds__(256) void svd_big_round_kernel(double *__restrict__
   if (ga * ga <= tol * tol * al * be) return;
   double c, s;
   jacobi_rotation(al, be, ga, c, s);
+  #pragma unroll 8
   for (int i = lane; i < q; i += 64) {
     const double x = wa[i], y = wb[i];
     wa[i] = c * x - s * y;
     wb[i] = s * x + c * y;
   }
   double *va = V + (int64_t)a * p, *vb = V + (int64_t)b * p;
+  #pragma unroll 8
   for (int i = lane; i < p; i += 64) {
     const double x = va[i], y = vb[i];
     va[i] = c * x - s * y;
@@ -237,14 +242,14 @@ constexpr int WG_P = 96;
 constexpr int VPL = 8;
 
 template <int G>
-__device__ __forceinline__ void jacobi_round(double *X, double *V, int p, int L, int P, int r, double tol2,
-                                             int *any_rot) {
+__device__ __forceinline__ void jacobi_round(double *X, int ldx, double *V, int ldv, int p, int L, int P, int r,
+                                             double tol2, int *any_rot) {
   const int tid = threadIdx.x, gl = tid & (G - 1), gid = tid / G, ng = blockDim.x / G;
   for (int k = gid; k < P / 2; k += ng) {
     int a, b;
     rr_pair(P, r, k, a, b);
     if (b >= p) continue;
-    double *wa = X + a * L, *wb = X + b * L;
+    double *wa = X + a * ldx, *wb = X + b * ldx;
     double xa[VPL], xb[VPL];
 #pragma unroll
     for (int v = 0; v < VPL; ++v) {
@@ -276,7 +281,7 @@ __device__ __forceinline__ void jacobi_round(double *X, double *V, int p, int L,
         wb[i] = sn * xa[v] + cs * xb[v];
       }
     }
-    double *va = V + a * p, *vb = V + b * p;
+    double *va = V + a * ldv, *vb = V + b * ldv;
 #pragma unroll
     for (int v = 0; v < VPL; ++v) {
       const int i = gl + v * G;
@@ -294,7 +299,7 @@ template <int G>
 __global__ __launch_bounds__(1024) void svd_wg_kernel(const double *__restrict__ A, int m, int n,
                                                       double *__restrict__ U, double *__restrict__ S,
                                                       double *__restrict__ Vt, double *__restrict__ gwork,
-                                                      int w_in_lds, int use_qr) {
+                                                      int w_in_lds, int use_qr, int timing) {
   extern __shared__ double lds[];
   __shared__ int s_piv, any_rot;
   __shared__ double red[16];
@@ -303,20 +308,36 @@ __global__ __launch_bounds__(1024) void svd_wg_kernel(const double *__restrict__
   const int L = use_qr ? p : q;  // Jacobi column length
   const int tid = threadIdx.x, nt = blockDim.x;
   const int lane = tid & 63, wid = tid >> 6, nw = nt >> 6;
-  // LDS: X (L*p) | V (p*p) | tau, vn1, vn2, sig (4p) | perm, rank (2p ints) | [W, M if w_in_lds]
-  double *X = lds, *V = X + L * p, *tau = V + p * p, *vn1 = tau + p, *vn2 = vn1 + p, *sig = vn2 + p;
+  unsigned long long t_ph = timing ? wall_clock64() : 0;
+#define TTK_PHASE(K)                                    \
+  if (timing && tid == 0) {                             \
+    const unsigned long long t1 = wall_clock64();       \
+    atomicAdd(&g_dbg[K], t1 - t_ph);                    \
+    t_ph = t1;                                          \
+  }
+  // LDS: X (ldx*p) | V (ldv*p) | tau, vn1, vn2, sig (4p) | perm, rank (2p ints) | [W, M if w_in_lds]
+  // odd leading dimensions: columns start on different LDS banks (even ones put every lane group
+  // of a wave on the same banks)
+  const int ldx = L | 1, ldv = p | 1;
+  // g2 lanes per column for the column-parallel QR phases: as many as fill the block, <= 64
+  int g2 = 64;
+  while (g2 > 1 && g2 * (p > 1 ? p - 1 : 1) > nt) g2 >>= 1;
+  const int gl2 = tid & (g2 - 1), gid2 = tid / g2, ng2 = nt / g2;
+  double *X = lds, *V = X + ldx * p, *tau = V + ldv * p, *vn1 = tau + p, *vn2 = vn1 + p, *sig = vn2 + p;
   int *perm = reinterpret_cast<int *>(sig + p), *rank = perm + p;
   double *W = use_qr ? (w_in_lds ? reinterpret_cast<double *>(rank + p + (p & 1)) : gwork) : X;
+  const int ldw = use_qr ? q : ldx;
   double *M = W + (int64_t)q * p;
   for (int e = tid; e < q * p; e += nt) {
     const int j = e / q, i = e - j * q;
-    W[e] = tall ? A[(int64_t)i * n + j] : A[(int64_t)j * n + i];
+    W[(int64_t)j * ldw + i] = tall ? A[(int64_t)i * n + j] : A[(int64_t)j * n + i];
   }
   __syncthreads();
   if (use_qr) {
     for (int j = wid; j < p; j += nw) {
       const double *w = W + (int64_t)j * q;
       double acc = 0.0;
+      #pragma unroll 8
       for (int i = lane; i < q; i += 64) acc += w[i] * w[i];
       acc = sqrt(ttk::wave_sum(acc));
       if (lane == 0) {
@@ -373,6 +394,7 @@ __global__ __launch_bounds__(1024) void svd_wg_kernel(const double *__restrict__
       double *x = W + (int64_t)c * q;
       if (wid == 0) {  // reflector (dlarfg) by wave 0
         double part = 0.0;
+        #pragma unroll 8
         for (int i = c + 1 + lane; i < q; i += 64) part += x[i] * x[i];
         const double sigma = ttk::wave_sum(part);
         const double alpha = x[c];
@@ -381,6 +403,7 @@ __global__ __launch_bounds__(1024) void svd_wg_kernel(const double *__restrict__
           beta = -copysign(sqrt(alpha * alpha + sigma), alpha);
           t = (beta - alpha) / beta;
           const double sc = 1.0 / (alpha - beta);
+          #pragma unroll 8
           for (int i = c + 1 + lane; i < q; i += 64) x[i] *= sc;
         }
         if (lane == 0) {
@@ -390,16 +413,19 @@ __global__ __launch_bounds__(1024) void svd_wg_kernel(const double *__restrict__
       }
       __syncthreads();
       const double t = tau[c];
-      for (int j = c + 1 + wid; j < p; j += nw) {  // trailing update + dlaqp2 norm downdate
+      // trailing update + dlaqp2 norm downdate: g2 lanes per column, all columns in flight
+      for (int j = c + 1 + gid2; j < p; j += ng2) {
         double *y = W + (int64_t)j * q;
         double yc = y[c];
         if (t != 0.0) {
           double acc = 0.0;
-          for (int i = c + 1 + lane; i < q; i += 64) acc += x[i] * y[i];
-          const double w = t * (ttk::wave_sum(acc) + yc);
-          for (int i = c + 1 + lane; i < q; i += 64) y[i] -= w * x[i];
+          #pragma unroll 8
+          for (int i = c + 1 + gl2; i < q; i += g2) acc += x[i] * y[i];
+          const double w = t * (ttk::group_sum_rt(acc, g2) + yc);
+          #pragma unroll 8
+          for (int i = c + 1 + gl2; i < q; i += g2) y[i] -= w * x[i];
           yc -= w;
-          if (lane == 0) y[c] = yc;
+          if (gl2 == 0) y[c] = yc;
         }
         const double a = vn1[j];
         if (a != 0.0) {
@@ -407,14 +433,16 @@ __global__ __launch_bounds__(1024) void svd_wg_kernel(const double *__restrict__
           temp = fmax(1.0 - temp * temp, 0.0);
           const double r = a / vn2[j];
           if (temp * r * r <= 1.4901161193847656e-08) {
+            __threadfence_block();  // the group reads back the updated column
             double acc = 0.0;
-            for (int i = c + 1 + lane; i < q; i += 64) acc += y[i] * y[i];
-            acc = sqrt(ttk::wave_sum(acc));
-            if (lane == 0) {
+            #pragma unroll 8
+            for (int i = c + 1 + gl2; i < q; i += g2) acc += y[i] * y[i];
+            acc = sqrt(ttk::group_sum_rt(acc, g2));
+            if (gl2 == 0) {
               vn1[j] = acc;
               vn2[j] = acc;
             }
-          } else if (lane == 0) {
+          } else if (gl2 == 0) {
             vn1[j] = a * sqrt(temp);
           }
         }
@@ -424,11 +452,15 @@ __global__ __launch_bounds__(1024) void svd_wg_kernel(const double *__restrict__
     // X = R^T (column length p)
     for (int e = tid; e < p * p; e += nt) {
       const int i = e / p, j = e - i * p;
-      X[e] = (j >= i) ? W[(int64_t)j * q + i] : 0.0;
+      X[i * ldx + j] = (j >= i) ? W[(int64_t)j * q + i] : 0.0;
     }
   }
-  for (int e = tid; e < p * p; e += nt) V[e] = ((e / p) == (e % p)) ? 1.0 : 0.0;
+  for (int e = tid; e < p * p; e += nt) {
+    const int j = e / p, i = e - j * p;
+    V[j * ldv + i] = (i == j) ? 1.0 : 0.0;
+  }
   __syncthreads();
+  TTK_PHASE(4)
   // ---- one-sided Jacobi on the p columns of X (length L)
   const int P = (p % 2) ? p + 1 : p;
   const double tol = EPS * (L > 16 ? (double)L : 16.0), tol2 = tol * tol;
@@ -436,15 +468,17 @@ __global__ __launch_bounds__(1024) void svd_wg_kernel(const double *__restrict__
     if (tid == 0) any_rot = 0;
     __syncthreads();
     for (int r = 0; r < P - 1; ++r) {
-      jacobi_round<G>(X, V, p, L, P, r, tol2, &any_rot);
+      jacobi_round<G>(X, ldx, V, ldv, p, L, P, r, tol2, &any_rot);
       __syncthreads();
     }
+    if (timing && tid == 0) atomicAdd(&g_dbg[1], 1ull);
     if (!any_rot) break;
     __syncthreads();
   }
+  TTK_PHASE(5)
   // ---- singular values, order, unit columns
   for (int j = wid; j < p; j += nw) {
-    const double *xj = X + j * L;
+    const double *xj = X + j * ldx;
     double s2 = 0.0;
     for (int i = lane; i < L; i += 64) s2 += xj[i] * xj[i];
     s2 = ttk::wave_sum(s2);
@@ -459,7 +493,7 @@ __global__ __launch_bounds__(1024) void svd_wg_kernel(const double *__restrict__
   }
   __syncthreads();
   for (int j = wid; j < p; j += nw) {
-    double *xj = X + j * L;
+    double *xj = X + j * ldx;
     const double sj = sig[j];
     const double inv = sj > 0.0 ? 1.0 / sj : 0.0;
     for (int i = lane; i < L; i += 64) xj[i] *= inv;
@@ -468,13 +502,13 @@ __global__ __launch_bounds__(1024) void svd_wg_kernel(const double *__restrict__
   // exact-zero columns: complete to an orthonormal set (rare; MGS against e_i candidates)
   for (int j = 0; j < p; ++j) {
     if (sig[j] > 0.0) continue;
-    double *xj = X + j * L;
+    double *xj = X + j * ldx;
     for (int cand = 0; cand < L; ++cand) {
       for (int i = tid; i < L; i += nt) xj[i] = (i == cand) ? 1.0 : 0.0;
       __syncthreads();
       for (int o = 0; o < p; ++o) {
         if (o == j || (sig[o] == 0.0 && o > j)) continue;
-        const double *xo = X + o * L;
+        const double *xo = X + o * ldx;
         double d = 0.0;
         for (int i = tid; i < L; i += nt) d += xo[i] * xj[i];
         d = ttk::block_sum(d, red);
@@ -496,27 +530,32 @@ __global__ __launch_bounds__(1024) void svd_wg_kernel(const double *__restrict__
   __syncthreads();
   for (int j = tid; j < p; j += nt) S[rank[j]] = sig[j];
   if (use_qr) {
-    // left factor of W: M(:, rank[j]) = Q [V(:, j); 0], one wave per column through all reflectors
-    for (int j = wid; j < p; j += nw) {
+    // left factor of W: M(:, rank[j]) = Q [V(:, j); 0]; g2 lanes per column, each column runs
+    // through all reflectors independently (no block barriers)
+    for (int j = gid2; j < p; j += ng2) {
       double *mc = M + (int64_t)rank[j] * q;
-      const double *vj = V + j * p;
-      for (int i = lane; i < q; i += 64) mc[i] = i < p ? vj[i] : 0.0;
+      const double *vj = V + j * ldv;
+      #pragma unroll 8
+      for (int i = gl2; i < q; i += g2) mc[i] = i < p ? vj[i] : 0.0;
       __threadfence_block();
       for (int c = p - 1; c >= 0; --c) {
         const double t = tau[c];
         if (t == 0.0) continue;
         const double *v = W + (int64_t)c * q;
         double acc = 0.0;
-        for (int i = c + 1 + lane; i < q; i += 64) acc += v[i] * mc[i];
-        const double w = t * (ttk::wave_sum(acc) + mc[c]);
-        for (int i = c + 1 + lane; i < q; i += 64) mc[i] -= w * v[i];
+        #pragma unroll 8
+        for (int i = c + 1 + gl2; i < q; i += g2) acc += v[i] * mc[i];
+        const double w = t * (ttk::group_sum_rt(acc, g2) + mc[c]);
+        #pragma unroll 8
+        for (int i = c + 1 + gl2; i < q; i += g2) mc[i] -= w * v[i];
         __threadfence_block();
-        if (lane == 0) mc[c] -= w;
+        if (gl2 == 0) mc[c] -= w;
         __threadfence_block();
       }
     }
   }
   __syncthreads();
+  TTK_PHASE(6)
   // ---- outputs
   if (use_qr) {  // left = M (q x p), right(perm[i], rank[j]) = X(i, j)
     for (int e = tid; e < q * p; e += nt) {
@@ -530,7 +569,7 @@ __global__ __launch_bounds__(1024) void svd_wg_kernel(const double *__restrict__
     for (int e = tid; e < p * p; e += nt) {
       const int j = e / p, i = e - j * p;  // X(i, j): pivoted row i, column j
       const int r = rank[j], oi = perm[i];
-      const double v = X[j * p + i];
+      const double v = X[j * ldx + i];
       if (tall)
         Vt[(int64_t)r * p + oi] = v;
       else
@@ -539,7 +578,7 @@ __global__ __launch_bounds__(1024) void svd_wg_kernel(const double *__restrict__
   } else {  // left(i, rank[j]) = X(i, j) (length q), right(i, rank[j]) = V(i, j)
     for (int e = tid; e < q * p; e += nt) {
       const int j = e / q, i = e - j * q;
-      const double v = X[e];
+      const double v = X[j * ldx + i];
       if (tall)
         U[(int64_t)i * p + rank[j]] = v;
       else
@@ -547,13 +586,19 @@ __global__ __launch_bounds__(1024) void svd_wg_kernel(const double *__restrict__
     }
     for (int e = tid; e < p * p; e += nt) {
       const int j = e / p, i = e - j * p;
-      const double v = V[e];
+      const double v = V[j * ldv + i];
       if (tall)
         Vt[(int64_t)rank[j] * p + i] = v;
       else
         U[(int64_t)i * p + rank[j]] = v;
     }
   }
+  if (timing) {
+    __syncthreads();
+    TTK_PHASE(7)
+    if (tid == 0) atomicAdd(&g_dbg[0], 1ull);
+  }
+#undef TTK_PHASE
 }
 
 // ------------------------------------------------------------------------------ QR
@@ -607,9 +652,11 @@ __global__ __launch_bounds__(1024) void qr_kernel(const double *__restrict__ A, 
       for (int c = j + 1 + wid; c < n; c += nw) {
         double *wc = W + (int64_t)c * m;
         double d = (lane == 0) ? wc[j] : 0.0;
+        #pragma unroll 8
         for (int i = j + 1 + lane; i < m; i += 64) d += wj[i] * wc[i];
         d = ttk::wave_sum(d) * tj;
         if (lane == 0) wc[j] -= d;
+        #pragma unroll 8
         for (int i = j + 1 + lane; i < m; i += 64) wc[i] -= d * wj[i];
       }
     }
@@ -633,9 +680,11 @@ __global__ __launch_bounds__(1024) void qr_kernel(const double *__restrict__ A, 
     for (int c = j + wid; c < k; c += nw) {
       double *qc = Qc + (int64_t)c * m;
       double d = (lane == 0) ? qc[j] : 0.0;
+      #pragma unroll 8
       for (int i = j + 1 + lane; i < m; i += 64) d += v[i] * qc[i];
       d = ttk::wave_sum(d) * tj;
       if (lane == 0) qc[j] -= d;
+      #pragma unroll 8
       for (int i = j + 1 + lane; i < m; i += 64) qc[i] -= d * v[i];
     }
     __syncthreads();
@@ -1087,6 +1136,7 @@ __global__ __launch_bounds__(1024) void syev_extreme_kernel(const double *__rest
     const int m = n - k - 1;
     if (wid == 0) {  // reflector by wave 0
       double part = 0.0;
+      #pragma unroll 8
       for (int i = 1 + lane; i < m; i += 64) part += v[i] * v[i];
       const double sigma = ttk::wave_sum(part);
       const double alpha = v[0];
@@ -1095,6 +1145,7 @@ __global__ __launch_bounds__(1024) void syev_extreme_kernel(const double *__rest
         beta = -copysign(sqrt(alpha * alpha + sigma), alpha);
         tau = (beta - alpha) / beta;
         const double sc = 1.0 / (alpha - beta);
+        #pragma unroll 8
         for (int i = 1 + lane; i < m; i += 64) v[i] *= sc;
       }
       if (lane == 0) {
@@ -1120,6 +1171,7 @@ __global__ __launch_bounds__(1024) void syev_extreme_kernel(const double *__rest
     }
     __syncthreads();
     double part = 0.0;  // every wave forms K = tau/2 p^T v itself (no barrier)
+    #pragma unroll 8
     for (int i = lane; i < m; i += 64) part += pv[i] * v[i];
     const double K = 0.5 * tau * ttk::wave_sum(part);
     for (int i = wid; i < m; i += nw) {  // A22 -= v w^T + w v^T, w = p - K v
@@ -1326,8 +1378,10 @@ __global__ __launch_bounds__(1024) void qrb_panel_kernel(double *W, int m, int l
     for (int c2 = c + 1 + wid; c2 < j0 + nbe; c2 += nw) {
       double *y = W + (int64_t)c2 * ld;
       double acc = 0.0;
+      #pragma unroll 8
       for (int i = c + 1 + lane; i < m; i += 64) acc += x[i] * y[i];
       const double w = t * (ttk::wave_sum(acc) + y[c]);
+      #pragma unroll 8
       for (int i = c + 1 + lane; i < m; i += 64) y[i] -= w * x[i];
       if (lane == 0) y[c] -= w;
     }
@@ -1335,6 +1389,7 @@ __global__ __launch_bounds__(1024) void qrb_panel_kernel(double *W, int m, int l
     for (int k = wid; k < jj; k += nw) {
       const double *yk = W + (int64_t)(j0 + k) * ld;
       double acc = 0.0;
+      #pragma unroll 8
       for (int i = c + 1 + lane; i < m; i += 64) acc += yk[i] * x[i];
       acc = ttk::wave_sum(acc) + yk[c];
       if (lane == 0) ytv[k] = acc;
@@ -1501,6 +1556,7 @@ __global__ __launch_bounds__(256) void qrcp_init_kernel(const double *__restrict
   if (j >= n) return;
   const double *w = W + (int64_t)j * m;
   double acc = 0.0;
+  #pragma unroll 8
   for (int i = lane; i < m; i += 64) acc += w[i] * w[i];
   acc = sqrt(ttk::wave_sum(acc));
   if (lane == 0) {
@@ -1617,8 +1673,10 @@ __global__ __launch_bounds__(256) void qrcp_update_kernel(double *__restrict__ W
   double yc = y[c];
   if (t != 0.0) {
     double acc = 0.0;
+    #pragma unroll 8
     for (int i = c + 1 + lane; i < m; i += 64) acc += v[i] * y[i];
     const double w = t * (ttk::wave_sum(acc) + yc);
+    #pragma unroll 8
     for (int i = c + 1 + lane; i < m; i += 64) y[i] -= w * v[i];
     yc -= w;
     if (lane == 0) y[c] = yc;
@@ -1630,6 +1688,7 @@ __global__ __launch_bounds__(256) void qrcp_update_kernel(double *__restrict__ W
     const double r = a / vn2[j];
     if (temp * r * r <= 1.4901161193847656e-08) {
       double acc = 0.0;
+      #pragma unroll 8
       for (int i = c + 1 + lane; i < m; i += 64) acc += y[i] * y[i];
       acc = sqrt(ttk::wave_sum(acc));
       if (lane == 0) {
@@ -1660,6 +1719,7 @@ __global__ __launch_bounds__(256) void tfactor_kernel(const double *__restrict__
     for (int k = wid; k < jj; k += nw) {
       const double *yk = W + (int64_t)(j0 + k) * m;
       double acc = 0.0;
+      #pragma unroll 8
       for (int i = c + 1 + lane; i < m; i += 64) acc += yk[i] * x[i];
       acc = ttk::wave_sum(acc) + yk[c];
       if (lane == 0) ytv[k] = acc;
@@ -1777,7 +1837,14 @@ int ensure_status() {
 
 extern "C" {
 
-static int g_svd_big_p = 64;  // smallest p that takes the multi-workgroup path (when W does not fit LDS)
+static int g_svd_big_p = 64;
+static int g_svd_timing = 0;  // phase timers of the one-workgroup SVD into the debug counters
+
+int ttk_svd_set_timing(int on) {
+  const int old = g_svd_timing;
+  g_svd_timing = on;
+  return old;
+}  // smallest p that takes the multi-workgroup path (when W does not fit LDS)
 
 static int64_t svd_big_work(int m, int n) {
   const int64_t p = m < n ? m : n, q = m < n ? n : m, npan = (p + QB - 1) / QB;
@@ -1918,7 +1985,7 @@ int ttk_svd_tol(void *stream, const double *A, int m, int n, double *U, double *
   // small near-square problems converge fast without QR preconditioning; otherwise QRCP first
   const int use_qr = !(p <= 16 && q <= 2 * p);
   const int L = use_qr ? p : q;
-  const int64_t fixed = (int64_t)L * p + (int64_t)p * p + 5 * (int64_t)p + 2;  // X, V, vectors
+  const int64_t fixed = (int64_t)(L | 1) * p + (int64_t)(p | 1) * p + 5 * (int64_t)p + 2;  // X, V, vectors
   const int64_t wm = use_qr ? 2 * (int64_t)q * p : 0;                          // W and M
   const int w_in_lds = fixed + wm <= LDS_DOUBLES;
   const size_t shm = (size_t)(fixed + (w_in_lds ? wm : 0)) * sizeof(double);
@@ -1927,17 +1994,14 @@ int ttk_svd_tol(void *stream, const double *A, int m, int n, double *U, double *
   int g = 1;
   while (g < 64 && g * VPL < L) g *= 2;  // <= VPL elements of a column per lane
   int nt = pairs * g;
-  if (use_qr) {  // the QRCP phase runs one wave per trailing column
-    const int qr = 64 * (p - 1 < 16 ? p - 1 : 16);
-    if (qr > nt) nt = qr;
-  }
+  if (use_qr && q * p > 2048) nt = 1024;  // column-parallel QR phases want a full block
   nt = nt < 64 ? 64 : (nt > 1024 ? 1024 : (nt + 63) / 64 * 64);
   (void)defl;  // no deflation on this path (every direction keeps an orthonormal vector)
 #define TTK_SVD_WG(GG)                                                                                    \
   case GG:                                                                                                \
     allow_big_lds(svd_wg_kernel<GG>, shm);                                                                \
     hipLaunchKernelGGL(svd_wg_kernel<GG>, dim3(1), dim3(nt), shm, TTK_STREAM(stream), A, m, n, U, S, Vt, work, \
-                       w_in_lds, use_qr);                                                                 \
+                       w_in_lds, use_qr, g_svd_timing);                                                   \
     break;
   switch (g) {
     TTK_SVD_WG(1)

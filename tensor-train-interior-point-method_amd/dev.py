@@ -202,12 +202,56 @@ def _out_shape(eq, shapes):
     return tuple(ext[c] for c in out)
 
 
-def einsum(eq, *ops, out=None, alpha=1.0, beta=0.0):
+_CHECK_FUSED = os.environ.get("TTIPM_CHECK_FUSED") == "1"
+_FUSED_EQS = ("lsr,smnS,LSR,rnR->lmL", "lsr,smnS,LSR,lmL->rnR")
+CHECK_LOG = []
+
+
+def _einsum_checked(eq, ops, out, alpha, beta):
+    """dev diagnostics: run a fused-kernel equation both ways and record the discrepancy"""
+    ref_out = None if out is None else clone(out)
+    old_host = None if out is None else read(out)
+    res = _einsum_native(eq, *ops, out=out, alpha=alpha, beta=beta, fused=True)
+    old = lib.ttk_einsum_set_fused(0)
+    try:
+        plain = _einsum_native(eq, *ops, out=ref_out, alpha=alpha, beta=beta)
+    finally:
+        lib.ttk_einsum_set_fused(old)
+    a, b = read(res), read(plain)
+    err = float(np.max(np.abs(a - b))) / max(float(np.max(np.abs(b))), 1e-300) if b.size else 0.0
+    if err > 1e-8 and sum(1 for e in CHECK_LOG if e[-1] > 1e-8) < 4:
+        os.makedirs("gpurun_out", exist_ok=True)
+        np.savez(f"gpurun_out/fused_bad_{len(CHECK_LOG)}.npz", *[read(o) for o in ops], fused=a, plain=b,
+                 old=old_host if old_host is not None else np.zeros(0), eq=np.array(eq), beta=np.array(beta), alpha=np.array(alpha))
+    def span(t):
+        return t.data_ptr(), t.data_ptr() + 8 * (1 + sum((e - 1) * st for e, st in zip(t.shape, t.stride())))
+
+    overlap = None
+    if out is not None:
+        o0, o1 = span(out)
+        overlap = [k for k, o in enumerate(ops) if span(o)[0] < o1 and o0 < span(o)[1]]
+    CHECK_LOG.append((overlap, eq, tuple(tuple(o.shape) for o in ops), tuple(tuple(o.stride()) for o in ops),
+                      None if out is None else (tuple(out.shape), tuple(out.stride())), alpha, beta, err))
+    return res
+
+
+def einsum(eq, *ops, out=None, alpha=1.0, beta=0.0, fused=False):
+    """`fused=True` lets the local-operator equations run as one fused launch (see ttk_einsum);
+    call sites whose results feed noise-level decisions keep the pairwise plan."""
+    if _CHECK_FUSED and fused and eq in _FUSED_EQS:
+        return _einsum_checked(eq, ops, out, alpha, beta)
+    return _einsum_native(eq, *ops, out=out, alpha=alpha, beta=beta, fused=fused)
+
+
+def _einsum_native(eq, *ops, out=None, alpha=1.0, beta=0.0, fused=False):
     """out = alpha * einsum(eq, *ops) + beta * out, on the device.  Planning (greedy pairwise
     order, offset tables) and execution (one fp64 MFMA GEMM launch per pairwise step) happen in
     the native engine `ttk_einsum` (csrc/ttk_einsum.hip); this wrapper only packs pointers,
     shapes and strides."""
-    desc = [len(ops)]
+    if OPSTATS is not None:
+        e = OPSTATS.setdefault("einsum_eq", {}).setdefault(eq, [0, 0.0])
+        e[0] += 1
+    desc = [len(ops) | (256 if fused else 0)]
     for o in ops:
         desc.append(o.data_ptr())
         desc.append(o.dim())
@@ -243,7 +287,8 @@ def matmul(a, b, out=None, alpha=1.0, beta=0.0):
 
 
 # ------------------------------------------------------------------------ factorisations
-_DUMP = {"min": int(os.environ.get("TTIPM_DUMP_SVD", "0")), "n": 0}
+_DUMP = {"min": int(os.environ.get("TTIPM_DUMP_SVD", "0")), "max": int(os.environ.get("TTIPM_DUMP_SVD_MAX", "1000000")),
+         "qmin": int(os.environ.get("TTIPM_DUMP_SVD_QMIN", "0")), "n": 0}
 
 
 def svd(A, defl=0.0):
@@ -252,7 +297,8 @@ def svd(A, defl=0.0):
     t0 = _tic() if OPSTATS is not None else 0
     A = A.contiguous()
     m, n = A.shape
-    if _DUMP["min"] and min(m, n) >= _DUMP["min"] and _DUMP["n"] < 12:  # dev diagnostics only
+    if _DUMP["min"] and _DUMP["min"] <= min(m, n) <= _DUMP["max"] and max(m, n) >= _DUMP["qmin"] \
+            and _DUMP["n"] < 12:  # dev diagnostics only
         os.makedirs("gpurun_out", exist_ok=True)
         np.save(f"gpurun_out/svd_in_{_DUMP['n']}.npy", read(A))
         _DUMP["n"] += 1

@@ -7,6 +7,7 @@ Local KKT solvers (`_ipm_local_solver`, `src/tt_ipm.py:183-282`; `_ipm_local_sol
 `:284-401`): dense Schur path = device assembly (MFMA GEMM), Cholesky, triangular solves, GEMMs
 and LU with the scipy rcond warning rule; iterative path = device LGMRES (PETSc semantics) on
 the Schur-reduced operator of `MatVecWrapper` (`cy_src/lgmres_cy.pyx:291-331`)."""
+import os
 import sys
 import traceback
 from dataclasses import dataclass
@@ -34,6 +35,10 @@ RHS = "br,bmB,BR->rmR"
 # inequality local solve raises.  Default: fixed (SURVEY.md §7 hard part 6).
 INEQ_MATVEC_BUG = False
 
+# LGMRES operator applies run as one fused launch each (Krylov iterates at rtol 1e-5 are insensitive
+# to the association order; the AMEn residuals keep the reference's pairwise order)
+FUSED_MATVEC = os.environ.get("TTIPM_FUSED_MATVEC", "1") == "1"
+
 
 class IneqMatvecBug(TypeError):
     pass
@@ -60,10 +65,10 @@ class MatVecWrapper:
         return [v[i * self.m:(i + 1) * self.m].view(r, n, R) for i in range(nb)]
 
     def _op(self, key, v, out, alpha=1.0, beta=0.0):
-        einsum(APPLY, self.L[key], self.A[key], self.R[key], v, out=out, alpha=alpha, beta=beta)
+        einsum(APPLY, self.L[key], self.A[key], self.R[key], v, out=out, alpha=alpha, beta=beta, fused=FUSED_MATVEC)
 
     def _schur_x(self, y):
-        einsum(APPLY_T, self.L[0, 1], self.A[0, 1], self.R[0, 1], y, out=self.tmp)
+        einsum(APPLY_T, self.L[0, 1], self.A[0, 1], self.R[0, 1], y, out=self.tmp, fused=FUSED_MATVEC)
         D.mul_(self.tmp, self.tmp, self.inv_I)
         return self.tmp
 

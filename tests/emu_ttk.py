@@ -64,7 +64,7 @@ class EmuLib:
         self.launches += 1
         eq = eq.decode() if isinstance(eq, bytes) else eq
         d = [int(v) for v in desc[:4096]]
-        nops, pos, views, shapes = d[0], 1, [], []
+        nops, pos, views, shapes = d[0] & 255, 1, [], []
         for _ in range(nops):
             ptr, nd = d[pos], d[pos + 1]
             shp, st = d[pos + 2:pos + 2 + nd], d[pos + 2 + nd:pos + 2 + 2 * nd]
@@ -89,6 +89,9 @@ class EmuLib:
             res = res + beta * ov
         ov[...] = res
         return 0
+
+    def ttk_einsum_set_fused(self, on):
+        return 1
 
     def ttk_einsum_stats(self, out):
         return 0
@@ -255,6 +258,9 @@ class EmuLib:
 
     def ttk_svd_set_big_threshold(self, p):
         return 64
+
+    def ttk_svd_set_timing(self, on):
+        return 0
 
     def ttk_debug_counters(self, out, reset):
         return 0

@@ -61,6 +61,35 @@ def test_einsum_strided_views_and_accumulate(dev):
     assert np.allclose(dev.read(big)[:, 1], ref / 2 + 0.5, rtol=1e-13, atol=1e-13)
 
 
+@pytest.mark.parametrize("eq", ["lsr,smnS,LSR,rnR->lmL", "lsr,smnS,LSR,lmL->rnR"])
+@pytest.mark.parametrize("dims", [(3, 2, 5, 4), (13, 10, 13, 4), (28, 11, 20, 4), (1, 1, 1, 4)])
+def test_fused_local_apply(dev, eq, dims):
+    """The one-launch local operator apply against NumPy and against the generic GEMM plan,
+    on strided operands (transposed operator view) with beta accumulation into a slice."""
+    from ttipm_amd._lib import lib
+    r, s, R, n = dims
+    rng = _rng(r * 7 + s)
+    P = rng.standard_normal((r + 1, s, r))
+    Q = rng.standard_normal((R + 2, s + 1, R))
+    A = rng.standard_normal((s, n, n, s + 1))
+    fwd = eq.endswith("lmL")
+    x = rng.standard_normal((r, n, R) if fwd else (r + 1, n, R + 2))
+    ref = np.einsum(eq, P, A.transpose(0, 2, 1, 3), Q, x)
+    dP, dQ, dx = dev.from_numpy(P), dev.from_numpy(Q), dev.from_numpy(x)
+    dA = dev.from_numpy(A).transpose(1, 2)  # strided view
+    out_full = dev.from_numpy(np.ones((2,) + ref.shape))
+    dev.einsum(eq, dP, dA, dQ, dx, out=out_full[1], alpha=2.0, beta=-1.0, fused=True)
+    got = dev.read(out_full)
+    assert np.allclose(got[1], 2.0 * ref - 1.0, rtol=1e-12, atol=1e-12 * np.abs(ref).max())
+    assert np.all(got[0] == 1.0)
+    old = lib.ttk_einsum_set_fused(0)
+    try:
+        plain = dev.read(dev.einsum(eq, dP, dA, dQ, dx))
+    finally:
+        lib.ttk_einsum_set_fused(old)
+    assert np.allclose(plain, ref, rtol=1e-12, atol=1e-12 * np.abs(ref).max())
+
+
 def test_mfma_layout_asymmetric(dev):
     """A = I with an asymmetric B catches transposed C/D fragment maps."""
     B = np.arange(32 * 32, dtype=np.float64).reshape(32, 32)

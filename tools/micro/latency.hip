@@ -29,6 +29,22 @@ __global__ void k_sync(int iters, unsigned long long *out, int mode, int div) {
       acc = sqrt(acc + 1.0);
     } else if (mode == 6) {  // group_sum_rt(g=2)
       acc = ttk::group_sum_rt(acc, 2) * 0.5 + 1.0;
+    } else if (mode == 7) {  // 8 dependent fp64 FMAs
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc = fma(acc, 0.999999, 1e-9);
+    } else if (mode == 8) {  // 8 dependent fp32 FMAs
+      float f = (float)acc;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) f = fmaf(f, 0.999999f, 1e-9f);
+      acc = f;
+    } else if (mode == 9) {  // 2 x 8 independent fp64 FMA chains
+      double b2 = acc + 1.0;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        acc = fma(acc, 0.999999, 1e-9);
+        b2 = fma(b2, 0.999999, 1e-9);
+      }
+      acc += b2;
     }
   }
   const unsigned long long t1 = wall_clock64(), c1 = clock64();
@@ -43,10 +59,10 @@ int main() {
   unsigned long long *d, h[3];
   hipMalloc(&d, 3 * sizeof(unsigned long long));
   const char *names[] = {"barrier", "lds+2 barriers", "int modulo", "wave_sum (DPP)", "fp64 div", "fp64 sqrt",
-                         "group_sum g=2"};
+                         "group_sum g=2", "8 dep fp64 fma", "8 dep fp32 fma", "2x8 fp64 fma"};
   const int iters = 20000;
-  for (int threads : {64, 256, 1024}) {
-    for (int mode = 0; mode < 7; ++mode) {
+  for (int threads : {64}) {
+    for (int mode = 0; mode < 10; ++mode) {
       hipLaunchKernelGGL(k_sync, dim3(1), dim3(threads), 0, 0, iters, d, mode, 7);
       hipMemcpy(h, d, sizeof(h), hipMemcpyDeviceToHost);
       const double ns = h[0] * 10.0 / iters;  // wall_clock64 = 100 MHz

@@ -44,6 +44,10 @@ from ttipm_amd import dev as _D  # noqa: E402
 ops = ""
 if _D.OPSTATS is not None:
     for name, d in _D.OPSTATS.items():
+        if name == "einsum_eq":
+            ops += "EINSUM equations by calls:\n" + "".join(
+                f"   {c[0]:8d}  {eq}\n" for eq, c in sorted(d.items(), key=lambda kv: -kv[1][0])[:30])
+            continue
         tot = sum(v[1] for v in d.values())
         cnt = sum(v[0] for v in d.values())
         ops += f"OP {name}: {cnt} calls {tot:.3f}s\n"

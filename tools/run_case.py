@@ -8,6 +8,10 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import yaml  # noqa: E402
 
 from ttipm_amd.utils import run_and_record  # noqa: E402
+from ttipm_amd._lib import lib  # noqa: E402
+
+if os.environ.get("TTIPM_FUSED") == "0":
+    lib.ttk_einsum_set_fused(0)
 
 prob, cfg_name, seed, rank = sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4])
 key = sys.argv[5] if len(sys.argv) > 5 else f"{cfg_name}_r{rank}_s{seed}"
@@ -21,5 +25,7 @@ if g:
     for k in ("num_iters", "gap", "feas", "dual_feas", "ranksX", "ranksZ"):
         print(f"{k:10s} gpu={r[k]} ref={g[k]}")
     for a, b in zip(trace, g["trace"]):
-        print(f"mu {a['mu']:.6e} {b['mu']:.6e}  primal {a['primal_error']:.6e} {b['primal_error']:.6e}  ranks {a['ranksX']} {b['ranksX']}")
-json.dump({"result": r, "trace": trace}, open(f"gpurun_out/run_{key}.json", "w"), indent=1)
+        print(f"mu {a['mu']:.6e} {b['mu']:.6e}  primal {a['primal_error']:.6e} {b['primal_error']:.6e}  "
+          f"sigma {a['sigma']:.4e} {b['sigma']:.4e}  ranks {a['ranksX']} {b['ranksX']}")
+tag = os.environ.get("TTIPM_TAG", "")
+json.dump({"result": r, "trace": trace}, open(f"gpurun_out/run_{key}{tag}.json", "w"), indent=1)
