@@ -1108,16 +1108,166 @@ __global__ __launch_bounds__(1024) void syev_kernel(double *__restrict__ Ain, in
 //   4. back-transform y = H_0 ... H_{n-3} z by one wave.
 // ~4/3 n^3 flops once, against ~10 sweeps x 4 n^3 for cyclic Jacobi; only the extreme pair is
 // used on the path (`_min_eigpair` / `_gen_max_eig` in tt_eig.py).
-int64_t syev_extreme_need(int n) { return (int64_t)n * n + 12 * (int64_t)n + 16; }
+// Phases 2-4 of the extreme eigenpair, shared by the one-workgroup kernel and the finish kernel of
+// the multi-workgroup tridiagonalisation: T from the reduced A (reflectors kept in A's rows), Sturm
+// multisection, inverse iteration, back-transform.
+__device__ void tridiag_extreme_finish(double *A, int n, int which, double *dv, double *ov, double *ev2, double *tv,
+                                       double *z, double *fd, double *fdu, double *fdu2, double *fdl, double *fpiv,
+                                       double *__restrict__ ev_out, double *__restrict__ vec_out) {
+  __shared__ double sh_a, sh_b;
+  __shared__ int sh_first;
+  const int tid = threadIdx.x, nt = blockDim.x;
+  const int lane = tid & 63, wid = tid >> 6;
+  if (tid == 0) {
+    if (n >= 2) {
+      dv[n - 2] = A[(int64_t)(n - 2) * n + n - 2];
+      ov[n - 2] = A[(int64_t)(n - 2) * n + n - 1];
+      tv[n - 2] = 0.0;
+    }
+    dv[n - 1] = A[(int64_t)(n - 1) * n + n - 1];
+  }
+  __syncthreads();
+  for (int i = tid; i + 1 < n; i += nt) ev2[i] = ov[i] * ov[i];
+  __syncthreads();
+  // Gershgorin bracket
+  double lo = 1e308, hi = -1e308, emax2 = 0.0;
+  for (int i = 0; i < n; ++i) {
+    const double r = (i > 0 ? fabs(ov[i - 1]) : 0.0) + (i + 1 < n ? fabs(ov[i]) : 0.0);
+    lo = fmin(lo, dv[i] - r);
+    hi = fmax(hi, dv[i] + r);
+    if (i + 1 < n) emax2 = fmax(emax2, ev2[i]);
+  }
+  const double tnorm = fmax(fmax(fabs(lo), fabs(hi)), 1e-300);
+  const double pivmin = fmax(2.2250738585072014e-308 * fmax(emax2, 1.0), 1e-290);
+  const double pad = 2.0 * EPS * tnorm + 4.0 * pivmin;
+  lo -= pad;
+  hi += pad;
+  const int target = which ? n : 1;  // smallest x with #{eig < x} >= target
+  if (tid == 0) {
+    sh_a = lo;
+    sh_b = hi;
+  }
+  __syncthreads();
+  // ---- 2. multisection
+  for (int round = 0; round < 16; ++round) {
+    const double a = sh_a, b = sh_b;
+    if (b - a <= 2.0 * EPS * fmax(fabs(a), fabs(b)) + 2.0 * pivmin) break;
+    if (tid == 0) atomicAdd(&g_dbg[3], 1ull);
+    const double x = a + (b - a) * (double)(tid + 1) / (double)(nt + 1);
+    int cnt = 0;
+    double q = dv[0] - x;
+    if (fabs(q) < pivmin) q = -pivmin;
+    cnt += q < 0.0;
+    for (int i = 1; i < n; ++i) {
+      q = dv[i] - x - ev2[i - 1] * fast_rcp(q);
+      if (fabs(q) < pivmin) q = -pivmin;
+      cnt += q < 0.0;
+    }
+    if (tid == 0) sh_first = nt;
+    __syncthreads();
+    if (cnt >= target) atomicMin(&sh_first, tid);
+    __syncthreads();
+    if (tid == 0) {
+      const int f = sh_first;
+      sh_a = (f == 0) ? a : a + (b - a) * (double)f / (double)(nt + 1);
+      sh_b = (f >= nt) ? b : a + (b - a) * (double)(f + 1) / (double)(nt + 1);
+    }
+    __syncthreads();
+  }
+  const double lam = 0.5 * (sh_a + sh_b);
+  if (tid == 0) atomicAdd(&g_dbg[2], 1ull);
+  // ---- 3. inverse iteration on T (thread 0, O(n) per solve)
+  if (tid == 0) {
+    for (int i = 0; i < n; ++i) {
+      fd[i] = dv[i] - lam;
+      fdu[i] = (i + 1 < n) ? ov[i] : 0.0;
+      fdl[i] = fdu[i];
+      fdu2[i] = 0.0;
+      fpiv[i] = 0.0;
+    }
+    for (int i = 0; i + 1 < n; ++i) {  // dgttrf
+      if (fabs(fd[i]) >= fabs(fdl[i])) {
+        if (fd[i] != 0.0) {
+          const double f = fdl[i] * fast_rcp(fd[i]);
+          fdl[i] = f;
+          fd[i + 1] -= f * fdu[i];
+        }
+      } else {
+        const double f = fd[i] * fast_rcp(fdl[i]);
+        fd[i] = fdl[i];
+        fdl[i] = f;
+        const double t = fdu[i];
+        fdu[i] = fd[i + 1];
+        fd[i + 1] = t - f * fd[i + 1];
+        if (i + 2 < n) {
+          fdu2[i] = fdu[i + 1];
+          fdu[i + 1] = -f * fdu[i + 1];
+        }
+        fpiv[i] = 1.0;
+      }
+    }
+    const double tiny = EPS * tnorm;
+    for (int i = 0; i < n; ++i)
+      if (fabs(fd[i]) < tiny) fd[i] = copysign(tiny, fd[i] == 0.0 ? 1.0 : fd[i]);
+    uint32_t h = 0x9e3779b9u;  // fixed pseudo-random start (dstein uses a random start)
+    for (int i = 0; i < n; ++i) {
+      h ^= h << 13;
+      h ^= h >> 17;
+      h ^= h << 5;
+      z[i] = 0.5 + (double)(h & 0xffffff) / 16777216.0;
+    }
+    for (int i = 0; i < n; ++i) fd[i] = fast_rcp(fd[i]);  // store 1/U(i,i) for the solves
+    for (int it = 0; it < 3; ++it) {
+      for (int i = 0; i + 1 < n; ++i) {  // dgtts2 forward
+        if (fpiv[i] == 0.0) {
+          z[i + 1] -= fdl[i] * z[i];
+        } else {
+          const double t = z[i];
+          z[i] = z[i + 1];
+          z[i + 1] = t - fdl[i] * z[i];
+        }
+      }
+      z[n - 1] *= fd[n - 1];
+      if (n > 1) z[n - 2] = (z[n - 2] - fdu[n - 2] * z[n - 1]) * fd[n - 2];
+      for (int i = n - 3; i >= 0; --i) z[i] = (z[i] - fdu[i] * z[i + 1] - fdu2[i] * z[i + 2]) * fd[i];
+      double mx = 0.0;
+      for (int i = 0; i < n; ++i) mx = fmax(mx, fabs(z[i]));
+      const double sc = mx > 0.0 ? fast_rcp(mx) : 1.0;
+      for (int i = 0; i < n; ++i) z[i] *= sc;
+    }
+    double nn = 0.0;
+    for (int i = 0; i < n; ++i) nn += z[i] * z[i];
+    const double sc = 1.0 / sqrt(nn);
+    for (int i = 0; i < n; ++i) z[i] *= sc;
+    ev_out[0] = lam;
+  }
+  __syncthreads();
+  // ---- 4. back-transform by wave 0 (no block barriers inside)
+  if (wid == 0) {
+    for (int k = n - 3; k >= 0; --k) {
+      const double tau = tv[k];
+      if (tau == 0.0) continue;
+      const double *v = A + (int64_t)k * n + k + 1;
+      double *zk = z + k + 1;
+      const int m = n - k - 1;
+      double acc = 0.0;
+      for (int j = lane; j < m; j += 64) acc += v[j] * zk[j];
+      acc = tau * ttk::wave_sum(acc);
+      for (int j = lane; j < m; j += 64) zk[j] -= acc * v[j];
+      __threadfence_block();
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < n; i += nt) vec_out[i] = z[i];
+}
+
+int64_t syev_extreme_need(int n) { return (int64_t)n * n + 13 * (int64_t)n + 32; }
 
 __global__ __launch_bounds__(1024) void syev_extreme_kernel(const double *__restrict__ Ain, int n, int which,
                                                             double *__restrict__ ev_out,
                                                             double *__restrict__ vec_out,
                                                             double *__restrict__ gwork, int use_lds) {
   extern __shared__ double lds[];
-  __shared__ double red[16];
-  __shared__ double sh_a, sh_b;
-  __shared__ int sh_first;
   double *A = use_lds ? lds : gwork;
   double *dv = A + (int64_t)n * n;  // diag(T)
   double *ov = dv + n;              // offdiag(T)
@@ -1184,146 +1334,107 @@ __global__ __launch_bounds__(1024) void syev_extreme_kernel(const double *__rest
     }
     __syncthreads();
   }
-  if (tid == 0) {
-    if (n >= 2) {
-      dv[n - 2] = A[(int64_t)(n - 2) * n + n - 2];
-      ov[n - 2] = A[(int64_t)(n - 2) * n + n - 1];
-      tv[n - 2] = 0.0;
+  tridiag_extreme_finish(A, n, which, dv, ov, ev2, tv, z, fd, fdu, fdu2, fdl, fpiv, ev_out, vec_out);
+}
+
+// Multi-workgroup Householder tridiagonalisation for n beyond LDS: per reflector k two launches over
+// row blocks of TRB rows, (1) rank-2 update of step k-1 on the block's rows, then the block owning
+// row k builds reflector k; (2) p = tau A22 v on the block's rows and the block's part of p^T v.
+// A is n x n row-major in global scratch; the reflectors stay in A's rows as in the LDS kernel.
+constexpr int TRB = 16;
+
+__global__ __launch_bounds__(256) void tri_update_kernel(double *A, int n, int k, double *tv, double *ov, double *dv,
+                                                         const double *pv, const double *partials, int nblk) {
+  __shared__ double red[16];
+  __shared__ double sK;
+  const int tid = threadIdx.x, nt = blockDim.x, lane = tid & 63, wid = tid >> 6, nw = nt >> 6;
+  const int r0 = blockIdx.x * TRB, r1 = r0 + TRB < n ? r0 + TRB : n;
+  const int kp = k - 1;
+  if (kp >= 0 && r1 > kp + 1) {
+    const double taup = tv[kp];
+    if (taup != 0.0) {
+      if (wid == 0) {
+        double acc = 0.0;
+        for (int i = lane; i < nblk; i += 64) acc += partials[i];
+        acc = ttk::wave_sum(acc);
+        if (lane == 0) sK = 0.5 * taup * acc;
+      }
+      __syncthreads();
+      const double K = sK;
+      const double *v = A + (int64_t)kp * n + kp + 1;
+      const int m = n - kp - 1;
+      const int rs = r0 > kp + 1 ? r0 : kp + 1;
+      for (int r = rs + wid; r < r1; r += nw) {
+        const int i = r - kp - 1;
+        const double vi = v[i], wi = pv[i] - K * vi;
+        double *ar = A + (int64_t)r * n + kp + 1;
+#pragma unroll 8
+        for (int j = lane; j < m; j += 64) {
+          const double vj = v[j];
+          ar[j] -= vi * (pv[j] - K * vj) + wi * vj;
+        }
+      }
     }
-    dv[n - 1] = A[(int64_t)(n - 1) * n + n - 1];
   }
-  __syncthreads();
-  for (int i = tid; i + 1 < n; i += nt) ev2[i] = ov[i] * ov[i];
-  __syncthreads();
-  // Gershgorin bracket
-  double lo = 1e308, hi = -1e308, emax2 = 0.0;
-  for (int i = 0; i < n; ++i) {
-    const double r = (i > 0 ? fabs(ov[i - 1]) : 0.0) + (i + 1 < n ? fabs(ov[i]) : 0.0);
-    lo = fmin(lo, dv[i] - r);
-    hi = fmax(hi, dv[i] + r);
-    if (i + 1 < n) emax2 = fmax(emax2, ev2[i]);
-  }
-  const double tnorm = fmax(fmax(fabs(lo), fabs(hi)), 1e-300);
-  const double pivmin = fmax(2.2250738585072014e-308 * fmax(emax2, 1.0), 1e-290);
-  const double pad = 2.0 * EPS * tnorm + 4.0 * pivmin;
-  lo -= pad;
-  hi += pad;
-  const int target = which ? n : 1;  // smallest x with #{eig < x} >= target
-  if (tid == 0) {
-    sh_a = lo;
-    sh_b = hi;
-  }
-  __syncthreads();
-  // ---- 2. multisection
-  for (int round = 0; round < 16; ++round) {
-    const double a = sh_a, b = sh_b;
-    if (b - a <= 2.0 * EPS * fmax(fabs(a), fabs(b)) + 2.0 * pivmin) break;
-    if (tid == 0) atomicAdd(&g_dbg[3], 1ull);
-    const double x = a + (b - a) * (double)(tid + 1) / (double)(nt + 1);
-    int cnt = 0;
-    double q = dv[0] - x;
-    if (fabs(q) < pivmin) q = -pivmin;
-    cnt += q < 0.0;
-    for (int i = 1; i < n; ++i) {
-      q = dv[i] - x - ev2[i - 1] / q;
-      if (fabs(q) < pivmin) q = -pivmin;
-      cnt += q < 0.0;
-    }
-    if (tid == 0) sh_first = nt;
+  if (k + 2 < n && k >= r0 && k < r1) {  // reflector k (dlarfg) from row k
     __syncthreads();
-    if (cnt >= target) atomicMin(&sh_first, tid);
+    double *x = A + (int64_t)k * n + k + 1;
+    const int m = n - k - 1;
+    double part = 0.0;
+    for (int i = 1 + tid; i < m; i += nt) part += x[i] * x[i];
+    const double sigma = ttk::block_sum(part, red);
+    const double alpha = x[0];
+    double tau = 0.0, beta = alpha;
+    if (sigma > 0.0) {
+      beta = -copysign(sqrt(alpha * alpha + sigma), alpha);
+      tau = (beta - alpha) / beta;
+      const double sc = 1.0 / (alpha - beta);
+      for (int i = 1 + tid; i < m; i += nt) x[i] *= sc;
+    }
     __syncthreads();
     if (tid == 0) {
-      const int f = sh_first;
-      sh_a = (f == 0) ? a : a + (b - a) * (double)f / (double)(nt + 1);
-      sh_b = (f >= nt) ? b : a + (b - a) * (double)(f + 1) / (double)(nt + 1);
-    }
-    __syncthreads();
-  }
-  const double lam = 0.5 * (sh_a + sh_b);
-  if (tid == 0) atomicAdd(&g_dbg[2], 1ull);
-  // ---- 3. inverse iteration on T (thread 0, O(n) per solve)
-  if (tid == 0) {
-    for (int i = 0; i < n; ++i) {
-      fd[i] = dv[i] - lam;
-      fdu[i] = (i + 1 < n) ? ov[i] : 0.0;
-      fdl[i] = fdu[i];
-      fdu2[i] = 0.0;
-      fpiv[i] = 0.0;
-    }
-    for (int i = 0; i + 1 < n; ++i) {  // dgttrf
-      if (fabs(fd[i]) >= fabs(fdl[i])) {
-        if (fd[i] != 0.0) {
-          const double f = fdl[i] / fd[i];
-          fdl[i] = f;
-          fd[i + 1] -= f * fdu[i];
-        }
-      } else {
-        const double f = fd[i] / fdl[i];
-        fd[i] = fdl[i];
-        fdl[i] = f;
-        const double t = fdu[i];
-        fdu[i] = fd[i + 1];
-        fd[i + 1] = t - f * fd[i + 1];
-        if (i + 2 < n) {
-          fdu2[i] = fdu[i + 1];
-          fdu[i + 1] = -f * fdu[i + 1];
-        }
-        fpiv[i] = 1.0;
-      }
-    }
-    const double tiny = EPS * tnorm;
-    for (int i = 0; i < n; ++i)
-      if (fabs(fd[i]) < tiny) fd[i] = copysign(tiny, fd[i] == 0.0 ? 1.0 : fd[i]);
-    uint32_t h = 0x9e3779b9u;  // fixed pseudo-random start (dstein uses a random start)
-    for (int i = 0; i < n; ++i) {
-      h ^= h << 13;
-      h ^= h >> 17;
-      h ^= h << 5;
-      z[i] = 0.5 + (double)(h & 0xffffff) / 16777216.0;
-    }
-    for (int it = 0; it < 3; ++it) {
-      for (int i = 0; i + 1 < n; ++i) {  // dgtts2 forward
-        if (fpiv[i] == 0.0) {
-          z[i + 1] -= fdl[i] * z[i];
-        } else {
-          const double t = z[i];
-          z[i] = z[i + 1];
-          z[i + 1] = t - fdl[i] * z[i];
-        }
-      }
-      z[n - 1] /= fd[n - 1];
-      if (n > 1) z[n - 2] = (z[n - 2] - fdu[n - 2] * z[n - 1]) / fd[n - 2];
-      for (int i = n - 3; i >= 0; --i) z[i] = (z[i] - fdu[i] * z[i + 1] - fdu2[i] * z[i + 2]) / fd[i];
-      double mx = 0.0;
-      for (int i = 0; i < n; ++i) mx = fmax(mx, fabs(z[i]));
-      const double sc = mx > 0.0 ? 1.0 / mx : 1.0;
-      for (int i = 0; i < n; ++i) z[i] *= sc;
-    }
-    double nn = 0.0;
-    for (int i = 0; i < n; ++i) nn += z[i] * z[i];
-    const double sc = 1.0 / sqrt(nn);
-    for (int i = 0; i < n; ++i) z[i] *= sc;
-    ev_out[0] = lam;
-  }
-  __syncthreads();
-  // ---- 4. back-transform by wave 0 (no block barriers inside)
-  if (wid == 0) {
-    for (int k = n - 3; k >= 0; --k) {
-      const double tau = tv[k];
-      if (tau == 0.0) continue;
-      const double *v = A + (int64_t)k * n + k + 1;
-      double *zk = z + k + 1;
-      const int m = n - k - 1;
-      double acc = 0.0;
-      for (int j = lane; j < m; j += 64) acc += v[j] * zk[j];
-      acc = tau * ttk::wave_sum(acc);
-      for (int j = lane; j < m; j += 64) zk[j] -= acc * v[j];
-      __threadfence_block();
+      x[0] = 1.0;
+      tv[k] = tau;
+      ov[k] = beta;
+      dv[k] = A[(int64_t)k * n + k];
     }
   }
-  __syncthreads();
-  for (int i = tid; i < n; i += nt) vec_out[i] = z[i];
+}
+
+__global__ __launch_bounds__(256) void tri_matvec_kernel(const double *__restrict__ A, int n, int k,
+                                                         const double *__restrict__ tv, double *__restrict__ pv,
+                                                         double *__restrict__ partials) {
+  __shared__ double red[16];
+  const int tid = threadIdx.x;
+  const int r0 = blockIdx.x * TRB, r1 = r0 + TRB < n ? r0 + TRB : n;
+  const double tau = tv[k];
+  const int m = n - k - 1;
+  const double *v = A + (int64_t)k * n + k + 1;
+  constexpr int G = 256 / TRB;  // lanes per row
+  const int gl = tid & (G - 1), rr = tid / G;
+  const int r = r0 + rr;
+  double contrib = 0.0;
+  if (tau != 0.0 && r < r1 && r >= k + 1) {
+    const double *ar = A + (int64_t)r * n + k + 1;
+    double acc = 0.0;
+#pragma unroll 8
+    for (int j = gl; j < m; j += G) acc += ar[j] * v[j];
+    acc = ttk::group_sum<G>(acc);
+    const int i = r - k - 1;
+    if (gl == 0) {
+      pv[i] = tau * acc;
+      contrib = tau * acc * v[i];
+    }
+  }
+  contrib = ttk::block_sum(contrib, red);
+  if (tid == 0) partials[blockIdx.x] = contrib;
+}
+
+__global__ __launch_bounds__(1024) void tri_finish_kernel(double *A, int n, int which, double *gv, double *ev_out,
+                                                          double *vec_out) {
+  double *dv = gv, *ov = dv + n, *ev2 = ov + n, *tv = ev2 + n, *z = tv + n;
+  double *fd = z + n, *fdu = fd + n, *fdu2 = fdu + n, *fdl = fdu2 + n, *fpiv = fdl + n;
+  tridiag_extreme_finish(A, n, which, dv, ov, ev2, tv, z, fd, fdu, fdu2, fdl, fpiv, ev_out, vec_out);
 }
 
 template <typename K>
@@ -2131,6 +2242,23 @@ int ttk_syev_extreme(void *stream, const double *A, int n, int which, double *ev
   }
   const int64_t need = syev_extreme_need(n);
   const int use_lds = need <= LDS_DOUBLES;
+  hipStream_t st = TTK_STREAM(stream);
+  if (!use_lds && n > 2) {  // multi-workgroup tridiagonalisation, one-workgroup finish
+    double *Aw = work, *gv = work + (int64_t)n * n;
+    double *dv = gv, *ov = dv + n, *tv = ov + 2 * n;  // layout of tri_finish_kernel: dv ov ev2 tv ...
+    double *pv = gv + 11 * (int64_t)n, *partials = gv + 12 * (int64_t)n;
+    const int nblk = (n + TRB - 1) / TRB;
+    TTK_HIP(hipMemcpyAsync(Aw, A, sizeof(double) * (size_t)n * n, hipMemcpyDeviceToDevice, st));
+    for (int k = 0; k + 2 < n; ++k) {
+      hipLaunchKernelGGL(tri_update_kernel, dim3(nblk), dim3(256), 0, st, Aw, n, k, tv, ov, dv, pv, partials, nblk);
+      hipLaunchKernelGGL(tri_matvec_kernel, dim3(nblk), dim3(256), 0, st, Aw, n, k, tv, pv, partials);
+      TTK_LAUNCH_CHECK();
+    }
+    hipLaunchKernelGGL(tri_update_kernel, dim3(nblk), dim3(256), 0, st, Aw, n, n - 2, tv, ov, dv, pv, partials, nblk);
+    hipLaunchKernelGGL(tri_finish_kernel, dim3(1), dim3(1024), 0, st, Aw, n, which, gv, ev, vec);
+    TTK_LAUNCH_CHECK();
+    return TTK_OK;
+  }
   const size_t shm = use_lds ? need * sizeof(double) : 0;
   allow_big_lds(syev_extreme_kernel, shm);
   int nt = 4 * n;

@@ -235,9 +235,13 @@ def _einsum_checked(eq, ops, out, alpha, beta):
     return res
 
 
+_FUSED_ALL = os.environ.get("TTIPM_FUSED_ALL") == "1"  # experiment switch: every local apply fused
+
+
 def einsum(eq, *ops, out=None, alpha=1.0, beta=0.0, fused=False):
     """`fused=True` lets the local-operator equations run as one fused launch (see ttk_einsum);
     call sites whose results feed noise-level decisions keep the pairwise plan."""
+    fused = fused or _FUSED_ALL
     if _CHECK_FUSED and fused and eq in _FUSED_EQS:
         return _einsum_checked(eq, ops, out, alpha, beta)
     return _einsum_native(eq, *ops, out=out, alpha=alpha, beta=beta, fused=fused)
