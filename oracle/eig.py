@@ -4,6 +4,7 @@
 Local eigenproblems go to SciPy ARPACK (`eigsh`, shift-invert via `splu`) or `lobpcg`
 exactly as the reference does; the MI355X product replaces them with device dense
 (generalised) symmetric eigensolvers."""
+import os
 import time
 
 import numpy as np
@@ -14,6 +15,8 @@ import scipy.sparse.linalg as spla
 from . import tt as T
 from .als import phi_bck_A, phi_fwd_A
 from .tt import einsum
+
+_DEBUG = bool(os.environ.get("TTIPM_EIG_DEBUG"))  # diagnostics: one line per local step-size solve
 
 
 def _v0(x):
@@ -129,14 +132,19 @@ def step_size_local_solve(p1, p2, XAX_k, A_k, A_kp1, XAX_k2, XDX_k, D_k, D_kp1, 
             ev = prev.T @ (M @ prev)
             sol = prev
         sol /= np.linalg.norm(sol)
+        step_in, branch, ev_in = step, "keep", float(np.ravel(ev)[0])
         if ev < 0:
             try:
                 ev, sol = spla.eigsh(-D, M=A, tol=eps, k=1, ncv=_ncv(m), which="LA", maxiter=_maxiter(m), v0=_v0(sol))
                 step = max(0, min(step, 1 / ev[0]))
+                branch = f"gen lam={ev[0]:.12e}"
             except Exception as e:
                 _quiet(e)
                 sol = prev
                 step *= (1 - eps)
+                branch = f"fail {type(e).__name__}"
+        if _DEBUG:
+            print(f"  ora two-site bwd={bwd} m={m} sh={sh} ev={ev_in:.6e} step {step_in:.12e} -> {step:.12e} {branch}")
         ev = prev.T @ (((1 / step) * A + D) @ prev)
         old_res = np.linalg.norm(((1 / step) * A + D) @ prev - ev * prev)
     else:
@@ -188,14 +196,19 @@ def step_size_local_solve_last(prev, XDX_k, Dk, XDX_k1, XAX_k, Ak, XAX_k1, dense
             _quiet(e)
             ev = prev.T @ ((1 / step) * A + D) @ prev
             sol = prev
+        step_in, branch, ev_in = step, "keep", float(np.ravel(ev)[0])
         if ev < 0:
             try:
                 ev, sol = spla.eigsh(-D, M=A, tol=eps, k=1, ncv=_ncv(m), which="LA", maxiter=_maxiter(m), v0=_v0(sol))
                 step = max(0, min(step, 1 / ev[0]))
+                branch = f"gen lam={ev[0]:.12e}"
             except Exception as e:
                 _quiet(e)
                 sol = prev
                 step *= (1 - eps)
+                branch = f"fail {type(e).__name__}"
+        if _DEBUG:
+            print(f"  ora one-site m={m} ev={ev_in:.6e} step {step_in:.12e} -> {step:.12e} {branch}")
         ev = prev.T @ ((1 / step) * A + D) @ prev
         old_res = np.linalg.norm(((1 / step) * A + D) @ prev - ev * prev)
     else:

@@ -8,7 +8,7 @@ import os
 import torch  # noqa: F401  -- load PyTorch's HIP runtime first so libttk binds to the same one
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libttk.so")
+LIB_PATH = os.environ.get("TTK_LIB_PATH") or os.path.join(HERE, "libttk.so")  # override: diagnostics builds
 
 if not os.path.exists(LIB_PATH):
     raise ImportError(f"libttk.so not found at {LIB_PATH}: run `python __graft_entry__.py build` "

@@ -1,34 +1,59 @@
-"""Build libttk.so for gfx950 (hipcc cross-compiles here; the .so travels to the GPU box)."""
+"""Build libttk.so for gfx950 (hipcc cross-compiles here; the .so travels to the GPU box).
+
+Each translation unit compiles to its own object in parallel (build/obj/), then one link."""
 import os
 import subprocess
 import sys
+from concurrent.futures import ThreadPoolExecutor
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libttk.so")
-SOURCES = ["ttk_runtime.hip", "ttk_contract.hip", "ttk_einsum.hip", "ttk_linalg.hip", "ttk_lgmres.hip"]
-HEADERS = ["ttk_common.h", os.path.join("..", "..", "include", "ttk.h")]
+SOURCES = ["ttk_runtime.hip", "ttk_contract.hip", "ttk_einsum.hip", "ttk_linalg.hip", "ttk_lgmres.hip",
+           "ttk_host.hip"]
+HEADERS = ["ttk_common.h", "ttk_internal.h", os.path.join("..", "..", "include", "ttk.h")]
+FLAGS = ["-O3", "-fPIC", "--offload-arch=gfx950", "-std=c++17", "-Wno-unused-variable",
+         "-Wno-unused-but-set-variable", "-I" + os.path.join(HERE, "..", "include")]
 
 
-def _stale():
-    if not os.path.exists(OUT):
+def _present(names):
+    return [os.path.join(CSRC, s) for s in names if os.path.exists(os.path.join(CSRC, s))]
+
+
+def _stale(out):
+    if not os.path.exists(out):
         return True
-    t = os.path.getmtime(OUT)
-    deps = [os.path.join(CSRC, s) for s in SOURCES + HEADERS if os.path.exists(os.path.join(CSRC, s))]
-    return any(os.path.getmtime(d) > t for d in deps)
+    t = os.path.getmtime(out)
+    return any(os.path.getmtime(d) > t for d in _present(SOURCES + HEADERS))
 
 
-def build(force=False, verbose=False):
-    if not force and not _stale():
-        return OUT
-    srcs = [os.path.join(CSRC, s) for s in SOURCES if os.path.exists(os.path.join(CSRC, s))]
-    cmd = ["hipcc", "-O3", "-fPIC", "-shared", "--offload-arch=gfx950", "-std=c++17",
-           "-Wno-unused-variable", "-Wno-unused-but-set-variable", "-o", OUT] + srcs
+def build(force=False, verbose=False, out=OUT, defines=()):
+    if not force and not _stale(out):
+        return out
+    tag = os.path.splitext(os.path.basename(out))[0]
+    objdir = os.path.join(HERE, "build", "obj", tag)
+    os.makedirs(objdir, exist_ok=True)
+    extra = [f"-D{d}" for d in defines]
+
+    def cc(src):
+        obj = os.path.join(objdir, os.path.basename(src) + ".o")
+        cmd = ["hipcc", "-c"] + FLAGS + extra + ["-o", obj, src]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.check_call(cmd, cwd=CSRC)
+        return obj
+
+    srcs = _present(SOURCES)
+    with ThreadPoolExecutor(max_workers=min(len(srcs), 6)) as ex:
+        objs = list(ex.map(cc, srcs))
+    cmd = ["hipcc", "-shared", "-fPIC", "--offload-arch=gfx950", "-o", out] + objs
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.check_call(cmd, cwd=CSRC)
-    return OUT
+    return out
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True))
+    defs = [a[2:] for a in sys.argv[1:] if a.startswith("-D")]
+    outs = [a[6:] for a in sys.argv[1:] if a.startswith("--out=")]
+    print(build(force="--force" in sys.argv, verbose=True, out=outs[0] if outs else OUT, defines=defs))

@@ -51,6 +51,9 @@ __device__ __forceinline__ void rr_pair(int P, int r, int k, int &p, int &q) {
 // 1/x and 1/sqrt(x) from the hardware estimates plus Newton steps (~1 ulp).  Rotation parameters
 // only need c^2 + s^2 = 1 to a few ulps; the IEEE div/sqrt expansions cost ~280 cycles each.
 __device__ __forceinline__ double fast_rcp(double x) {
+#ifdef TTK_EXACT_DIV
+  return 1.0 / x;
+#endif
   double r = __builtin_amdgcn_rcp(x);
   r = fma(fma(-x, r, 1.0), r, r);
   r = fma(fma(-x, r, 1.0), r, r);
@@ -58,6 +61,9 @@ __device__ __forceinline__ double fast_rcp(double x) {
 }
 
 __device__ __forceinline__ double fast_rsqrt(double x) {
+#ifdef TTK_EXACT_DIV
+  return 1.0 / sqrt(x);
+#endif
   double r = __builtin_amdgcn_rsq(x);
   double h = 0.5 * x * r;
   double e = fma(-h, r, 0.5);

@@ -7,6 +7,7 @@ or `lobpcg`, are solved exactly with the device extreme-eigenpair solver (`ttk_s
 generalised problem `-D v = lambda A v` goes through a device Cholesky of A.  The converged
 eigenpair is the same to the reference's tolerance (tol = 1e-8); ARPACK's failure branches
 (exceptions) map to the same fallbacks."""
+import os
 import time
 
 import numpy as np
@@ -19,6 +20,7 @@ from .tt_als import compute_phi_bck_A, compute_phi_fwd_A
 TWO_SITE = "lsr,smnk,kptS,LSR->lmpLrntR"
 ONE_SITE = "lsr,smnS,LSR->lmLrnR"
 MAX_DENSE = 4096
+_DEBUG = bool(os.environ.get("TTIPM_EIG_DEBUG"))  # diagnostics: one line per local step-size solve
 
 
 def _sym(Mt, m):
@@ -122,13 +124,18 @@ def _step_size_local_solve(p1, p2, XAX_k, A_k, A_kp1, XAX_k2, XDX_k, D_k, D_kp1,
     D.copy_(M, Dm, 1.0, 1.0)
     ev, sol = _min_eigpair(M)
     sol = _normalise(sol)
+    step_in, branch = step, "keep"
     if ev < 0:
         try:
             lam, sol = _gen_max_eig(Dm, Am)
             step = max(0, min(step, 1 / lam))
-        except Exception:
+            branch = f"gen lam={lam:.12e}"
+        except Exception as e:
             sol = prev
             step *= (1 - eps)
+            branch = f"fail {type(e).__name__}"
+    if _DEBUG:
+        print(f"  dev two-site bwd={bwd} m={m} sh={sh} ev={ev:.6e} step {step_in:.12e} -> {step:.12e} {branch}")
     _, old_res = _rayleigh(Am, Dm, step, prev)  # 1/step raises ZeroDivisionError at step 0, as in the reference
     sol = _normalise(sol)
     s1, s2 = _split(sol, sh, trunc_tol, max_rank, bwd)
@@ -147,13 +154,18 @@ def _step_size_local_solve_last(prev, XDX_k, Dk, XDX_k1, XAX_k, Ak, XAX_k1, step
     M = D.scaled(Am, 1.0 / step)
     D.copy_(M, Dm, 1.0, 1.0)
     ev, sol = _min_eigpair(M)
+    step_in, branch = step, "keep"
     if ev < 0:
         try:
             lam, sol = _gen_max_eig(Dm, Am)
             step = max(0, min(step, 1 / lam))
-        except Exception:
+            branch = f"gen lam={lam:.12e}"
+        except Exception as e:
             sol = prev
             step *= (1 - eps)
+            branch = f"fail {type(e).__name__}"
+    if _DEBUG:
+        print(f"  dev one-site m={m} ev={ev:.6e} step {step_in:.12e} -> {step:.12e} {branch}")
     old_res = _rayleigh(Am, Dm, step, prev)[1]
     return sol, step, old_res
 

@@ -141,6 +141,9 @@ def _fbsub_(LZ, B):
     return B
 
 
+_LOCAL_TRACE = bool(os.environ.get("TTIPM_LOCAL_TRACE"))  # diagnostics: one line per local KKT solve
+
+
 def _run_lgmres(op, rhs_flat, m, rtol):
     restart = min(m, 100)
     aug = max(restart // 10, 3)
@@ -230,6 +233,8 @@ def _ipm_local_solver(XAX_k, A_k, XAX_k1, Xb_k, b_k, Xb_k1, prev, size_limit, de
             einsum(APPLY_T, XAX_k[0, 1], A_k[0, 1], XAX_k1[0, 1], sol[:, 0], out=zt, alpha=-1.0, beta=1.0)
             D.mul_(sol[:, 2], inv_I, zt)
     res_new = _residual_norm(A_k, XAX_k, XAX_k1, sol, rhs, nrhs)
+    if _LOCAL_TRACE:
+        print(f"  local m={m} dense={dense_solve} failed={failed} res_old={res_old:.6e} res_new={res_new:.6e}")
     if res_old < res_new:
         sol = prev
     return sol, res_old, min(res_old, res_new), rhs, nrhs, failed
@@ -577,13 +582,36 @@ def _tt_get_ineq_step_sizes(xs, zs, X, Tt, DX, DT, mask, st):
     return xs, zs
 
 
+_DUMP_DIR = os.environ.get("TTIPM_DUMP_STEP")  # diagnostics: dump step-size eigenproblem inputs
+_dump_count = [0]
+
+
+def _dump_step_inputs(X, Z, DX, DZ, x0s, rng, xs, zs):
+    """Write the inputs/outputs of one `_tt_get_step_sizes` eigen pair to TTIPM_DUMP_STEP/step_NNN.npz
+    (replayed against the oracle by tools/replay_step.py)."""
+    arr = {"xs": xs, "zs": zs, "rng_key": rng[1], "rng_pos": rng[2], "rng_g": rng[3], "rng_c": rng[4]}
+    for name, tt in (("X", X), ("Z", Z), ("DX", DX), ("DZ", DZ), ("x0", x0s[0]), ("z0", x0s[1])):
+        if tt is None:
+            continue
+        arr[name + "/n"] = len(tt)
+        for i, c in enumerate(tt):
+            arr[f"{name}/{i}"] = D.read(c)
+    os.makedirs(_DUMP_DIR, exist_ok=True)
+    np.savez(os.path.join(_DUMP_DIR, f"step_{_dump_count[0]:03d}.npz"), **arr)
+    _dump_count[0] += 1
+
+
 def _tt_get_step_sizes(X, Z, Tt, DX, DZ, DT, mask, st):
     """`src/tt_ipm.py:700-727`"""
     if st.is_last_iter:
         X = T.tt_add(X, T.tt_scale(st.boundary_val, T.tt_identity(len(X))))
         Z = T.tt_add(Z, T.tt_scale(st.boundary_val, T.tt_identity(len(Z))))
+    x0s = (st.eigen_x0, st.eigen_z0)
+    rng = np.random.get_state()
     xs, st.eigen_x0 = tt_max_generalised_eigen(X, DX, x0=st.eigen_x0, tol=1e-8, verbose=st.verbose)
     zs, st.eigen_z0 = tt_max_generalised_eigen(Z, DZ, x0=st.eigen_z0, tol=1e-8, verbose=st.verbose)
+    if _DUMP_DIR:
+        _dump_step_inputs(X, Z, DX, DZ, x0s, rng, xs, zs)
     if st.ineq_status is not IneqStatus.NOT_IN_USE:
         if st.is_last_iter:
             X = T.tt_add(X, T.tt_scale(st.ineq_boundary_val + st.boundary_val, mask))
