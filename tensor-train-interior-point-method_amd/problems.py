@@ -130,7 +130,7 @@ def maxcut_create_problem(dim, rank, verbose=True):
         print(f"Creating Problem for dim={dim}, rank={rank}...")
     scale = np.sqrt(dim)
     g = T.tt_rank_reduce(tt_random_graph(dim, rank, verbose=verbose))
-    lap = T.tt_sub(T.tt_diag(T.tt_fast_matrix_vec_mul(g, _ones_vec(dim), 1e-12)), g)
+    lap = T.tt_sub(T.tt_diag(T._zipup_matrix_vec_mul(g, _ones_vec(dim), 1e-12)), g)
     L, b = _diag_constraint_op(dim)
     lag_y = T.tt_diag_op(T.tt_sub(T.tt_one_matrix(dim), T.tt_identity(dim)))
     return (T.tt_reshape(T.tt_normalise(lap, radius=scale), (4,)), L,
@@ -145,9 +145,9 @@ def corr_clust_create_problem(dim, rank, verbose=True):
     scale = np.sqrt(dim)
     g = T.tt_rank_reduce(tt_random_graph(dim, rank, verbose=verbose), 1e-10)
     mg = T.tt_rank_reduce(tt_random_graph(dim, 1, verbose=verbose), 1e-10)
-    sim = T.tt_rank_reduce(T.tt_fast_hadamard(g, mg, 1e-12), 1e-10)
-    dis = T.tt_rank_reduce(T.tt_fast_hadamard(g, T.tt_sub(T.tt_one_matrix(dim), mg), 1e-12), 1e-10)
-    lap = T.tt_sub(T.tt_diag(T.tt_fast_matrix_vec_mul(dis, _ones_vec(dim), 1e-12)), dis)
+    sim = T.tt_rank_reduce(T._zipup_hadamard(g, mg, 1e-12), 1e-10)
+    dis = T.tt_rank_reduce(T._zipup_hadamard(g, T.tt_sub(T.tt_one_matrix(dim), mg), 1e-12), 1e-10)
+    lap = T.tt_sub(T.tt_diag(T._zipup_matrix_vec_mul(dis, _ones_vec(dim), 1e-12)), dis)
     obj = T.tt_rank_reduce(T.tt_add(sim, lap), 1e-10)
     if verbose:
         print("Actual graph TT-rank:", T.tt_ranks(g))

@@ -13,6 +13,8 @@ Semantics kept from the reference:
 """
 from functools import reduce
 
+import os
+
 import numpy as np
 from . import dev as D
 
@@ -357,8 +359,8 @@ def _bubble(cores, i, eps):
         cores[j], cores[j + 1] = swap_cores(cores[j], cores[j + 1], eps)
 
 
-def tt_fast_matrix_vec_mul(mat, vec, eps=1e-18):
-    """`cy_src/tt_ops_cy.pyx:428-447`"""
+def _zipup_matrix_vec_mul(mat, vec, eps=1e-18):
+    """`cy_src/tt_ops_cy.pyx:428-447` as written (bubble zip-up); kept for the parity tests."""
     d = len(mat)
     leps = eps / np.sqrt(d - 1) if d > 1 else eps
     cores = [c.permute(2, 1, 0) for c in reversed(vec)]
@@ -369,8 +371,8 @@ def tt_fast_matrix_vec_mul(mat, vec, eps=1e-18):
     return cores
 
 
-def tt_fast_mat_mat_mul(m1, m2, eps=1e-18):
-    """`cy_src/tt_ops_cy.pyx:449-464`"""
+def _zipup_mat_mat_mul(m1, m2, eps=1e-18):
+    """`cy_src/tt_ops_cy.pyx:449-464` as written (bubble zip-up); kept for the parity tests."""
     d = len(m1)
     leps = eps / np.sqrt(d - 1) if d > 1 else eps
     cores = [c.permute(3, 1, 2, 0) for c in reversed(m2)]
@@ -381,8 +383,8 @@ def tt_fast_mat_mat_mul(m1, m2, eps=1e-18):
     return cores
 
 
-def tt_fast_hadamard(t1, t2, eps=1e-18):
-    """`cy_src/tt_ops_cy.pyx:466-502`"""
+def _zipup_hadamard(t1, t2, eps=1e-18):
+    """`cy_src/tt_ops_cy.pyx:466-502` as written (bubble zip-up); kept for the parity tests."""
     d = len(t1)
     leps = eps / np.sqrt(d - 1) if d > 1 else eps
     if t1[0].dim() == 4 and t2[0].dim() == 4:
@@ -398,6 +400,68 @@ def tt_fast_hadamard(t1, t2, eps=1e-18):
         if i != d - 1:
             _bubble(cores, i, leps)
     return cores
+
+
+# The reference's zip-up products contract each operator core into the reversed operand and
+# bubble it through the processed cores with a truncated SVD per swap (eps/sqrt(d-1), absolute),
+# i.e. d(d-1)/2 SVDs whose unfoldings live in a mode-permuted order: at maxcut_10 the bonds of
+# those intermediates reach ~220 (888 x 1024 swap matrices) even though the product itself has
+# rank <= rank_A * rank_x.  The device path computes the same product -- the exact core-wise
+# (Kronecker-bond) contraction, truncated to the same absolute accuracy by one TT rounding at eps
+# (QR sweep + d-1 truncated SVDs, `tt_rank_reduce`) -- so the represented tensor agrees with the
+# zip-up's to within the eps both truncate at, without the mode-swapped intermediates.  The
+# output ranks are the product's numerical ranks at eps (the zip-up's can only be larger, its
+# per-swap truncation is not optimal); every hot call site rounds the result again
+# (`tt_mat_vec_mul`, `tt_mat_mat_mul`, the residual / Y-update / centrality chains).
+# TTIPM_ZIPUP=1 restores the bubble zip-up everywhere (parity experiments).
+ZIPUP = os.environ.get("TTIPM_ZIPUP") == "1"
+
+
+def _kron_round(cores, eps):
+    if len(cores) > 1 and eps > 0:
+        return tt_rank_reduce(cores, eps)
+    return cores
+
+
+def tt_fast_matrix_vec_mul(mat, vec, eps=1e-18):
+    """`cy_src/tt_ops_cy.pyx:428-447`: mat (r_A,m,n,R_A) x vec (r,n,R) -> (r_A r, m, R_A R), rounded
+    at eps (see the note above)."""
+    if ZIPUP:
+        return _zipup_matrix_vec_mul(mat, vec, eps)
+    cores = []
+    for a, x in zip(mat, vec):
+        ra, m, _, Ra = a.shape
+        r, _, R = x.shape
+        cores.append(D.einsum("amnA,rnR->armAR", a, x).view(ra * r, m, Ra * R))
+    return _kron_round(cores, eps)
+
+
+def tt_fast_mat_mat_mul(m1, m2, eps=1e-18):
+    """`cy_src/tt_ops_cy.pyx:449-464`: core-wise matrix product, rounded at eps."""
+    if ZIPUP:
+        return _zipup_mat_mat_mul(m1, m2, eps)
+    cores = []
+    for a, b in zip(m1, m2):
+        ra, m, _, Ra = a.shape
+        rb, _, n, Rb = b.shape
+        cores.append(D.einsum("amkA,bknB->abmnAB", a, b).view(ra * rb, m, n, Ra * Rb))
+    return _kron_round(cores, eps)
+
+
+def tt_fast_hadamard(t1, t2, eps=1e-18):
+    """`cy_src/tt_ops_cy.pyx:466-502`: core-wise Hadamard product, rounded at eps."""
+    if ZIPUP:
+        return _zipup_hadamard(t1, t2, eps)
+    cores = []
+    four = t1[0].dim() == 4 and t2[0].dim() == 4
+    for a, b in zip(t1, t2):
+        if four:
+            cores.append(D.einsum("aijA,bijB->abijAB", a, b).view(a.shape[0] * b.shape[0], a.shape[1], a.shape[2],
+                                                                  a.shape[3] * b.shape[3]))
+        else:
+            cores.append(D.einsum("aiA,biB->abiAB", a, b).view(a.shape[0] * b.shape[0], a.shape[1],
+                                                             a.shape[2] * b.shape[2]))
+    return _kron_round(cores, eps)
 
 
 # ------------------------------------------------------------------ `src/tt_ops.py` helpers

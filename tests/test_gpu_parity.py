@@ -88,16 +88,24 @@ def test_rank_reduce(dev, ci):
 
 @pytest.mark.parametrize("ci", range(3))
 def test_zipup_products(dev, ci):
+    """Products against the reference zip-up's outputs.  The product path (exact core-wise product
+    rounded at eps, tt_ops.py note) must represent the same tensor to 1e-11 with ranks no larger
+    than the zip-up's (the zip-up's per-swap truncation is not optimal: zip0's first bond keeps 12
+    where the product's numerical rank is 4); the bubble zip-up restatement kept for parity
+    (`_zipup_*`) must also reproduce the reference's ranks."""
     from ttipm_amd import tt_ops as T
     Am, x, M1, M2 = (_tt(f"zip{ci}/{k}") for k in ("A", "x", "M1", "M2"))
     eps = float(G[f"zip{ci}/eps"])
-    mv = T.tt_fast_matrix_vec_mul(_up(dev, Am), _up(dev, x), eps)
-    _ranks_match(T.tt_ranks(mv), G[f"zip{ci}/mv_ranks"])
-    _close(_dense(_down(dev, mv)), G[f"zip{ci}/mv_dense"], 1e-11)
-    mm = T.tt_fast_mat_mat_mul(_up(dev, M1), _up(dev, M2), eps)
-    _ranks_match(T.tt_ranks(mm), G[f"zip{ci}/mm_ranks"])
-    _close(_dense(_down(dev, mm)), G[f"zip{ci}/mm_dense"], 1e-11)
+    for fast, zipup, key, a, b in ((T.tt_fast_matrix_vec_mul, T._zipup_matrix_vec_mul, "mv", Am, x),
+                                   (T.tt_fast_mat_mat_mul, T._zipup_mat_mat_mul, "mm", M1, M2)):
+        got = fast(_up(dev, a), _up(dev, b), eps)
+        assert all(int(r) <= int(w) for r, w in zip(T.tt_ranks(got), G[f"zip{ci}/{key}_ranks"]))
+        _close(_dense(_down(dev, got)), G[f"zip{ci}/{key}_dense"], 1e-11)
+        zz = zipup(_up(dev, a), _up(dev, b), eps)
+        _ranks_match(T.tt_ranks(zz), G[f"zip{ci}/{key}_ranks"])
+        _close(_dense(_down(dev, zz)), G[f"zip{ci}/{key}_dense"], 1e-11)
     _close(_dense(_down(dev, T.tt_fast_hadamard(_up(dev, M1), _up(dev, M2), eps))), G[f"zip{ci}/had_dense"], 1e-11)
+    _close(_dense(_down(dev, T._zipup_hadamard(_up(dev, M1), _up(dev, M2), eps))), G[f"zip{ci}/had_dense"], 1e-11)
     _close(np.array(T.tt_inner_prod(_up(dev, M1), _up(dev, M2))), G[f"zip{ci}/ip"], 1e-12)
 
 
