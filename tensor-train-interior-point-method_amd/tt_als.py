@@ -565,18 +565,150 @@ def tt_restarted_block_amen(block_A, block_b, rank_restriction, op_tol, terminat
                        "Consider increasing rank ceiling.")
 
 
+# ------------------------------------------------------------------ ALS approximate products
+_APPROX_EQ = {  # (local solution, backward environment, forward environment)
+    4: ("rab,amkA,bknB,RAB->rmnR", "RAB,amkA,bknB,rmnR->rab", "rab,amkA,bknB,rmnR->RAB"),
+    3: ("rab,amkA,bkB,RAB->rmR", "RAB,amkA,bkB,rmR->rab", "rab,amkA,bkB,rmR->RAB"),
+}
+
+
+def _tt_approx_product(A, Dm, x0, kick_rank, nswp, tol, verbose):
+    """Shared body of `tt_approx_mat_mat_mul` (`src/tt_als.py:1502-1628`) and
+    `tt_approx_mat_vec_mul` (`:1637-1762`): ALS projection of the product A.Dm onto a TT with
+    SVD truncation at tol/sqrt(d) and random kicks (host MT19937 draws in the reference's order);
+    environments are normalised and the scale carried in `nrmsc` exactly as the reference does."""
+    nd = Dm[0].dim()
+    e_loc, e_bck, e_fwd = _APPROX_EQ[nd]
+    if x0 is None:
+        mr = np.maximum((np.array(T.tt_ranks(A)) + np.array(T.tt_ranks(Dm))) / 2, 2).astype(int)
+        shape = tuple(A[0].shape[1:-1]) if nd == 4 else (A[0].shape[2],)
+        x = T.tt_random_gaussian(list(mr), shape)
+    else:
+        x = list(x0)
+        mr = np.array(T.tt_ranks(x0))
+    if kick_rank is None:
+        kick_rank = np.maximum(((T.symmetric_powers_of_two(len(A) - 1) - mr) / (nswp / 2)), 2).astype(int)
+    d = len(x)
+    rx = np.array([1] + T.tt_ranks(x) + [1])
+    modes = [tuple(c.shape[1:-1]) for c in x]
+    nmod = [int(np.prod(m)) for m in modes]
+    o3 = _ones3()
+    P = [o3] + [None] * (d - 1) + [o3]
+    nAD = np.ones(d - 1)
+    nrmsc = 1.0
+    nx = np.ones(d - 1)
+    tol = tol / np.sqrt(d)
+
+    def local(k):
+        return einsum(e_loc, P[k], A[k], Dm[k], P[k + 1], alpha=nrmsc)
+
+    def rel_change(sol, prev):
+        diff = D.clone(sol)
+        D.copy_(diff, prev, -1.0, 1.0)
+        return D.norm(diff) / max(D.norm(sol), 1e-8)
+
+    def unit(t):
+        nn = D.norm(t)
+        return D.scaled(t, 1.0 / nn), nn
+
+    last = False
+    swp = 0
+    mres = 0.0
+    for swp in range(nswp):
+        mres = np.inf if swp == 0 else 0
+        for k in range(d - 1, -1, -1):
+            if swp > 0:
+                sol = local(k)
+                mres = max(mres, rel_change(sol, x[k]))
+            else:
+                sol = D.contig(x[k])
+            if k > 0:
+                mat = D.clone(sol.view(rx[k], nmod[k] * rx[k + 1]).t())
+                U, S, Vt, s = D.svd(mat)
+                v = einsum("r,rj->rj", S, Vt)
+                r = T.prune_singular_vals(s, tol)
+                if not last:
+                    u, v, r = T.add_kick_rank(D.contig(U[:, :r]), D.contig(v[:r]), int(kick_rank[k - 1]))
+                else:
+                    u, v = U[:, :r], v[:r]
+                nrmsc *= nx[k - 1] / nAD[k - 1]
+                x[k] = D.clone(u.t()).view(r, *modes[k], rx[k + 1])
+                prev = D.contig(x[k - 1]).view(-1, rx[k])
+                x[k - 1], nn = unit(einsum("ic,jc->ij", prev, v).view(rx[k - 1], *modes[k - 1], r))
+                nx[k - 1] *= nn
+                rx[k] = r
+                Pk = einsum(e_bck, P[k + 1], A[k], Dm[k], x[k])
+                nrm = D.norm(Pk)
+                nrm = nrm if nrm > 0 else 1.0
+                P[k] = D.scaled(Pk, 1.0 / nrm)
+                nAD[k - 1] = nrm
+                nrmsc *= nAD[k - 1] / nx[k - 1]
+            else:
+                x[k] = D.contig(sol).view(rx[k], *modes[k], rx[k + 1])
+        if last:
+            break
+        if mres < tol or swp == nswp - 1:
+            last = True
+        mres = 0
+        for k in range(d):
+            sol = local(k)
+            mres = max(mres, rel_change(sol, x[k]))
+            if k < d - 1:
+                nrmsc *= nx[k] / nAD[k]
+                U, S, Vt, s = D.svd(D.contig(sol).view(rx[k] * nmod[k], rx[k + 1]))
+                v = einsum("r,rj->rj", S, Vt)
+                r = T.prune_singular_vals(s, tol)
+                if not last:
+                    u, v, r = T.add_kick_rank(D.contig(U[:, :r]), D.contig(v[:r]), int(kick_rank[k]))
+                else:
+                    u, v = U[:, :r], v[:r]
+                x[k] = D.contig(u).view(rx[k], *modes[k], r)
+                nxt = D.contig(x[k + 1]).view(rx[k + 1], -1)
+                x[k + 1], nn = unit(einsum("ij,jk->ik", v, nxt).view(r, *modes[k + 1], rx[k + 2]))
+                nx[k] *= nn
+                rx[k + 1] = r
+                Pk = einsum(e_fwd, P[k], A[k], Dm[k], x[k])
+                nrm = D.norm(Pk)
+                nrm = nrm if nrm > 0 else 1.0
+                P[k + 1] = D.scaled(Pk, 1.0 / nrm)
+                nAD[k] = nrm
+                nrmsc *= nAD[k] / nx[k]
+            else:
+                x[k] = D.contig(sol).view(rx[k], *modes[k], rx[k + 1])
+        if last:
+            break
+        if mres < tol:
+            last = True
+        if verbose:
+            print('\tStarting Sweep: %d' % swp)
+            print(f'\tResidual {mres}')
+            print(f"\tTT-sol rank: {T.tt_ranks(x)}", flush=True)
+    if verbose:
+        print(f"\t Solution rank is {rx[1:-1]}\n\t Residual {mres}\n\t Number of sweeps {swp + 1}", flush=True)
+    nxs = float(np.exp(np.sum(np.log(nx)) / d))
+    return [D.scaled(c, nxs) for c in x]
+
+
+def tt_approx_mat_mat_mul(A, Dm, x0=None, kick_rank=None, nswp=50, tol=1e-6, verbose=False):
+    """`src/tt_als.py:1502-1628`"""
+    return _tt_approx_product(A, Dm, x0, kick_rank, nswp, tol, verbose)
+
+
+def tt_approx_mat_vec_mul(A, d_vec, x0=None, kick_rank=None, nswp=50, tol=1e-6, verbose=False):
+    """`src/tt_als.py:1637-1762`"""
+    return _tt_approx_product(A, d_vec, x0, kick_rank, nswp, tol, verbose)
+
+
 # ------------------------------------------------------------------ product dispatch (`:1631-1768`)
 def tt_mat_mat_mul(m1, m2, op_tol, eps, verbose=False):
     """`src/tt_als.py:1631-1634`"""
     if np.max(np.array(T.tt_ranks(m1)) * np.array(T.tt_ranks(m2))) <= 40:
         return T.tt_rank_reduce(T.tt_fast_mat_mat_mul(m1, m2, eps), eps=op_tol)
-    raise NotImplementedError("tt_approx_mat_mat_mul (src/tt_als.py:1502-1634; SURVEY.md 8(f3)): rank product "
-                              "exceeds the exact zip-up limit 40")
+    return tt_approx_mat_mat_mul(m1, m2, tol=op_tol, verbose=verbose)
 
 
 def tt_mat_vec_mul(mat, vec, op_tol, eps, verbose=False):
     """`src/tt_als.py:1765-1768`"""
     if np.max(np.array(T.tt_ranks(mat)) * np.array(T.tt_ranks(vec))) <= 80:
         return T.tt_rank_reduce(T.tt_fast_matrix_vec_mul(mat, vec, eps), op_tol)
-    raise NotImplementedError("tt_approx_mat_vec_mul (src/tt_als.py:1637-1768; SURVEY.md 8(f3)): rank product "
-                              "exceeds the exact zip-up limit 80")
+    return tt_approx_mat_vec_mul(mat, vec, tol=op_tol, verbose=verbose)

@@ -108,66 +108,248 @@ def _check_dense(m):
         raise NotImplementedError(f"local eigenproblem of size {m} exceeds the dense device solver cap {MAX_DENSE}")
 
 
+class LobpcgFailure(UserWarning):
+    """scipy.sparse.linalg.lobpcg's UserWarnings (not converged / B-orthonormalisation failed), which
+    the reference turns into exceptions (`warnings.simplefilter("error")`, src/tt_ipm.py:16)."""
+
+
+def _lobpcg_maxiter(m):
+    """`src/tt_als.py:907-909`"""
+    return max(20, min(100, int(max(1, m))))
+
+
+def lobpcg(A, x0, B=None, tol=1e-8, maxiter=20, largest=True, restart_control=20):
+    """Single-vector LOBPCG on the device with scipy.sparse.linalg.lobpcg's control flow (scipy 1.15:
+    B-orthonormalisation by Cholesky, implicit Gram blocks until the residual drops below
+    sqrt(eps_mach), 3x3 Rayleigh-Ritz with a 2x2 restart, best-iterate return), used where the
+    reference calls `scp.sparse.linalg.lobpcg` (`src/tt_als.py:1006,1013,1114,1120,1320,1382`).
+    A, B: callables mapping a device vector (m,) to a new device vector.  The m-length work
+    (operator applies, axpys, the 3x6 Gram block as one GEMM) stays on the device; the host solves
+    the 3x3 pencil.  Non-convergence raises LobpcgFailure, as the reference's warnings do."""
+    import scipy.linalg as sla
+    m = x0.numel()
+    V = D.empty(3, m)    # X, R, P
+    W = D.empty(6, m)    # AX, AR, AP, BX, BR, BP
+    X, R, P = V[0], V[1], V[2]
+    AX, AR, AP, BX, BR, BP = W[0], W[1], W[2], W[3], W[4], W[5]
+
+    def apply(op, src, dst):
+        D.copy_(dst, op(src) if op is not None else src)
+
+    D.copy_(X, x0.reshape(-1))
+    apply(B, X, BX)
+    vbv = D.dot(X, BX)
+    if not vbv > 0:
+        raise ValueError("Linearly dependent initial approximations")
+    sc = 1.0 / np.sqrt(vbv)
+    D.copy_(X, X, sc)
+    D.copy_(BX, BX, sc)
+    apply(A, X, AX)
+    lam = D.dot(X, AX)
+    best = D.clone(X)
+    smallest = np.finfo(np.float64).max
+    it, restart, forced, explicit, have_p = -1, True, False, False, False
+    myeps = np.sqrt(np.finfo(np.float64).eps)
+    rn = np.inf
+    while it < maxiter:
+        it += 1
+        D.copy_(R, AX)
+        D.copy_(R, BX, -lam, 1.0)
+        rn = D.norm(R)
+        if rn < smallest:
+            smallest = rn
+            D.copy_(best, X)
+        elif rn > 2 ** restart_control * smallest:
+            forced = True
+            apply(A, X, AX)
+            apply(B, X, BX)
+        if not rn > tol:
+            break
+        D.copy_(R, X, -D.dot(BX, R), 1.0)  # R -= X (BX^T R)
+        apply(B, R, BR)
+        rbr = D.dot(R, BR)
+        if not rbr > 0:
+            raise LobpcgFailure(f"Failed at iteration {it} with accuracies {rn} not reaching the requested "
+                                f"tolerance {tol}.")
+        sc = 1.0 / np.sqrt(rbr)
+        D.copy_(R, R, sc)
+        D.copy_(BR, BR, sc)
+        apply(A, R, AR)
+        if it > 0:
+            pbp = D.dot(P, BP)
+            if pbp > 0:
+                sc = 1.0 / np.sqrt(pbp)
+                D.copy_(P, P, sc)
+                D.copy_(BP, BP, sc)
+                D.copy_(AP, AP, sc)
+                restart = forced
+            else:
+                restart = True
+        explicit = not (rn > myeps and not explicit)
+        G = D.read(einsum("im,jm->ij", V, W))  # rows X,R,P; cols AX,AR,AP,BX,BR,BP
+        xar, rar = G[0, 1], G[1, 1]
+        if explicit:
+            xax, xbx, rbr_, xbr = G[0, 0], G[0, 3], G[1, 4], G[0, 4]
+        else:
+            xax, xbx, rbr_, xbr = lam, 1.0, 1.0, 0.0
+        ev_vec = None
+        if not restart:
+            xap, rap, pap, xbp, rbp = G[0, 2], G[1, 2], G[2, 2], G[0, 5], G[1, 5]
+            pbp_ = G[2, 5] if explicit else 1.0
+            gA = np.array([[xax, xar, xap], [xar, rar, rap], [xap, rap, pap]])
+            gB = np.array([[xbx, xbr, xbp], [xbr, rbr_, rbp], [xbp, rbp, pbp_]])
+            try:
+                lams, vecs = sla.eigh(gA, gB, check_finite=False)
+                ev_vec = vecs
+            except np.linalg.LinAlgError:
+                restart = True
+        if restart:
+            gA = np.array([[xax, xar], [xar, rar]])
+            gB = np.array([[xbx, xbr], [xbr, rbr_]])
+            try:
+                lams, vecs = sla.eigh(gA, gB, check_finite=False)
+                ev_vec = vecs
+            except np.linalg.LinAlgError as e:
+                raise LobpcgFailure(f"eigh failed at iteration {it} with error {e}")
+        i = len(lams) - 1 if largest else 0
+        lam = float(lams[i])
+        c = ev_vec[:, i]
+        cx, cr = float(c[0]), float(c[1])
+        cp = float(c[2]) if not restart else 0.0
+        # pp = R cr + P cp (likewise A-, B-images), X = X cx + pp, P = pp
+        for vx, vr, vp in ((X, R, P), (AX, AR, AP), (BX, BR, BP)):
+            if not restart:
+                D.copy_(vp, vp, cp)
+                D.copy_(vp, vr, cr, 1.0)
+            else:
+                D.copy_(vp, vr, cr)
+            D.copy_(vx, vx, cx)
+            D.copy_(vx, vp, 1.0, 1.0)
+        have_p = True
+    D.copy_(R, AX)
+    D.copy_(R, BX, -lam, 1.0)
+    rn = D.norm(R)
+    if rn < smallest:
+        smallest = rn
+        D.copy_(best, X)
+    if rn > tol:
+        raise LobpcgFailure(f"Exited at iteration {it} with accuracies {rn} not reaching the requested "
+                            f"tolerance {tol}.")
+    return lam, best
+
+
+def _dense_step(prev, Am, Dm, step, eps, tag):
+    """dense branch of the step-size local solves: M = A/step + D, smallest eigenpair; if negative,
+    the largest lambda of -D v = lambda A v bounds the step (`src/tt_als.py:957-996,1060-1101`)."""
+    M = D.scaled(Am, 1.0 / step)
+    D.copy_(M, Dm, 1.0, 1.0)
+    ev, sol = _min_eigpair(M)
+    step_in, branch = step, "keep"
+    if tag == "two-site":
+        sol = _normalise(sol)
+    if ev < 0:
+        try:
+            lam, sol = _gen_max_eig(Dm, Am)
+            step = max(0, min(step, 1 / lam))
+            branch = f"gen lam={lam:.12e}"
+        except Exception as e:
+            sol = prev
+            step *= (1 - eps)
+            branch = f"fail {type(e).__name__}"
+    if _DEBUG:
+        print(f"  dev {tag} m={prev.numel()} ev={ev:.6e} step {step_in:.12e} -> {step:.12e} {branch}")
+    old_res = _rayleigh(Am, Dm, step, prev)[1]  # 1/step raises ZeroDivisionError at step 0, as the reference
+    return sol, step, old_res
+
+
+def _iterative_step(prev, apply_A, apply_D, step, eps, tag):
+    """LOBPCG branch of the step-size local solves (`src/tt_als.py:997-1021,1102-1127`):
+    A_op = A + 1e-12 I, D_op = -D, AD_op = A_op/step - D_op (reads the current step)."""
+    m = prev.numel()
+    st = [step]
+
+    def A_op(v):
+        out = apply_A(v)
+        D.copy_(out, v, 1e-12, 1.0)
+        return out
+
+    def D_op(v):
+        return D.scaled(apply_D(v), -1.0)
+
+    def AD_op(v):
+        out = D.scaled(A_op(v), 1.0 / st[0])
+        D.copy_(out, D_op(v), -1.0, 1.0)
+        return out
+
+    step_in, branch = step, "keep"
+    try:
+        ev, sol = lobpcg(AD_op, prev, tol=eps, largest=False, maxiter=_lobpcg_maxiter(m))
+    except Exception as e:
+        ev, sol = D.dot(prev, AD_op(prev)), prev
+        branch = f"lobpcg-fail {type(e).__name__}"
+    if tag == "two-site":
+        sol = _normalise(sol)
+    if ev < 0:
+        try:
+            lam, sol = lobpcg(D_op, sol, B=A_op, tol=eps, maxiter=_lobpcg_maxiter(m))
+            st[0] = max(0, min(st[0], 1 / lam))
+            branch = f"gen lam={lam:.12e}"
+        except Exception as e:
+            print(f"\tAttention: {e}")
+            sol = prev
+            st[0] *= (1 - eps)
+            branch = f"gen-fail {type(e).__name__}"
+    step = st[0]
+    if _DEBUG:
+        print(f"  dev {tag} lobpcg m={m} ev={ev:.6e} step {step_in:.12e} -> {step:.12e} {branch}")
+    ADp = AD_op(prev)
+    evp = D.dot(prev, ADp)
+    D.copy_(ADp, prev, -evp, 1.0)
+    return sol, step, D.norm(ADp)
+
+
 def _step_size_local_solve(p1, p2, XAX_k, A_k, A_kp1, XAX_k2, XDX_k, D_k, D_kp1, XDX_k2, step, size_limit,
                            trunc_tol, eps, max_rank, bwd=True):
-    """`_step_size_local_solve` (`src/tt_als.py:931-1038`)."""
+    """`_step_size_local_solve` (`src/tt_als.py:931-1038`): dense exact local eigensolve when
+    r*R <= size_limit (the reference's ARPACK branch), device LOBPCG otherwise (its lobpcg branch)."""
     if (not np.isfinite(step)) or step <= 0:
         return p1, p2, 0.0, np.inf
     prev = einsum("rny,ytR->rntR", p1, p2)
     sh = tuple(prev.shape)
     m = int(np.prod(sh))
-    _check_dense(m)
-    prev = prev.view(-1)
-    Dm = _sym(einsum(TWO_SITE, XDX_k, D_k, D_kp1, XDX_k2), m)
-    Am = _sym(einsum(TWO_SITE, XAX_k, A_k, A_kp1, XAX_k2), m)
-    M = D.scaled(Am, 1.0 / step)
-    D.copy_(M, Dm, 1.0, 1.0)
-    ev, sol = _min_eigpair(M)
-    sol = _normalise(sol)
-    step_in, branch = step, "keep"
-    if ev < 0:
-        try:
-            lam, sol = _gen_max_eig(Dm, Am)
-            step = max(0, min(step, 1 / lam))
-            branch = f"gen lam={lam:.12e}"
-        except Exception as e:
-            sol = prev
-            step *= (1 - eps)
-            branch = f"fail {type(e).__name__}"
-    if _DEBUG:
-        print(f"  dev two-site bwd={bwd} m={m} sh={sh} ev={ev:.6e} step {step_in:.12e} -> {step:.12e} {branch}")
-    _, old_res = _rayleigh(Am, Dm, step, prev)  # 1/step raises ZeroDivisionError at step 0, as in the reference
+    if sh[0] * sh[-1] <= size_limit:
+        _check_dense(m)
+        pv = prev.view(-1)
+        Dm = _sym(einsum(TWO_SITE, XDX_k, D_k, D_kp1, XDX_k2), m)
+        Am = _sym(einsum(TWO_SITE, XAX_k, A_k, A_kp1, XAX_k2), m)
+        sol, step, old_res = _dense_step(pv, Am, Dm, step, eps, "two-site")
+    else:
+        pv = prev.view(-1)
+        eq = "lsr,smnk,kptS,LSR,rntR->lmpL"
+        sol, step, old_res = _iterative_step(
+            pv, lambda v: einsum(eq, XAX_k, A_k, A_kp1, XAX_k2, v.view(*sh)).view(-1),
+            lambda v: einsum(eq, XDX_k, D_k, D_kp1, XDX_k2, v.view(*sh)).view(-1), step, eps, "two-site")
     sol = _normalise(sol)
     s1, s2 = _split(sol, sh, trunc_tol, max_rank, bwd)
     return s1, s2, step, old_res
 
 
-def _step_size_local_solve_last(prev, XDX_k, Dk, XDX_k1, XAX_k, Ak, XAX_k1, step, eps):
-    """`_step_size_local_solve_last` (`src/tt_als.py:1056-1129`)."""
+def _step_size_local_solve_last(prev, XDX_k, Dk, XDX_k1, XAX_k, Ak, XAX_k1, dense, step, eps):
+    """`_step_size_local_solve_last` (`src/tt_als.py:1056-1129`); `dense` is the reference's
+    sqrt(r R) < size_limit flag."""
     if (not np.isfinite(step)) or step <= 0:
         return prev.reshape(-1) if prev.is_contiguous() else D.clone(prev).view(-1), 0.0, np.inf
     m = int(np.prod(prev.shape))
-    _check_dense(m)
-    prev = D.contig(prev).view(-1)
-    Dm = _sym(einsum(ONE_SITE, XDX_k, Dk, XDX_k1), m)
-    Am = _sym(einsum(ONE_SITE, XAX_k, Ak, XAX_k1), m)
-    M = D.scaled(Am, 1.0 / step)
-    D.copy_(M, Dm, 1.0, 1.0)
-    ev, sol = _min_eigpair(M)
-    step_in, branch = step, "keep"
-    if ev < 0:
-        try:
-            lam, sol = _gen_max_eig(Dm, Am)
-            step = max(0, min(step, 1 / lam))
-            branch = f"gen lam={lam:.12e}"
-        except Exception as e:
-            sol = prev
-            step *= (1 - eps)
-            branch = f"fail {type(e).__name__}"
-    if _DEBUG:
-        print(f"  dev one-site m={m} ev={ev:.6e} step {step_in:.12e} -> {step:.12e} {branch}")
-    old_res = _rayleigh(Am, Dm, step, prev)[1]
-    return sol, step, old_res
+    xs = tuple(prev.shape)
+    pv = D.contig(prev).view(-1)
+    if dense:
+        _check_dense(m)
+        Dm = _sym(einsum(ONE_SITE, XDX_k, Dk, XDX_k1), m)
+        Am = _sym(einsum(ONE_SITE, XAX_k, Ak, XAX_k1), m)
+        return _dense_step(pv, Am, Dm, step, eps, "one-site")
+    eq = "lsr,smnS,LSR,rnR->lmL"
+    return _iterative_step(pv, lambda v: einsum(eq, XAX_k, Ak, XAX_k1, v.view(*xs)).view(-1),
+                           lambda v: einsum(eq, XDX_k, Dk, XDX_k1, v.view(*xs)).view(-1), step, eps, "one-site")
 
 
 def _res_stalled(prev, res, tol):
@@ -214,7 +396,7 @@ def tt_max_generalised_eigen(A, Delta, x0=None, nswp=10, tol=1e-8, size_limit=25
         nonlocal step
         for k in range(d):
             sol, step, _ = _step_size_local_solve_last(x[k], XDX[k], Delta[k], XDX[k + 1], XAX[k], A[k], XAX[k + 1],
-                                                       step, tol)
+                                                       np.sqrt(rx[k] * rx[k + 1]) < size_limit, step, tol)
             sol = sol.view(rx[k] * N[k], rx[k + 1])
             if k < d - 1:
                 U, S, Vt, s = D.svd(sol)
@@ -232,7 +414,7 @@ def tt_max_generalised_eigen(A, Delta, x0=None, nswp=10, tol=1e-8, size_limit=25
         nonlocal step
         for k in range(d - 1, -1, -1):
             sol, step, _ = _step_size_local_solve_last(x[k], XDX[k], Delta[k], XDX[k + 1], XAX[k], A[k], XAX[k + 1],
-                                                       step, tol)
+                                                       np.sqrt(rx[k] * rx[k + 1]) < size_limit, step, tol)
             if k > 0:
                 mat = D.clone(sol.view(rx[k], N[k] * rx[k + 1]).t())
                 U, S, Vt, s = D.svd(mat)
@@ -310,28 +492,57 @@ def tt_max_generalised_eigen(A, Delta, x0=None, nswp=10, tol=1e-8, size_limit=25
     return step, x
 
 
-def _eigen_local_solve(p1, p2, XAX_k, A_k, A_kp1, XAX_k2, trunc_tol, max_rank, bwd=True):
-    """`_eigen_local_solve` (`src/tt_als.py:1286-1343`) with a dense device eigensolve."""
+def _min_lobpcg(apply_A, prev):
+    """`lobpcg(A_op, X=prev, tol, largest=False)` with the reference's fallback to prev."""
+    m = prev.numel()
+    try:
+        return lobpcg(apply_A, prev, tol=_MIN_EIG_TOL[0], largest=False, maxiter=_lobpcg_maxiter(m))
+    except Exception as e:
+        if not isinstance(e, LobpcgFailure):
+            print(f"\tAttention: {e}")
+        return D.dot(prev, apply_A(prev)), prev
+
+
+_MIN_EIG_TOL = [1e-8]
+
+
+def _eigen_local_solve(p1, p2, XAX_k, A_k, A_kp1, XAX_k2, size_limit, trunc_tol, max_rank, bwd=True):
+    """`_eigen_local_solve` (`src/tt_als.py:1286-1343`): dense device eigensolve when
+    m <= size_limit (the reference's eigsh branch), device LOBPCG otherwise."""
     prev = einsum("rny,ytR->rntR", p1, p2)
     sh = tuple(prev.shape)
     m = int(np.prod(sh))
-    _check_dense(m)
     prev = prev.view(-1)
-    Am = _sym(einsum(TWO_SITE, XAX_k, A_k, A_kp1, XAX_k2), m)
-    ev, sol = _min_eigpair(Am)
-    Ap = D.matmul(Am, prev.view(-1, 1)).view(-1)
+    if m <= size_limit:
+        _check_dense(m)
+        Am = _sym(einsum(TWO_SITE, XAX_k, A_k, A_kp1, XAX_k2), m)
+        ev, sol = _min_eigpair(Am)
+        Ap = D.matmul(Am, prev.view(-1, 1)).view(-1)
+    else:
+        eq = "lsr,smnk,kptS,LSR,rntR->lmpL"
+
+        def apply_A(v):
+            return einsum(eq, XAX_k, A_k, A_kp1, XAX_k2, v.view(*sh)).view(-1)
+        ev, sol = _min_lobpcg(apply_A, prev)
+        Ap = apply_A(prev)
     D.copy_(Ap, prev, ev, -1.0)  # ev*prev - A prev
     old_res = D.norm(Ap)
     s1, s2 = _split(sol, sh, trunc_tol, max_rank, bwd)
     return s1, s2, old_res
 
 
-def _eigen_local_solve_last(prev, XAX_k, A_k, XAX_k1, m):
-    """`_eigen_local_solve_last` (`src/tt_als.py:1346-1389`)."""
-    _check_dense(m)
+def _eigen_local_solve_last(prev, XAX_k, A_k, XAX_k1, m, size_limit):
+    """`_eigen_local_solve_last` (`src/tt_als.py:1346-1389`): dense when r*R <= size_limit."""
+    xs = tuple(prev.shape)
+    dense = xs[0] * xs[-1] <= size_limit
     prev = D.contig(prev).view(-1)
-    Am = _sym(einsum(ONE_SITE, XAX_k, A_k, XAX_k1), m)
-    ev, sol = _min_eigpair(Am)
+    if dense:
+        _check_dense(m)
+        Am = _sym(einsum(ONE_SITE, XAX_k, A_k, XAX_k1), m)
+        ev, sol = _min_eigpair(Am)
+        return sol
+    eq = "lsr,smnS,LSR,rnR->lmL"
+    ev, sol = _min_lobpcg(lambda v: einsum(eq, XAX_k, A_k, XAX_k1, v.view(*xs)).view(-1), prev)
     return sol
 
 
@@ -346,10 +557,11 @@ def tt_min_eig(A, x0=None, nswp=10, tol=1e-8, size_limit=64, return_eig_val=Fals
     max_rank = int(np.floor(2 ** (d / 2)))
     trunc_tol = 0.1 * tol / np.sqrt(d)
     prev_res = np.inf
+    _MIN_EIG_TOL[0] = tol
 
     def finish_fwd():
         for k in range(d):
-            sol = _eigen_local_solve_last(x[k], XAX[k], A[k], XAX[k + 1], int(rx[k] * N[k] * rx[k + 1]))
+            sol = _eigen_local_solve_last(x[k], XAX[k], A[k], XAX[k + 1], int(rx[k] * N[k] * rx[k + 1]), size_limit)
             sol = sol.view(rx[k] * N[k], rx[k + 1])
             if k < d - 1:
                 U, S, Vt, s = D.svd(sol)
@@ -364,7 +576,7 @@ def tt_min_eig(A, x0=None, nswp=10, tol=1e-8, size_limit=64, return_eig_val=Fals
 
     def finish_bck():
         for k in range(d - 1, -1, -1):
-            sol = _eigen_local_solve_last(x[k], XAX[k], A[k], XAX[k + 1], int(rx[k] * N[k] * rx[k + 1]))
+            sol = _eigen_local_solve_last(x[k], XAX[k], A[k], XAX[k + 1], int(rx[k] * N[k] * rx[k + 1]), size_limit)
             if k > 0:
                 mat = D.clone(sol.view(rx[k], N[k] * rx[k + 1]).t())
                 U, S, Vt, s = D.svd(mat)
@@ -382,7 +594,7 @@ def tt_min_eig(A, x0=None, nswp=10, tol=1e-8, size_limit=64, return_eig_val=Fals
         for k in range(d - 1, 0, -1):
             if swp > 0:
                 x[k - 1], x[k], lr = _eigen_local_solve(x[k - 1], x[k], XAX[k - 1], A[k - 1], A[k], XAX[k + 1],
-                                                        trunc_tol, max_rank, bwd=True)
+                                                        size_limit, trunc_tol, max_rank, bwd=True)
                 max_res = max(max_res, lr)
             else:
                 x[k], vr, r = _svd_left(x, k, rx, N, trunc_tol, max_rank)
@@ -395,7 +607,7 @@ def tt_min_eig(A, x0=None, nswp=10, tol=1e-8, size_limit=64, return_eig_val=Fals
         max_res = 0
         for k in range(d - 1):
             x[k], x[k + 1], lr = _eigen_local_solve(x[k], x[k + 1], XAX[k], A[k], A[k + 1], XAX[k + 2],
-                                                    trunc_tol, max_rank, bwd=False)
+                                                    size_limit, trunc_tol, max_rank, bwd=False)
             max_res = max(max_res, lr)
             rx[k + 1] = x[k + 1].shape[0]
             XAX[k + 1] = compute_phi_fwd_A(XAX[k], x[k], A[k], x[k])

@@ -206,3 +206,24 @@ def test_full_solve_matches_reference(dev, key):
         tol = TRAJ_RTOL if i < len(trace) - 1 else FINAL_RTOL
         for k in ("mu", "primal_error", "dual_error", "centrality_error"):
             assert abs(a[k] - b[k]) <= tol * abs(b[k]) + 1e-14, (i, k, a[k], b[k])
+
+
+AP = np.load(os.path.join(HERE, "golden", "approx.npz"))
+
+
+@pytest.mark.parametrize("name", ["mm0", "mv0", "mm1"])
+def test_approx_products(dev, name):
+    """device ALS approximate products (`src/tt_als.py:1502-1762`) vs the reference's outputs."""
+    from ttipm_amd import tt_als as A
+    from ttipm_amd import tt_ops as T
+    a = [AP[f"{name}/a/{i}"].copy() for i in range(int(AP[f"{name}/a/n"]))]
+    b = [AP[f"{name}/b/{i}"].copy() for i in range(int(AP[f"{name}/b/n"]))]
+    np.random.seed(int(AP[f"{name}/seed"]))
+    fn = A.tt_approx_mat_mat_mul if b[0].ndim == 4 else A.tt_approx_mat_vec_mul
+    res = fn(_up(dev, a), _up(dev, b), tol=float(AP[f"{name}/tol"]))
+    assert np.random.randint(0, 1 << 30) == int(AP[f"{name}/next_randint"])
+    assert T.tt_ranks(res) == list(AP[f"{name}/ranks"])
+    t = dev.read(res[0])
+    for c in res[1:]:
+        t = np.tensordot(t, dev.read(c), axes=(-1, 0))
+    _close(t, AP[f"{name}/dense"], 1e-9)

@@ -51,3 +51,79 @@ def test_shard_pack_roundtrip(pkg):
             assert bool((a == b).all())
     s0, s1 = prep["rng_state"], back["rng_state"]
     assert s0[0] == s1[0] and np.array_equal(s0[1], s1[1]) and s0[2:] == s1[2:]
+
+
+APPROX = os.path.join(ROOT, "tests", "golden", "approx.npz")
+
+
+def _approx_case(name):
+    import numpy as np
+    f = np.load(APPROX)
+    tt = lambda k: [f[f"{name}/{k}/{i}"].copy() for i in range(int(f[f"{name}/{k}/n"]))]  # noqa: E731
+    return f, tt("a"), tt("b")
+
+
+def _dense(tt):
+    import numpy as np
+    t = tt[0]
+    for c in tt[1:]:
+        t = np.tensordot(t, c, axes=(-1, 0))
+    return t
+
+
+@pytest.mark.parametrize("name", ["mm0", "mv0", "mm1"])
+def test_approx_products_match_reference(pkg, name):
+    """ALS approximate products (`src/tt_als.py:1502-1762`, taken when a rank product exceeds the
+    exact limits 40/80): device host logic vs the reference's outputs (tests/golden/approx.npz),
+    same MT19937 stream (ranks, draw count and the represented tensor)."""
+    import numpy as np
+    from ttipm_amd import dev as D
+    from ttipm_amd import tt_als as A
+    f, a, b = _approx_case(name)
+    np.random.seed(int(f[f"{name}/seed"]))
+    fn = A.tt_approx_mat_mat_mul if b[0].ndim == 4 else A.tt_approx_mat_vec_mul
+    got = fn([D.from_numpy(c) for c in a], [D.from_numpy(c) for c in b], tol=float(f[f"{name}/tol"]))
+    assert np.random.randint(0, 1 << 30) == int(f[f"{name}/next_randint"])
+    got = [D.read(c) for c in got]
+    assert [c.shape[-1] for c in got[:-1]] == list(f[f"{name}/ranks"])
+    want = f[f"{name}/dense"]
+    assert np.max(np.abs(_dense(got) - want)) <= 1e-9 * np.max(np.abs(want))
+
+
+@pytest.mark.parametrize("gen,largest,n,maxiter", [(False, False, 60, 100), (True, True, 60, 100),
+                                                   (False, False, 400, 20), (True, True, 400, 20)])
+def test_lobpcg_matches_scipy(pkg, gen, largest, n, maxiter):
+    """device single-vector LOBPCG (tt_eig.lobpcg) vs scipy.sparse.linalg.lobpcg with warnings as
+    errors (the reference's setting): same outcome (converged / raises), same eigenvalue."""
+    import warnings
+    import numpy as np
+    import scipy.sparse.linalg as spla
+    from ttipm_amd import dev as D
+    from ttipm_amd import tt_eig as E
+    rng = np.random.RandomState(n + 7 * gen)
+    Q, _ = np.linalg.qr(rng.randn(n, n))
+    A = (Q * np.linspace(1.0, 40.0, n)) @ Q.T
+    Bm = None
+    if gen:
+        Bq, _ = np.linalg.qr(rng.randn(n, n))
+        Bm = (Bq * np.linspace(1.0, 3.0, n)) @ Bq.T
+    x0 = rng.randn(n, 1)
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")
+        try:
+            lam_ref, v_ref = spla.lobpcg(A, x0.copy(), B=Bm, tol=1e-8, largest=largest, maxiter=maxiter)
+            ref_ok = True
+        except UserWarning:
+            ref_ok = False
+    Ad = D.from_numpy(A)
+    Bd = D.from_numpy(Bm) if gen else None
+    opA = lambda v: D.matmul(Ad, v.view(-1, 1)).view(-1)  # noqa: E731
+    opB = (lambda v: D.matmul(Bd, v.view(-1, 1)).view(-1)) if gen else None  # noqa: E731
+    try:
+        lam, v = E.lobpcg(opA, D.from_numpy(x0.reshape(-1)), B=opB, tol=1e-8, largest=largest, maxiter=maxiter)
+        ok = True
+    except E.LobpcgFailure:
+        ok = False
+    assert ok == ref_ok
+    if ok:
+        assert abs(lam - float(lam_ref[0])) <= 1e-10 * abs(float(lam_ref[0]))

@@ -115,3 +115,22 @@ def test_oracle_full_run_maxcut5():
     for a, b in zip(trace, g["trace"]):
         assert a["ranksX"] == b["ranksX"]
         assert abs(a["mu"] - b["mu"]) <= 1e-5 * abs(b["mu"])
+
+
+AP = np.load(os.path.join(HERE, "golden", "approx.npz"))
+
+
+@pytest.mark.parametrize("name", ["mm0", "mv0", "mm1"])
+def test_approx_products(name):
+    """oracle ALS approximate products vs the reference's (same seed): ranks, draws, tensor."""
+    a = [AP[f"{name}/a/{i}"].copy() for i in range(int(AP[f"{name}/a/n"]))]
+    b = [AP[f"{name}/b/{i}"].copy() for i in range(int(AP[f"{name}/b/n"]))]
+    np.random.seed(int(AP[f"{name}/seed"]))
+    fn = A.approx_mat_mat_mul if b[0].ndim == 4 else A.approx_mat_vec_mul
+    res = fn(a, b, tol=float(AP[f"{name}/tol"]))
+    assert np.random.randint(0, 1 << 30) == int(AP[f"{name}/next_randint"])
+    assert T.ranks(res) == list(AP[f"{name}/ranks"])
+    t = res[0]
+    for c in res[1:]:
+        t = np.tensordot(t, c, axes=(-1, 0))
+    _close(t, AP[f"{name}/dense"], 1e-10)

@@ -18,7 +18,7 @@ key = sys.argv[5] if len(sys.argv) > 5 else f"{cfg_name}_r{rank}_s{seed}"
 cfg = yaml.safe_load(open(os.path.join("configs", cfg_name + ".yaml")))
 trace = []
 t = time.time()
-r = run_and_record(prob, cfg, seed, rank, trace=trace, verbose=False)
+r = run_and_record(prob, cfg, seed, rank, trace=trace, verbose=bool(os.environ.get("TTIPM_VERBOSE")))
 print("wall", time.time() - t)
 g = json.load(open("tests/golden/runs.json")).get(key)
 if g:
