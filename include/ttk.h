@@ -156,6 +156,10 @@ int ttk_syev(void *stream, double *A, int n, double *ev, double *W, double *work
  * calls of the step-size ALS (`src/tt_als.py:963-993` (_step_size_local_solve),
  * `:1069-1098`, `:1308` (_eigen_local_solve)). */
 int64_t ttk_syev_extreme_work(int n);
+/* 3 <= n <= 128 takes a latency-optimised 4-wave kernel (A in LDS, 3 barriers per reflector);
+ * on = 0 routes every size through the general one-workgroup / multi-workgroup kernels (tests).
+ * Returns the previous setting. */
+int ttk_syev_set_small(int on);
 /* diagnostic counters of the factorisation kernels (8 x u64: svd calls, svd sweeps, eig calls,
  * multisection rounds, ...); synchronous; reset != 0 zeroes them */
 int ttk_debug_counters(unsigned long long *out, int reset);

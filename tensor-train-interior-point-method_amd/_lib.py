@@ -49,6 +49,7 @@ _SIGS = {
     "ttk_syev_work": (i64, [i32]),
     "ttk_syev": (i32, [vp, vp, i32, vp, vp, vp]),
     "ttk_syev_extreme_work": (i64, [i32]),
+    "ttk_syev_set_small": (i32, [i32]),
     "ttk_debug_counters": (i32, [vp, i32]),
     "ttk_svd_set_timing": (i32, [i32]),
     "ttk_svd_set_big_threshold": (i32, [i32]),

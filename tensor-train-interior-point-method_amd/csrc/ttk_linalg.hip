@@ -1119,18 +1119,18 @@ __global__ __launch_bounds__(1024) void syev_kernel(double *__restrict__ Ain, in
 // multisection, inverse iteration, back-transform.
 __device__ void tridiag_extreme_finish(double *A, int n, int which, double *dv, double *ov, double *ev2, double *tv,
                                        double *z, double *fd, double *fdu, double *fdu2, double *fdl, double *fpiv,
-                                       double *__restrict__ ev_out, double *__restrict__ vec_out) {
+                                       double *__restrict__ ev_out, double *__restrict__ vec_out, int lda) {
   __shared__ double sh_a, sh_b;
   __shared__ int sh_first;
   const int tid = threadIdx.x, nt = blockDim.x;
   const int lane = tid & 63, wid = tid >> 6;
   if (tid == 0) {
     if (n >= 2) {
-      dv[n - 2] = A[(int64_t)(n - 2) * n + n - 2];
-      ov[n - 2] = A[(int64_t)(n - 2) * n + n - 1];
+      dv[n - 2] = A[(int64_t)(n - 2) * lda + n - 2];
+      ov[n - 2] = A[(int64_t)(n - 2) * lda + n - 1];
       tv[n - 2] = 0.0;
     }
-    dv[n - 1] = A[(int64_t)(n - 1) * n + n - 1];
+    dv[n - 1] = A[(int64_t)(n - 1) * lda + n - 1];
   }
   __syncthreads();
   for (int i = tid; i + 1 < n; i += nt) ev2[i] = ov[i] * ov[i];
@@ -1253,7 +1253,7 @@ __device__ void tridiag_extreme_finish(double *A, int n, int which, double *dv, 
     for (int k = n - 3; k >= 0; --k) {
       const double tau = tv[k];
       if (tau == 0.0) continue;
-      const double *v = A + (int64_t)k * n + k + 1;
+      const double *v = A + (int64_t)k * lda + k + 1;
       double *zk = z + k + 1;
       const int m = n - k - 1;
       double acc = 0.0;
@@ -1340,8 +1340,88 @@ __global__ __launch_bounds__(1024) void syev_extreme_kernel(const double *__rest
     }
     __syncthreads();
   }
-  tridiag_extreme_finish(A, n, which, dv, ov, ev2, tv, z, fd, fdu, fdu2, fdl, fpiv, ev_out, vec_out);
+  tridiag_extreme_finish(A, n, which, dv, ov, ev2, tv, z, fd, fdu, fdu2, fdl, fpiv, ev_out, vec_out, n);
 }
+
+// Small-n extreme eigenpair (n <= SYEV_SMALL_N), built for latency: 4 waves, A in LDS with an odd
+// leading dimension (row starts on different banks), 3 cheap 4-wave barriers per reflector.
+//   reflector  wave 0 (dlarfg on row k, which holds the sub-column by symmetry)
+//   p = tau A22 v   two lanes per row (row i -> lanes 2i, 2i+1 of one wave), halves combined by a
+//                   lane-pair shuffle; v read as LDS broadcasts
+//   K = tau/2 p^T v every wave redundantly (no barrier); w = p - K v kept in registers per column
+//   A22 -= v w^T + w v^T   one wave per row, lanes over columns (<= 2 per lane), A touched once
+// Same reflector convention (LAPACK dlarfg) and finish (Sturm multisection + inverse iteration) as
+// syev_extreme_kernel, so both paths produce the same eigenpair to rounding.
+constexpr int SYEV_SMALL_N = 128;
+
+__global__ __launch_bounds__(256) void syev_small_kernel(const double *__restrict__ Ain, int n, int which,
+                                                         double *__restrict__ ev_out, double *__restrict__ vec_out) {
+  extern __shared__ double lds[];
+  const int ld = n | 1;
+  double *A = lds;
+  double *dv = A + (int64_t)n * ld, *ov = dv + n, *ev2 = ov + n, *tv = ev2 + n, *pv = tv + n, *z = pv + n;
+  double *fd = z + n, *fdu = fd + n, *fdu2 = fdu + n, *fdl = fdu2 + n, *fpiv = fdl + n;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  for (int e = tid; e < n * n; e += 256) {
+    const int i = e / n, j = e - i * n;
+    A[i * ld + j] = Ain[e];
+  }
+  __syncthreads();
+  for (int k = 0; k + 2 < n; ++k) {
+    double *v = A + k * ld + k + 1;
+    const int m = n - k - 1;
+    if (wid == 0) {
+      const double x1 = (1 + lane < m) ? v[1 + lane] : 0.0;
+      const double x2 = (65 + lane < m) ? v[65 + lane] : 0.0;
+      const double sigma = ttk::wave_sum(fma(x1, x1, x2 * x2));
+      const double alpha = v[0];
+      double tau = 0.0, beta = alpha;
+      if (sigma > 0.0) {
+        beta = -copysign(sqrt(fma(alpha, alpha, sigma)), alpha);
+        tau = (beta - alpha) / beta;
+        const double sc = 1.0 / (alpha - beta);
+        if (1 + lane < m) v[1 + lane] = x1 * sc;
+        if (65 + lane < m) v[65 + lane] = x2 * sc;
+      }
+      if (lane == 0) {
+        v[0] = 1.0;
+        tv[k] = tau;
+        ov[k] = beta;
+        dv[k] = A[k * ld + k];
+      }
+    }
+    __syncthreads();
+    const double tau = tv[k];
+    if (tau == 0.0) continue;
+    const double *A22 = A + (k + 1) * ld + k + 1;
+    {  // p = tau A22 v: row r = tid / 2, half h = tid & 1 (columns h, h+2, ...)
+      const int r = tid >> 1, h = tid & 1;
+      double acc = 0.0;
+      if (r < m) {
+        const double *ar = A22 + r * ld;
+        for (int j = h; j < m; j += 2) acc = fma(ar[j], v[j], acc);
+      }
+      acc += __shfl_xor(acc, 1, 64);
+      if (h == 0 && r < m) pv[r] = tau * acc;
+    }
+    __syncthreads();
+    const int j0 = lane, j1 = lane + 64;
+    const double v0 = j0 < m ? v[j0] : 0.0, v1 = j1 < m ? v[j1] : 0.0;
+    const double p0 = j0 < m ? pv[j0] : 0.0, p1 = j1 < m ? pv[j1] : 0.0;
+    const double K = 0.5 * tau * ttk::wave_sum(fma(p0, v0, p1 * v1));
+    const double w0 = fma(-K, v0, p0), w1 = fma(-K, v1, p1);
+    for (int i = wid; i < m; i += 4) {
+      const double vi = v[i], wi = fma(-K, vi, pv[i]);
+      double *ai = A + (k + 1 + i) * ld + k + 1;
+      if (j0 < m) ai[j0] -= fma(vi, w0, wi * v0);
+      if (j1 < m) ai[j1] -= fma(vi, w1, wi * v1);
+    }
+    __syncthreads();
+  }
+  tridiag_extreme_finish(A, n, which, dv, ov, ev2, tv, z, fd, fdu, fdu2, fdl, fpiv, ev_out, vec_out, ld);
+}
+
+int64_t syev_small_need(int n) { return (int64_t)n * (n | 1) + 13 * (int64_t)n + 32; }
 
 // Multi-workgroup Householder tridiagonalisation for n beyond LDS: per reflector k two launches over
 // row blocks of TRB rows, (1) rank-2 update of step k-1 on the block's rows, then the block owning
@@ -1440,7 +1520,7 @@ __global__ __launch_bounds__(1024) void tri_finish_kernel(double *A, int n, int 
                                                           double *vec_out) {
   double *dv = gv, *ov = dv + n, *ev2 = ov + n, *tv = ev2 + n, *z = tv + n;
   double *fd = z + n, *fdu = fd + n, *fdu2 = fdu + n, *fdl = fdu2 + n, *fpiv = fdl + n;
-  tridiag_extreme_finish(A, n, which, dv, ov, ev2, tv, z, fd, fdu, fdu2, fdl, fpiv, ev_out, vec_out);
+  tridiag_extreme_finish(A, n, which, dv, ov, ev2, tv, z, fd, fdu, fdu2, fdl, fpiv, ev_out, vec_out, n);
 }
 
 template <typename K>
@@ -2239,6 +2319,14 @@ int ttk_debug_counters(unsigned long long *out, int reset) {
   return TTK_OK;
 }
 
+static int g_syev_small = 1;
+
+int ttk_syev_set_small(int on) {
+  const int old = g_syev_small;
+  g_syev_small = on;
+  return old;
+}
+
 int64_t ttk_syev_extreme_work(int n) { return n > 0 ? syev_extreme_need(n) : 0; }
 
 int ttk_syev_extreme(void *stream, const double *A, int n, int which, double *ev, double *vec, double *work) {
@@ -2262,6 +2350,13 @@ int ttk_syev_extreme(void *stream, const double *A, int n, int which, double *ev
     }
     hipLaunchKernelGGL(tri_update_kernel, dim3(nblk), dim3(256), 0, st, Aw, n, n - 2, tv, ov, dv, pv, partials, nblk);
     hipLaunchKernelGGL(tri_finish_kernel, dim3(1), dim3(1024), 0, st, Aw, n, which, gv, ev, vec);
+    TTK_LAUNCH_CHECK();
+    return TTK_OK;
+  }
+  if (n >= 3 && n <= SYEV_SMALL_N && g_syev_small) {
+    const size_t shm_s = (size_t)syev_small_need(n) * sizeof(double);
+    allow_big_lds(syev_small_kernel, shm_s);
+    hipLaunchKernelGGL(syev_small_kernel, dim3(1), dim3(256), shm_s, st, A, n, which, ev, vec);
     TTK_LAUNCH_CHECK();
     return TTK_OK;
   }

@@ -170,11 +170,19 @@ def test_normalise_rng_coupling(dev):
 
 
 def _run(key, trace=None):
+    """`_shipped` keys ran the reference with `cy_src/lgmres_cy.pyx:510` as written (the memoryview
+    TypeError on the first iterative inequality solve); the device reproduces it on request."""
     import yaml
+    from ttipm_amd import tt_ipm
     from ttipm_amd.utils import run_and_record
     g = RUNS[key]
     cfg = yaml.safe_load(open(os.path.join(ROOT, "configs", g["config"] + ".yaml")))
-    return g, run_and_record(g["problem"], cfg, g["seed"], g["rank"], trace=trace, verbose=False)
+    old = tt_ipm.INEQ_MATVEC_BUG
+    tt_ipm.INEQ_MATVEC_BUG = not g.get("fixed_ineq", True)
+    try:
+        return g, run_and_record(g["problem"], cfg, g["seed"], g["rank"], trace=trace, verbose=False)
+    finally:
+        tt_ipm.INEQ_MATVEC_BUG = old
 
 
 # Whole-solve tolerances.  The trajectory (every Newton-system assembly except the last) must agree
@@ -189,7 +197,8 @@ TRAJ_RTOL = 1e-4
 FINAL_RTOL = 1e-2
 
 
-@pytest.mark.parametrize("key", ["maxcut_5_r1_s0", "maxcut_5_r1_s319", "maxcut_10_r1_s41", "corr_clust_9_r1_s764"])
+@pytest.mark.parametrize("key", ["maxcut_5_r1_s0", "maxcut_5_r1_s319", "maxcut_10_r1_s41",
+                                 "corr_clust_9_r1_s764_shipped"])
 def test_full_solve_matches_reference(dev, key):
     from ttipm_amd._lib import lib
     l0 = lib.ttk_launch_count()
