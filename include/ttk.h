@@ -185,6 +185,11 @@ int ttk_lgmres_build(void *stream, double *hh, int max_k, int it, const double *
 int ttk_lgmres_aug(void *stream, const double *hh, int max_k, int it_total, const double *V,
                    int n, double unused, const double *aug_temp, double *augvec, double *a_augvec);
 
+/* (it+1)*n at or above which the Arnoldi / build / augmentation steps run as multi-workgroup
+ * kernels (default 16384 elements); 0 forces them everywhere, INT_MAX disables them (tests).
+ * Returns the previous threshold. */
+int ttk_lgmres_set_mw_threshold(int elems);
+
 #ifdef __cplusplus
 }
 #endif

@@ -157,6 +157,197 @@ __global__ __launch_bounds__(1024) void aug_kernel(const double *base_c, int max
   }
 }
 
+// ---------------------------------------------------------------- multi-workgroup variants
+// One workgroup streams the whole basis (it+1 vectors of length n, twice per Arnoldi step) through
+// a single CU; for the long local vectors of the iterative solves (3m ~ 1e4-3e4 doubles, restart
+// up to 100, i.e. tens of MB per step) that is bandwidth-bound at one CU's share of L2.  These
+// split the same classical Gram-Schmidt over the chip: (1) per (vector j, chunk) partial dots,
+// (2) per chunk: h_j = sum of partials (fixed order), w -= sum_j h_j V_j, partial |w|^2,
+// (3) one workgroup: |w|, breakdown test, w /= |w|, Hessenberg + Givens update.  Every reduction
+// runs in a fixed order, so results are deterministic run to run.
+constexpr int ARN_CHUNK = 2048;  // elements of one (j, chunk) partial dot
+constexpr int ARN_UPD = 512;     // elements per update block
+
+__global__ __launch_bounds__(256) void arnoldi_dot_kernel(const double *__restrict__ V, int n, int it,
+                                                          double *__restrict__ partials, int nchunk) {
+  __shared__ double red[16];
+  const int c = blockIdx.x, j = blockIdx.y, tid = threadIdx.x;
+  const double *vj = V + (int64_t)j * n, *w = V + (int64_t)(it + 1) * n;
+  const int i0 = c * ARN_CHUNK, i1 = i0 + ARN_CHUNK < n ? i0 + ARN_CHUNK : n;
+  double s = 0.0;
+#pragma unroll 4
+  for (int i = i0 + tid; i < i1; i += 256) s = fma(vj[i], w[i], s);
+  s = ttk::block_sum(s, red);
+  if (tid == 0) partials[(int64_t)j * nchunk + c] = s;
+}
+
+__global__ __launch_bounds__(256) void arnoldi_update_kernel(double *__restrict__ V, int n, int it,
+                                                             const double *__restrict__ partials, int nchunk,
+                                                             double *__restrict__ normpart, double *base,
+                                                             int max_k) {
+  __shared__ double h[MAXV + 2];
+  __shared__ double red[16];
+  const int tid = threadIdx.x;
+  for (int j = tid; j <= it; j += 256) {
+    double acc = 0.0;
+    for (int c = 0; c < nchunk; ++c) acc += partials[(int64_t)j * nchunk + c];
+    h[j] = acc;
+  }
+  __syncthreads();
+  if (blockIdx.x == 0) {
+    HH H(base, max_k);
+    for (int j = tid; j <= it; j += 256) {
+      H.hh[j * H.ld + it] = h[j];
+      H.hes[j * H.ld + it] = h[j];
+    }
+  }
+  double *w = V + (int64_t)(it + 1) * n;
+  const int i = blockIdx.x * ARN_UPD + tid;
+  double s2 = 0.0;
+  for (int ii = i; ii < n && ii < (blockIdx.x + 1) * ARN_UPD; ii += 256) {
+    double acc = w[ii];
+    for (int j = 0; j <= it; ++j) acc -= h[j] * V[(int64_t)j * n + ii];
+    w[ii] = acc;
+    s2 = fma(acc, acc, s2);
+  }
+  s2 = ttk::block_sum(s2, red);
+  if (tid == 0) normpart[blockIdx.x] = s2;
+}
+
+__global__ __launch_bounds__(1024) void arnoldi_finish_kernel(double *V, int n, int it, const double *normpart,
+                                                              int nblk, double *base, int max_k, double haptol) {
+  __shared__ double s_tt;
+  HH H(base, max_k);
+  const int tid = threadIdx.x, nt = blockDim.x;
+  if (tid == 0) {
+    double s2 = 0.0;
+    for (int b = 0; b < nblk; ++b) s2 += normpart[b];
+    s_tt = sqrt(s2);
+  }
+  __syncthreads();
+  const double tt = s_tt;
+  const int ld = H.ld;
+  double hapbnd = fabs(tt / H.grs[it]);
+  if (hapbnd > haptol) hapbnd = haptol;
+  const bool hapend = !(tt > hapbnd);
+  double *w = V + (int64_t)(it + 1) * n;
+  if (!hapend) {
+    const double inv = 1.0 / tt;
+    for (int i = tid; i < n; i += nt) w[i] *= inv;
+  }
+  if (tid == 0) {
+    H.hh[(it + 1) * ld + it] = tt;
+    H.hes[(it + 1) * ld + it] = tt;
+    for (int j = 1; j <= it; ++j) {
+      const double t0 = H.hh[(j - 1) * ld + it];
+      const double t1 = H.hh[j * ld + it];
+      H.hh[(j - 1) * ld + it] = H.cc[j - 1] * t0 + H.ss[j - 1] * t1;
+      H.hh[j * ld + it] = H.cc[j - 1] * t1 - H.ss[j - 1] * t0;
+    }
+    double res = 0.0, null_flag = 0.0;
+    if (!hapend) {
+      const double hv = H.hh[it * ld + it], hv1 = H.hh[(it + 1) * ld + it];
+      const double tr = sqrt(hv * hv + hv1 * hv1);
+      if (tr == 0.0) {
+        null_flag = 1.0;
+      } else {
+        H.cc[it] = hv / tr;
+        H.ss[it] = hv1 / tr;
+        H.grs[it + 1] = -(H.ss[it] * H.grs[it]);
+        H.grs[it] = H.cc[it] * H.grs[it];
+        H.hh[it * ld + it] = H.cc[it] * hv + H.ss[it] * hv1;
+        res = fabs(H.grs[it + 1]);
+      }
+    }
+    H.st[0] = res;
+    H.st[1] = hapend ? 1.0 : 0.0;
+    H.st[2] = null_flag;
+    H.st[3] = H.hh[it * ld + it];
+  }
+}
+
+// y = HH \ GRS (back substitution in GRS), once, by a single thread (it <= 100)
+__global__ void build_solve_kernel(double *base, int max_k, int it) {
+  HH H(base, max_k);
+  const int ld = H.ld;
+  H.grs[it] = H.grs[it] / H.hh[it * ld + it];
+  for (int k = it - 1; k >= 0; --k) {
+    double t0 = H.grs[k];
+    for (int j = k + 1; j <= it; ++j) t0 -= H.hh[k * ld + j] * H.grs[j];
+    H.grs[k] = t0 / H.hh[k * ld + k];
+  }
+}
+
+// temp = sum_j y_j basis_j, x += temp (chunks over the chip; y = GRS after build_solve_kernel)
+__global__ __launch_bounds__(256) void build_axpy_kernel(const double *base, int max_k, PtrList basis, int nvec,
+                                                         int n, double *x, double *aug_temp) {
+  __shared__ double y[MAXV + 2];
+  HH H(const_cast<double *>(base), max_k);
+  for (int j = threadIdx.x; j < nvec; j += 256) y[j] = H.grs[j];
+  __syncthreads();
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  double t = 0.0;
+  for (int j = 0; j < nvec; ++j) t += y[j] * basis.p[j][i];
+  aug_temp[i] = t;
+  x[i] += t;
+}
+
+// partial |aug_temp|^2 per block
+__global__ __launch_bounds__(256) void sumsq_part_kernel(const double *__restrict__ a, int n, double *part) {
+  __shared__ double red[16];
+  const int i0 = blockIdx.x * ARN_UPD;
+  double s2 = 0.0;
+  for (int i = i0 + threadIdx.x; i < n && i < i0 + ARN_UPD; i += 256) s2 = fma(a[i], a[i], s2);
+  s2 = ttk::block_sum(s2, red);
+  if (threadIdx.x == 0) part[blockIdx.x] = s2;
+}
+
+// augvec = aug_temp / |aug_temp|, A*aug = V (HES GRS) / |aug_temp|
+__global__ __launch_bounds__(256) void aug_apply_kernel(const double *base_c, int max_k, int it_total,
+                                                        const double *V, int n, const double *aug_temp,
+                                                        const double *part, int nblk, double *augvec,
+                                                        double *a_augvec) {
+  __shared__ double avec[MAXV + 2];
+  __shared__ double s_inv;
+  HH H(const_cast<double *>(base_c), max_k);
+  const int ld = H.ld, tid = threadIdx.x;
+  if (tid == 0) {
+    for (int j = 0; j <= it_total; ++j) avec[j] = 0.0;
+    for (int ii = 0; ii <= it_total; ++ii)
+      for (int jj = 0; jj <= ii + 1 && jj <= it_total; ++jj) avec[jj] += H.hes[jj * ld + ii] * H.grs[ii];
+    double s2 = 0.0;
+    for (int b = 0; b < nblk; ++b) s2 += part[b];
+    s_inv = 1.0 / sqrt(s2);
+  }
+  __syncthreads();
+  const int i = blockIdx.x * 256 + tid;
+  if (i >= n) return;
+  const double inv = s_inv;
+  augvec[i] = aug_temp[i] * inv;
+  double t = 0.0;
+  for (int j = 0; j <= it_total; ++j) t += avec[j] * V[(int64_t)j * n + i];
+  a_augvec[i] = t * inv;
+}
+
+double *lgmres_scratch(int64_t n) {  // partials / norm parts (grown, never shrunk; one stream)
+  static double *p = nullptr;
+  static int64_t cap = 0;
+  if (n > cap) {
+    if (p) (void)hipFree(p);
+    const int64_t want = n < 65536 ? 65536 : n;
+    if (hipMalloc(reinterpret_cast<void **>(&p), want * sizeof(double)) != hipSuccess) {
+      p = nullptr;
+      cap = 0;
+      return nullptr;
+    }
+    cap = want;
+  }
+  return p;
+}
+
+int g_lgmres_mw_min = 16384;  // (it+1)*n at or above which the multi-workgroup kernels run
+
 }  // namespace
 
 extern "C" {
@@ -167,8 +358,25 @@ int ttk_lgmres_arnoldi_sync(void *stream, double *V, int n, int it, double *hh, 
     ttk::set_error("ttk_lgmres_arnoldi_sync: restart %d too large (max %d)", max_k, MAXV);
     return TTK_ERR_ARG;
   }
-  hipLaunchKernelGGL(arnoldi_kernel, dim3(1), dim3(1024), 0, TTK_STREAM(stream), V, n, it, hh, max_k, haptol);
-  TTK_LAUNCH_CHECK();
+  hipStream_t st_ = TTK_STREAM(stream);
+  if ((int64_t)(it + 1) * n >= g_lgmres_mw_min) {
+    const int nchunk = (n + ARN_CHUNK - 1) / ARN_CHUNK, nblk = (n + ARN_UPD - 1) / ARN_UPD;
+    double *partials = lgmres_scratch((int64_t)(it + 1) * nchunk + nblk + 64);
+    if (!partials) {
+      ttk::set_error("ttk_lgmres_arnoldi_sync: scratch allocation failed");
+      return TTK_ERR_HIP;
+    }
+    double *normpart = partials + (int64_t)(it + 1) * nchunk;
+    hipLaunchKernelGGL(arnoldi_dot_kernel, dim3(nchunk, it + 1), dim3(256), 0, st_, V, n, it, partials, nchunk);
+    hipLaunchKernelGGL(arnoldi_update_kernel, dim3(nblk), dim3(256), 0, st_, V, n, it, partials, nchunk, normpart,
+                       hh, max_k);
+    hipLaunchKernelGGL(arnoldi_finish_kernel, dim3(1), dim3(1024), 0, st_, V, n, it, normpart, nblk, hh, max_k,
+                       haptol);
+    TTK_LAUNCH_CHECK();
+  } else {
+    hipLaunchKernelGGL(arnoldi_kernel, dim3(1), dim3(1024), 0, st_, V, n, it, hh, max_k, haptol);
+    TTK_LAUNCH_CHECK();
+  }
   const int ld = max_k + 1;
   const int64_t st_off = 2 * (int64_t)(max_k + 2) * ld + (max_k + 2) + 2 * ld;
   double st[4];
@@ -189,7 +397,14 @@ int ttk_lgmres_build(void *stream, double *hh, int max_k, int it, const double *
   }
   PtrList pl;
   for (int j = 0; j < nvec; ++j) pl.p[j] = basis[j];
-  hipLaunchKernelGGL(build_kernel, dim3(1), dim3(1024), 0, TTK_STREAM(stream), hh, max_k, it, pl, nvec, n, x, aug_temp);
+  if ((int64_t)nvec * n >= g_lgmres_mw_min) {
+    hipLaunchKernelGGL(build_solve_kernel, dim3(1), dim3(1), 0, TTK_STREAM(stream), hh, max_k, it);
+    hipLaunchKernelGGL(build_axpy_kernel, dim3((n + 255) / 256), dim3(256), 0, TTK_STREAM(stream), hh, max_k, pl,
+                       nvec, n, x, aug_temp);
+  } else {
+    hipLaunchKernelGGL(build_kernel, dim3(1), dim3(1024), 0, TTK_STREAM(stream), hh, max_k, it, pl, nvec, n, x,
+                       aug_temp);
+  }
   TTK_LAUNCH_CHECK();
   return TTK_OK;
 }
@@ -201,10 +416,28 @@ int ttk_lgmres_aug(void *stream, const double *hh, int max_k, int it_total, cons
     ttk::set_error("ttk_lgmres_aug: it_total %d too large", it_total);
     return TTK_ERR_ARG;
   }
-  hipLaunchKernelGGL(aug_kernel, dim3(1), dim3(1024), 0, TTK_STREAM(stream), hh, max_k, it_total, V, n, aug_temp,
-                     augvec, a_augvec);
+  if ((int64_t)(it_total + 1) * n >= g_lgmres_mw_min) {
+    const int nblk = (n + ARN_UPD - 1) / ARN_UPD;
+    double *part = lgmres_scratch(nblk + 64);
+    if (!part) {
+      ttk::set_error("ttk_lgmres_aug: scratch allocation failed");
+      return TTK_ERR_HIP;
+    }
+    hipLaunchKernelGGL(sumsq_part_kernel, dim3(nblk), dim3(256), 0, TTK_STREAM(stream), aug_temp, n, part);
+    hipLaunchKernelGGL(aug_apply_kernel, dim3((n + 255) / 256), dim3(256), 0, TTK_STREAM(stream), hh, max_k, it_total,
+                       V, n, aug_temp, part, nblk, augvec, a_augvec);
+  } else {
+    hipLaunchKernelGGL(aug_kernel, dim3(1), dim3(1024), 0, TTK_STREAM(stream), hh, max_k, it_total, V, n, aug_temp,
+                       augvec, a_augvec);
+  }
   TTK_LAUNCH_CHECK();
   return TTK_OK;
+}
+
+int ttk_lgmres_set_mw_threshold(int elems) {
+  const int old = g_lgmres_mw_min;
+  g_lgmres_mw_min = elems;
+  return old;
 }
 
 }  // extern "C"

@@ -140,8 +140,19 @@ def test_schur_matvec(dev, ci):
     _close(dev.read(y), G[f"mv{ci}/y"], 1e-13)
 
 
+@pytest.mark.parametrize("mw", [None, 0, 1 << 30])  # default / all multi-workgroup / all one-workgroup
 @pytest.mark.parametrize("ci", range(3))
-def test_lgmres_matches_petsc_restatement(dev, ci):
+def test_lgmres_matches_petsc_restatement(dev, ci, mw):
+    from ttipm_amd._lib import lib
+    old = lib.ttk_lgmres_set_mw_threshold(mw) if mw is not None else None
+    try:
+        _lgmres_case(dev, ci)
+    finally:
+        if old is not None:
+            lib.ttk_lgmres_set_mw_threshold(old)
+
+
+def _lgmres_case(dev, ci):
     from oracle.ipm import SchurMatVec
     from oracle.petsc_lgmres import lgmres as ref_lgmres
     from ttipm_amd.lgmres import lgmres
