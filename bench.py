@@ -108,6 +108,18 @@ def cpu_baseline(problem, config, seed, rank_tt, iters):
                       f"restatement of the reference path, 1 BLAS thread"}
 
 
+def _pmc_traffic():
+    """HBM bytes per gemm_offs_kernel launch (FETCH_SIZE + WRITE_SIZE, raw rocprofv3 KB x 1024) from
+    the committed PMC passes over the same workload (profiles/r01_pmc_maxcut10.json; counters need
+    their own rocprofv3 runs, so they cannot be read live here)."""
+    path = os.path.join(HERE, "profiles", "r01_pmc_maxcut10.json")
+    try:
+        k = json.load(open(path))["kernels"]["gemm_offs_kernel"]
+        return (k["FETCH_SIZE_KB"] + k["WRITE_SIZE_KB"]) * 1024.0
+    except (OSError, KeyError, ValueError):
+        return None
+
+
 def main():
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
     ap.add_argument("--gpus", type=int, default=1)
@@ -187,7 +199,7 @@ def main():
         if tms > 0:
             ach = tflops / (tms * 1e-3)
             roofline = {"bound": "mfma", "achieved": ach / 1e12, "peak": FP64_MATRIX_PEAK / 1e12,
-                        "unit": "TFLOP/s", "frac": ach / FP64_MATRIX_PEAK, "traffic": None,
+                        "unit": "TFLOP/s", "frac": ach / FP64_MATRIX_PEAK, "traffic": _pmc_traffic(),
                         "kernel": "gemm_offs_kernel (fp64 MFMA 16x16x4, offset-table batched GEMM)",
                         "flops_per_launch": tflops / max(tl, 1), "avg_launch_us": tms * 1e3 / max(tl, 1),
                         "launches_per_solve": int(tl), "kernel_ms_per_solve": tms}

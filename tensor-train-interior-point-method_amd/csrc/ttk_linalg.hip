@@ -1119,10 +1119,18 @@ __global__ __launch_bounds__(1024) void syev_kernel(double *__restrict__ Ain, in
 // multisection, inverse iteration, back-transform.
 __device__ void tridiag_extreme_finish(double *A, int n, int which, double *dv, double *ov, double *ev2, double *tv,
                                        double *z, double *fd, double *fdu, double *fdu2, double *fdl, double *fpiv,
-                                       double *__restrict__ ev_out, double *__restrict__ vec_out, int lda) {
+                                       double *__restrict__ ev_out, double *__restrict__ vec_out, int lda,
+                                       int timing = 0) {
   __shared__ double sh_a, sh_b;
   __shared__ int sh_first;
   const int tid = threadIdx.x, nt = blockDim.x;
+  unsigned long long t_ph = timing ? wall_clock64() : 0;
+#define TTK_EPHASE(K)                                   \
+  if (timing && tid == 0) {                             \
+    const unsigned long long t1 = wall_clock64();       \
+    atomicAdd(&g_dbg[K], t1 - t_ph);                    \
+    t_ph = t1;                                          \
+  }
   const int lane = tid & 63, wid = tid >> 6;
   if (tid == 0) {
     if (n >= 2) {
@@ -1182,6 +1190,7 @@ __device__ void tridiag_extreme_finish(double *A, int n, int which, double *dv, 
   }
   const double lam = 0.5 * (sh_a + sh_b);
   if (tid == 0) atomicAdd(&g_dbg[2], 1ull);
+  TTK_EPHASE(5)
   // ---- 3. inverse iteration on T (thread 0, O(n) per solve)
   if (tid == 0) {
     for (int i = 0; i < n; ++i) {
@@ -1248,6 +1257,7 @@ __device__ void tridiag_extreme_finish(double *A, int n, int which, double *dv, 
     ev_out[0] = lam;
   }
   __syncthreads();
+  TTK_EPHASE(6)
   // ---- 4. back-transform by wave 0 (no block barriers inside)
   if (wid == 0) {
     for (int k = n - 3; k >= 0; --k) {
@@ -1264,6 +1274,8 @@ __device__ void tridiag_extreme_finish(double *A, int n, int which, double *dv, 
     }
   }
   __syncthreads();
+  TTK_EPHASE(7)
+#undef TTK_EPHASE
   for (int i = tid; i < n; i += nt) vec_out[i] = z[i];
 }
 
@@ -1355,13 +1367,15 @@ __global__ __launch_bounds__(1024) void syev_extreme_kernel(const double *__rest
 constexpr int SYEV_SMALL_N = 128;
 
 __global__ __launch_bounds__(256) void syev_small_kernel(const double *__restrict__ Ain, int n, int which,
-                                                         double *__restrict__ ev_out, double *__restrict__ vec_out) {
+                                                         double *__restrict__ ev_out, double *__restrict__ vec_out,
+                                                         int timing) {
   extern __shared__ double lds[];
   const int ld = n | 1;
   double *A = lds;
   double *dv = A + (int64_t)n * ld, *ov = dv + n, *ev2 = ov + n, *tv = ev2 + n, *pv = tv + n, *z = pv + n;
   double *fd = z + n, *fdu = fd + n, *fdu2 = fdu + n, *fdl = fdu2 + n, *fpiv = fdl + n;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const unsigned long long t_ph0 = timing ? wall_clock64() : 0;
   for (int e = tid; e < n * n; e += 256) {
     const int i = e / n, j = e - i * n;
     A[i * ld + j] = Ain[e];
@@ -1418,7 +1432,8 @@ __global__ __launch_bounds__(256) void syev_small_kernel(const double *__restric
     }
     __syncthreads();
   }
-  tridiag_extreme_finish(A, n, which, dv, ov, ev2, tv, z, fd, fdu, fdu2, fdl, fpiv, ev_out, vec_out, ld);
+  if (timing && tid == 0) atomicAdd(&g_dbg[4], wall_clock64() - t_ph0);
+  tridiag_extreme_finish(A, n, which, dv, ov, ev2, tv, z, fd, fdu, fdu2, fdl, fpiv, ev_out, vec_out, ld, timing);
 }
 
 int64_t syev_small_need(int n) { return (int64_t)n * (n | 1) + 13 * (int64_t)n + 32; }
@@ -2356,7 +2371,7 @@ int ttk_syev_extreme(void *stream, const double *A, int n, int which, double *ev
   if (n >= 3 && n <= SYEV_SMALL_N && g_syev_small) {
     const size_t shm_s = (size_t)syev_small_need(n) * sizeof(double);
     allow_big_lds(syev_small_kernel, shm_s);
-    hipLaunchKernelGGL(syev_small_kernel, dim3(1), dim3(256), shm_s, st, A, n, which, ev, vec);
+    hipLaunchKernelGGL(syev_small_kernel, dim3(1), dim3(256), shm_s, st, A, n, which, ev, vec, g_svd_timing);
     TTK_LAUNCH_CHECK();
     return TTK_OK;
   }

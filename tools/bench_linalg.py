@@ -68,6 +68,21 @@ def main():
             D.svd(A)
         t_h = (time.perf_counter() - t0) / 20 * 1e6
         print(f"  svd {m:4d}x{n:<4d} kernel {t_k:9.1f}  wrapper {t_h:9.1f}", flush=True)
+    print("small eig phases (us per call): tridiag, multisection, inverse iteration, back-transform")
+    lib.ttk_svd_set_timing(1)
+    for n in [10, 40, 80, 100, 128]:
+        M = rng.standard_normal((n, n))
+        A = D.from_numpy(M + M.T)
+        wx = D.empty(int(lib.ttk_syev_extreme_work(n)))
+        buf = D.empty(n + 1)
+        st = D._stream()
+        counters()
+        t_x = timed(lambda: lib.ttk_syev_extreme(st, D._p(A), n, 0, D._p(buf), D._p(buf[1:]), D._p(wx)))
+        c = counters()
+        calls = max(c[2], 1)
+        print(f"  n={n:4d} total {t_x:8.1f}  phases {[round(c[k] / 100.0 / calls, 1) for k in (4, 5, 6, 7)]}",
+              flush=True)
+    lib.ttk_svd_set_timing(0)
     print("eig kernel-only (us)")
     for n in [4, 10, 20, 40, 80, 100, 139, 160, 288, 500]:
         M = rng.standard_normal((n, n))
