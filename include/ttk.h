@@ -79,6 +79,14 @@ int ttk_contract_timing(int on);
  * timed launches, summed kernel ms of the timed launches}; synchronises pending events */
 int ttk_contract_stats(double *out, int reset);
 
+/* split-K for GEMM steps whose tile grid cannot fill the chip (< 256 tiles) and K >= 512: the K
+ * range is split over workgroups into partial slabs summed in a fixed order by a second kernel.
+ * on = 0 disables it (tests).  Returns the previous setting. */
+int ttk_gemm_set_splitk(int on);
+/* diagnostics: on > 0 records a (nb,M,N,K) histogram of ttk_gemm_offs launches, on < 0 clears it;
+ * dump_path != NULL writes "nb M N K launches flops" lines */
+int ttk_gemm_hist(int on, const char *dump_path);
+
 /* ---------------------------------------------------------------------------------------
  * Strided element-wise kernels (up to 6-D).  `shape`, `sstride`, `dstride` are host arrays.
  * copy:  dst = alpha * src + beta * dst     (tt_add block-diagonal assembly

@@ -59,6 +59,8 @@ _SIGS = {
     "ttk_einsum_set_fused": (i32, [i32]),
     "ttk_qr_set_big_threshold": (i32, [i32]),
     "ttk_contract_timing": (i32, [i32]),
+    "ttk_gemm_hist": (i32, [i32, ctypes.c_char_p]),
+    "ttk_gemm_set_splitk": (i32, [i32]),
     "ttk_contract_stats": (i32, [vp, i32]),
     "ttk_syev_extreme": (i32, [vp, vp, i32, i32, vp, vp, vp]),
     "ttk_lgmres_arnoldi_sync": (i32, [vp, vp, i32, i32, vp, i32, f64, c_dp, c_ip]),

@@ -13,6 +13,9 @@
 // (MI355X guide §3): A[i=l&15][k=l>>4], B[k=l>>4][j=l&15], D: col=l&15, row=(l>>4)+4*r.
 #include <hip/hip_ext.h>
 
+#include <array>
+#include <cstdio>
+#include <map>
 #include <vector>
 
 #include "ttk_common.h"
@@ -38,10 +41,16 @@ struct GroupPtrs {
 
 typedef double double4_t __attribute__((ext_vector_type(4)));
 
+// One 32x32 output tile over the K range [kb, ke).  The next K stage's offsets and operands are
+// loaded into registers while the MFMAs consume the current stage from LDS (one barrier pair per
+// stage), so the two dependent global loads of the offset-table gather (table entry, then
+// operand) overlap with compute instead of serialising every stage.
+// out != nullptr: raw partial sums (no alpha/beta) to a dense [M][N] slab (split-K);
+// out == nullptr: alpha/beta epilogue into C through the output offset tables.
 __device__ __forceinline__ void gemm_tile(const double *__restrict__ A, const double *__restrict__ B,
                                           double *__restrict__ C, const int64_t *__restrict__ offs,
                                           int nb, int M, int N, int K, double alpha, double beta,
-                                          int b, int m0, int n0) {
+                                          int b, int m0, int n0, int kb, int ke, double *__restrict__ out) {
   __shared__ double As[TK][TM + 1];
   __shared__ double Bs[TK][TN + 1];
   const int64_t *a_b = offs;
@@ -57,23 +66,32 @@ __device__ __forceinline__ void gemm_tile(const double *__restrict__ A, const do
   const int lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 1, wc = wid & 1;
   const int64_t abase = a_b[b], bbase = b_b[b];
-  // each thread stages 2 A and 2 B elements per K stage
-  const int la_m0 = tid & 31, la_k0 = tid >> 5;  // (m, k) and (m, k+8)
-  const int lb_n0 = tid & 31, lb_k0 = tid >> 5;
-  const bool am_ok = (m0 + la_m0) < M;
-  const bool bn_ok = (n0 + lb_n0) < N;
-  const int64_t aoff_m = am_ok ? a_m[m0 + la_m0] : 0;
-  const int64_t boff_n = bn_ok ? b_n[n0 + lb_n0] : 0;
+  // each thread stages 2 A and 2 B elements per K stage: (m, k), (m, k+8) and (k, n), (k+8, n)
+  const int l_mn = tid & 31, l_k = tid >> 5;
+  const bool am_ok = (m0 + l_mn) < M;
+  const bool bn_ok = (n0 + l_mn) < N;
+  const double *Ap = A + abase + (am_ok ? a_m[m0 + l_mn] : 0);
+  const double *Bp = B + bbase + (bn_ok ? b_n[n0 + l_mn] : 0);
+  double ra0, ra1, rb0, rb1;
+  auto fetch = [&](int k0) {
+    const int k_0 = k0 + l_k, k_1 = k0 + l_k + 8;
+    const bool ok0 = k_0 < ke, ok1 = k_1 < ke;
+    const int64_t o_a0 = ok0 ? a_k[k_0] : 0, o_a1 = ok1 ? a_k[k_1] : 0;
+    const int64_t o_b0 = ok0 ? b_k[k_0] : 0, o_b1 = ok1 ? b_k[k_1] : 0;
+    ra0 = (am_ok && ok0) ? Ap[o_a0] : 0.0;
+    ra1 = (am_ok && ok1) ? Ap[o_a1] : 0.0;
+    rb0 = (bn_ok && ok0) ? Bp[o_b0] : 0.0;
+    rb1 = (bn_ok && ok1) ? Bp[o_b1] : 0.0;
+  };
   double4_t acc = {0.0, 0.0, 0.0, 0.0};
-  for (int k0 = 0; k0 < K; k0 += TK) {
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int kk = la_k0 + 8 * h;
-      const int k = k0 + kk;
-      As[kk][la_m0] = (am_ok && k < K) ? A[abase + aoff_m + a_k[k]] : 0.0;
-      Bs[kk][lb_n0] = (bn_ok && k < K) ? B[bbase + b_k[k] + boff_n] : 0.0;
-    }
+  if (kb < ke) fetch(kb);
+  for (int k0 = kb; k0 < ke; k0 += TK) {
+    As[l_k][l_mn] = ra0;
+    As[l_k + 8][l_mn] = ra1;
+    Bs[l_k][l_mn] = rb0;
+    Bs[l_k + 8][l_mn] = rb1;
     __syncthreads();
+    if (k0 + TK < ke) fetch(k0 + TK);
 #pragma unroll
     for (int s = 0; s < TK / 4; ++s) {
       const double a = As[s * 4 + (lane >> 4)][wr * 16 + (lane & 15)];
@@ -84,6 +102,14 @@ __device__ __forceinline__ void gemm_tile(const double *__restrict__ A, const do
   }
   const int col = n0 + wc * 16 + (lane & 15);
   if (col >= N) return;
+  if (out) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = m0 + wr * 16 + (lane >> 4) + 4 * r;
+      if (row < M) out[(int64_t)row * N + col] = acc[r];
+    }
+    return;
+  }
   const int64_t cb = c_b[b] + c_n[col];
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
@@ -98,13 +124,42 @@ __device__ __forceinline__ void gemm_tile(const double *__restrict__ A, const do
 
 __global__ __launch_bounds__(256) void gemm_offs_kernel(GemmArgs g) {
   const int n0 = blockIdx.x * TN, m0 = blockIdx.y * TM, b = blockIdx.z;
-  gemm_tile(g.A, g.B, g.C, g.offs, g.nb, g.M, g.N, g.K, g.alpha, g.beta, b, m0, n0);
+  gemm_tile(g.A, g.B, g.C, g.offs, g.nb, g.M, g.N, g.K, g.alpha, g.beta, b, m0, n0, 0, g.K, nullptr);
+}
+
+// split-K: blockIdx.z = b * nsplit + split; partial tile sums to part[split][b][M][N]
+__global__ __launch_bounds__(256) void gemm_offs_splitk_kernel(GemmArgs g, int nsplit, int kc, double *part) {
+  const int n0 = blockIdx.x * TN, m0 = blockIdx.y * TM;
+  const int b = blockIdx.z / nsplit, sp = blockIdx.z % nsplit;
+  const int kb = sp * kc, ke = kb + kc < g.K ? kb + kc : g.K;
+  double *out = part + ((int64_t)sp * g.nb + b) * g.M * g.N;
+  gemm_tile(g.A, g.B, g.C, g.offs, g.nb, g.M, g.N, g.K, g.alpha, g.beta, b, m0, n0, kb, ke, out);
+}
+
+// C = alpha * sum_split part + beta * C (fixed summation order: deterministic)
+__global__ __launch_bounds__(256) void gemm_splitk_reduce_kernel(GemmArgs g, int nsplit, const double *part) {
+  const int64_t mn = (int64_t)g.M * g.N;
+  const int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (e >= mn * g.nb) return;
+  const int b = (int)(e / mn);
+  const int64_t r = e - b * mn;
+  const int row = (int)(r / g.N), col = (int)(r - (int64_t)row * g.N);
+  double acc = 0.0;
+  for (int sp = 0; sp < nsplit; ++sp) acc += part[((int64_t)sp * g.nb + b) * mn + r];
+  const int64_t *a_b = g.offs;
+  const int64_t *c_b = a_b + g.nb + g.M + g.K + g.nb + g.K + g.N;
+  const int64_t *c_m = c_b + g.nb;
+  const int64_t *c_n = c_m + g.M;
+  double *p = g.C + c_b[b] + c_m[row] + c_n[col];
+  const double v = g.alpha * acc;
+  *p = (g.beta == 0.0) ? v : v + g.beta * (*p);
 }
 
 __global__ __launch_bounds__(256) void gemm_offs_grouped_kernel(GemmArgs g, GroupPtrs p) {
   const int n0 = blockIdx.x * TN, m0 = blockIdx.y * TM;
   const int grp = blockIdx.z / g.nb, b = blockIdx.z % g.nb;
-  gemm_tile(p.A[grp], p.B[grp], p.C[grp], g.offs, g.nb, g.M, g.N, g.K, g.alpha, g.beta, b, m0, n0);
+  gemm_tile(p.A[grp], p.B[grp], p.C[grp], g.offs, g.nb, g.M, g.N, g.K, g.alpha, g.beta, b, m0, n0, 0, g.K,
+            nullptr);
 }
 
 // ------------------------------------------------------------------ element-wise (N-D strided)
@@ -273,9 +328,66 @@ void contract_count_ext(double flops) { contract_count(flops); }
 
 extern "C" {
 
+}  // extern "C"
+
+namespace {
+bool g_splitk_on = true;
+
+double *splitk_scratch(int64_t n) {  // partial-sum slabs (grown, never shrunk; one stream)
+  static double *p = nullptr;
+  static int64_t cap = 0;
+  if (n > cap) {
+    if (p) {
+      (void)hipDeviceSynchronize();  // earlier split-K launches may still read the old slab
+      (void)hipFree(p);
+    }
+    const int64_t want = n < (1 << 20) ? (1 << 20) : 2 * n;
+    if (hipMalloc(reinterpret_cast<void **>(&p), want * sizeof(double)) != hipSuccess) {
+      p = nullptr;
+      cap = 0;
+      return nullptr;
+    }
+    cap = want;
+  }
+  return p;
+}
+
+// diagnostics: launch-shape histogram of the GEMM steps (ttk_gemm_hist)
+bool g_hist_on = false;
+std::map<std::array<int, 4>, std::pair<long long, double>> g_hist;
+}  // namespace
+
+extern "C" {
+
+int ttk_gemm_set_splitk(int on) {
+  const int old = g_splitk_on ? 1 : 0;
+  g_splitk_on = on != 0;
+  return old;
+}
+
+int ttk_gemm_hist(int on, const char *dump_path) {
+  if (dump_path) {
+    FILE *f = std::fopen(dump_path, "w");
+    if (!f) return TTK_ERR_ARG;
+    std::fprintf(f, "nb M N K launches flops\n");
+    for (const auto &kv : g_hist)
+      std::fprintf(f, "%d %d %d %d %lld %.6g\n", kv.first[0], kv.first[1], kv.first[2], kv.first[3],
+                   kv.second.first, kv.second.second);
+    std::fclose(f);
+  }
+  if (on < 0) g_hist.clear();
+  g_hist_on = on > 0;
+  return TTK_OK;
+}
+
 int ttk_gemm_offs(void *stream, const double *A, const double *B, double *C, const int64_t *offs,
                   int nb, int M, int N, int K, double alpha, double beta) {
   if (nb <= 0 || M <= 0 || N <= 0) return TTK_OK;
+  if (g_hist_on) {
+    auto &e = g_hist[{nb, M, N, K}];
+    e.first += 1;
+    e.second += 2.0 * M * N * (double)K * nb;
+  }
   if (K <= 0 || nb > 65535) {
     ttk::set_error("ttk_gemm_offs: bad shape nb=%d M=%d N=%d K=%d", nb, M, N, K);
     return TTK_ERR_ARG;
@@ -285,7 +397,32 @@ int ttk_gemm_offs(void *stream, const double *A, const double *B, double *C, con
   hipEvent_t e0, e1;
   int rc = contract_events(&e0, &e1);
   if (rc != TTK_OK) return rc;
-  hipExtLaunchKernelGGL(gemm_offs_kernel, grid, dim3(256), 0, TTK_STREAM(stream), e0, e1, 0, g);
+  // split-K when the tile grid cannot fill the chip and K is long: each split runs >= 256 of K
+  const int64_t tiles = (int64_t)grid.x * grid.y * nb;
+  int nsplit = 1;
+  if (g_splitk_on && tiles < 256 && K >= 512) {
+    nsplit = (int)(K / 256);
+    const int64_t cap = (512 + tiles - 1) / tiles;
+    if (nsplit > cap) nsplit = (int)cap;
+    if ((int64_t)nsplit * nb > 65535) nsplit = (int)(65535 / nb);
+  }
+  if (nsplit > 1) {
+    const int kc = ((K + nsplit - 1) / nsplit + TK - 1) / TK * TK;
+    nsplit = (K + kc - 1) / kc;
+    double *part = splitk_scratch((int64_t)nsplit * nb * M * N);
+    if (!part) {
+      ttk::set_error("ttk_gemm_offs: split-K scratch allocation failed");
+      return TTK_ERR_HIP;
+    }
+    dim3 gs(grid.x, grid.y, nb * nsplit);
+    hipExtLaunchKernelGGL(gemm_offs_splitk_kernel, gs, dim3(256), 0, TTK_STREAM(stream), e0, nullptr, 0, g, nsplit,
+                          kc, part);
+    const int64_t tot = (int64_t)nb * M * N;
+    hipExtLaunchKernelGGL(gemm_splitk_reduce_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0,
+                          TTK_STREAM(stream), nullptr, e1, 0, g, nsplit, part);
+  } else {
+    hipExtLaunchKernelGGL(gemm_offs_kernel, grid, dim3(256), 0, TTK_STREAM(stream), e0, e1, 0, g);
+  }
   TTK_LAUNCH_CHECK();
   contract_count(2.0 * M * N * (double)K * nb);
   return TTK_OK;

@@ -1191,39 +1191,55 @@ __device__ void tridiag_extreme_finish(double *A, int n, int which, double *dv, 
   const double lam = 0.5 * (sh_a + sh_b);
   if (tid == 0) atomicAdd(&g_dbg[2], 1ull);
   TTK_EPHASE(5)
-  // ---- 3. inverse iteration on T (thread 0, O(n) per solve)
+  // ---- 3. inverse iteration on T (thread 0, O(n) per solve).  The running pivot row, the next
+  // diagonal and the solve recurrences are carried in registers; the LDS arrays are written once
+  // per element and never read back inside a recurrence (LDS store->load latency would otherwise
+  // sit on every step of the serial chain).  Same operations in the same order as dgttrf/dgtts2.
   if (tid == 0) {
-    for (int i = 0; i < n; ++i) {
-      fd[i] = dv[i] - lam;
-      fdu[i] = (i + 1 < n) ? ov[i] : 0.0;
-      fdl[i] = fdu[i];
-      fdu2[i] = 0.0;
-      fpiv[i] = 0.0;
-    }
+    double d = dv[0] - lam;
+    double u = (1 < n) ? ov[0] : 0.0;
     for (int i = 0; i + 1 < n; ++i) {  // dgttrf
-      if (fabs(fd[i]) >= fabs(fdl[i])) {
-        if (fd[i] != 0.0) {
-          const double f = fdl[i] * fast_rcp(fd[i]);
-          fdl[i] = f;
-          fd[i + 1] -= f * fdu[i];
+      const double l = ov[i];
+      double dn = dv[i + 1] - lam;
+      double un = (i + 2 < n) ? ov[i + 1] : 0.0;
+      double u2 = 0.0, pvt = 0.0, lf = l, dfin = d;
+      if (fabs(d) >= fabs(l)) {
+        if (d != 0.0) {
+          const double f = l * fast_rcp(d);
+          lf = f;
+          dn -= f * u;
         }
+        fdu[i] = u;
       } else {
-        const double f = fd[i] * fast_rcp(fdl[i]);
-        fd[i] = fdl[i];
-        fdl[i] = f;
-        const double t = fdu[i];
-        fdu[i] = fd[i + 1];
-        fd[i + 1] = t - f * fd[i + 1];
+        const double f = d * fast_rcp(l);
+        dfin = l;
+        lf = f;
+        fdu[i] = dn;
+        dn = u - f * dn;
         if (i + 2 < n) {
-          fdu2[i] = fdu[i + 1];
-          fdu[i + 1] = -f * fdu[i + 1];
+          u2 = un;
+          un = -f * un;
         }
-        fpiv[i] = 1.0;
+        pvt = 1.0;
       }
+      fd[i] = dfin;
+      fdl[i] = lf;
+      fdu2[i] = u2;
+      fpiv[i] = pvt;
+      d = dn;
+      u = un;
     }
+    fd[n - 1] = d;
+    fdu[n - 1] = 0.0;
+    fdl[n - 1] = 0.0;
+    fdu2[n - 1] = 0.0;
+    fpiv[n - 1] = 0.0;
     const double tiny = EPS * tnorm;
-    for (int i = 0; i < n; ++i)
-      if (fabs(fd[i]) < tiny) fd[i] = copysign(tiny, fd[i] == 0.0 ? 1.0 : fd[i]);
+    for (int i = 0; i < n; ++i) {  // store 1/U(i,i) for the solves
+      double di = fd[i];
+      if (fabs(di) < tiny) di = copysign(tiny, di == 0.0 ? 1.0 : di);
+      fd[i] = fast_rcp(di);
+    }
     uint32_t h = 0x9e3779b9u;  // fixed pseudo-random start (dstein uses a random start)
     for (int i = 0; i < n; ++i) {
       h ^= h << 13;
@@ -1231,29 +1247,45 @@ __device__ void tridiag_extreme_finish(double *A, int n, int which, double *dv, 
       h ^= h << 5;
       z[i] = 0.5 + (double)(h & 0xffffff) / 16777216.0;
     }
-    for (int i = 0; i < n; ++i) fd[i] = fast_rcp(fd[i]);  // store 1/U(i,i) for the solves
+    double sc = 1.0;  // scale of the previous iterate, applied as it is loaded
     for (int it = 0; it < 3; ++it) {
+      double zc = z[0] * sc;
       for (int i = 0; i + 1 < n; ++i) {  // dgtts2 forward
+        double zn = z[i + 1] * sc;
+        const double l = fdl[i];
         if (fpiv[i] == 0.0) {
-          z[i + 1] -= fdl[i] * z[i];
+          zn -= l * zc;
+          z[i] = zc;
+          zc = zn;
         } else {
-          const double t = z[i];
-          z[i] = z[i + 1];
-          z[i + 1] = t - fdl[i] * z[i];
+          z[i] = zn;
+          zc = zc - l * zn;
         }
       }
-      z[n - 1] *= fd[n - 1];
-      if (n > 1) z[n - 2] = (z[n - 2] - fdu[n - 2] * z[n - 1]) * fd[n - 2];
-      for (int i = n - 3; i >= 0; --i) z[i] = (z[i] - fdu[i] * z[i + 1] - fdu2[i] * z[i + 2]) * fd[i];
-      double mx = 0.0;
-      for (int i = 0; i < n; ++i) mx = fmax(mx, fabs(z[i]));
-      const double sc = mx > 0.0 ? fast_rcp(mx) : 1.0;
-      for (int i = 0; i < n; ++i) z[i] *= sc;
+      double z1 = zc * fd[n - 1], z2 = 0.0;
+      z[n - 1] = z1;
+      double mx = fabs(z1);
+      if (n > 1) {
+        const double zz = (z[n - 2] - fdu[n - 2] * z1) * fd[n - 2];
+        z[n - 2] = zz;
+        z2 = z1;
+        z1 = zz;
+        mx = fmax(mx, fabs(zz));
+      }
+      for (int i = n - 3; i >= 0; --i) {
+        const double zz = (z[i] - fdu[i] * z1 - fdu2[i] * z2) * fd[i];
+        z[i] = zz;
+        z2 = z1;
+        z1 = zz;
+        mx = fmax(mx, fabs(zz));
+      }
+      sc = mx > 0.0 ? fast_rcp(mx) : 1.0;
     }
+    for (int i = 0; i < n; ++i) z[i] *= sc;
     double nn = 0.0;
     for (int i = 0; i < n; ++i) nn += z[i] * z[i];
-    const double sc = 1.0 / sqrt(nn);
-    for (int i = 0; i < n; ++i) z[i] *= sc;
+    const double sc2 = 1.0 / sqrt(nn);
+    for (int i = 0; i < n; ++i) z[i] *= sc2;
     ev_out[0] = lam;
   }
   __syncthreads();
@@ -1411,9 +1443,18 @@ __global__ __launch_bounds__(256) void syev_small_kernel(const double *__restric
     {  // p = tau A22 v: row r = tid / 2, half h = tid & 1 (columns h, h+2, ...)
       const int r = tid >> 1, h = tid & 1;
       double acc = 0.0;
-      if (r < m) {
+      if (r < m) {  // four independent chains: the LDS loads of one batch overlap
         const double *ar = A22 + r * ld;
-        for (int j = h; j < m; j += 2) acc = fma(ar[j], v[j], acc);
+        double a1 = 0.0, a2 = 0.0, a3 = 0.0;
+        int j = h;
+        for (; j + 6 < m; j += 8) {
+          acc = fma(ar[j], v[j], acc);
+          a1 = fma(ar[j + 2], v[j + 2], a1);
+          a2 = fma(ar[j + 4], v[j + 4], a2);
+          a3 = fma(ar[j + 6], v[j + 6], a3);
+        }
+        for (; j < m; j += 2) acc = fma(ar[j], v[j], acc);
+        acc = (acc + a1) + (a2 + a3);
       }
       acc += __shfl_xor(acc, 1, 64);
       if (h == 0 && r < m) pv[r] = tau * acc;
@@ -1424,6 +1465,7 @@ __global__ __launch_bounds__(256) void syev_small_kernel(const double *__restric
     const double p0 = j0 < m ? pv[j0] : 0.0, p1 = j1 < m ? pv[j1] : 0.0;
     const double K = 0.5 * tau * ttk::wave_sum(fma(p0, v0, p1 * v1));
     const double w0 = fma(-K, v0, p0), w1 = fma(-K, v1, p1);
+#pragma unroll 4
     for (int i = wid; i < m; i += 4) {
       const double vi = v[i], wi = fma(-K, vi, pv[i]);
       double *ai = A + (k + 1 + i) * ld + k + 1;

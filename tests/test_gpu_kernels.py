@@ -90,6 +90,32 @@ def test_fused_local_apply(dev, eq, dims):
     assert np.allclose(plain, ref, rtol=1e-12, atol=1e-12 * np.abs(ref).max())
 
 
+@pytest.mark.parametrize("eq,shapes", [
+    ("ik,kj->ij", ((60, 2580), (2580, 40))),            # split-K: 4 tiles, long K
+    ("ik,kj->ij", ((841, 15624), (15624, 31))),         # graphm_3's widest env step
+    ("bik,bkj->bij", ((3, 17, 1100), (3, 1100, 9))),    # batched, ragged tiles
+    ("lsr,lML,sMNS,rNR->LSR", ((40, 9, 40), (40, 4, 44), (9, 4, 4, 10), (40, 4, 44))),
+])
+@pytest.mark.parametrize("splitk", [1, 0])
+def test_einsum_long_k(dev, eq, shapes, splitk):
+    """long-K contraction steps (graphm_3 r=2 sizes) with and without the split-K path, with an
+    accumulate (beta = 1) epilogue through the output offset tables"""
+    from ttipm_amd._lib import lib
+    rng = _rng(len(shapes[0]) * 31 + splitk)
+    ops = [rng.standard_normal(sh) for sh in shapes]
+    want = np.einsum(eq, *ops, optimize="greedy")
+    base = rng.standard_normal(want.shape)
+    old = lib.ttk_gemm_set_splitk(splitk)
+    try:
+        out = dev.from_numpy(base)
+        dev.einsum(eq, *[dev.from_numpy(o) for o in ops], out=out, alpha=0.5, beta=1.0)
+        got = dev.read(out)
+    finally:
+        lib.ttk_gemm_set_splitk(old)
+    ref = 0.5 * want + base
+    assert np.max(np.abs(got - ref)) <= 1e-12 * max(np.max(np.abs(ref)), 1.0) * np.sqrt(max(sh[-1] for sh in shapes))
+
+
 def test_mfma_layout_asymmetric(dev):
     """A = I with an asymmetric B catches transposed C/D fragment maps."""
     B = np.arange(32 * 32, dtype=np.float64).reshape(32, 32)
