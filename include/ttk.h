@@ -144,6 +144,9 @@ int ttk_qr_set_big_threshold(int k);
 /* Cholesky (lower) in place on A(n,n); status TTK_ERR_NOT_PD like LAPACK potrf info>0
  * (`src/tt_ipm.py:204-207,300-303`). Blocks on the stream to return the status. */
 int ttk_cholesky_sync(void *stream, double *A, int n);
+/* n at or above which ttk_cholesky_sync / ttk_trsm_lower run the blocked multi-workgroup kernels
+ * (32-column panels, fp64-MFMA trailing updates; default 96).  Returns the previous value. */
+int ttk_dense_set_block_min(int n);
 /* triangular solve with matrix RHS B(n,nrhs) in place: op(L) X = B, L lower (trans=0) or
  * L^T (trans=1) (`forward_backward_sub`, `src/tt_ipm.py:178-181`). */
 int ttk_trsm_lower(void *stream, const double *L, int n, double *B, int nrhs, int ldb, int trans);

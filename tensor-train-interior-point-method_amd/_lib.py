@@ -43,6 +43,7 @@ _SIGS = {
     "ttk_qr_work": (i64, [i32, i32]),
     "ttk_qr": (i32, [vp, vp, i32, i32, vp, vp, vp]),
     "ttk_cholesky_sync": (i32, [vp, vp, i32]),
+    "ttk_dense_set_block_min": (i32, [i32]),
     "ttk_trsm_lower": (i32, [vp, vp, i32, vp, i32, i32, i32]),
     "ttk_lu_sync": (i32, [vp, vp, i32, vp, vp, c_dp]),
     "ttk_lu_solve": (i32, [vp, vp, i32, vp, vp, i32, i32]),

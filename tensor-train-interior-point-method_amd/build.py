@@ -9,7 +9,7 @@ from concurrent.futures import ThreadPoolExecutor
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libttk.so")
-SOURCES = ["ttk_runtime.hip", "ttk_contract.hip", "ttk_einsum.hip", "ttk_linalg.hip", "ttk_lgmres.hip",
+SOURCES = ["ttk_runtime.hip", "ttk_contract.hip", "ttk_einsum.hip", "ttk_linalg.hip", "ttk_lgmres.hip", "ttk_dense.hip",
            "ttk_host.hip"]
 HEADERS = ["ttk_common.h", "ttk_internal.h", os.path.join("..", "..", "include", "ttk.h")]
 FLAGS = ["-O3", "-fPIC", "--offload-arch=gfx950", "-std=c++17", "-Wno-unused-variable",

@@ -587,6 +587,13 @@ int fused_apply_try(void *stream, const char *eq, const int64_t *desc, double *o
   }
   const int64_t need = apply_lds(g.nb, g.nj, g.nd, g.nS, g.ns, g.ni);
   if (need > APPLY_LDS_DOUBLES || g.na < 1 || g.na > 65535) return 0;
+  // one workgroup per output row runs the three stages on the VALU: past a few MFLOP per launch
+  // the pairwise MFMA plan (with split-K) is faster (graphm_3 r=2 sizes)
+  const double flops = 2.0 * g.na *
+                       ((double)g.ns * g.nj * g.nd * g.nb + (double)g.ni * g.nS * g.nd * g.ns * g.nj +
+                        (double)g.ni * g.nc * g.nS * g.nd);
+  static const double max_flops = getenv("TTK_FUSED_MAX_FLOPS") ? atof(getenv("TTK_FUSED_MAX_FLOPS")) : 4e6;
+  if (flops > max_flops) return 0;
   const size_t shm = need * sizeof(double);
   if (shm > 65536)
     (void)hipFuncSetAttribute(reinterpret_cast<const void *>(fused_apply_kernel),
@@ -597,8 +604,6 @@ int fused_apply_try(void *stream, const char *eq, const int64_t *desc, double *o
   if (ttk::contract_events_ext(&e0, &e1) != TTK_OK) return -1;
   hipExtLaunchKernelGGL(fused_apply_kernel, dim3(g.na), dim3(256), shm, TTK_STREAM(stream), e0, e1, 0, g);
   TTK_LAUNCH_CHECK();
-  ttk::contract_count_ext(2.0 * g.na *
-                          ((double)g.ns * g.nj * g.nd * g.nb + (double)g.ni * g.nS * g.nd * g.ns * g.nj +
-                           (double)g.ni * g.nc * g.nS * g.nd));
+  ttk::contract_count_ext(flops);
   return 1;
 }

@@ -18,6 +18,7 @@
 #include <math.h>
 
 #include "ttk_common.h"
+#include "ttk_internal.h"
 
 namespace {
 
@@ -2302,13 +2303,26 @@ int ttk_qr(void *stream, const double *A, int m, int n, double *Q, double *R, do
   return TTK_OK;
 }
 
+static int g_dense_block_min = 96;  // n at or above which Cholesky / TRSM take the blocked kernels
+
+int ttk_dense_set_block_min(int n) {
+  const int old = g_dense_block_min;
+  g_dense_block_min = n;
+  return old;
+}
+
 int ttk_cholesky_sync(void *stream, double *A, int n) {
   if (ensure_status()) {
     ttk::set_error("ttk_cholesky_sync: status alloc failed");
     return TTK_ERR_HIP;
   }
-  hipLaunchKernelGGL(chol_kernel, dim3(1), dim3(1024), 0, TTK_STREAM(stream), A, n, g_status);
-  TTK_LAUNCH_CHECK();
+  if (n >= g_dense_block_min) {
+    const int rc = ttk::cholesky_blocked(TTK_STREAM(stream), A, n, g_status);
+    if (rc) return rc;
+  } else {
+    hipLaunchKernelGGL(chol_kernel, dim3(1), dim3(1024), 0, TTK_STREAM(stream), A, n, g_status);
+    TTK_LAUNCH_CHECK();
+  }
   int st = 0;
   TTK_HIP(hipMemcpyAsync(&st, g_status, sizeof(int), hipMemcpyDeviceToHost, TTK_STREAM(stream)));
   TTK_HIP(hipStreamSynchronize(TTK_STREAM(stream)));
@@ -2321,6 +2335,7 @@ int ttk_cholesky_sync(void *stream, double *A, int n) {
 
 int ttk_trsm_lower(void *stream, const double *L, int n, double *B, int nrhs, int ldb, int trans) {
   if (n <= 0 || nrhs <= 0) return TTK_OK;
+  if (n >= g_dense_block_min) return ttk::trsm_blocked(TTK_STREAM(stream), L, n, B, nrhs, ldb, trans);
   hipLaunchKernelGGL(trsm_kernel, dim3((nrhs + 63) / 64), dim3(256), 0, TTK_STREAM(stream), L, n, B, nrhs, ldb, trans);
   TTK_LAUNCH_CHECK();
   return TTK_OK;

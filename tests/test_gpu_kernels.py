@@ -255,28 +255,41 @@ def test_qr_and_rq(dev, m, n):
     assert np.allclose(Qr @ Qr.T, np.eye(k), atol=1e-12)
 
 
-@pytest.mark.parametrize("n", [1, 5, 40, 130])
-def test_cholesky_trsm(dev, n):
-    rng = _rng(n)
+@pytest.mark.parametrize("n,nrhs", [(1, 7), (5, 7), (40, 7), (130, 7), (200, 300), (333, 45), (700, 700)])
+@pytest.mark.parametrize("blocked", [None, 1])  # default dispatch / blocked kernels forced at every n
+def test_cholesky_trsm(dev, n, nrhs, blocked):
+    from ttipm_amd._lib import lib
+    old = lib.ttk_dense_set_block_min(blocked) if blocked else None
+    try:
+        rng = _rng(n)
+        M = rng.standard_normal((n, n))
+        A = M @ M.T + n * np.eye(n)
+        L = dev.from_numpy(A)
+        dev.cholesky_(L)
+        Lh = dev.read(L)
+        assert np.allclose(Lh, np.linalg.cholesky(A), rtol=1e-12, atol=1e-12)
+        B = rng.standard_normal((n, nrhs))
+        X = dev.from_numpy(B)
+        dev.trsm_(L, X)
+        assert np.allclose(Lh @ dev.read(X), B, atol=1e-10)
+        X2 = dev.from_numpy(B)
+        dev.trsm_(L, X2, trans=True)
+        assert np.allclose(Lh.T @ dev.read(X2), B, atol=1e-10)
+    finally:
+        if old is not None:
+            lib.ttk_dense_set_block_min(old)
+
+
+@pytest.mark.parametrize("n,bad", [(2, 1), (150, 1), (150, 77), (300, 299)])
+def test_cholesky_not_pd_raises(dev, n, bad):
+    """LAPACK info semantics: the first non-positive leading minor (1-based) is reported"""
+    rng = _rng(n + bad)
     M = rng.standard_normal((n, n))
     A = M @ M.T + n * np.eye(n)
+    A[bad, bad] = -1e3 * n  # leading minor bad+1 is indefinite
     L = dev.from_numpy(A)
-    dev.cholesky_(L)
-    Lh = dev.read(L)
-    assert np.allclose(Lh, np.linalg.cholesky(A), rtol=1e-12, atol=1e-12)
-    B = rng.standard_normal((n, 7))
-    X = dev.from_numpy(B)
-    dev.trsm_(L, X)
-    assert np.allclose(Lh @ dev.read(X), B, atol=1e-10)
-    X2 = dev.from_numpy(B)
-    dev.trsm_(L, X2, trans=True)
-    assert np.allclose(Lh.T @ dev.read(X2), B, atol=1e-10)
-
-
-def test_cholesky_not_pd_raises(dev):
-    A = dev.from_numpy(np.array([[1.0, 2.0], [2.0, 1.0]]))
-    with pytest.raises(dev.LinAlgError):
-        dev.cholesky_(A)
+    with pytest.raises(dev.LinAlgError, match=f"{bad + 1}-th leading minor"):
+        dev.cholesky_(L)
 
 
 @pytest.mark.parametrize("n", [1, 6, 50, 200])

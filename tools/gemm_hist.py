@@ -24,9 +24,15 @@ class Tr(list):
             raise Stop
 
 
+import time  # noqa: E402
+import torch  # noqa: E402
+
 lib.ttk_gemm_hist(1, None)
+t0 = time.time()
 try:
     run_and_record(prob, config, seed, rank, trace=Tr(), verbose=False)
 except Stop:
     pass
+torch.cuda.synchronize()
+print(f"wall to Newton system {nstop + 1}: {time.time() - t0:.2f}s", flush=True)
 lib.ttk_gemm_hist(0, out.encode())
