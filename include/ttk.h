@@ -188,6 +188,15 @@ int ttk_syev_extreme(void *stream, const double *A, int n, int which, double *ev
  * flags_out[2] = {happy breakdown, DIVERGED_NULL (zero rotation norm)} */
 int ttk_lgmres_arnoldi_sync(void *stream, double *V, int n, int it, double *hh, int max_k,
                             double haptol, double *res_out, int *flags_out);
+/* Same step without a host read, for speculative chunks of Arnoldi steps between two host syncs
+ * (the host's per-step PETSc convergence test, `src/tt_ipm.py:149-154`, replayed on the chunk's
+ * records afterwards).  ctl (device, zeroed once per solve): ctl[0] = stop flag; step record at
+ * ctl[1 + 5*slot] = {marker, res, happy breakdown, null rotation, HH(it,it)}.  The step sets the
+ * stop flag when res <= ttol, res >= divtol, res is not finite, or on breakdown / null rotation;
+ * every later step's kernels return at entry, leaving V/HH exactly at the stopping step. */
+int ttk_lgmres_arnoldi_async(void *stream, double *V, int n, int it, double *hh, int max_k,
+                             double haptol, double ttol, double divtol, double *ctl, int slot,
+                             double marker);
 /* Build the correction y = HH \ GRS (in place in GRS), temp = sum_j y_j basis_j where the
  * basis list is given as a device pointer array of `nvec` vectors; x += temp; aug_temp = temp. */
 int ttk_lgmres_build(void *stream, double *hh, int max_k, int it, const double *const *basis,

@@ -65,6 +65,7 @@ _SIGS = {
     "ttk_contract_stats": (i32, [vp, i32]),
     "ttk_syev_extreme": (i32, [vp, vp, i32, i32, vp, vp, vp]),
     "ttk_lgmres_arnoldi_sync": (i32, [vp, vp, i32, i32, vp, i32, f64, c_dp, c_ip]),
+    "ttk_lgmres_arnoldi_async": (i32, [vp, vp, i32, i32, vp, i32, f64, f64, f64, vp, i32, f64]),
     "ttk_lgmres_build": (i32, [vp, vp, i32, i32, ctypes.POINTER(vp), i32, i32, vp, vp]),
     "ttk_lgmres_aug": (i32, [vp, vp, i32, i32, vp, i32, f64, vp, vp, vp]),
     "ttk_lgmres_set_mw_threshold": (i32, [i32]),

@@ -53,7 +53,33 @@ def build(force=False, verbose=False, out=OUT, defines=()):
     return out
 
 
+BIND_SRC = os.path.join(CSRC, "ttk_host_bind.cpp")
+BIND_OUT = os.path.join(HERE, "_ttkbind" + __import__("sysconfig").get_config_var("EXT_SUFFIX"))
+
+
+def build_bind(force=False, verbose=False):
+    """Host-side argument packer (`csrc/ttk_host_bind.cpp`): a torch C++ extension compiled with
+    g++ (no device code), loaded next to libttk.so by dev.py."""
+    if not force and os.path.exists(BIND_OUT) and os.path.getmtime(BIND_OUT) >= os.path.getmtime(BIND_SRC):
+        return BIND_OUT
+    import sysconfig
+    import torch
+    from torch.utils import cpp_extension as ce
+    inc = ce.include_paths() + [sysconfig.get_paths()["include"]]
+    libdir = ce.library_paths()[0]
+    abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+    cmd = (["g++", "-O2", "-fPIC", "-shared", "-std=c++17", "-w", f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
+            "-DTORCH_EXTENSION_NAME=_ttkbind", "-DTORCH_API_INCLUDE_EXTENSION_H"] + [f"-I{i}" for i in inc] +
+           [BIND_SRC, "-o", BIND_OUT, f"-L{libdir}", "-lc10", "-ltorch", "-ltorch_cpu", "-ltorch_python",
+            f"-Wl,-rpath,{libdir}"])
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.check_call(cmd, cwd=CSRC)
+    return BIND_OUT
+
+
 if __name__ == "__main__":
     defs = [a[2:] for a in sys.argv[1:] if a.startswith("-D")]
     outs = [a[6:] for a in sys.argv[1:] if a.startswith("--out=")]
     print(build(force="--force" in sys.argv, verbose=True, out=outs[0] if outs else OUT, defines=defs))
+    print(build_bind(force="--force" in sys.argv, verbose=True))

@@ -1,0 +1,154 @@
+// Host-side argument packing for the hot einsum / element-wise entry points of libttk.
+//
+// The TT-IPM host loop issues ~10^5 contraction and copy calls per solve; packing pointers,
+// shapes and strides of torch tensors in Python costs ~8 us per call (attribute lookups + a
+// ctypes array), more than the kernel itself.  This module reads them natively and calls the
+// same C ABI (`include/ttk.h`: ttk_einsum, ttk_copy_nd, ttk_mul_nd) through function pointers
+// handed over from the ctypes handle, so both paths share one libttk instance (plan cache,
+// event counters).  No arithmetic happens here.
+#include <torch/extension.h>
+
+#include <cstdint>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+namespace {
+
+using einsum_fn = int (*)(void *, const char *, const int64_t *, double *, double, double);
+using copy_fn = int (*)(void *, const double *, double *, int, const int64_t *, const int64_t *, const int64_t *,
+                        double, double);
+using mul_fn = int (*)(void *, const double *, const double *, double *, int, const int64_t *, const int64_t *,
+                       const int64_t *, const int64_t *, double, double);
+
+einsum_fn g_einsum = nullptr;
+copy_fn g_copy = nullptr;
+mul_fn g_mul = nullptr;
+void *g_stream = nullptr;
+
+void bind(int64_t einsum_addr, int64_t copy_addr, int64_t mul_addr, int64_t stream) {
+  g_einsum = reinterpret_cast<einsum_fn>(einsum_addr);
+  g_copy = reinterpret_cast<copy_fn>(copy_addr);
+  g_mul = reinterpret_cast<mul_fn>(mul_addr);
+  g_stream = reinterpret_cast<void *>(stream);
+}
+
+// output index string -> positions (operand, axis) of each output letter, per (equation)
+struct OutMap {
+  std::vector<std::pair<int, int>> src;
+};
+std::unordered_map<std::string, OutMap> g_out;
+
+const OutMap &out_map(const std::string &eq) {
+  auto it = g_out.find(eq);
+  if (it != g_out.end()) return it->second;
+  OutMap m;
+  const auto arrow = eq.find("->");
+  TORCH_CHECK(arrow != std::string::npos, "einsum: missing '->' in ", eq);
+  const std::string lhs = eq.substr(0, arrow), rhs = eq.substr(arrow + 2);
+  std::vector<std::string> ins;
+  size_t s = 0;
+  for (size_t i = 0; i <= lhs.size(); ++i)
+    if (i == lhs.size() || lhs[i] == ',') {
+      ins.push_back(lhs.substr(s, i - s));
+      s = i + 1;
+    }
+  for (char c : rhs) {
+    bool found = false;
+    for (int o = 0; o < (int)ins.size() && !found; ++o) {
+      const auto p = ins[o].find(c);
+      if (p != std::string::npos) {
+        m.src.emplace_back(o, (int)p);
+        found = true;
+      }
+    }
+    TORCH_CHECK(found, "einsum: output index ", c, " not in inputs of ", eq);
+  }
+  return g_out.emplace(eq, std::move(m)).first->second;
+}
+
+void check(int rc, const char *what) { TORCH_CHECK(rc == 0, "libttk ", what, " failed with status ", rc); }
+
+// out = alpha * einsum(eq, ops) + beta * out (out allocated when None); flags: 256 = fused opt-in
+at::Tensor einsum(const std::string &eq, const std::vector<at::Tensor> &ops, c10::optional<at::Tensor> out,
+                  double alpha, double beta, int64_t flags) {
+  TORCH_CHECK(g_einsum, "ttk_host_bind: bind() not called");
+  const int nops = (int)ops.size();
+  TORCH_CHECK(nops >= 1 && nops <= 8, "einsum: ", nops, " operands");
+  int64_t desc[8 * 34 + 20];
+  int64_t pos = 0;
+  desc[pos++] = nops | flags;
+  for (const auto &o : ops) {
+    const int nd = (int)o.dim();
+    TORCH_CHECK(nd <= 16, "einsum: operand rank ", nd);
+    desc[pos++] = reinterpret_cast<int64_t>(o.data_ptr());
+    desc[pos++] = nd;
+    const auto sz = o.sizes();
+    const auto st = o.strides();
+    for (int i = 0; i < nd; ++i) desc[pos++] = sz[i];
+    for (int i = 0; i < nd; ++i) desc[pos++] = st[i];
+  }
+  at::Tensor res;
+  if (out.has_value()) {
+    res = *out;
+    const int nd = (int)res.dim();
+    desc[pos++] = 1;
+    desc[pos++] = nd;
+    const auto st = res.strides();
+    for (int i = 0; i < nd; ++i) desc[pos++] = st[i];
+  } else {
+    const OutMap &m = out_map(eq);
+    std::vector<int64_t> shp(m.src.size());
+    for (size_t i = 0; i < m.src.size(); ++i) shp[i] = ops[m.src[i].first].size(m.src[i].second);
+    res = at::empty(shp, ops[0].options());
+    beta = 0.0;
+    desc[pos++] = 0;
+  }
+  check(g_einsum(g_stream, eq.c_str(), desc, res.data_ptr<double>(), alpha, beta), "einsum");
+  return res;
+}
+
+at::Tensor copy_(at::Tensor dst, const at::Tensor &src, double alpha, double beta) {
+  TORCH_CHECK(dst.sizes() == src.sizes(), "copy_: shape mismatch ", dst.sizes(), " vs ", src.sizes());
+  int nd = (int)dst.dim();
+  int64_t shp[16], ss[16], ds[16];
+  TORCH_CHECK(nd <= 16, "copy_: rank ", nd);
+  if (nd == 0) {
+    nd = 1;
+    shp[0] = 1;
+    ss[0] = ds[0] = 1;
+  } else {
+    for (int i = 0; i < nd; ++i) {
+      shp[i] = dst.size(i);
+      ss[i] = src.stride(i);
+      ds[i] = dst.stride(i);
+    }
+  }
+  check(g_copy(g_stream, src.data_ptr<double>(), dst.data_ptr<double>(), nd, shp, ss, ds, alpha, beta), "copy_nd");
+  return dst;
+}
+
+at::Tensor mul_(at::Tensor dst, const at::Tensor &a, const at::Tensor &b, double alpha, double beta) {
+  const int nd = (int)dst.dim();
+  TORCH_CHECK(nd >= 1 && nd <= 16 && a.dim() == nd && b.dim() == nd, "mul_: rank mismatch");
+  int64_t shp[16], as[16], bs[16], ds[16];
+  for (int i = 0; i < nd; ++i) {
+    shp[i] = dst.size(i);
+    as[i] = a.stride(i);
+    bs[i] = b.stride(i);
+    ds[i] = dst.stride(i);
+  }
+  check(g_mul(g_stream, a.data_ptr<double>(), b.data_ptr<double>(), dst.data_ptr<double>(), nd, shp, as, bs, ds,
+              alpha, beta),
+        "mul_nd");
+  return dst;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.def("bind", &bind);
+  m.def("einsum", &einsum);
+  m.def("copy_", &copy_);
+  m.def("mul_", &mul_);
+}

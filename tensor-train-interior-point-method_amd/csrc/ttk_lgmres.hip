@@ -27,6 +27,30 @@ struct HH {
   }
 };
 
+// Speculative (host-sync-free) Arnoldi chunks: `Ctl` carries the stop flag ctl[0] and one record
+// (step marker, res, hapend, null, HH(it,it)) per step of the chunk at ctl[1 + 5*slot].  Once a
+// step meets a stop condition every later kernel of the chunk returns at entry, so the Hessenberg
+// state stays exactly where the host-side loop stops.
+struct Ctl {
+  double *ctl;
+  int slot;
+  double marker, ttol, divtol;
+};
+
+__device__ inline bool ctl_stopped(const Ctl &c) { return c.ctl && c.ctl[0] != 0.0; }
+
+__device__ inline void ctl_record(const Ctl &c, double res, bool hapend, bool null_flag, double diag) {
+  if (!c.ctl) return;
+  double *r = c.ctl + 1 + 5 * c.slot;
+  r[0] = c.marker;
+  r[1] = res;
+  r[2] = hapend ? 1.0 : 0.0;
+  r[3] = null_flag ? 1.0 : 0.0;
+  r[4] = diag;
+  // KSPConvergedDefault's tests (rtol/atol, divergence, non-finite) plus breakdown / null rotation
+  if (hapend || null_flag || !(res == res) || isinf(res) || res <= c.ttol || res >= c.divtol) c.ctl[0] = 1.0;
+}
+
 constexpr int MAXV = 128;
 struct PtrList {
   const double *p[MAXV];
@@ -36,7 +60,8 @@ struct PtrList {
 // happy-breakdown test + KSPLGMRESUpdateHessenberg.  st[0]=res, st[1]=hapend, st[2]=null,
 // st[3]=HH(it,it) after rotation.
 __global__ __launch_bounds__(1024) void arnoldi_kernel(double *V, int n, int it, double *base, int max_k,
-                                                       double haptol) {
+                                                       double haptol, Ctl cl) {
+  if (ctl_stopped(cl)) return;
   __shared__ double h[MAXV + 2];
   __shared__ double red[16];
   HH H(base, max_k);
@@ -104,6 +129,7 @@ __global__ __launch_bounds__(1024) void arnoldi_kernel(double *V, int n, int it,
     H.st[1] = hapend ? 1.0 : 0.0;
     H.st[2] = null_flag;
     H.st[3] = H.hh[it * ld + it];
+    ctl_record(cl, res, hapend, null_flag != 0.0, H.st[3]);
   }
 }
 
@@ -169,7 +195,8 @@ constexpr int ARN_CHUNK = 2048;  // elements of one (j, chunk) partial dot
 constexpr int ARN_UPD = 512;     // elements per update block
 
 __global__ __launch_bounds__(256) void arnoldi_dot_kernel(const double *__restrict__ V, int n, int it,
-                                                          double *__restrict__ partials, int nchunk) {
+                                                          double *__restrict__ partials, int nchunk, Ctl cl) {
+  if (ctl_stopped(cl)) return;
   __shared__ double red[16];
   const int c = blockIdx.x, j = blockIdx.y, tid = threadIdx.x;
   const double *vj = V + (int64_t)j * n, *w = V + (int64_t)(it + 1) * n;
@@ -184,7 +211,8 @@ __global__ __launch_bounds__(256) void arnoldi_dot_kernel(const double *__restri
 __global__ __launch_bounds__(256) void arnoldi_update_kernel(double *__restrict__ V, int n, int it,
                                                              const double *__restrict__ partials, int nchunk,
                                                              double *__restrict__ normpart, double *base,
-                                                             int max_k) {
+                                                             int max_k, Ctl cl) {
+  if (ctl_stopped(cl)) return;
   __shared__ double h[MAXV + 2];
   __shared__ double red[16];
   const int tid = threadIdx.x;
@@ -215,7 +243,9 @@ __global__ __launch_bounds__(256) void arnoldi_update_kernel(double *__restrict_
 }
 
 __global__ __launch_bounds__(1024) void arnoldi_finish_kernel(double *V, int n, int it, const double *normpart,
-                                                              int nblk, double *base, int max_k, double haptol) {
+                                                              int nblk, double *base, int max_k, double haptol,
+                                                              Ctl cl) {
+  if (ctl_stopped(cl)) return;
   __shared__ double s_tt;
   HH H(base, max_k);
   const int tid = threadIdx.x, nt = blockDim.x;
@@ -263,6 +293,7 @@ __global__ __launch_bounds__(1024) void arnoldi_finish_kernel(double *V, int n, 
     H.st[1] = hapend ? 1.0 : 0.0;
     H.st[2] = null_flag;
     H.st[3] = H.hh[it * ld + it];
+    ctl_record(cl, res, hapend, null_flag != 0.0, H.st[3]);
   }
 }
 
@@ -352,41 +383,58 @@ int g_lgmres_mw_min = 16384;  // (it+1)*n at or above which the multi-workgroup 
 
 extern "C" {
 
-int ttk_lgmres_arnoldi_sync(void *stream, double *V, int n, int it, double *hh, int max_k, double haptol,
-                            double *res_out, int *hapend_out) {
+}  // extern "C"
+
+static int arnoldi_launch(hipStream_t st_, double *V, int n, int it, double *hh, int max_k, double haptol,
+                          const Ctl &cl, const char *who) {
   if (it + 1 > MAXV || max_k + 2 > MAXV + 2) {
-    ttk::set_error("ttk_lgmres_arnoldi_sync: restart %d too large (max %d)", max_k, MAXV);
+    ttk::set_error("%s: restart %d too large (max %d)", who, max_k, MAXV);
     return TTK_ERR_ARG;
   }
-  hipStream_t st_ = TTK_STREAM(stream);
   if ((int64_t)(it + 1) * n >= g_lgmres_mw_min) {
     const int nchunk = (n + ARN_CHUNK - 1) / ARN_CHUNK, nblk = (n + ARN_UPD - 1) / ARN_UPD;
     double *partials = lgmres_scratch((int64_t)(it + 1) * nchunk + nblk + 64);
     if (!partials) {
-      ttk::set_error("ttk_lgmres_arnoldi_sync: scratch allocation failed");
+      ttk::set_error("%s: scratch allocation failed", who);
       return TTK_ERR_HIP;
     }
     double *normpart = partials + (int64_t)(it + 1) * nchunk;
-    hipLaunchKernelGGL(arnoldi_dot_kernel, dim3(nchunk, it + 1), dim3(256), 0, st_, V, n, it, partials, nchunk);
+    hipLaunchKernelGGL(arnoldi_dot_kernel, dim3(nchunk, it + 1), dim3(256), 0, st_, V, n, it, partials, nchunk, cl);
     hipLaunchKernelGGL(arnoldi_update_kernel, dim3(nblk), dim3(256), 0, st_, V, n, it, partials, nchunk, normpart,
-                       hh, max_k);
+                       hh, max_k, cl);
     hipLaunchKernelGGL(arnoldi_finish_kernel, dim3(1), dim3(1024), 0, st_, V, n, it, normpart, nblk, hh, max_k,
-                       haptol);
+                       haptol, cl);
     TTK_LAUNCH_CHECK();
   } else {
-    hipLaunchKernelGGL(arnoldi_kernel, dim3(1), dim3(1024), 0, st_, V, n, it, hh, max_k, haptol);
+    hipLaunchKernelGGL(arnoldi_kernel, dim3(1), dim3(1024), 0, st_, V, n, it, hh, max_k, haptol, cl);
     TTK_LAUNCH_CHECK();
   }
+  return TTK_OK;
+}
+
+extern "C" {
+
+int ttk_lgmres_arnoldi_sync(void *stream, double *V, int n, int it, double *hh, int max_k, double haptol,
+                            double *res_out, int *hapend_out) {
+  const Ctl none{nullptr, 0, 0.0, 0.0, 0.0};
+  int rc = arnoldi_launch(TTK_STREAM(stream), V, n, it, hh, max_k, haptol, none, "ttk_lgmres_arnoldi_sync");
+  if (rc) return rc;
   const int ld = max_k + 1;
   const int64_t st_off = 2 * (int64_t)(max_k + 2) * ld + (max_k + 2) + 2 * ld;
   double st[4];
-  int rc = ttk_read_sync(stream, hh + st_off, st, 4);
+  rc = ttk_read_sync(stream, hh + st_off, st, 4);
   if (rc) return rc;
   res_out[0] = st[0];
   res_out[1] = st[3];
   hapend_out[0] = (int)st[1];
   hapend_out[1] = (int)st[2];
   return TTK_OK;
+}
+
+int ttk_lgmres_arnoldi_async(void *stream, double *V, int n, int it, double *hh, int max_k, double haptol,
+                             double ttol, double divtol, double *ctl, int slot, double marker) {
+  const Ctl cl{ctl, slot, marker, ttol, divtol};
+  return arnoldi_launch(TTK_STREAM(stream), V, n, it, hh, max_k, haptol, cl, "ttk_lgmres_arnoldi_async");
 }
 
 int ttk_lgmres_build(void *stream, double *hh, int max_k, int it, const double *const *basis, int nvec, int n,

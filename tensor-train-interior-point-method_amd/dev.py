@@ -40,6 +40,36 @@ def _p(t):
     return t.data_ptr()
 
 
+def _load_bind():
+    """`_ttkbind` (csrc/ttk_host_bind.cpp): packs tensor pointers/shapes/strides natively for the
+    hot einsum / copy / mul entry points (same libttk calls; ~8 us of Python packing saved per call)."""
+    import glob
+    import importlib.util
+    if os.environ.get("TTIPM_NO_BIND") == "1":
+        return None
+    paths = glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "_ttkbind*.so"))
+    if not paths:
+        return None
+    spec = importlib.util.spec_from_file_location("_ttkbind", paths[0])
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+_BIND = _load_bind()
+_FAST = None
+
+
+def _fast():
+    global _FAST
+    if _FAST is None and _BIND is not None:
+        def addr(f):
+            return ctypes.cast(f, ctypes.c_void_p).value
+        _BIND.bind(addr(lib.ttk_einsum), addr(lib.ttk_copy_nd), addr(lib.ttk_mul_nd), _stream() or 0)
+        _FAST = _BIND
+    return _FAST
+
+
 def empty(*shape):
     return torch.empty(shape, dtype=F64, device=DEV)
 
@@ -96,6 +126,9 @@ def _arr(vals):
 # ------------------------------------------------------------------------ element-wise
 def copy_(dst, src, alpha=1.0, beta=0.0):
     """dst = alpha * src + beta * dst (shapes must match; any strides)."""
+    f = _FAST or _fast()
+    if f is not None:
+        return f.copy_(dst, src, float(alpha), float(beta))
     assert tuple(dst.shape) == tuple(src.shape), (dst.shape, src.shape)
     nd = dst.dim()
     if nd == 0:
@@ -120,6 +153,9 @@ def clone(src):
 
 def mul_(dst, a, b, alpha=1.0, beta=0.0):
     """dst = alpha * a * b + beta * dst (element-wise, same shapes, any strides)."""
+    f = _FAST or _fast()
+    if f is not None:
+        return f.mul_(dst, a, b, float(alpha), float(beta))
     nd = dst.dim()
     check(lib.ttk_mul_nd(_stream(), _p(a), _p(b), _p(dst), nd, _arr(dst.shape), _arr(a.stride()),
                          _arr(b.stride()), _arr(dst.stride()), float(alpha), float(beta)), "mul_nd")
@@ -258,6 +294,9 @@ def _einsum_native(eq, *ops, out=None, alpha=1.0, beta=0.0, fused=False):
     if OPSTATS is not None:
         e = OPSTATS.setdefault("einsum_eq", {}).setdefault(eq, [0, 0.0])
         e[0] += 1
+    f = _FAST or _fast()
+    if f is not None:
+        return f.einsum(eq, ops, out, float(alpha), float(beta), 256 if fused else 0)
     desc = [len(ops) | (256 if fused else 0)]
     for o in ops:
         desc.append(o.data_ptr())

@@ -4,8 +4,14 @@
 The Krylov basis, Hessenberg matrices and Givens rotations live on the device
 (`ttk_lgmres_*` kernels); the host runs PETSc's integer bookkeeping (restart cycles,
 augmentation order) and reads one residual estimate per Arnoldi step for the convergence test
-(KSPConvergedDefault).  The algorithm is restated in `oracle/petsc_lgmres.py`."""
+(KSPConvergedDefault).  The algorithm is restated in `oracle/petsc_lgmres.py`.
+
+Host syncs: Arnoldi steps are enqueued in speculative chunks of up to CHUNK steps
+(`ttk_lgmres_arnoldi_async`); the device stops modifying the Krylov state at the first step that
+meets a stop condition, and the host replays the per-step test on the chunk's records after ONE
+read, so decisions, iteration counts and iterates are those of the step-by-step loop."""
 import ctypes
+import os
 
 import numpy as np
 
@@ -14,6 +20,9 @@ from ._lib import lib
 
 CONVERGED_RTOL, CONVERGED_ATOL = 2, 3
 DIVERGED_NULL, DIVERGED_ITS, DIVERGED_DTOL, DIVERGED_BREAKDOWN, DIVERGED_NANORINF = -2, -3, -4, -5, -9
+
+
+CHUNK = int(os.environ.get("TTIPM_LGMRES_CHUNK", "8"))
 
 
 class PetscConvFailed(RuntimeError):
@@ -55,6 +64,19 @@ def lgmres(matvec_into, b, rtol=1e-8, max_it=300, restart=30, augment=2, abstol=
     s = D._stream()
     resbuf = (ctypes.c_double * 2)()
     flags = (ctypes.c_int * 2)()
+    ctl = D.zeros(1 + 5 * max(CHUNK, 1))
+
+    def _matvec_or_aug(li):
+        if li < it_arnoldi:
+            matvec_into(V[li], V[li + 1])
+        else:
+            order = li - it_arnoldi + 1
+            spot = 0
+            for ii in range(aug_dim):
+                if aug_order[ii] == order:
+                    spot = ii
+                    break
+            D.copy_(V[li + 1], a_augvecs[spot])
 
     def converged(k, rnorm):
         if k == 0:
@@ -87,29 +109,40 @@ def lgmres(matvec_into, b, rtol=1e-8, max_it=300, restart=30, augment=2, abstol=
         hapend = False
         last_diag = 1.0
         while (not reason) and loc_it < it_total and its < max_it:
-            if loc_it < it_arnoldi:
-                matvec_into(V[loc_it], V[loc_it + 1])
+            kmax = min(CHUNK, it_total - loc_it, max_it - its)
+            if kmax <= 1:
+                _matvec_or_aug(loc_it)
+                D.check(lib.ttk_lgmres_arnoldi_sync(s, V.data_ptr(), n, loc_it, hh.data_ptr(), max_k, haptol,
+                                                    resbuf, flags), "lgmres_arnoldi")
+                recs = [(float(its + 1), resbuf[0], float(flags[0]), float(flags[1]), resbuf[1])]
             else:
-                order = loc_it - it_arnoldi + 1
-                spot = 0
-                for ii in range(aug_dim):
-                    if aug_order[ii] == order:
-                        spot = ii
-                        break
-                D.copy_(V[loc_it + 1], a_augvecs[spot])
-            D.check(lib.ttk_lgmres_arnoldi_sync(s, V.data_ptr(), n, loc_it, hh.data_ptr(), max_k, haptol,
-                                                resbuf, flags), "lgmres_arnoldi")
-            hapend = bool(flags[0])
-            if flags[1]:
-                reason = DIVERGED_NULL
-                break
-            res = resbuf[0]
-            last_diag = resbuf[1]
-            loc_it += 1
-            its += 1
-            reason = converged(its, res)
-            if hapend and not reason:
-                reason = DIVERGED_BREAKDOWN
+                ttol, divtol = state["ttol"], dtol * state["rnorm0"]
+                for q in range(kmax):
+                    _matvec_or_aug(loc_it + q)
+                    D.check(lib.ttk_lgmres_arnoldi_async(s, V.data_ptr(), n, loc_it + q, hh.data_ptr(), max_k,
+                                                         haptol, ttol, divtol, ctl.data_ptr(), q,
+                                                         float(its + q + 1)), "lgmres_arnoldi")
+                h = D.read(ctl[:1 + 5 * kmax])
+                recs = [tuple(h[1 + 5 * q:6 + 5 * q]) for q in range(kmax)]
+            for q, (marker, r_, hap_, null_, diag_) in enumerate(recs):
+                if marker != its + 1:
+                    raise RuntimeError(f"lgmres: device stopped the Arnoldi chunk at step {its} without a "
+                                       "host-side stop reason")
+                hapend = bool(hap_)
+                if null_:
+                    reason = DIVERGED_NULL
+                    break
+                res = r_
+                last_diag = diag_
+                loc_it += 1
+                its += 1
+                reason = converged(its, res)
+                if hapend and not reason:
+                    reason = DIVERGED_BREAKDOWN
+                    break
+                if reason:
+                    break
+            if reason == DIVERGED_NULL or reason == DIVERGED_BREAKDOWN:
                 break
         cycle_its = loc_it
         it = loc_it - 1

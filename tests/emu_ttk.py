@@ -327,6 +327,18 @@ class EmuLib:
         flags[1] = null
         return 0
 
+    def ttk_lgmres_arnoldi_async(self, s, V, n, it, hh, max_k, haptol, ttol, divtol, ctl, slot, marker):
+        c = _dv(ctl, 1 + 5 * (slot + 1))
+        if c[0] != 0.0:
+            return 0
+        res, flags = (ctypes.c_double * 2)(), (ctypes.c_int * 2)()
+        self.ttk_lgmres_arnoldi_sync(s, V, n, it, hh, max_k, haptol, res, flags)
+        c[1 + 5 * slot:6 + 5 * slot] = (marker, res[0], flags[0], flags[1], res[1])
+        r = res[0]
+        if flags[0] or flags[1] or not np.isfinite(r) or r <= ttol or r >= divtol:
+            c[0] = 1.0
+        return 0
+
     def ttk_lgmres_build(self, s, hh, max_k, it, basis, nvec, n, x, aug_temp):
         HH, HES, GRS, CC, SS = self._hh(hh, max_k)
         GRS[it] = GRS[it] / HH[it, it]
@@ -359,6 +371,7 @@ class EmuLib:
 def emulated_ttipm():
     """Import `ttipm_amd` with CPU tensors and the NumPy emulator in place of libttk.so."""
     os.environ["TTIPM_DEVICE"] = "cpu"
+    os.environ["TTIPM_NO_BIND"] = "1"  # the native packer calls libttk function pointers directly
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     if root not in sys.path:
         sys.path.insert(0, root)
