@@ -100,6 +100,10 @@ int ttk_mul_nd(void *stream, const double *src, const double *src2, double *dst,
                const int64_t *shape, const int64_t *sstride, const int64_t *s2stride,
                const int64_t *dstride, double alpha, double beta);
 int ttk_recip(void *stream, const double *src, double *dst, int64_t n);
+/* dst = src * scales[i_axis] with the (<= 16) scales passed by value from the host: the per-block
+ * column scaling / unscaling of the AMEn sweep (`src/tt_als.py:321-322,444-446`), no H2D copy. */
+int ttk_scale_axis(void *stream, const double *src, double *dst, int ndim, const int64_t *shape,
+                   const int64_t *sstride, const int64_t *dstride, int axis, const double *scales);
 int ttk_fill(void *stream, double *dst, int64_t n, double value);
 int ttk_add_diag(void *stream, double *A, int n, int lda, double value);
 
@@ -167,10 +171,15 @@ int ttk_syev(void *stream, double *A, int n, double *ev, double *W, double *work
  * calls of the step-size ALS (`src/tt_als.py:963-993` (_step_size_local_solve),
  * `:1069-1098`, `:1308` (_eigen_local_solve)). */
 int64_t ttk_syev_extreme_work(int n);
-/* 3 <= n <= 128 takes a latency-optimised 4-wave kernel (A in LDS, 3 barriers per reflector);
+/* 3 <= n <= 128 takes a latency-optimised LDS kernel (4 waves below n = 64, 16 waves above;
+ * Sturm multisection on 4 waves; 3 barriers per reflector);
  * on = 0 routes every size through the general one-workgroup / multi-workgroup kernels (tests).
  * Returns the previous setting. */
 int ttk_syev_set_small(int on);
+/* Beyond the LDS kernels, n <= this limit (default and maximum 2048) runs the multi-workgroup
+ * tridiagonalisation with ONE launch per Householder step (reflector rebuilt per block in LDS);
+ * larger n (or limit 0) the two-launch variant.  Returns the previous limit. */
+int ttk_syev_set_fused_max(int n);
 /* diagnostic counters of the factorisation kernels (8 x u64: svd calls, svd sweeps, eig calls,
  * multisection rounds, ...); synchronous; reset != 0 zeroes them */
 int ttk_debug_counters(unsigned long long *out, int reset);

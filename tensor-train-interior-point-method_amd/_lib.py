@@ -33,6 +33,7 @@ _SIGS = {
     "ttk_copy_nd": (i32, [vp, vp, vp, i32, c_i64p, c_i64p, c_i64p, f64, f64]),
     "ttk_mul_nd": (i32, [vp, vp, vp, vp, i32, c_i64p, c_i64p, c_i64p, c_i64p, f64, f64]),
     "ttk_recip": (i32, [vp, vp, vp, i64]),
+    "ttk_scale_axis": (i32, [vp, vp, vp, i32, c_i64p, c_i64p, c_i64p, i32, c_dp]),
     "ttk_fill": (i32, [vp, vp, i64, f64]),
     "ttk_add_diag": (i32, [vp, vp, i32, i32, f64]),
     "ttk_dot_nd_sync": (i32, [vp, vp, vp, i32, c_i64p, c_i64p, c_i64p, c_dp]),
@@ -51,6 +52,7 @@ _SIGS = {
     "ttk_syev": (i32, [vp, vp, i32, vp, vp, vp]),
     "ttk_syev_extreme_work": (i64, [i32]),
     "ttk_syev_set_small": (i32, [i32]),
+    "ttk_syev_set_fused_max": (i32, [i32]),
     "ttk_debug_counters": (i32, [vp, i32]),
     "ttk_svd_set_timing": (i32, [i32]),
     "ttk_svd_set_big_threshold": (i32, [i32]),

@@ -199,6 +199,29 @@ __global__ void mul_nd_kernel(const double *__restrict__ s1, const double *__res
   }
 }
 
+struct AxisScales {
+  double v[16];
+};
+
+// dst = src * scale[coordinate along `axis`] (per-block column scaling of the AMEn sweep)
+__global__ void scale_axis_kernel(const double *__restrict__ src, double *__restrict__ dst, ttk::NdDesc d, int axis,
+                                  AxisScales sc) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < d.total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t lin = i, os = 0, od = 0, ca = 0;
+    for (int k = d.ndim - 1; k >= 0; --k) {
+      const int64_t e = d.shape[k];
+      const int64_t q = lin / e;
+      const int64_t r = lin - q * e;
+      lin = q;
+      os += r * d.s0[k];
+      od += r * d.s1[k];
+      if (k == axis) ca = r;
+    }
+    dst[od] = src[os] * sc.v[ca];
+  }
+}
+
 __global__ void recip_kernel(const double *__restrict__ src, double *__restrict__ dst, int64_t n) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
     dst[i] = 1.0 / src[i];
@@ -469,6 +492,25 @@ int ttk_mul_nd(void *stream, const double *src, const double *src2, double *dst,
   if (d.total == 0) return TTK_OK;
   hipLaunchKernelGGL(mul_nd_kernel, dim3(grid_for(d.total, 256)), dim3(256), 0, TTK_STREAM(stream), src,
                      src2, dst, d, alpha, beta);
+  TTK_LAUNCH_CHECK();
+  return TTK_OK;
+}
+
+int ttk_scale_axis(void *stream, const double *src, double *dst, int ndim, const int64_t *shape,
+                   const int64_t *sstride, const int64_t *dstride, int axis, const double *scales) {
+  ttk::NdDesc d;
+  int st = make_nd(d, ndim, shape, sstride, dstride, nullptr);
+  if (st) return st;
+  if (axis < 0 || axis >= ndim || shape[axis] > 16) {
+    ttk::set_error("ttk_scale_axis: axis %d (extent %lld) out of range (max extent 16)", axis,
+                   axis >= 0 && axis < ndim ? (long long)shape[axis] : -1LL);
+    return TTK_ERR_ARG;
+  }
+  if (d.total == 0) return TTK_OK;
+  AxisScales sc;
+  for (int i = 0; i < 16; ++i) sc.v[i] = i < shape[axis] ? scales[i] : 0.0;
+  hipLaunchKernelGGL(scale_axis_kernel, dim3(grid_for(d.total, 256)), dim3(256), 0, TTK_STREAM(stream), src, dst,
+                     d, axis, sc);
   TTK_LAUNCH_CHECK();
   return TTK_OK;
 }

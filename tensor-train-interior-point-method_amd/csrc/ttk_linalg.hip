@@ -16,6 +16,7 @@
 //          estimate (Hager / Higham) for scipy.linalg.solve's ill-conditioning warning.
 //  syev  : cyclic two-sided Jacobi with round-robin ordering (eigenvalues ascending).
 #include <math.h>
+#include <stdlib.h>
 
 #include "ttk_common.h"
 #include "ttk_internal.h"
@@ -1164,28 +1165,50 @@ __device__ void tridiag_extreme_finish(double *A, int n, int which, double *dv, 
   }
   __syncthreads();
   // ---- 2. multisection
+  // at most 4 waves evaluate shifts: the Sturm recurrence is issue-bound, more waves per SIMD only
+  // stretch each round (the extra waves of a 16-wave block wait at the barriers)
+  const int ns = nt < 256 ? nt : 256;
   for (int round = 0; round < 16; ++round) {
     const double a = sh_a, b = sh_b;
     if (b - a <= 2.0 * EPS * fmax(fabs(a), fabs(b)) + 2.0 * pivmin) break;
     if (tid == 0) atomicAdd(&g_dbg[3], 1ull);
-    const double x = a + (b - a) * (double)(tid + 1) / (double)(nt + 1);
-    int cnt = 0;
-    double q = dv[0] - x;
-    if (fabs(q) < pivmin) q = -pivmin;
-    cnt += q < 0.0;
-    for (int i = 1; i < n; ++i) {
-      q = dv[i] - x - ev2[i - 1] * fast_rcp(q);
+    if (tid == 0) sh_first = ns;
+    __syncthreads();
+    if (tid < ns) {
+      const double x = a + (b - a) * (double)(tid + 1) / (double)(ns + 1);
+      int cnt = 0;
+      double q = dv[0] - x;
       if (fabs(q) < pivmin) q = -pivmin;
       cnt += q < 0.0;
+      int i = 1;
+      for (; i + 3 < n; i += 4) {  // operands of 4 steps loaded ahead of the recurrence
+        const double d0 = dv[i] - x, d1 = dv[i + 1] - x, d2 = dv[i + 2] - x, d3 = dv[i + 3] - x;
+        const double e0 = ev2[i - 1], e1 = ev2[i], e2 = ev2[i + 1], e3 = ev2[i + 2];
+        q = d0 - e0 * fast_rcp(q);
+        if (fabs(q) < pivmin) q = -pivmin;
+        cnt += q < 0.0;
+        q = d1 - e1 * fast_rcp(q);
+        if (fabs(q) < pivmin) q = -pivmin;
+        cnt += q < 0.0;
+        q = d2 - e2 * fast_rcp(q);
+        if (fabs(q) < pivmin) q = -pivmin;
+        cnt += q < 0.0;
+        q = d3 - e3 * fast_rcp(q);
+        if (fabs(q) < pivmin) q = -pivmin;
+        cnt += q < 0.0;
+      }
+      for (; i < n; ++i) {
+        q = dv[i] - x - ev2[i - 1] * fast_rcp(q);
+        if (fabs(q) < pivmin) q = -pivmin;
+        cnt += q < 0.0;
+      }
+      if (cnt >= target) atomicMin(&sh_first, tid);
     }
-    if (tid == 0) sh_first = nt;
-    __syncthreads();
-    if (cnt >= target) atomicMin(&sh_first, tid);
     __syncthreads();
     if (tid == 0) {
       const int f = sh_first;
-      sh_a = (f == 0) ? a : a + (b - a) * (double)f / (double)(nt + 1);
-      sh_b = (f >= nt) ? b : a + (b - a) * (double)(f + 1) / (double)(nt + 1);
+      sh_a = (f == 0) ? a : a + (b - a) * (double)f / (double)(ns + 1);
+      sh_b = (f >= ns) ? b : a + (b - a) * (double)(f + 1) / (double)(ns + 1);
     }
     __syncthreads();
   }
@@ -1399,9 +1422,11 @@ __global__ __launch_bounds__(1024) void syev_extreme_kernel(const double *__rest
 // syev_extreme_kernel, so both paths produce the same eigenpair to rounding.
 constexpr int SYEV_SMALL_N = 128;
 
-__global__ __launch_bounds__(256) void syev_small_kernel(const double *__restrict__ Ain, int n, int which,
-                                                         double *__restrict__ ev_out, double *__restrict__ vec_out,
-                                                         int timing) {
+template <int NT>
+__global__ __launch_bounds__(NT) void syev_small_kernel(const double *__restrict__ Ain, int n, int which,
+                                                        double *__restrict__ ev_out, double *__restrict__ vec_out,
+                                                        int timing) {
+  constexpr int NW = NT / 64, G = NT / 128;  // waves; lanes per row in the symv (rows <= 127)
   extern __shared__ double lds[];
   const int ld = n | 1;
   double *A = lds;
@@ -1409,7 +1434,7 @@ __global__ __launch_bounds__(256) void syev_small_kernel(const double *__restric
   double *fd = z + n, *fdu = fd + n, *fdu2 = fdu + n, *fdl = fdu2 + n, *fpiv = fdl + n;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const unsigned long long t_ph0 = timing ? wall_clock64() : 0;
-  for (int e = tid; e < n * n; e += 256) {
+  for (int e = tid; e < n * n; e += NT) {
     const int i = e / n, j = e - i * n;
     A[i * ld + j] = Ain[e];
   }
@@ -1441,23 +1466,24 @@ __global__ __launch_bounds__(256) void syev_small_kernel(const double *__restric
     const double tau = tv[k];
     if (tau == 0.0) continue;
     const double *A22 = A + (k + 1) * ld + k + 1;
-    {  // p = tau A22 v: row r = tid / 2, half h = tid & 1 (columns h, h+2, ...)
-      const int r = tid >> 1, h = tid & 1;
+    {  // p = tau A22 v: row r = tid / G, lane h = tid % G of the row takes columns h, h+G, ...
+      const int r = tid / G, h = tid % G;
       double acc = 0.0;
       if (r < m) {  // four independent chains: the LDS loads of one batch overlap
         const double *ar = A22 + r * ld;
         double a1 = 0.0, a2 = 0.0, a3 = 0.0;
         int j = h;
-        for (; j + 6 < m; j += 8) {
+        for (; j + 3 * G < m; j += 4 * G) {
           acc = fma(ar[j], v[j], acc);
-          a1 = fma(ar[j + 2], v[j + 2], a1);
-          a2 = fma(ar[j + 4], v[j + 4], a2);
-          a3 = fma(ar[j + 6], v[j + 6], a3);
+          a1 = fma(ar[j + G], v[j + G], a1);
+          a2 = fma(ar[j + 2 * G], v[j + 2 * G], a2);
+          a3 = fma(ar[j + 3 * G], v[j + 3 * G], a3);
         }
-        for (; j < m; j += 2) acc = fma(ar[j], v[j], acc);
+        for (; j < m; j += G) acc = fma(ar[j], v[j], acc);
         acc = (acc + a1) + (a2 + a3);
       }
-      acc += __shfl_xor(acc, 1, 64);
+#pragma unroll
+      for (int o = 1; o < G; o <<= 1) acc += __shfl_xor(acc, o, 64);
       if (h == 0 && r < m) pv[r] = tau * acc;
     }
     __syncthreads();
@@ -1467,7 +1493,7 @@ __global__ __launch_bounds__(256) void syev_small_kernel(const double *__restric
     const double K = 0.5 * tau * ttk::wave_sum(fma(p0, v0, p1 * v1));
     const double w0 = fma(-K, v0, p0), w1 = fma(-K, v1, p1);
 #pragma unroll 4
-    for (int i = wid; i < m; i += 4) {
+    for (int i = wid; i < m; i += NW) {
       const double vi = v[i], wi = fma(-K, vi, pv[i]);
       double *ai = A + (k + 1 + i) * ld + k + 1;
       if (j0 < m) ai[j0] -= fma(vi, w0, wi * v0);
@@ -1579,6 +1605,134 @@ __global__ __launch_bounds__(1024) void tri_finish_kernel(double *A, int n, int 
   double *dv = gv, *ov = dv + n, *ev2 = ov + n, *tv = ev2 + n, *z = tv + n;
   double *fd = z + n, *fdu = fd + n, *fdu2 = fdu + n, *fdl = fdu2 + n, *fpiv = fdl + n;
   tridiag_extreme_finish(A, n, which, dv, ov, ev2, tv, z, fd, fdu, fdu2, fdl, fpiv, ev_out, vec_out, n);
+}
+
+// One launch per Householder step (replaces tri_update + tri_matvec): every block rebuilds row k
+// with the pending rank-2 update of step k-1 and reflector k in LDS (redundantly: no extra launch
+// or grid sync), then updates its own rows and forms their part of p = tau A22 v.  The only
+// cross-block dependency per step is p itself, carried to the next launch in double-buffered
+// global vectors; reflector k reaches A's row k one launch later, when no block reads that row.
+constexpr int TRI_FUSED_MAX = 2048;
+
+__global__ __launch_bounds__(256) void tri_step_kernel(double *A, int n, int k, double *tv, double *ov, double *dv,
+                                                       double *pvb, double *partb, double *vbuf, int nblk, int rb) {
+  __shared__ double xs[TRI_FUSED_MAX + 1];
+  __shared__ double red[16];
+  __shared__ double s_k, s_tau;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int r0 = blockIdx.x * rb, r1 = r0 + rb < n ? r0 + rb : n;
+  const int kp = k - 1;
+  const double *pvp = pvb + (kp & 1) * (int64_t)n, *ptp = partb + (kp & 1) * (int64_t)nblk;
+  const double *vp = vbuf + (kp & 1) * (int64_t)n;  // reflector k-1, relative index (vp[0] = 1)
+  double *pvc = pvb + (k & 1) * (int64_t)n, *ptc = partb + (k & 1) * (int64_t)nblk, *vc = vbuf + (k & 1) * (int64_t)n;
+  const double taup = kp >= 0 ? tv[kp] : 0.0;
+  if (wid == 0) {
+    double acc = 0.0;
+    if (taup != 0.0)
+      for (int i = lane; i < nblk; i += 64) acc += ptp[i];
+    acc = ttk::wave_sum(acc);
+    if (lane == 0) s_k = 0.5 * taup * acc;
+  }
+  __syncthreads();
+  const double K = s_k;
+  // reflector k of the pending-updated row k (relative index jj = j - kp - 1 into step k-1's vectors)
+  const int m = n - k - 1;
+  {
+    const double wk = taup != 0.0 ? pvp[0] - K * vp[0] : 0.0, vk = taup != 0.0 ? vp[0] : 0.0;
+    const double *ak = A + (int64_t)k * n;
+    for (int j = k + tid; j < n; j += 256) {
+      double a = ak[j];
+      if (taup != 0.0) {
+        const int jj = j - kp - 1;
+        const double vj = vp[jj];
+        a -= vk * (pvp[jj] - K * vj) + wk * vj;
+      }
+      xs[j - k] = a;
+    }
+  }
+  __syncthreads();
+  double part = 0.0;
+  for (int i = 2 + tid; i <= m; i += 256) part += xs[i] * xs[i];
+  const double sigma = ttk::block_sum(part, red);
+  const double alpha = xs[1];
+  double tau = 0.0, beta = alpha;
+  if (sigma > 0.0) {
+    beta = -copysign(sqrt(alpha * alpha + sigma), alpha);
+    tau = (beta - alpha) / beta;
+  }
+  const double sc = sigma > 0.0 ? 1.0 / (alpha - beta) : 1.0;
+  const bool owner_k = k >= r0 && k < r1;
+  if (tid == 0) s_tau = tau;
+  __syncthreads();  // every thread has read xs[1] / the sigma partials
+  for (int i = 1 + tid; i <= m; i += 256) {
+    const double v = (i == 1) ? 1.0 : xs[i] * sc;
+    xs[i] = v;  // xs[1 + jj] = v_k[jj]
+    if (owner_k) vc[i - 1] = v;
+  }
+  if (owner_k && tid == 0) {
+    tv[k] = tau;
+    ov[k] = beta;
+    dv[k] = xs[0];
+  }
+  // reflector k-1 into A's row k-1 (nobody reads that row in this launch)
+  if (kp >= 0 && kp >= r0 && kp < r1)
+    for (int j = kp + 1 + tid; j < n; j += 256) A[(int64_t)kp * n + j] = vp[j - kp - 1];
+  __syncthreads();
+  // own rows r > k: pending update of step k-1, then p_r = tau <A[r, k+1:], v_k>
+  const int rs = r0 > k + 1 ? r0 : k + 1;
+  double contrib = 0.0;
+  for (int r = rs + wid; r < r1; r += 4) {
+    double *ar = A + (int64_t)r * n;
+    const int ir = r - kp - 1;
+    const double vi = taup != 0.0 ? vp[ir] : 0.0, wi = taup != 0.0 ? pvp[ir] - K * vi : 0.0;
+    double acc = 0.0;
+    for (int j = k + 1 + lane; j < n; j += 64) {
+      double a = ar[j];
+      if (taup != 0.0) {
+        const int jj = j - kp - 1;
+        const double vj = vp[jj];
+        a -= vi * (pvp[jj] - K * vj) + wi * vj;
+        ar[j] = a;
+      }
+      acc = fma(a, xs[j - k], acc);
+    }
+    acc = ttk::wave_sum(acc);
+    if (lane == 0) {
+      const double pr = tau * acc;
+      pvc[r - k - 1] = pr;
+      contrib += pr * xs[r - k];
+    }
+  }
+  contrib = ttk::block_sum(contrib, red);
+  if (tid == 0) ptc[blockIdx.x] = contrib;
+  (void)s_tau;
+}
+
+// after the last step (k = n-3): pending update of step n-3 on the trailing 2 x 2 block and
+// reflector n-3 into A's row n-3 (one block)
+__global__ __launch_bounds__(256) void tri_tail_kernel(double *A, int n, double *tv, double *pvb, double *partb,
+                                                       double *vbuf, int nblk) {
+  __shared__ double s_k;
+  const int kp = n - 3, tid = threadIdx.x, lane = tid & 63;
+  const double *pvp = pvb + (kp & 1) * (int64_t)n, *ptp = partb + (kp & 1) * (int64_t)nblk;
+  const double *vp = vbuf + (kp & 1) * (int64_t)n;
+  const double taup = tv[kp];
+  if (tid < 64) {
+    double acc = 0.0;
+    if (taup != 0.0)
+      for (int i = lane; i < nblk; i += 64) acc += ptp[i];
+    acc = ttk::wave_sum(acc);
+    if (lane == 0) s_k = 0.5 * taup * acc;
+  }
+  __syncthreads();
+  const double K = s_k;
+  if (tid < 4 && taup != 0.0) {
+    const int r = n - 2 + (tid >> 1), j = n - 2 + (tid & 1);
+    const int ir = r - kp - 1, jj = j - kp - 1;
+    const double vi = vp[ir], wi = pvp[ir] - K * vi, vj = vp[jj];
+    A[(int64_t)r * n + j] -= vi * (pvp[jj] - K * vj) + wi * vj;
+  }
+  for (int j = kp + 1 + tid; j < n; j += 256) A[(int64_t)kp * n + j] = vp[j - kp - 1];
 }
 
 template <typename K>
@@ -2399,7 +2553,22 @@ int ttk_syev_set_small(int on) {
   return old;
 }
 
-int64_t ttk_syev_extreme_work(int n) { return n > 0 ? syev_extreme_need(n) : 0; }
+int64_t ttk_syev_extreme_work(int n) {
+  if (n <= 0) return 0;
+  const int64_t fused = (int64_t)n * n + 18 * (int64_t)n + 64;  // tri_step_kernel layout
+  const int64_t need = syev_extreme_need(n);
+  return need > fused ? need : fused;
+}
+
+static int g_syev_fused_max = TRI_FUSED_MAX;
+static int g_syev_small_wide = getenv("TTK_SYEV_WIDE") ? atoi(getenv("TTK_SYEV_WIDE")) : 64;  // 16-wave small kernel from this n
+static int g_tri_rows = getenv("TTK_TRI_ROWS") ? atoi(getenv("TTK_TRI_ROWS")) : 4;  // largest n for the one-launch-per-step tridiagonalisation
+
+int ttk_syev_set_fused_max(int n) {
+  const int old = g_syev_fused_max;
+  g_syev_fused_max = n < TRI_FUSED_MAX ? n : TRI_FUSED_MAX;
+  return old;
+}
 
 int ttk_syev_extreme(void *stream, const double *A, int n, int which, double *ev, double *vec, double *work) {
   if (n <= 0 || (which != 0 && which != 1)) {
@@ -2409,6 +2578,21 @@ int ttk_syev_extreme(void *stream, const double *A, int n, int which, double *ev
   const int64_t need = syev_extreme_need(n);
   const int use_lds = need <= LDS_DOUBLES;
   hipStream_t st = TTK_STREAM(stream);
+  if (!use_lds && n > 2 && n <= g_syev_fused_max) {  // one launch per Householder step
+    double *Aw = work, *gv = work + (int64_t)n * n;
+    double *dv = gv, *ov = dv + n, *tv = ov + 2 * n;  // layout of tri_finish_kernel: dv ov ev2 tv ...
+    const int rb = g_tri_rows;  // rows per block (4 = one row per wave)
+    const int nblk = (n + rb - 1) / rb;
+    double *pvb = gv + 11 * (int64_t)n, *vbuf = pvb + 2 * (int64_t)n, *partb = vbuf + 2 * (int64_t)n;
+    TTK_HIP(hipMemcpyAsync(Aw, A, sizeof(double) * (size_t)n * n, hipMemcpyDeviceToDevice, st));
+    for (int k = 0; k + 2 < n; ++k)
+      hipLaunchKernelGGL(tri_step_kernel, dim3(nblk), dim3(256), 0, st, Aw, n, k, tv, ov, dv, pvb, partb, vbuf, nblk,
+                         rb);
+    hipLaunchKernelGGL(tri_tail_kernel, dim3(1), dim3(256), 0, st, Aw, n, tv, pvb, partb, vbuf, nblk);
+    hipLaunchKernelGGL(tri_finish_kernel, dim3(1), dim3(1024), 0, st, Aw, n, which, gv, ev, vec);
+    TTK_LAUNCH_CHECK();
+    return TTK_OK;
+  }
   if (!use_lds && n > 2) {  // multi-workgroup tridiagonalisation, one-workgroup finish
     double *Aw = work, *gv = work + (int64_t)n * n;
     double *dv = gv, *ov = dv + n, *tv = ov + 2 * n;  // layout of tri_finish_kernel: dv ov ev2 tv ...
@@ -2427,8 +2611,13 @@ int ttk_syev_extreme(void *stream, const double *A, int n, int which, double *ev
   }
   if (n >= 3 && n <= SYEV_SMALL_N && g_syev_small) {
     const size_t shm_s = (size_t)syev_small_need(n) * sizeof(double);
-    allow_big_lds(syev_small_kernel, shm_s);
-    hipLaunchKernelGGL(syev_small_kernel, dim3(1), dim3(256), shm_s, st, A, n, which, ev, vec, g_svd_timing);
+    if (n >= g_syev_small_wide) {
+      allow_big_lds(syev_small_kernel<1024>, shm_s);
+      hipLaunchKernelGGL(syev_small_kernel<1024>, dim3(1), dim3(1024), shm_s, st, A, n, which, ev, vec, g_svd_timing);
+    } else {
+      allow_big_lds(syev_small_kernel<256>, shm_s);
+      hipLaunchKernelGGL(syev_small_kernel<256>, dim3(1), dim3(256), shm_s, st, A, n, which, ev, vec, g_svd_timing);
+    }
     TTK_LAUNCH_CHECK();
     return TTK_OK;
   }

@@ -79,7 +79,12 @@ def zeros(*shape):
 
 
 def from_numpy(a):
-    return torch.from_numpy(np.array(a, dtype=np.float64, order="C", copy=True)).to(DEV)
+    """Host array -> new device tensor.  Staged through torch's caching pinned-host allocator and
+    copied asynchronously on the launch stream (a pageable copy would drain the stream)."""
+    h = torch.from_numpy(np.array(a, dtype=np.float64, order="C", copy=True))
+    if DEV.type != "cuda":
+        return h.to(DEV)
+    return h.pin_memory().to(DEV, non_blocking=True)
 
 
 def contig(t):
@@ -160,6 +165,16 @@ def mul_(dst, a, b, alpha=1.0, beta=0.0):
     check(lib.ttk_mul_nd(_stream(), _p(a), _p(b), _p(dst), nd, _arr(dst.shape), _arr(a.stride()),
                          _arr(b.stride()), _arr(dst.stride()), float(alpha), float(beta)), "mul_nd")
     return dst
+
+
+def scale_axis(src, axis, scales, out=None):
+    """out = src * scales[i] along `axis` (host scales, <= 16; no H2D copy)."""
+    out = empty(*src.shape) if out is None else out
+    nd = src.dim()
+    sc = (ctypes.c_double * 16)(*[float(v) for v in scales])
+    check(lib.ttk_scale_axis(_stream(), _p(src), _p(out), nd, _arr(src.shape), _arr(src.stride()), _arr(out.stride()),
+                             int(axis), sc), "scale_axis")
+    return out
 
 
 def recip(src):
@@ -463,6 +478,6 @@ def syev_extreme(A, largest=False):
     return lam, buf[1:]
 
 
-__all__ = ["syev_extreme", "einsum", "tensordot", "matmul", "copy_", "scaled", "clone", "mul_", "recip", "fill_", "add_diag_",
+__all__ = ["scale_axis", "syev_extreme", "einsum", "tensordot", "matmul", "copy_", "scaled", "clone", "mul_", "recip", "fill_", "add_diag_",
            "dot", "norm", "read", "svd", "qr", "rq", "cholesky_", "trsm_", "lu_", "lu_solve_", "syev", "empty",
            "zeros", "from_numpy", "to_numpy", "LinAlgError", "LinAlgWarning"]

@@ -222,26 +222,19 @@ def _block_norms(sol):
 
 
 def _scales(sol):
-    """`np.maximum([||sol[:, b]||], 1e-10)` as host array + device (1,B,1,1) tensors sc, 1/sc."""
+    """`np.maximum([||sol[:, b]||], 1e-10)` and its reciprocal, as host arrays (`src/tt_als.py:321-322`)."""
     sc = np.maximum(_block_norms(sol), 1e-10)
-    scd = D.from_numpy(sc.reshape(1, -1, 1, 1))
-    inv = D.from_numpy((1.0 / sc).reshape(1, -1, 1, 1))
-    return sc, scd, inv
+    return sc, sc, 1.0 / sc
 
 
-def _scale_blocks(t, s_dev):
-    """t * s (s broadcast over the block axis 1 of a (r, B, n, R) tensor) -> new tensor."""
-    out = D.empty(*t.shape)
-    return D.mul_(out, t, s_dev.expand(t.shape))
+def _scale_blocks(t, sc):
+    """t * sc[b] along the block axis 1 of a (r, B, n, R) tensor -> new tensor."""
+    return D.scale_axis(t, 1, sc)
 
 
-def _div_blocks_bdim(t, inv_dev, axis):
-    """t / scales where the block axis of t is `axis` (4-D)."""
-    shp = [1, 1, 1, 1]
-    shp[axis] = inv_dev.numel()
-    s = inv_dev.view(*shp).expand(t.shape)
-    out = D.empty(*t.shape)
-    return D.mul_(out, t, s)
+def _div_blocks_bdim(t, inv, axis):
+    """t * inv[b] along the block axis `axis` (inv = 1 / scales, host)."""
+    return D.scale_axis(t, axis, inv)
 
 
 class _Ctx:
@@ -302,15 +295,15 @@ def _sweep(c, backward, swp, last, dsf):
         interior = (k > 0) if backward else (k < d - 1)
         if not interior:
             if backward:
-                x[k] = _div_blocks_bdim(scaled, inv.view(-1), 1)
+                x[k] = _div_blocks_bdim(scaled, inv, 1)
                 if amen and not last:
                     zz = D.contig(resz.t()).view(rz[k], B, N[k], rz[k + 1])
-                    z[k] = _div_blocks_bdim(zz, inv.view(-1), 1)
+                    z[k] = _div_blocks_bdim(zz, inv, 1)
             else:
-                x[k] = _div_blocks_bdim(scaled, inv.view(-1), 1)
+                x[k] = _div_blocks_bdim(scaled, inv, 1)
                 if amen and not last:
                     zz = resz.view(rz[k], N[k], B, rz[k + 1]).permute(0, 2, 1, 3)
-                    z[k] = _div_blocks_bdim(zz, inv.view(-1), 1)
+                    z[k] = _div_blocks_bdim(zz, inv, 1)
             continue
 
         U, S, Vt, s = D.svd(D.contig(mat))
@@ -393,14 +386,14 @@ def _sweep(c, backward, swp, last, dsf):
 
         if backward:
             x[k] = D.contig(u)
-            x[k - 1] = _div_blocks_bdim(einsum("rdc,cbR->rbdR", x[k - 1], vv), inv.view(-1), 1)
+            x[k - 1] = _div_blocks_bdim(einsum("rdc,cbR->rbdR", x[k - 1], vv), inv, 1)
             rx[k] = r
             c.XAX[k] = {key: compute_phi_bck_A(c.XAX[k + 1][key], x[k], Ak[key], x[k]) for key in Ak.keys()}
             c.Xb[k] = {i: compute_phi_bck_rhs(c.Xb[k + 1][i], bk[i], x[k]) for i in bk}
         else:
             nv = einsum("rbR,Rdk->rbdk", vv, x[k + 1])
             x[k] = D.contig(u)
-            x[k + 1] = _div_blocks_bdim(nv.view(r, B, N[k + 1], rx[k + 2]), inv.view(-1), 1)
+            x[k + 1] = _div_blocks_bdim(nv.view(r, B, N[k + 1], rx[k + 2]), inv, 1)
             rx[k + 1] = r
             c.XAX[k + 1] = {key: compute_phi_fwd_A(c.XAX[k][key], x[k], Ak[key], x[k]) for key in Ak.keys()}
             c.Xb[k + 1] = {i: compute_phi_fwd_rhs(c.Xb[k][i], bk[i], x[k]) for i in bk}
@@ -412,7 +405,7 @@ def _sweep(c, backward, swp, last, dsf):
                 uzc = D.clone(uz.t()).view(kr, N[k], rz[k + 1])
                 vzc = D.clone(vz.t()).view(rz[k], B, kr)
                 z[k] = uzc
-                z[k - 1] = _div_blocks_bdim(einsum("rdc,cbR->rbdR", z[k - 1], vzc), inv.view(-1), 1)
+                z[k - 1] = _div_blocks_bdim(einsum("rdc,cbR->rbdR", z[k - 1], vzc), inv, 1)
                 rz[k] = kr
                 zz = {key: compute_phi_bck_A(c.ZAX[k + 1][key], z[k], Ak[key], x[k]) for key in Ak.keys()}
                 zz.update({lt: compute_phi_bck_A(c.ZAX[k + 1][lt], z[k], Ak[ij].transpose(1, 2), x[k])
@@ -423,7 +416,7 @@ def _sweep(c, backward, swp, last, dsf):
                 uzc = D.contig(uz).view(rz[k], N[k], kr)
                 vzc = D.contig(vz).view(kr, B, rz[k + 1])
                 z[k] = uzc
-                z[k + 1] = _div_blocks_bdim(einsum("rbR,Rdk->rbdk", vzc, z[k + 1]), inv.view(-1), 1)
+                z[k + 1] = _div_blocks_bdim(einsum("rbR,Rdk->rbdk", vzc, z[k + 1]), inv, 1)
                 rz[k + 1] = kr
                 zz = {key: compute_phi_fwd_A(c.ZAX[k][key], z[k], Ak[key], x[k]) for key in Ak.keys()}
                 zz.update({lt: compute_phi_fwd_A(c.ZAX[k][lt], z[k], Ak[ij].transpose(1, 2), x[k])

@@ -142,6 +142,18 @@ class EmuLib:
         Dm[idd] = v
         return 0
 
+    def ttk_scale_axis(self, s, src, dst, nd, shape, ss, ds, axis, scales):
+        self.launches += 1
+        i_s, i_d = _nd_index(nd, shape, ss), _nd_index(nd, shape, ds)
+        if i_s.size == 0:
+            return 0
+        shp = [int(shape[i]) for i in range(nd)]
+        coord = np.indices(shp)[axis].reshape(-1)
+        sc = np.array([scales[i] for i in range(shp[axis])])
+        v = _dv(src, i_s.max() + 1)[i_s] * sc[coord]
+        _dv(dst, i_d.max() + 1)[i_d] = v
+        return 0
+
     def ttk_recip(self, s, src, dst, n):
         _dv(dst, n)[:] = 1.0 / _dv(src, n)
         return 0

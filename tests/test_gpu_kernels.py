@@ -336,7 +336,7 @@ def _sym_cases(n, rng):
     yield "scaled", 1e-6 * (M + M.T) + np.diag(np.arange(n, dtype=float))
 
 
-@pytest.mark.parametrize("n", [1, 2, 3, 4, 10, 64, 100, 127, 128, 129, 139, 140, 288])
+@pytest.mark.parametrize("n", [1, 2, 3, 4, 10, 64, 100, 127, 128, 129, 139, 140, 288, 600, 800])
 @pytest.mark.parametrize("largest", [False, True])
 def test_syev_extreme(dev, n, largest):
     rng = _rng(7 * n + largest)
@@ -368,6 +368,29 @@ def test_syev_small_matches_general_kernel(dev, n):
                 l2, v2 = dev.syev_extreme(dev.from_numpy(A), largest=largest)
             finally:
                 lib.ttk_syev_set_small(old)
+            v1, v2 = dev.read(v1), dev.read(v2)
+            scale = max(1.0, np.abs(A).max())
+            assert abs(l1 - l2) <= 1e-13 * scale * n, (name, l1, l2)
+            assert min(np.abs(v1 - v2).max(), np.abs(v1 + v2).max()) <= 1e-8, name
+
+
+@pytest.mark.parametrize("n", [150, 301])
+def test_syev_fused_matches_two_launch(dev, n):
+    """the one-launch-per-step and the two-launch multi-workgroup tridiagonalisations agree"""
+    from ttipm_amd._lib import lib
+    rng = _rng(13 * n)
+    for name, A in _sym_cases(n, rng):
+        w = np.linalg.eigvalsh(A)
+        for largest in (False, True):
+            gap = (w[-1] - w[-2]) if largest else (w[1] - w[0])
+            if gap <= 1e-8 * max(1.0, np.abs(w).max()):
+                continue
+            l1, v1 = dev.syev_extreme(dev.from_numpy(A), largest=largest)
+            old = lib.ttk_syev_set_fused_max(0)
+            try:
+                l2, v2 = dev.syev_extreme(dev.from_numpy(A), largest=largest)
+            finally:
+                lib.ttk_syev_set_fused_max(old)
             v1, v2 = dev.read(v1), dev.read(v2)
             scale = max(1.0, np.abs(A).max())
             assert abs(l1 - l2) <= 1e-13 * scale * n, (name, l1, l2)

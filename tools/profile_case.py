@@ -40,6 +40,7 @@ s = io.StringIO()
 ps = pstats.Stats(pr, stream=s).sort_stats("tottime")
 ps.print_stats(45)
 ps.sort_stats("cumulative").print_stats(60)
+ps.print_callers(r"\(read\)|\(dot\)|\(norm\)")
 from ttipm_amd import dev as _D  # noqa: E402
 ops = ""
 if _D.OPSTATS is not None:
