@@ -208,9 +208,493 @@ __global__ __launch_bounds__(256) void trsm_diag_kernel(const double *__restrict
     if (j < kb) B[(int64_t)(r0 + j) * ldb + c] = x[j];
 }
 
+
+// ---------------------------------------------------------------- blocked LU (dgetrf) + gecon
+// Per NB-column panel: (1) dgetf2 of the panel over rows [k0, n) in one workgroup (idamax pivot:
+// first index of the largest |a|; rows swapped inside the panel only), (2) the panel's row swaps
+// on every other column (dlaswp, one thread per column), (3) U12 = L11^-1 A12 (one thread per
+// column, L11 in LDS), (4) A22 -= L21 U12 on fp64 MFMA.  LAPACK's right-looking dgetrf order.
+// The 1-norm condition estimate (dgecon with dlacn2's Hager/Higham iteration) then runs in one
+// workgroup on 32-row blocks: wave 0 solves the diagonal block with lane shuffles, all waves
+// apply the block to the remaining rows, so a triangular solve costs n/16 barriers, not 2n.
+
+__global__ __launch_bounds__(256) void colsum_kernel(const double *__restrict__ A, int n, double *__restrict__ out) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= n) return;
+  double s = 0.0;
+  for (int r = 0; r < n; ++r) s += fabs(A[(int64_t)r * n + c]);
+  out[c] = s;
+}
+
+__global__ __launch_bounds__(1024) void getf2_panel_kernel(double *A, int n, int k0, int kb, int *piv, int *status) {
+  __shared__ double wv[16];
+  __shared__ int wi[16];
+  __shared__ int s_p;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  for (int c = 0; c < kb; ++c) {
+    const int j = k0 + c;
+    double best = -1.0;
+    int bi = j;
+    for (int i = j + tid; i < n; i += 1024) {
+      const double v = fabs(A[(int64_t)i * n + j]);
+      if (v > best) {
+        best = v;
+        bi = i;
+      }
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      const double ov = __shfl_xor(best, o, 64);
+      const int oi = __shfl_xor(bi, o, 64);
+      if (ov > best || (ov == best && oi < bi)) {
+        best = ov;
+        bi = oi;
+      }
+    }
+    if (lane == 0) {
+      wv[wid] = best;
+      wi[wid] = bi;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      double b = wv[0];
+      int p = wi[0];
+      for (int w = 1; w < 16; ++w)
+        if (wv[w] > b || (wv[w] == b && wi[w] < p)) {
+          b = wv[w];
+          p = wi[w];
+        }
+      s_p = p;
+      piv[j] = p;
+    }
+    __syncthreads();
+    const int p = s_p;
+    if (p != j && tid < kb) {
+      double *a = A + (int64_t)j * n + k0 + tid, *b = A + (int64_t)p * n + k0 + tid;
+      const double t = *a;
+      *a = *b;
+      *b = t;
+    }
+    __syncthreads();
+    const double d = A[(int64_t)j * n + j];
+    if (d == 0.0) {  // LAPACK: info = first zero pivot, no scaling, factorisation continues
+      if (tid == 0 && *status == 0) *status = j + 1;
+      continue;
+    }
+    const double inv = 1.0 / d;
+    const double *prow = A + (int64_t)j * n + k0;
+    for (int i = j + 1 + tid; i < n; i += 1024) {
+      double *ai = A + (int64_t)i * n + k0;
+      const double l = ai[c] * inv;
+      ai[c] = l;
+      for (int cc = c + 1; cc < kb; ++cc) ai[cc] -= l * prow[cc];
+    }
+    __syncthreads();
+  }
+}
+
+// the same panel factorisation with the (n-k0) x kb panel staged in LDS (row stride kb+1)
+__global__ __launch_bounds__(1024) void getf2_panel_lds_kernel(double *A, int n, int k0, int kb, int *piv,
+                                                               int *status) {
+  extern __shared__ double P[];
+  __shared__ double wv[16];
+  __shared__ int wi[16];
+  __shared__ int s_p;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int rows = n - k0, ld = kb + 1;
+  for (int e = tid; e < rows * kb; e += 1024) {
+    const int i = e / kb, c = e - i * kb;
+    P[i * ld + c] = A[(int64_t)(k0 + i) * n + k0 + c];
+  }
+  __syncthreads();
+  for (int c = 0; c < kb; ++c) {
+    double best = -1.0;
+    int bi = c;
+    for (int i = c + tid; i < rows; i += 1024) {
+      const double v = fabs(P[i * ld + c]);
+      if (v > best) {
+        best = v;
+        bi = i;
+      }
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      const double ov = __shfl_xor(best, o, 64);
+      const int oi = __shfl_xor(bi, o, 64);
+      if (ov > best || (ov == best && oi < bi)) {
+        best = ov;
+        bi = oi;
+      }
+    }
+    if (lane == 0) {
+      wv[wid] = best;
+      wi[wid] = bi;
+    }
+    __syncthreads();
+    if (tid < 64) {  // wave 0: reduce the 16 wave winners, swap the two panel rows
+      double b = tid < 16 ? wv[tid] : -2.0;
+      int p = tid < 16 ? wi[tid] : 0x7fffffff;
+#pragma unroll
+      for (int o = 8; o >= 1; o >>= 1) {
+        const double ob = __shfl_xor(b, o, 64);
+        const int op = __shfl_xor(p, o, 64);
+        if (ob > b || (ob == b && op < p)) {
+          b = ob;
+          p = op;
+        }
+      }
+      p = __shfl(p, 0, 64);
+      if (p != c && tid < kb) {
+        const double t = P[c * ld + tid];
+        P[c * ld + tid] = P[p * ld + tid];
+        P[p * ld + tid] = t;
+      }
+      if (tid == 0) {
+        s_p = p;
+        piv[k0 + c] = k0 + p;
+      }
+    }
+    __syncthreads();
+    const double d = P[c * ld + c];
+    if (d == 0.0) {
+      if (tid == 0 && *status == 0) *status = k0 + c + 1;
+      continue;
+    }
+    const double inv = 1.0 / d;
+    const double *prow = P + c * ld;
+    for (int i = c + 1 + tid; i < rows; i += 1024) {
+      double *pi = P + i * ld;
+      const double l = pi[c] * inv;
+      pi[c] = l;
+      for (int cc = c + 1; cc < kb; ++cc) pi[cc] -= l * prow[cc];
+    }
+    __syncthreads();
+  }
+  for (int e = tid; e < rows * kb; e += 1024) {
+    const int i = e / kb, c = e - i * kb;
+    A[(int64_t)(k0 + i) * n + k0 + c] = P[i * ld + c];
+  }
+}
+
+// row swaps of panel [k0, k0+kb) on the columns outside it
+__global__ __launch_bounds__(256) void laswp_kernel(double *A, int n, int k0, int kb, const int *piv) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= n || (c >= k0 && c < k0 + kb)) return;
+  for (int jj = k0; jj < k0 + kb; ++jj) {
+    const int p = piv[jj];
+    if (p != jj) {
+      const double t = A[(int64_t)jj * n + c];
+      A[(int64_t)jj * n + c] = A[(int64_t)p * n + c];
+      A[(int64_t)p * n + c] = t;
+    }
+  }
+}
+
+// U12 = L11^-1 A12 (L11 unit lower kb x kb), one thread per column c >= k0+kb
+__global__ __launch_bounds__(256) void lu_u12_kernel(double *A, int n, int k0, int kb) {
+  __shared__ double Ls[NB][NB + 1];
+  const int tid = threadIdx.x;
+  for (int e = tid; e < kb * kb; e += 256) {
+    const int i = e / kb, j = e - i * kb;
+    Ls[i][j] = A[(int64_t)(k0 + i) * n + k0 + j];
+  }
+  __syncthreads();
+  const int c = k0 + kb + blockIdx.x * 256 + tid;
+  if (c >= n) return;
+  double x[NB];
+#pragma unroll
+  for (int q = 0; q < NB; ++q) x[q] = q < kb ? A[(int64_t)(k0 + q) * n + c] : 0.0;
+#pragma unroll
+  for (int q = 1; q < NB; ++q) {
+    if (q < kb) {
+      double v = x[q];
+#pragma unroll
+      for (int p = 0; p < NB; ++p)
+        if (p < q) v -= Ls[q][p] * x[p];
+      x[q] = v;
+    }
+  }
+#pragma unroll
+  for (int q = 1; q < NB; ++q)
+    if (q < kb) A[(int64_t)(k0 + q) * n + c] = x[q];
+}
+
+constexpr int TB = 32;  // diagonal block of the one-workgroup triangular solves
+
+// one workgroup (1024 threads): x (in LDS) <- A^-1 x (trans = 0) or A^-T x (trans = 1), with the
+// dgetrf factors LU (row-major n x n) and pivots
+__device__ void lu_solve_blk(const double *__restrict__ LU, int n, const int *__restrict__ piv, double *x,
+                             int trans) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int half = lane >> 5, hl = lane & 31;
+  if (!trans) {
+    if (tid == 0)
+      for (int i = 0; i < n; ++i) {
+        const int p = piv[i];
+        if (p != i) {
+          const double t = x[i];
+          x[i] = x[p];
+          x[p] = t;
+        }
+      }
+    __syncthreads();
+    for (int b0 = 0; b0 < n; b0 += TB) {  // L y = P x, L unit lower
+      const int bs = n - b0 < TB ? n - b0 : TB;
+      if (wid == 0) {
+        double lr[TB];
+        const double *row = LU + (int64_t)(b0 + hl) * n + b0;
+#pragma unroll
+        for (int p = 0; p < TB; ++p) lr[p] = (p < hl && hl < bs) ? row[p] : 0.0;
+        double xq = hl < bs ? x[b0 + hl] : 0.0;
+#pragma unroll
+        for (int p = 0; p < TB - 1; ++p) {
+          const double xp = __shfl(xq, p, 64);
+          xq -= lr[p] * xp;
+        }
+        if (half == 0 && hl < bs) x[b0 + hl] = xq;
+      }
+      __syncthreads();
+      for (int r = b0 + bs + 2 * wid + half; r < n; r += 32) {  // two rows per wave, 32 lanes each
+        double v = hl < bs ? LU[(int64_t)r * n + b0 + hl] * x[b0 + hl] : 0.0;
+#pragma unroll
+        for (int o = 16; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+        if (hl == 0) x[r] -= v;
+      }
+      __syncthreads();
+    }
+    for (int bend = n; bend > 0; bend -= TB) {  // U z = y
+      const int b0 = bend - TB > 0 ? bend - TB : 0, bs = bend - b0;
+      if (wid == 0) {
+        double ur[TB];
+        const double *row = LU + (int64_t)(b0 + hl) * n + b0;
+#pragma unroll
+        for (int p = 0; p < TB; ++p) ur[p] = (p > hl && p < bs && hl < bs) ? row[p] : 0.0;
+        const double d = hl < bs ? row[hl] : 1.0;
+        double xq = hl < bs ? x[b0 + hl] : 0.0;
+#pragma unroll
+        for (int p = TB - 1; p >= 0; --p) {
+          if (p < bs) {
+            if (hl == p) xq = xq / d;
+            const double xp = __shfl(xq, p, 64);
+            xq -= ur[p] * xp;
+          }
+        }
+        if (half == 0 && hl < bs) x[b0 + hl] = xq;
+      }
+      __syncthreads();
+      for (int r = 2 * wid + half; r < b0; r += 32) {
+        double v = hl < bs ? LU[(int64_t)r * n + b0 + hl] * x[b0 + hl] : 0.0;
+#pragma unroll
+        for (int o = 16; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+        if (hl == 0) x[r] -= v;
+      }
+      __syncthreads();
+    }
+  } else {
+    for (int b0 = 0; b0 < n; b0 += TB) {  // U^T y = b (lower, non-unit)
+      const int bs = n - b0 < TB ? n - b0 : TB;
+      if (wid == 0) {
+        double uc[TB];
+#pragma unroll
+        for (int p = 0; p < TB; ++p) uc[p] = (p < hl && hl < bs) ? LU[(int64_t)(b0 + p) * n + b0 + hl] : 0.0;
+        const double d = hl < bs ? LU[(int64_t)(b0 + hl) * n + b0 + hl] : 1.0;
+        double xq = hl < bs ? x[b0 + hl] : 0.0;
+#pragma unroll
+        for (int p = 0; p < TB; ++p) {
+          if (p < bs) {
+            if (hl == p) xq = xq / d;
+            const double xp = __shfl(xq, p, 64);
+            xq -= uc[p] * xp;
+          }
+        }
+        if (half == 0 && hl < bs) x[b0 + hl] = xq;
+      }
+      __syncthreads();
+      for (int r = b0 + bs + tid; r < n; r += 1024) {  // one thread per row, coalesced over r
+        double v = 0.0;
+        for (int p = 0; p < bs; ++p) v += LU[(int64_t)(b0 + p) * n + r] * x[b0 + p];
+        x[r] -= v;
+      }
+      __syncthreads();
+    }
+    for (int bend = n; bend > 0; bend -= TB) {  // L^T z = y (upper, unit)
+      const int b0 = bend - TB > 0 ? bend - TB : 0, bs = bend - b0;
+      if (wid == 0) {
+        double lc[TB];
+#pragma unroll
+        for (int p = 0; p < TB; ++p) lc[p] = (p > hl && p < bs && hl < bs) ? LU[(int64_t)(b0 + p) * n + b0 + hl] : 0.0;
+        double xq = hl < bs ? x[b0 + hl] : 0.0;
+#pragma unroll
+        for (int p = TB - 1; p >= 0; --p) {
+          const double xp = __shfl(xq, p, 64);
+          xq -= lc[p] * xp;
+        }
+        if (half == 0 && hl < bs) x[b0 + hl] = xq;
+      }
+      __syncthreads();
+      for (int r = tid; r < b0; r += 1024) {
+        double v = 0.0;
+        for (int p = 0; p < bs; ++p) v += LU[(int64_t)(b0 + p) * n + r] * x[b0 + p];
+        x[r] -= v;
+      }
+      __syncthreads();
+    }
+    if (tid == 0)
+      for (int i = n - 1; i >= 0; --i) {
+        const int p = piv[i];
+        if (p != i) {
+          const double t = x[i];
+          x[i] = x[p];
+          x[p] = t;
+        }
+      }
+    __syncthreads();
+  }
+}
+
+// dgecon (1-norm) from the factors: colsum = column sums of |A| before factorisation
+__global__ __launch_bounds__(1024) void lu_rcond_kernel(const double *__restrict__ LU, int n, const int *piv,
+                                                        const double *__restrict__ colsum, const int *status,
+                                                        double *rcond_out) {
+  extern __shared__ double xl[];
+  double *x = xl, *xs = xl + n;
+  __shared__ double red[16];
+  __shared__ double rv[1024];
+  __shared__ int ri[1024];
+  __shared__ double s_est, s_anorm;
+  const int tid = threadIdx.x, nt = blockDim.x;
+  if (*status) {
+    if (tid == 0) *rcond_out = 0.0;
+    return;
+  }
+  double cm = 0.0;
+  for (int c = tid; c < n; c += nt) cm = fmax(cm, colsum[c]);
+  rv[tid] = cm;
+  __syncthreads();
+  if (tid == 0) {
+    double mx = 0.0;
+    for (int i = 0; i < nt; ++i) mx = fmax(mx, rv[i]);
+    s_anorm = mx;
+    s_est = 0.0;
+  }
+  for (int i = tid; i < n; i += nt) x[i] = 1.0 / n;
+  __syncthreads();
+  int jlast = -1;
+  for (int iter = 0; iter < 5; ++iter) {
+    lu_solve_blk(LU, n, piv, x, 0);
+    double s1 = 0.0;
+    for (int i = tid; i < n; i += nt) s1 += fabs(x[i]);
+    s1 = ttk::block_sum(s1, red);
+    if (iter > 0 && s1 <= s_est) {
+      __syncthreads();
+      break;
+    }
+    __syncthreads();
+    if (tid == 0) s_est = s1;
+    for (int i = tid; i < n; i += nt) xs[i] = (x[i] >= 0.0) ? 1.0 : -1.0;
+    __syncthreads();
+    lu_solve_blk(LU, n, piv, xs, 1);
+    double best = -1.0;
+    int bi = 0;
+    for (int i = tid; i < n; i += nt)
+      if (fabs(xs[i]) > best) {
+        best = fabs(xs[i]);
+        bi = i;
+      }
+    rv[tid] = best;
+    ri[tid] = bi;
+    __syncthreads();
+    for (int s = nt / 2; s > 0; s >>= 1) {
+      if (tid < s) {
+        if (rv[tid + s] > rv[tid] || (rv[tid + s] == rv[tid] && ri[tid + s] < ri[tid])) {
+          rv[tid] = rv[tid + s];
+          ri[tid] = ri[tid + s];
+        }
+      }
+      __syncthreads();
+    }
+    const int jn = ri[0];
+    __syncthreads();
+    if (jn == jlast) break;
+    jlast = jn;
+    for (int i = tid; i < n; i += nt) x[i] = (i == jn) ? 1.0 : 0.0;
+    __syncthreads();
+  }
+  for (int i = tid; i < n; i += nt) x[i] = ((i & 1) ? -1.0 : 1.0) * (1.0 + (n > 1 ? (double)i / (n - 1) : 0.0));
+  __syncthreads();
+  lu_solve_blk(LU, n, piv, x, 0);
+  double s1 = 0.0;
+  for (int i = tid; i < n; i += nt) s1 += fabs(x[i]);
+  s1 = ttk::block_sum(s1, red);
+  if (tid == 0) {
+    const double temp = 2.0 * s1 / (3.0 * n);
+    const double est = fmax(s_est, temp);
+    *rcond_out = (s_anorm == 0.0 || est == 0.0) ? 0.0 : (1.0 / s_anorm) / est;
+  }
+}
+
+// getrs for a few right-hand sides: one workgroup per column, x in LDS
+__global__ __launch_bounds__(1024) void lu_solve_cols_kernel(const double *__restrict__ LU, int n, const int *piv,
+                                                             double *B, int ldb) {
+  extern __shared__ double xl[];
+  const int c = blockIdx.x, tid = threadIdx.x;
+  for (int i = tid; i < n; i += 1024) xl[i] = B[(int64_t)i * ldb + c];
+  __syncthreads();
+  lu_solve_blk(LU, n, piv, xl, 0);
+  for (int i = tid; i < n; i += 1024) B[(int64_t)i * ldb + c] = xl[i];
+}
+
 }  // namespace
 
 namespace ttk {
+
+int lu_blocked(hipStream_t st, double *A, int n, int *piv, double *work, int *status, double *rcond, int want_rcond) {
+  TTK_HIP(hipMemsetAsync(status, 0, sizeof(int), st));
+  double *colsum = work;  // n doubles
+  if (want_rcond) hipLaunchKernelGGL(colsum_kernel, dim3((n + 255) / 256), dim3(256), 0, st, A, n, colsum);
+  for (int k0 = 0; k0 < n; k0 += NB) {
+    const int kb = n - k0 < NB ? n - k0 : NB;
+    const size_t pshm = (size_t)(n - k0) * (kb + 1) * sizeof(double);
+    if (pshm <= 150000) {
+      if (pshm > 65536)
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(getf2_panel_lds_kernel),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)pshm);
+      hipLaunchKernelGGL(getf2_panel_lds_kernel, dim3(1), dim3(1024), pshm, st, A, n, k0, kb, piv, status);
+    } else {
+      hipLaunchKernelGGL(getf2_panel_kernel, dim3(1), dim3(1024), 0, st, A, n, k0, kb, piv, status);
+    }
+    hipLaunchKernelGGL(laswp_kernel, dim3((n + 255) / 256), dim3(256), 0, st, A, n, k0, kb, piv);
+    const int rest = n - k0 - kb;
+    if (rest > 0) {
+      hipLaunchKernelGGL(lu_u12_kernel, dim3((rest + 255) / 256), dim3(256), 0, st, A, n, k0, kb);
+      dim3 grid((rest + GT - 1) / GT, (rest + GT - 1) / GT);
+      hipLaunchKernelGGL((gemm_strided_kernel<false, false>), grid, dim3(256), 0, st,
+                         A + (int64_t)(k0 + kb) * n + k0, n, A + (int64_t)k0 * n + k0 + kb, n,
+                         A + (int64_t)(k0 + kb) * n + k0 + kb, n, rest, rest, kb, -1.0, 1.0, 0);
+    }
+    TTK_LAUNCH_CHECK();
+  }
+  if (want_rcond) {
+    const size_t shm = 2 * (size_t)n * sizeof(double);
+    if (shm > 65536)
+      (void)hipFuncSetAttribute(reinterpret_cast<const void *>(lu_rcond_kernel),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+    hipLaunchKernelGGL(lu_rcond_kernel, dim3(1), dim3(1024), shm, st, A, n, piv, colsum, status, rcond);
+    TTK_LAUNCH_CHECK();
+  }
+  return TTK_OK;
+}
+
+int lu_solve_cols(hipStream_t st, const double *LU, int n, const int *piv, double *B, int nrhs, int ldb) {
+  const size_t shm = (size_t)n * sizeof(double);
+  if (shm > 65536)
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(lu_solve_cols_kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+  hipLaunchKernelGGL(lu_solve_cols_kernel, dim3(nrhs), dim3(1024), shm, st, LU, n, piv, B, ldb);
+  TTK_LAUNCH_CHECK();
+  return TTK_OK;
+}
+
 
 int cholesky_blocked(hipStream_t st, double *A, int n, int *status) {
   TTK_HIP(hipMemsetAsync(status, 0, sizeof(int), st));

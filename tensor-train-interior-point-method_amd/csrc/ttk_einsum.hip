@@ -593,7 +593,11 @@ int fused_apply_try(void *stream, const char *eq, const int64_t *desc, double *o
                        ((double)g.ns * g.nj * g.nd * g.nb + (double)g.ni * g.nS * g.nd * g.ns * g.nj +
                         (double)g.ni * g.nc * g.nS * g.nd);
   static const double max_flops = getenv("TTK_FUSED_MAX_FLOPS") ? atof(getenv("TTK_FUSED_MAX_FLOPS")) : 4e6;
-  if (flops > max_flops) return 0;
+  // relabelled environment updates (desc flag 512) have few output rows, so each workgroup carries
+  // a larger share of the chain: fused only while small
+  static const double env_max_flops =
+      getenv("TTK_FUSED_ENV_MAX_FLOPS") ? atof(getenv("TTK_FUSED_ENV_MAX_FLOPS")) : 1e6;
+  if (flops > ((desc[0] & 512) ? env_max_flops : max_flops)) return 0;
   const size_t shm = need * sizeof(double);
   if (shm > 65536)
     (void)hipFuncSetAttribute(reinterpret_cast<const void *>(fused_apply_kernel),

@@ -2458,6 +2458,7 @@ int ttk_qr(void *stream, const double *A, int m, int n, double *Q, double *R, do
 }
 
 static int g_dense_block_min = 96;  // n at or above which Cholesky / TRSM take the blocked kernels
+static int g_lu_block_min = getenv("TTK_LU_BLOCK_MIN") ? atoi(getenv("TTK_LU_BLOCK_MIN")) : 96;  // LU / getrs
 
 int ttk_dense_set_block_min(int n) {
   const int old = g_dense_block_min;
@@ -2500,8 +2501,13 @@ int ttk_lu_sync(void *stream, double *A, int n, int *piv, double *work, double *
     ttk::set_error("ttk_lu_sync: status alloc failed");
     return TTK_ERR_HIP;
   }
-  hipLaunchKernelGGL(lu_kernel, dim3(1), dim3(1024), 0, TTK_STREAM(stream), A, n, piv, work, g_status, g_rcond);
-  TTK_LAUNCH_CHECK();
+  if (n >= g_lu_block_min && n <= 9000) {
+    const int rc = ttk::lu_blocked(TTK_STREAM(stream), A, n, piv, work, g_status, g_rcond, 1);
+    if (rc) return rc;
+  } else {
+    hipLaunchKernelGGL(lu_kernel, dim3(1), dim3(1024), 0, TTK_STREAM(stream), A, n, piv, work, g_status, g_rcond);
+    TTK_LAUNCH_CHECK();
+  }
   int st = 0;
   TTK_HIP(hipMemcpyAsync(&st, g_status, sizeof(int), hipMemcpyDeviceToHost, TTK_STREAM(stream)));
   TTK_HIP(hipMemcpyAsync(rcond_out, g_rcond, sizeof(double), hipMemcpyDeviceToHost, TTK_STREAM(stream)));
@@ -2514,6 +2520,7 @@ int ttk_lu_sync(void *stream, double *A, int n, int *piv, double *work, double *
 }
 
 int ttk_lu_solve(void *stream, const double *LU, int n, const int *piv, double *B, int nrhs, int ldb) {
+  if (n >= g_lu_block_min && n <= 18000 && nrhs <= 8 && nrhs > 0) return ttk::lu_solve_cols(TTK_STREAM(stream), LU, n, piv, B, nrhs, ldb);
   if (n <= 0 || nrhs <= 0) return TTK_OK;
   hipLaunchKernelGGL(lu_solve_kernel, dim3((nrhs + 63) / 64), dim3(256), 0, TTK_STREAM(stream), LU, n, piv, B, nrhs, ldb);
   TTK_LAUNCH_CHECK();

@@ -294,7 +294,8 @@ _FUSED_ALL = os.environ.get("TTIPM_FUSED_ALL") == "1"  # experiment switch: ever
 
 def einsum(eq, *ops, out=None, alpha=1.0, beta=0.0, fused=False):
     """`fused=True` lets the local-operator equations run as one fused launch (see ttk_einsum);
-    call sites whose results feed noise-level decisions keep the pairwise plan."""
+    call sites whose results feed noise-level decisions keep the pairwise plan.  `fused="env"`:
+    a relabelled environment update (fused under a smaller FLOP limit)."""
     fused = fused or _FUSED_ALL
     if _CHECK_FUSED and fused and eq in _FUSED_EQS:
         return _einsum_checked(eq, ops, out, alpha, beta)
@@ -311,8 +312,8 @@ def _einsum_native(eq, *ops, out=None, alpha=1.0, beta=0.0, fused=False):
         e[0] += 1
     f = _FAST or _fast()
     if f is not None:
-        return f.einsum(eq, ops, out, float(alpha), float(beta), 256 if fused else 0)
-    desc = [len(ops) | (256 if fused else 0)]
+        return f.einsum(eq, ops, out, float(alpha), float(beta), (256 | 512) if fused == "env" else (256 if fused else 0))
+    desc = [len(ops) | ((256 | 512) if fused == "env" else (256 if fused else 0))]
     for o in ops:
         desc.append(o.data_ptr())
         desc.append(o.dim())

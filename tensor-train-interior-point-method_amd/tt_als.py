@@ -7,6 +7,8 @@ its compressed variants) are the core-contraction kernels of the path: each is a
 whose pairwise steps run on the fp64-MFMA offset-table GEMM."""
 import time
 
+import os
+
 import numpy as np
 
 from . import dev as D
@@ -185,13 +187,25 @@ def rhs_local_product(bcore, L, R, out, alpha=1.0):
     return out
 
 
+# Environment updates as the one-launch fused local-apply kernel: relabelled, the 4-operand chain
+# 'LSR,lML,sMNS,rNR->lsr' is the apply 'lsr,smnS,LSR,rnR->lmL' on strided views (no copies), so one
+# launch replaces the three pairwise GEMM steps (same contraction, association as the greedy plan
+# of the apply; operands beyond the fused kernel's LDS/FLOP limits fall back to the pairwise plan).
+FUSED_ENV = os.environ.get("TTIPM_FUSED_ENV", "1") == "1"
+_APPLY = "lsr,smnS,LSR,rnR->lmL"
+
+
 def compute_phi_bck_A(P, xl, A, xr):
     """`src/tt_als.py:252-253`"""
+    if FUSED_ENV:
+        return einsum(_APPLY, xl, A.permute(1, 0, 3, 2), xr, P, fused="env")
     return einsum("LSR,lML,sMNS,rNR->lsr", P, xl, A, xr)
 
 
 def compute_phi_fwd_A(P, xl, A, xr):
     """`src/tt_als.py:256-257`"""
+    if FUSED_ENV:
+        return einsum(_APPLY, xl.permute(2, 1, 0), A.permute(1, 3, 0, 2), xr.permute(2, 1, 0), P, fused="env")
     return einsum("lsr,lML,sMNS,rNR->LSR", P, xl, A, xr)
 
 

@@ -292,7 +292,7 @@ def test_cholesky_not_pd_raises(dev, n, bad):
         dev.cholesky_(L)
 
 
-@pytest.mark.parametrize("n", [1, 6, 50, 200])
+@pytest.mark.parametrize("n", [1, 6, 50, 95, 96, 200, 700, 1500])
 def test_lu_solve_rcond(dev, n):
     rng = _rng(3 * n)
     A = rng.standard_normal((n, n)) + 0.1 * np.eye(n)
@@ -302,6 +302,31 @@ def test_lu_solve_rcond(dev, n):
     X = dev.from_numpy(b)
     dev.lu_solve_(LU, piv, X)
     assert np.allclose(A @ dev.read(X), b, atol=1e-8 * np.linalg.cond(A))
+
+
+@pytest.mark.parametrize("n", [50, 96, 333, 1200])
+def test_lu_matches_lapack(dev, n):
+    """pivots, factors and the rcond estimate against LAPACK dgetrf / dgecon (blocked path from n=96)"""
+    import ctypes
+    import scipy.linalg as sla
+    from ttipm_amd._lib import lib
+    rng = _rng(17 * n)
+    A = rng.standard_normal((n, n))
+    lu_ref, piv_ref = sla.lu_factor(A)
+    LU = dev.from_numpy(A)
+    piv = dev.torch.empty(n, dtype=dev.torch.int32, device=dev.DEV)
+    work = dev.empty(2 * n + 16)
+    rc = ctypes.c_double(0.0)
+    assert lib.ttk_lu_sync(dev._stream(), LU.data_ptr(), n, piv.data_ptr(), work.data_ptr(), ctypes.byref(rc)) == 0
+    assert np.array_equal(piv.cpu().numpy(), piv_ref)
+    assert np.abs(dev.read(LU) - lu_ref).max() <= 1e-10 * np.abs(lu_ref).max()
+    anorm = np.abs(A).sum(axis=0).max()
+    rcond_ref, info = sla.lapack.dgecon(lu_ref, anorm, norm="1")
+    assert 0.3 * rcond_ref <= rc.value <= 3.0 * rcond_ref, (rc.value, rcond_ref)
+    B = rng.standard_normal((n, 2))
+    X = dev.from_numpy(B)
+    dev.lu_solve_(LU, piv, X)
+    assert np.allclose(dev.read(X), sla.lu_solve((lu_ref, piv_ref), B), rtol=1e-8, atol=1e-10)
 
 
 def test_lu_ill_conditioned_raises_warning(dev):
