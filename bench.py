@@ -7,8 +7,10 @@
         --master-port P bench.py --gpus N --steps K --warmup W
 
 * A "step" is one full `tt_ipm` solve of one seed per GPU (the reference's unit of work,
-  `src/utils.py:245-321`).  Rank p solves seeds[i*N + p] at step i (weak scaling: per-GPU work is
-  fixed as N grows).  Problems are created on rank 0 and delivered by ONE RCCL broadcast before
+  `src/utils.py:245-321`).  Default `--schedule replica`: every rank solves the seed of step i of
+  the N=1 run, so per-GPU work is fixed as N grows (weak scaling).  `--schedule shard`: rank p
+  solves seeds[i*N + p] (distinct seeds; the makespan is the slowest seed's -- maxcut_10 seed 23
+  needs ~6x the work of seed 41).  Problems are created on rank 0 and delivered by ONE RCCL broadcast before
   the timed region (`shard.broadcast_problems`); there is no collective inside the IPM loop.
 * Timed region: barrier + device sync on both sides of the K steps, max over ranks.
   value = (max-over-ranks wall) / (IPM iterations of all ranks) -- whole-job s per IPM-iteration.
@@ -132,6 +134,9 @@ def main():
                     help="IPM iterations in the CPU-baseline sample (0 = the full solve of the step-0 seed)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--schedule", choices=("replica", "shard"), default="replica",
+                    help="replica: every rank solves the seed of the N=1 step (fixed per-GPU work: weak "
+                         "scaling); shard: ranks take distinct seeds of the config (makespan = slowest seed)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -153,8 +158,12 @@ def main():
 
     with open(args.config) as f:
         config = yaml.safe_load(f)
-    seeds = _seed_list(config, args.steps * world)
-    step_seeds = [seeds[(i * world + p) % len(seeds)] for i in range(args.steps) for p in range(world)]
+    if args.schedule == "shard":
+        seeds = _seed_list(config, args.steps * world)
+        step_seeds = [seeds[(i * world + p) % len(seeds)] for i in range(args.steps) for p in range(world)]
+    else:
+        seeds = _seed_list(config, args.steps)
+        step_seeds = [seeds[i % len(seeds)] for i in range(args.steps) for p in range(world)]
     sched = [step_seeds[i * world:(i + 1) * world] for i in range(args.steps)]
     with contextlib.redirect_stdout(sys.stderr):
         packed = shard.broadcast_problems(args.problem, config, step_seeds, args.rank)
@@ -217,7 +226,7 @@ def main():
                        "from rank 0",
                "config": {"workload": f"{args.problem} dim={config['dim']} rank={args.rank} "
                                       f"({os.path.basename(args.config)}), one tt_ipm solve per GPU per step",
-                          "seeds_per_step": sched, "parallelism": f"seed-sharded x{world}",
+                          "seeds_per_step": sched, "parallelism": f"seed-parallel x{world} ({args.schedule})",
                           "total_ipm_iters": iters},
                "roofline": roofline, "cpu_baseline": cpu,
                "mfma_util_pct": None if roofline is None else 100.0 * roofline["frac"],

@@ -421,8 +421,39 @@ __global__ __launch_bounds__(256) void lu_u12_kernel(double *A, int n, int k0, i
 
 constexpr int TB = 32;  // diagonal block of the one-workgroup triangular solves
 
+// x[r] -= sum_p LU[r][b0+p] x[b0+p] for r in [r0, r1): half-waves own rows (32 lanes over the
+// block's columns, coalesced); beyond 4096 rows one thread per row
+__device__ __forceinline__ double row_dot(const double *__restrict__ a, const double *x, int bs);
+__device__ void rows_update(const double *__restrict__ LU, int n, double *x, int b0, int bs, int r0, int r1) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, half = lane >> 5, hl = lane & 31;
+  if (r1 - r0 > 4096) {
+    for (int r = r0 + tid; r < r1; r += 1024) x[r] -= row_dot(LU + (int64_t)r * n + b0, x + b0, bs);
+    return;
+  }
+  for (int r = r0 + 2 * wid + half; r < r1; r += 32) {  // two rows per wave, 32 lanes each
+    double v = hl < bs ? LU[(int64_t)r * n + b0 + hl] * x[b0 + hl] : 0.0;
+#pragma unroll
+    for (int o = 16; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    if (hl == 0) x[r] -= v;
+  }
+}
+
+// sum_p a[p] x[p] over one row segment (bs <= TB), loads issued ahead of the FMAs
+__device__ __forceinline__ double row_dot(const double *__restrict__ a, const double *x, int bs) {
+  double v[TB];
+#pragma unroll
+  for (int p = 0; p < TB; ++p) v[p] = p < bs ? a[p] : 0.0;
+  double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+  for (int p = 0; p < TB; p += 2) {
+    s0 = fma(v[p], p < bs ? x[p] : 0.0, s0);
+    s1 = fma(v[p + 1], p + 1 < bs ? x[p + 1] : 0.0, s1);
+  }
+  return s0 + s1;
+}
+
 // one workgroup (1024 threads): x (in LDS) <- A^-1 x (trans = 0) or A^-T x (trans = 1), with the
-// dgetrf factors LU (row-major n x n) and pivots
+// dgetrf factors LU (row-major n x n) and pivots (staged in LDS: the swap chain is serial)
 __device__ void lu_solve_blk(const double *__restrict__ LU, int n, const int *__restrict__ piv, double *x,
                              int trans) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -454,12 +485,7 @@ __device__ void lu_solve_blk(const double *__restrict__ LU, int n, const int *__
         if (half == 0 && hl < bs) x[b0 + hl] = xq;
       }
       __syncthreads();
-      for (int r = b0 + bs + 2 * wid + half; r < n; r += 32) {  // two rows per wave, 32 lanes each
-        double v = hl < bs ? LU[(int64_t)r * n + b0 + hl] * x[b0 + hl] : 0.0;
-#pragma unroll
-        for (int o = 16; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-        if (hl == 0) x[r] -= v;
-      }
+      rows_update(LU, n, x, b0, bs, b0 + bs, n);
       __syncthreads();
     }
     for (int bend = n; bend > 0; bend -= TB) {  // U z = y
@@ -482,12 +508,7 @@ __device__ void lu_solve_blk(const double *__restrict__ LU, int n, const int *__
         if (half == 0 && hl < bs) x[b0 + hl] = xq;
       }
       __syncthreads();
-      for (int r = 2 * wid + half; r < b0; r += 32) {
-        double v = hl < bs ? LU[(int64_t)r * n + b0 + hl] * x[b0 + hl] : 0.0;
-#pragma unroll
-        for (int o = 16; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-        if (hl == 0) x[r] -= v;
-      }
+      rows_update(LU, n, x, b0, bs, 0, b0);
       __syncthreads();
     }
   } else {
@@ -553,11 +574,13 @@ __device__ void lu_solve_blk(const double *__restrict__ LU, int n, const int *__
 }
 
 // dgecon (1-norm) from the factors: colsum = column sums of |A| before factorisation
-__global__ __launch_bounds__(1024) void lu_rcond_kernel(const double *__restrict__ LU, int n, const int *piv,
+__global__ __launch_bounds__(1024) void lu_rcond_kernel(const double *__restrict__ LU, int n, const int *gpiv,
                                                         const double *__restrict__ colsum, const int *status,
                                                         double *rcond_out) {
   extern __shared__ double xl[];
   double *x = xl, *xs = xl + n;
+  int *piv = reinterpret_cast<int *>(xl + 2 * n);
+  for (int i = threadIdx.x; i < n; i += blockDim.x) piv[i] = gpiv[i];
   __shared__ double red[16];
   __shared__ double rv[1024];
   __shared__ int ri[1024];
@@ -634,10 +657,12 @@ __global__ __launch_bounds__(1024) void lu_rcond_kernel(const double *__restrict
 }
 
 // getrs for a few right-hand sides: one workgroup per column, x in LDS
-__global__ __launch_bounds__(1024) void lu_solve_cols_kernel(const double *__restrict__ LU, int n, const int *piv,
+__global__ __launch_bounds__(1024) void lu_solve_cols_kernel(const double *__restrict__ LU, int n, const int *gpiv,
                                                              double *B, int ldb) {
   extern __shared__ double xl[];
   const int c = blockIdx.x, tid = threadIdx.x;
+  int *piv = reinterpret_cast<int *>(xl + n);
+  for (int i = tid; i < n; i += 1024) piv[i] = gpiv[i];
   for (int i = tid; i < n; i += 1024) xl[i] = B[(int64_t)i * ldb + c];
   __syncthreads();
   lu_solve_blk(LU, n, piv, xl, 0);
@@ -652,8 +677,11 @@ int lu_blocked(hipStream_t st, double *A, int n, int *piv, double *work, int *st
   TTK_HIP(hipMemsetAsync(status, 0, sizeof(int), st));
   double *colsum = work;  // n doubles
   if (want_rcond) hipLaunchKernelGGL(colsum_kernel, dim3((n + 255) / 256), dim3(256), 0, st, A, n, colsum);
-  for (int k0 = 0; k0 < n; k0 += NB) {
-    const int kb = n - k0 < NB ? n - k0 : NB;
+  for (int k0 = 0; k0 < n;) {
+    // widest panel (32, 16 or 8 columns) whose (n-k0) x kb block fits the 150 KB LDS staging
+    int kb = NB;
+    while (kb > 8 && (size_t)(n - k0) * (kb + 1) * sizeof(double) > 150000) kb >>= 1;
+    if (kb > n - k0) kb = n - k0;
     const size_t pshm = (size_t)(n - k0) * (kb + 1) * sizeof(double);
     if (pshm <= 150000) {
       if (pshm > 65536)
@@ -673,9 +701,10 @@ int lu_blocked(hipStream_t st, double *A, int n, int *piv, double *work, int *st
                          A + (int64_t)(k0 + kb) * n + k0 + kb, n, rest, rest, kb, -1.0, 1.0, 0);
     }
     TTK_LAUNCH_CHECK();
+    k0 += kb;
   }
   if (want_rcond) {
-    const size_t shm = 2 * (size_t)n * sizeof(double);
+    const size_t shm = 2 * (size_t)n * sizeof(double) + (size_t)n * sizeof(int);
     if (shm > 65536)
       (void)hipFuncSetAttribute(reinterpret_cast<const void *>(lu_rcond_kernel),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
@@ -686,7 +715,7 @@ int lu_blocked(hipStream_t st, double *A, int n, int *piv, double *work, int *st
 }
 
 int lu_solve_cols(hipStream_t st, const double *LU, int n, const int *piv, double *B, int nrhs, int ldb) {
-  const size_t shm = (size_t)n * sizeof(double);
+  const size_t shm = (size_t)n * (sizeof(double) + sizeof(int));
   if (shm > 65536)
     (void)hipFuncSetAttribute(reinterpret_cast<const void *>(lu_solve_cols_kernel),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);

@@ -12,7 +12,7 @@ int trsm_blocked(hipStream_t st, const double *L, int n, double *B, int nrhs, in
 // blocked getrf (device pivots and LAPACK info in `status`) and, if want_rcond, the dgecon
 // 1-norm estimate into device `rcond`; work >= n doubles.  Enqueued without synchronising.
 int lu_blocked(hipStream_t st, double *A, int n, int *piv, double *work, int *status, double *rcond, int want_rcond);
-// getrs for nrhs columns of B (one workgroup per column, n <= 18000)
+// getrs for nrhs columns of B (one workgroup per column, n <= 12000)
 int lu_solve_cols(hipStream_t st, const double *LU, int n, const int *piv, double *B, int nrhs, int ldb);
 }  // namespace ttk
 

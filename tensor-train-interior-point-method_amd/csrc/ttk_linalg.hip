@@ -2501,7 +2501,7 @@ int ttk_lu_sync(void *stream, double *A, int n, int *piv, double *work, double *
     ttk::set_error("ttk_lu_sync: status alloc failed");
     return TTK_ERR_HIP;
   }
-  if (n >= g_lu_block_min && n <= 9000) {
+  if (n >= g_lu_block_min && n <= 7000) {
     const int rc = ttk::lu_blocked(TTK_STREAM(stream), A, n, piv, work, g_status, g_rcond, 1);
     if (rc) return rc;
   } else {
@@ -2520,7 +2520,7 @@ int ttk_lu_sync(void *stream, double *A, int n, int *piv, double *work, double *
 }
 
 int ttk_lu_solve(void *stream, const double *LU, int n, const int *piv, double *B, int nrhs, int ldb) {
-  if (n >= g_lu_block_min && n <= 18000 && nrhs <= 8 && nrhs > 0) return ttk::lu_solve_cols(TTK_STREAM(stream), LU, n, piv, B, nrhs, ldb);
+  if (n >= g_lu_block_min && n <= 12000 && nrhs <= 8 && nrhs > 0) return ttk::lu_solve_cols(TTK_STREAM(stream), LU, n, piv, B, nrhs, ldb);
   if (n <= 0 || nrhs <= 0) return TTK_OK;
   hipLaunchKernelGGL(lu_solve_kernel, dim3((nrhs + 63) / 64), dim3(256), 0, TTK_STREAM(stream), LU, n, piv, B, nrhs, ldb);
   TTK_LAUNCH_CHECK();

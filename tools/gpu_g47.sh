@@ -1,0 +1,6 @@
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+timeout -k 10 300 python -u -m pytest tests/test_gpu_kernels.py -q -x --timeout 120 --timeout-method thread -k "lu" > gpurun_out/g47_pytest.log 2>&1 && \
+timeout -k 10 300 python -u tools/bench_lu.py > gpurun_out/g47_lu.log 2>&1 && \
+timeout -k 10 300 python -u tools/run_case.py maxcut maxcut_10 23 1 > gpurun_out/g47_mc10_s23.log 2>&1
