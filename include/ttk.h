@@ -187,6 +187,18 @@ int ttk_debug_counters(unsigned long long *out, int reset);
 int ttk_svd_set_timing(int on);
 int ttk_syev_extreme(void *stream, const double *A, int n, int which, double *ev, double *vec, double *work);
 
+/* Schur-reduced local KKT operator of the iterative local solve (`MatVecWrapper` /
+ * `IneqMatVecWrapper`, cy_src/lgmres_cy.pyx:203-331,379-510) as a handle.  `descs`: 5 (ineq = 0)
+ * or 7 block descriptors of 34 int64 words each, in ttk_einsum's format for the local apply
+ * 'lsr,smnS,LSR,rnR->lmL' (4 operands: XAX_k, A_k, XAX_k1, x with any pointer; has_out = 0):
+ * B00, B01, B21, B22, B01 (read as its transpose 'lsr,smnS,LSR,lmL->rnR') [, B31, B33].
+ * inv_I: m device doubles.  *handle = 0 when a block exceeds the fused kernel's limits (the
+ * caller keeps the per-block path).  ttk_schur_apply: out = A v for v = [y; x (; t)] in 2
+ * launches, the same operations (and rounding) as the per-block fused applies. */
+int ttk_schur_build(int ineq, int64_t m, const int64_t *descs, const double *inv_I, int64_t *handle);
+int ttk_schur_apply(void *stream, int64_t handle, const double *v, double *out);
+int ttk_schur_free(int64_t handle);
+
 /* ---------------------------------------------------------------------------------------
  * LGMRES building blocks (PETSc KSPLGMRES semantics, see oracle/petsc_lgmres.py):
  * one Arnoldi orthogonalisation + Hessenberg/Givens update per call.  V is (ldv x n)

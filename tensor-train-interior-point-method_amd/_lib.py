@@ -67,6 +67,9 @@ _SIGS = {
     "ttk_contract_stats": (i32, [vp, i32]),
     "ttk_syev_extreme": (i32, [vp, vp, i32, i32, vp, vp, vp]),
     "ttk_lgmres_arnoldi_sync": (i32, [vp, vp, i32, i32, vp, i32, f64, c_dp, c_ip]),
+    "ttk_schur_build": (i32, [i32, i64, c_i64p, vp, c_i64p]),
+    "ttk_schur_apply": (i32, [vp, i64, vp, vp]),
+    "ttk_schur_free": (i32, [i64]),
     "ttk_lgmres_arnoldi_async": (i32, [vp, vp, i32, i32, vp, i32, f64, f64, f64, vp, i32, f64]),
     "ttk_lgmres_build": (i32, [vp, vp, i32, i32, ctypes.POINTER(vp), i32, i32, vp, vp]),
     "ttk_lgmres_aug": (i32, [vp, vp, i32, i32, vp, i32, f64, vp, vp, vp]),

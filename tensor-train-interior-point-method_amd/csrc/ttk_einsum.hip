@@ -456,9 +456,11 @@ struct ApplyArgs {
 // Association follows the greedy pairwise plan the reference's opt_einsum picks for these shapes
 // (t1 = P x over r, t2 = A t1 over (s,n), out = Q t2 over (S,R)), so intermediates and rounding
 // behave like the plan path's.  One workgroup per output index a.
-__global__ __launch_bounds__(256) void fused_apply_kernel(ApplyArgs g) {
-  extern __shared__ double sm[];
-  const int a = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
+// the three stages of one output row a; DIRECT writes out = alpha*acc + beta*out, otherwise the raw
+// row goes to orow[i*nc + c] (LDS)
+template <bool DIRECT>
+__device__ void apply_row(const ApplyArgs &g, int a, double *sm, double *orow) {
+  const int tid = threadIdx.x, nt = blockDim.x;
   const int nb = g.nb, nj = g.nj, nd = g.nd, nS = g.nS, ns = g.ns, ni = g.ni, nc = g.nc;
   double *X = sm;                       // nb*nj*nd     [b][j][d]
   double *Pa = X + nb * nj * nd;        // ns*nb        [s][b]   (P[a, s, b])
@@ -508,8 +510,63 @@ __global__ __launch_bounds__(256) void fused_apply_kernel(ApplyArgs g) {
       const double *qr = g.Q + c * g.qs[0] + S * g.qs[1];
       for (int d = 0; d < nd; ++d) acc = fma(qr[d * g.qs[2]], tr[S * nd + d], acc);
     }
-    double *o = g.out + a * g.os[0] + i * g.os[1] + c * g.os[2];
-    *o = g.beta != 0.0 ? g.alpha * acc + g.beta * *o : g.alpha * acc;
+    if (DIRECT) {
+      double *o = g.out + a * g.os[0] + i * g.os[1] + c * g.os[2];
+      *o = g.beta != 0.0 ? g.alpha * acc + g.beta * *o : g.alpha * acc;
+    } else {
+      orow[e] = acc;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void fused_apply_kernel(ApplyArgs g) {
+  extern __shared__ double sm[];
+  apply_row<true>(g, blockIdx.x, sm, nullptr);
+}
+
+// Several local applies in ONE launch (the Schur-reduced KKT matvec of LGMRES): task t owns
+// workgroups [off[t], off[t+1]) = its output rows; a task sums up to two applies into one output
+// (out = alpha0*apply0; out = alpha1*apply1 + out, the same operations as two fused launches with
+// beta = 1), then optionally out = out * oscale and out = addv + out (inv_I o v, + t).
+struct ApplyTask {
+  ApplyArgs t[2];
+  int nterms;
+  const double *oscale, *addv;  // same layout as the output, or null
+};
+struct ApplyLaunch {
+  ApplyTask task[3];
+  int ntask;
+  int off[4];
+};
+
+__global__ __launch_bounds__(256) void fused_apply_multi_kernel(ApplyLaunch L) {
+  extern __shared__ double sm[];
+  int t = 0;
+  while (t + 1 < L.ntask && (int)blockIdx.x >= L.off[t + 1]) ++t;
+  const ApplyTask &T = L.task[t];
+  const int a = (int)blockIdx.x - L.off[t];
+  const ApplyArgs &g0 = T.t[0];
+  const int ni = g0.ni, nc = g0.nc, tid = threadIdx.x, nt = blockDim.x;
+  double *orow = sm, *acc = sm + ni * nc, *work = acc + ni * nc;
+  for (int k = 0; k < T.nterms; ++k) {
+    apply_row<false>(T.t[k], a, work, k == 0 ? orow : acc);
+    __syncthreads();
+    if (k > 0) {
+      const double al = T.t[k].alpha;
+      for (int e = tid; e < ni * nc; e += nt) orow[e] = al * acc[e] + 1.0 * orow[e];
+    } else {
+      const double al = g0.alpha;
+      for (int e = tid; e < ni * nc; e += nt) orow[e] = al * orow[e];
+    }
+    __syncthreads();
+  }
+  for (int e = tid; e < ni * nc; e += nt) {
+    const int i = e / nc, c = e - i * nc;
+    const int64_t oi = a * g0.os[0] + i * g0.os[1] + c * g0.os[2];
+    double v = orow[e];
+    if (T.oscale) v = (1.0 * v) * T.oscale[oi];
+    if (T.addv) v = 1.0 * T.addv[oi] + 1.0 * v;
+    g0.out[oi] = v;
   }
 }
 
@@ -524,8 +581,14 @@ int64_t apply_lds(int nb, int nj, int nd, int nS, int ns, int ni) {
 
 // Try the fused kernel for the two local-apply equations; returns 1 if handled, 0 if the caller
 // should run the generic plan, <0 on error.  desc as in ttk_einsum.
-int fused_apply_try(void *stream, const char *eq, const int64_t *desc, double *out, double alpha, double beta) {
-  if (!(desc[0] & 256)) return 0;  // caller did not opt in
+static double fused_max_flops() {
+  static const double v = getenv("TTK_FUSED_MAX_FLOPS") ? atof(getenv("TTK_FUSED_MAX_FLOPS")) : 4e6;
+  return v;
+}
+
+// ApplyArgs of a local-apply equation from an einsum descriptor (see ttk_einsum); 1 if the fused
+// kernel can run it (LDS and grid limits), 0 otherwise
+static int apply_args(const char *eq, const int64_t *desc, double *out, double alpha, double beta, ApplyArgs &g) {
   const bool fwd = std::strcmp(eq, "lsr,smnS,LSR,rnR->lmL") == 0;
   const bool bwd = !fwd && std::strcmp(eq, "lsr,smnS,LSR,lmL->rnR") == 0;
   if (!fwd && !bwd) return 0;
@@ -536,7 +599,6 @@ int fused_apply_try(void *stream, const char *eq, const int64_t *desc, double *o
   if (rP[1] != 3 || rA[1] != 4 || rQ[1] != 3 || rx[1] != 3) return 0;
   const int64_t *Psh = rP + 2, *Pst = rP + 5, *Ash = rA + 2, *Ast = rA + 6, *Qsh = rQ + 2, *Qst = rQ + 5;
   const int64_t *xst = rx + 5;
-  ApplyArgs g;
   g.P = reinterpret_cast<const double *>(rP[0]);
   g.A = reinterpret_cast<const double *>(rA[0]);
   g.Q = reinterpret_cast<const double *>(rQ[0]);
@@ -587,12 +649,20 @@ int fused_apply_try(void *stream, const char *eq, const int64_t *desc, double *o
   }
   const int64_t need = apply_lds(g.nb, g.nj, g.nd, g.nS, g.ns, g.ni);
   if (need > APPLY_LDS_DOUBLES || g.na < 1 || g.na > 65535) return 0;
+  return 1;
+}
+
+int fused_apply_try(void *stream, const char *eq, const int64_t *desc, double *out, double alpha, double beta) {
+  if (!(desc[0] & 256)) return 0;  // caller did not opt in
+  ApplyArgs g;
+  if (!apply_args(eq, desc, out, alpha, beta, g)) return 0;
+  const int64_t need = apply_lds(g.nb, g.nj, g.nd, g.nS, g.ns, g.ni);
   // one workgroup per output row runs the three stages on the VALU: past a few MFLOP per launch
   // the pairwise MFMA plan (with split-K) is faster (graphm_3 r=2 sizes)
   const double flops = 2.0 * g.na *
                        ((double)g.ns * g.nj * g.nd * g.nb + (double)g.ni * g.nS * g.nd * g.ns * g.nj +
                         (double)g.ni * g.nc * g.nS * g.nd);
-  static const double max_flops = getenv("TTK_FUSED_MAX_FLOPS") ? atof(getenv("TTK_FUSED_MAX_FLOPS")) : 4e6;
+  const double max_flops = fused_max_flops();
   // relabelled environment updates (desc flag 512) have few output rows, so each workgroup carries
   // a larger share of the chain: fused only while small
   static const double env_max_flops =
@@ -611,3 +681,163 @@ int fused_apply_try(void *stream, const char *eq, const int64_t *desc, double *o
   ttk::contract_count_ext(flops);
   return 1;
 }
+
+// ------------------------------------------------------------------ Schur-reduced KKT operator
+// `MatVecWrapper` / `IneqMatVecWrapper` (cy_src/lgmres_cy.pyx:203-331,379-510) as a handle: the
+// blocks' local-apply descriptors are parsed once per LGMRES solve; each matvec is 2 launches
+// (stage 1: o0 = B00 y + B01 x, w = inv_I o B01^T y (+ t), [o2 = B31 x + B33 t]; stage 2:
+// o1 = B21 x - B22 w) instead of 5-8 fused applies + element-wise kernels, same arithmetic.
+namespace {
+
+struct SchurOp {
+  ApplyLaunch st[2];
+  int xseg[2][3][2];  // input segment of each term: 0 y, 1 x, 2 t, 3 w
+  int oseg[2][3];     // output segment of each task: 0, 1, 2, 3 = w
+  size_t shm[2];
+  int64_t m;
+  int ineq;
+  double flops;
+  bool used;
+};
+std::vector<SchurOp> g_schur;
+double *g_schur_w = nullptr;
+int64_t g_schur_wcap = 0;
+
+size_t multi_lds(const ApplyLaunch &L) {
+  int64_t mx = 0;
+  for (int t = 0; t < L.ntask; ++t) {
+    const ApplyTask &T = L.task[t];
+    int64_t need = 2 * (int64_t)T.t[0].ni * T.t[0].nc;
+    int64_t w = 0;
+    for (int k = 0; k < T.nterms; ++k) {
+      const ApplyArgs &g = T.t[k];
+      const int64_t l = apply_lds(g.nb, g.nj, g.nd, g.nS, g.ns, g.ni);
+      w = l > w ? l : w;
+    }
+    need += w;
+    mx = need > mx ? need : mx;
+  }
+  return (size_t)mx * sizeof(double);
+}
+
+double term_flops(const ApplyArgs &g) {
+  return 2.0 * g.na *
+         ((double)g.ns * g.nj * g.nd * g.nb + (double)g.ni * g.nS * g.nd * g.ns * g.nj +
+          (double)g.ni * g.nc * g.nS * g.nd);
+}
+
+}  // namespace
+
+extern "C" {
+
+int ttk_schur_build(int ineq, int64_t m, const int64_t *descs, const double *inv_I, int64_t *handle) {
+  *handle = 0;
+  constexpr int W = 34;  // words per block descriptor: 4 operand records (3/4/3/3-D) + has_out = 0
+  const int nblk = ineq ? 7 : 5;
+  ApplyArgs g[7];
+  static const char *F = "lsr,smnS,LSR,rnR->lmL", *T = "lsr,smnS,LSR,lmL->rnR";
+  for (int b = 0; b < nblk; ++b) {
+    if (!apply_args(b == 4 ? T : F, descs + (int64_t)b * W, nullptr, 1.0, 0.0, g[b])) return TTK_OK;
+    if ((int64_t)g[b].na * g[b].ni * g[b].nc != m) return TTK_OK;
+    if (term_flops(g[b]) > fused_max_flops()) return TTK_OK;  // the pairwise MFMA plan is faster there
+  }
+  SchurOp op{};
+  op.m = m;
+  op.ineq = ineq;
+  // stage 1
+  ApplyLaunch &L1 = op.st[0];
+  L1.ntask = ineq ? 3 : 2;
+  L1.task[0].nterms = 2;
+  L1.task[0].t[0] = g[0];  // B00 y
+  L1.task[0].t[1] = g[1];  // + B01 x
+  L1.task[0].t[1].alpha = 1.0;
+  op.xseg[0][0][0] = 0;
+  op.xseg[0][0][1] = 1;
+  op.oseg[0][0] = 0;
+  L1.task[1].nterms = 1;
+  L1.task[1].t[0] = g[4];  // B01^T y
+  L1.task[1].oscale = inv_I;
+  op.xseg[0][1][0] = 0;
+  op.oseg[0][1] = 3;
+  if (ineq) {
+    L1.task[2].nterms = 2;
+    L1.task[2].t[0] = g[5];  // B31 x
+    L1.task[2].t[1] = g[6];  // + B33 t
+    op.xseg[0][2][0] = 1;
+    op.xseg[0][2][1] = 2;
+    op.oseg[0][2] = 2;
+  }
+  // stage 2: o1 = B21 x - B22 w
+  ApplyLaunch &L2 = op.st[1];
+  L2.ntask = 1;
+  L2.task[0].nterms = 2;
+  L2.task[0].t[0] = g[2];
+  L2.task[0].t[1] = g[3];
+  L2.task[0].t[1].alpha = -1.0;
+  op.xseg[1][0][0] = 1;
+  op.xseg[1][0][1] = 3;
+  op.oseg[1][0] = 1;
+  for (int s = 0; s < 2; ++s) {
+    ApplyLaunch &L = op.st[s];
+    L.off[0] = 0;
+    for (int t = 0; t < L.ntask; ++t) {
+      L.off[t + 1] = L.off[t] + L.task[t].t[0].na;
+      for (int k = 0; k < L.task[t].nterms; ++k) op.flops += term_flops(L.task[t].t[k]);
+    }
+    op.shm[s] = multi_lds(L);
+    if (op.shm[s] > (size_t)APPLY_LDS_DOUBLES * sizeof(double)) return TTK_OK;
+  }
+  if (m > g_schur_wcap) {
+    if (g_schur_w) (void)hipFree(g_schur_w);
+    g_schur_w = nullptr;
+    g_schur_wcap = 0;
+    const int64_t want = m < 65536 ? 65536 : m;
+    TTK_HIP(hipMalloc(reinterpret_cast<void **>(&g_schur_w), want * sizeof(double)));
+    g_schur_wcap = want;
+  }
+  op.used = true;
+  size_t slot = 0;
+  while (slot < g_schur.size() && g_schur[slot].used) ++slot;
+  if (slot == g_schur.size()) g_schur.push_back(op);
+  else g_schur[slot] = op;
+  *handle = (int64_t)slot + 1;
+  return TTK_OK;
+}
+
+int ttk_schur_apply(void *stream, int64_t handle, const double *v, double *out) {
+  if (handle < 1 || handle > (int64_t)g_schur.size() || !g_schur[handle - 1].used) {
+    ttk::set_error("ttk_schur_apply: bad handle %lld", (long long)handle);
+    return TTK_ERR_ARG;
+  }
+  SchurOp &op = g_schur[handle - 1];
+  const int64_t m = op.m;
+  const double *in[4] = {v, v + m, v + 2 * m, g_schur_w};
+  double *o[4] = {out, out + m, out + 2 * m, g_schur_w};
+  for (int s = 0; s < 2; ++s) {
+    ApplyLaunch L = op.st[s];
+    for (int t = 0; t < L.ntask; ++t) {
+      for (int k = 0; k < L.task[t].nterms; ++k) {
+        L.task[t].t[k].x = in[op.xseg[s][t][k]];
+        L.task[t].t[k].out = o[op.oseg[s][t]];
+      }
+      if (s == 0 && t == 1 && op.ineq) L.task[t].addv = v + 2 * m;  // w = inv_I o B01^T y + t
+    }
+    if (op.shm[s] > 65536)
+      (void)hipFuncSetAttribute(reinterpret_cast<const void *>(fused_apply_multi_kernel),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)op.shm[s]);
+    hipEvent_t e0, e1;
+    if (ttk::contract_events_ext(&e0, &e1) != TTK_OK) return TTK_ERR_HIP;
+    hipExtLaunchKernelGGL(fused_apply_multi_kernel, dim3(L.off[L.ntask]), dim3(256), op.shm[s], TTK_STREAM(stream),
+                          e0, e1, 0, L);
+    TTK_LAUNCH_CHECK();
+  }
+  ttk::contract_count_ext(op.flops);
+  return TTK_OK;
+}
+
+int ttk_schur_free(int64_t handle) {
+  if (handle >= 1 && handle <= (int64_t)g_schur.size()) g_schur[handle - 1].used = false;
+  return TTK_OK;
+}
+
+}  // extern "C"

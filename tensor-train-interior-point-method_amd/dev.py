@@ -332,6 +332,20 @@ def _einsum_native(eq, *ops, out=None, alpha=1.0, beta=0.0, fused=False):
     return out
 
 
+def apply_desc(P, A, Q, xshape):
+    """ttk_einsum descriptor of the local apply 'lsr,smnS,LSR,rnR->lmL' with operands P, A, Q and a
+    placeholder x of shape `xshape` (pointer patched per call by ttk_schur_apply); 34 words."""
+    d = [4 | 256]
+    for o in (P, A, Q):
+        d.append(o.data_ptr())
+        d.append(o.dim())
+        d.extend(o.shape)
+        d.extend(o.stride())
+    r, n, R = xshape
+    d.extend([0, 3, r, n, R, n * R, R, 1, 0])
+    return d
+
+
 def tensordot(a, b, axes):
     """numpy-style tensordot via the einsum executor."""
     ax_a, ax_b = axes

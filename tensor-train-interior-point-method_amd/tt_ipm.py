@@ -7,6 +7,7 @@ Local KKT solvers (`_ipm_local_solver`, `src/tt_ipm.py:183-282`; `_ipm_local_sol
 `:284-401`): dense Schur path = device assembly (MFMA GEMM), Cholesky, triangular solves, GEMMs
 and LU with the scipy rcond warning rule; iterative path = device LGMRES (PETSc semantics) on
 the Schur-reduced operator of `MatVecWrapper` (`cy_src/lgmres_cy.pyx:291-331`)."""
+import ctypes
 import os
 import sys
 import traceback
@@ -18,6 +19,7 @@ import time
 import numpy as np
 
 from . import dev as D
+from ._lib import lib
 from . import tt_ops as T
 from .dev import einsum
 from .lgmres import lgmres
@@ -38,6 +40,8 @@ INEQ_MATVEC_BUG = False
 # LGMRES operator applies run as one fused launch each (Krylov iterates at rtol 1e-5 are insensitive
 # to the association order; the AMEn residuals keep the reference's pairwise order)
 FUSED_MATVEC = os.environ.get("TTIPM_FUSED_MATVEC", "1") == "1"
+# ... and the whole Schur matvec as one native operator (2 launches per matvec, same arithmetic)
+SCHUR_OP = os.environ.get("TTIPM_SCHUR_OP", "1") == "1"
 
 
 class IneqMatvecBug(TypeError):
@@ -59,6 +63,25 @@ class MatVecWrapper:
         r, n, RR = shape
         self.m = r * n * RR
         self.tmp = D.empty(r, n, RR)
+        self.h = 0
+        if FUSED_MATVEC and SCHUR_OP and not INEQ_MATVEC_BUG:
+            order = [(0, 0), (0, 1), (2, 1), (2, 2), (0, 1)] + ([(3, 1), (3, 3)] if len(self.keys) > 4 else [])
+            desc = []
+            for k in order:
+                desc += D.apply_desc(self.L[k], self.A[k], self.R[k], shape)
+            h = ctypes.c_int64(0)
+            arr = (ctypes.c_int64 * len(desc))(*desc)
+            D.check(lib.ttk_schur_build(int(len(self.keys) > 4), self.m, arr, inv_I.contiguous().data_ptr(),
+                                        ctypes.byref(h)), "schur_build")
+            self.h = h.value
+            self._inv = inv_I  # keep the operands alive while the handle exists
+
+    def __del__(self):
+        if getattr(self, "h", 0):
+            try:
+                lib.ttk_schur_free(self.h)
+            except Exception:
+                pass
 
     def _parts(self, v, nb):
         r, n, R = self.shape
@@ -73,6 +96,9 @@ class MatVecWrapper:
         return self.tmp
 
     def matvec_into(self, v, out):
+        if self.h:
+            D.check(lib.ttk_schur_apply(D._stream(), self.h, v.data_ptr(), out.data_ptr()), "schur_apply")
+            return out
         y, x = self._parts(v, 2)
         o0, o1 = self._parts(out, 2)
         self._op((0, 0), y, o0)
@@ -94,6 +120,9 @@ class IneqMatVecWrapper(MatVecWrapper):
     def matvec_into(self, v, out):
         if INEQ_MATVEC_BUG:
             raise IneqMatvecBug("reference bug: IneqMatVecWrapper.matvec returns a memoryview")
+        if self.h:
+            D.check(lib.ttk_schur_apply(D._stream(), self.h, v.data_ptr(), out.data_ptr()), "schur_apply")
+            return out
         y, x, t = self._parts(v, 3)
         o0, o1, o2 = self._parts(out, 3)
         self._op((0, 0), y, o0)

@@ -339,6 +339,13 @@ class EmuLib:
         flags[1] = null
         return 0
 
+    def ttk_schur_build(self, ineq, m, descs, inv_I, handle):
+        handle._obj.value = 0  # no native operator: the per-block path runs
+        return 0
+
+    def ttk_schur_free(self, h):
+        return 0
+
     def ttk_lgmres_arnoldi_async(self, s, V, n, it, hh, max_k, haptol, ttol, divtol, ctl, slot, marker):
         c = _dv(ctl, 1 + 5 * (slot + 1))
         if c[0] != 0.0:
@@ -392,7 +399,7 @@ def emulated_ttipm():
     import ttipm_amd  # noqa: F401
     lib_mod = importlib.import_module("ttipm_amd._lib")
     lib_mod.lib = EmuLib()
-    for name in ("dev", "lgmres"):
+    for name in ("dev", "lgmres", "tt_ipm"):
         m = importlib.import_module("ttipm_amd." + name)
         m.lib = lib_mod.lib
     return ttipm_amd
