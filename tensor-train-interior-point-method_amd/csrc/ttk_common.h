@@ -10,6 +10,7 @@ namespace ttk {
 void set_error(const char *fmt, ...);
 void note_launch();
 double *pinned_stage(size_t n_doubles);  // per-thread pinned host staging buffer
+double *mapped_stage(size_t n_doubles, double **dev_ptr);  // host-coherent mapped buffer (host ptr)
 int contract_events_ext(hipEvent_t *ev0, hipEvent_t *ev1);  // roofline accounting (ttk_contract.hip)
 void contract_count_ext(double flops);
 

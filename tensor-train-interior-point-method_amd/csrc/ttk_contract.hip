@@ -546,9 +546,15 @@ int ttk_dot_nd_sync(void *stream, const double *x, const double *y, int ndim, co
     *result = 0.0;
     return TTK_OK;
   }
-  hipLaunchKernelGGL(dot_nd_kernel, dim3(1), dim3(1024), 0, TTK_STREAM(stream), x, y, d, g_dev_scalar);
+  static const int mapped = getenv("TTK_MAPPED_READS") ? atoi(getenv("TTK_MAPPED_READS")) : 1;
+  double *dev = nullptr;
+  double *h = mapped ? ttk::mapped_stage(1, &dev) : nullptr;  // the reduction writes to host-coherent memory
+  hipLaunchKernelGGL(dot_nd_kernel, dim3(1), dim3(1024), 0, TTK_STREAM(stream), x, y, d, h ? dev : g_dev_scalar);
   TTK_LAUNCH_CHECK();
-  return ttk_read_sync(stream, g_dev_scalar, result, 1);
+  if (!h) return ttk_read_sync(stream, g_dev_scalar, result, 1);
+  TTK_HIP(hipStreamSynchronize(TTK_STREAM(stream)));
+  *result = h[0];
+  return TTK_OK;
 }
 
 int ttk_sumsq_batched(void *stream, const double *x, int64_t n, int nb, int64_t bstride, double *out) {
