@@ -15,6 +15,7 @@
 
 #include <array>
 #include <cstdio>
+#include <cstdlib>
 #include <map>
 #include <vector>
 
@@ -119,6 +120,89 @@ __device__ __forceinline__ void gemm_tile(const double *__restrict__ A, const do
       const double v = alpha * acc[r];
       *p = (beta == 0.0) ? v : v + beta * (*p);
     }
+  }
+}
+
+// Throughput variant for large steps (dense Schur GEMMs, graphm-sized contractions): 64x64 outputs
+// per workgroup, each wave a 32x32 block as 2x2 MFMA tiles (4 accumulators: 16 MFMAs per LDS
+// stage instead of 4).  Same K order per output element as gemm_tile, so results are identical.
+constexpr int BM = 64, BN = 64;
+
+template <int KS>
+__global__ __launch_bounds__(256) void gemm_offs64_kernel(GemmArgs g) {
+  constexpr int NQ = KS / 4;  // staged elements per thread per operand
+  __shared__ double As[KS][BM + 1];
+  __shared__ double Bs[KS][BN + 1];
+  const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM, b = blockIdx.z;
+  const int M = g.M, N = g.N, K = g.K, nb = g.nb;
+  const int64_t *a_b = g.offs;
+  const int64_t *a_m = a_b + nb;
+  const int64_t *a_k = a_m + M;
+  const int64_t *b_b = a_k + K;
+  const int64_t *b_k = b_b + nb;
+  const int64_t *b_n = b_k + K;
+  const int64_t *c_b = b_n + N;
+  const int64_t *c_m = c_b + nb;
+  const int64_t *c_n = c_m + M;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1;
+  const int l_mn = tid & 63, l_k = tid >> 6;  // stages (m|n = l_mn, k = l_k + 4q), q = 0..3
+  const bool am_ok = (m0 + l_mn) < M, bn_ok = (n0 + l_mn) < N;
+  const double *Ap = g.A + a_b[b] + (am_ok ? a_m[m0 + l_mn] : 0);
+  const double *Bp = g.B + b_b[b] + (bn_ok ? b_n[n0 + l_mn] : 0);
+  double ra[NQ], rb[NQ];
+  auto fetch = [&](int k0) {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const int k = k0 + l_k + 4 * q;
+      const bool ok = k < K;
+      const int64_t oa = ok ? a_k[k] : 0, ob = ok ? b_k[k] : 0;
+      ra[q] = (am_ok && ok) ? Ap[oa] : 0.0;
+      rb[q] = (bn_ok && ok) ? Bp[ob] : 0.0;
+    }
+  };
+  double4_t acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = double4_t{0.0, 0.0, 0.0, 0.0};
+  fetch(0);
+  for (int k0 = 0; k0 < K; k0 += KS) {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      As[l_k + 4 * q][l_mn] = ra[q];
+      Bs[l_k + 4 * q][l_mn] = rb[q];
+    }
+    __syncthreads();
+    if (k0 + KS < K) fetch(k0 + KS);
+#pragma unroll
+    for (int s = 0; s < KS / 4; ++s) {
+      const int kr = s * 4 + (lane >> 4);
+      const double a0 = As[kr][wr * 32 + (lane & 15)], a1 = As[kr][wr * 32 + 16 + (lane & 15)];
+      const double b0 = Bs[kr][wc * 32 + (lane & 15)], b1 = Bs[kr][wc * 32 + 16 + (lane & 15)];
+      acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1][1], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int col = n0 + wc * 32 + j * 16 + (lane & 15);
+    if (col >= N) continue;
+    const int64_t cb = c_b[b] + c_n[col];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wr * 32 + i * 16 + (lane >> 4) + 4 * r;
+        if (row < M) {
+          double *p = g.C + cb + c_m[row];
+          const double v = g.alpha * acc[i][j][r];
+          *p = (g.beta == 0.0) ? v : v + g.beta * (*p);
+        }
+      }
   }
 }
 
@@ -403,6 +487,9 @@ int ttk_gemm_hist(int on, const char *dump_path) {
   return TTK_OK;
 }
 
+static int g_gemm64_min = getenv("TTK_GEMM64_MIN") ? atoi(getenv("TTK_GEMM64_MIN")) : 64;
+static int g_gemm64_ks = getenv("TTK_GEMM64_KS") ? atoi(getenv("TTK_GEMM64_KS")) : 16;
+
 int ttk_gemm_offs(void *stream, const double *A, const double *B, double *C, const int64_t *offs,
                   int nb, int M, int N, int K, double alpha, double beta) {
   if (nb <= 0 || M <= 0 || N <= 0) return TTK_OK;
@@ -443,6 +530,13 @@ int ttk_gemm_offs(void *stream, const double *A, const double *B, double *C, con
     const int64_t tot = (int64_t)nb * M * N;
     hipExtLaunchKernelGGL(gemm_splitk_reduce_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0,
                           TTK_STREAM(stream), nullptr, e1, 0, g, nsplit, part);
+  } else if (M >= g_gemm64_min && N >= g_gemm64_min && K >= 64 &&
+             (int64_t)((M + BM - 1) / BM) * ((N + BN - 1) / BN) * nb >= 512) {
+    dim3 g64((N + BN - 1) / BN, (M + BM - 1) / BM, nb);
+    if (g_gemm64_ks == 32)
+      hipExtLaunchKernelGGL(gemm_offs64_kernel<32>, g64, dim3(256), 0, TTK_STREAM(stream), e0, e1, 0, g);
+    else
+      hipExtLaunchKernelGGL(gemm_offs64_kernel<16>, g64, dim3(256), 0, TTK_STREAM(stream), e0, e1, 0, g);
   } else {
     hipExtLaunchKernelGGL(gemm_offs_kernel, grid, dim3(256), 0, TTK_STREAM(stream), e0, e1, 0, g);
   }
