@@ -56,6 +56,50 @@ struct PtrList {
   const double *p[MAXV];
 };
 
+// Hessenberg column `it` update: apply the previous Givens rotations, form the new one, update
+// GRS.  `col` (LDS, it+2 entries) holds HH(0..it+1, it) on entry; the rotations are read into LDS
+// first and the serial chain runs on LDS (not on dependent global loads), then the column is
+// written back in parallel.  Returns (via the Ctl / st record) res, hapend, null, HH(it,it).
+__device__ void hess_update(HH &H, int it, double *col, double *cs, double *sn, bool hapend, const Ctl &cl) {
+  const int tid = threadIdx.x, nt = blockDim.x, ld = H.ld;
+  for (int j = tid; j < it; j += nt) {
+    cs[j] = H.cc[j];
+    sn[j] = H.ss[j];
+  }
+  __syncthreads();
+  if (tid == 0) {
+    for (int j = 1; j <= it; ++j) {
+      const double t0 = col[j - 1];
+      const double t1 = col[j];
+      col[j - 1] = cs[j - 1] * t0 + sn[j - 1] * t1;
+      col[j] = cs[j - 1] * t1 - sn[j - 1] * t0;
+    }
+    double res = 0.0, null_flag = 0.0;
+    if (!hapend) {
+      const double hv = col[it], hv1 = col[it + 1];
+      const double tr = sqrt(hv * hv + hv1 * hv1);
+      if (tr == 0.0) {
+        null_flag = 1.0;
+      } else {
+        H.cc[it] = hv / tr;
+        H.ss[it] = hv1 / tr;
+        H.grs[it + 1] = -(H.ss[it] * H.grs[it]);
+        H.grs[it] = H.cc[it] * H.grs[it];
+        col[it] = H.cc[it] * hv + H.ss[it] * hv1;
+        res = fabs(H.grs[it + 1]);
+      }
+    }
+    H.st[0] = res;
+    H.st[1] = hapend ? 1.0 : 0.0;
+    H.st[2] = null_flag;
+    H.st[3] = col[it];
+    ctl_record(cl, res, hapend, null_flag != 0.0, col[it]);
+  }
+  __syncthreads();
+  for (int j = tid; j <= it + 1; j += nt) H.hh[j * ld + it] = col[j];
+}
+
+
 // KSPGMRESClassicalGramSchmidtOrthogonalization (REFINE_NEVER) + new HH/HES column +
 // happy-breakdown test + KSPLGMRESUpdateHessenberg.  st[0]=res, st[1]=hapend, st[2]=null,
 // st[3]=HH(it,it) after rotation.
@@ -89,10 +133,8 @@ __global__ __launch_bounds__(1024) void arnoldi_kernel(double *V, int n, int it,
   s2 = ttk::block_sum(s2, red);
   const double tt = sqrt(s2);
   const int ld = H.ld;
-  for (int j = tid; j <= it; j += nt) {
-    H.hh[j * ld + it] = h[j];
-    H.hes[j * ld + it] = h[j];
-  }
+  __shared__ double cs[MAXV + 2], sn[MAXV + 2];
+  for (int j = tid; j <= it; j += nt) H.hes[j * ld + it] = h[j];
   double hapbnd = fabs(tt / H.grs[it]);
   if (hapbnd > haptol) hapbnd = haptol;
   const bool hapend = !(tt > hapbnd);
@@ -100,37 +142,12 @@ __global__ __launch_bounds__(1024) void arnoldi_kernel(double *V, int n, int it,
     const double inv = 1.0 / tt;
     for (int i = tid; i < n; i += nt) w[i] *= inv;
   }
-  __syncthreads();
   if (tid == 0) {
-    H.hh[(it + 1) * ld + it] = tt;
     H.hes[(it + 1) * ld + it] = tt;
-    for (int j = 1; j <= it; ++j) {
-      const double t0 = H.hh[(j - 1) * ld + it];
-      const double t1 = H.hh[j * ld + it];
-      H.hh[(j - 1) * ld + it] = H.cc[j - 1] * t0 + H.ss[j - 1] * t1;
-      H.hh[j * ld + it] = H.cc[j - 1] * t1 - H.ss[j - 1] * t0;
-    }
-    double res = 0.0, null_flag = 0.0;
-    if (!hapend) {
-      const double hv = H.hh[it * ld + it], hv1 = H.hh[(it + 1) * ld + it];
-      const double tr = sqrt(hv * hv + hv1 * hv1);
-      if (tr == 0.0) {
-        null_flag = 1.0;
-      } else {
-        H.cc[it] = hv / tr;
-        H.ss[it] = hv1 / tr;
-        H.grs[it + 1] = -(H.ss[it] * H.grs[it]);
-        H.grs[it] = H.cc[it] * H.grs[it];
-        H.hh[it * ld + it] = H.cc[it] * hv + H.ss[it] * hv1;
-        res = fabs(H.grs[it + 1]);
-      }
-    }
-    H.st[0] = res;
-    H.st[1] = hapend ? 1.0 : 0.0;
-    H.st[2] = null_flag;
-    H.st[3] = H.hh[it * ld + it];
-    ctl_record(cl, res, hapend, null_flag != 0.0, H.st[3]);
+    h[it + 1] = tt;
   }
+  __syncthreads();
+  hess_update(H, it, h, cs, sn, hapend, cl);
 }
 
 // KSPLGMRESBuildSoln: back substitution in place in GRS, temp = sum y_j basis_j, x += temp.
@@ -257,6 +274,8 @@ __global__ __launch_bounds__(1024) void arnoldi_finish_kernel(double *V, int n, 
   __syncthreads();
   const double tt = s_tt;
   const int ld = H.ld;
+  __shared__ double col[MAXV + 2], cs[MAXV + 2], sn[MAXV + 2];
+  for (int j = tid; j <= it; j += nt) col[j] = H.hh[j * ld + it];  // h_j from arnoldi_update_kernel
   double hapbnd = fabs(tt / H.grs[it]);
   if (hapbnd > haptol) hapbnd = haptol;
   const bool hapend = !(tt > hapbnd);
@@ -266,35 +285,11 @@ __global__ __launch_bounds__(1024) void arnoldi_finish_kernel(double *V, int n, 
     for (int i = tid; i < n; i += nt) w[i] *= inv;
   }
   if (tid == 0) {
-    H.hh[(it + 1) * ld + it] = tt;
     H.hes[(it + 1) * ld + it] = tt;
-    for (int j = 1; j <= it; ++j) {
-      const double t0 = H.hh[(j - 1) * ld + it];
-      const double t1 = H.hh[j * ld + it];
-      H.hh[(j - 1) * ld + it] = H.cc[j - 1] * t0 + H.ss[j - 1] * t1;
-      H.hh[j * ld + it] = H.cc[j - 1] * t1 - H.ss[j - 1] * t0;
-    }
-    double res = 0.0, null_flag = 0.0;
-    if (!hapend) {
-      const double hv = H.hh[it * ld + it], hv1 = H.hh[(it + 1) * ld + it];
-      const double tr = sqrt(hv * hv + hv1 * hv1);
-      if (tr == 0.0) {
-        null_flag = 1.0;
-      } else {
-        H.cc[it] = hv / tr;
-        H.ss[it] = hv1 / tr;
-        H.grs[it + 1] = -(H.ss[it] * H.grs[it]);
-        H.grs[it] = H.cc[it] * H.grs[it];
-        H.hh[it * ld + it] = H.cc[it] * hv + H.ss[it] * hv1;
-        res = fabs(H.grs[it + 1]);
-      }
-    }
-    H.st[0] = res;
-    H.st[1] = hapend ? 1.0 : 0.0;
-    H.st[2] = null_flag;
-    H.st[3] = H.hh[it * ld + it];
-    ctl_record(cl, res, hapend, null_flag != 0.0, H.st[3]);
+    col[it + 1] = tt;
   }
+  __syncthreads();
+  hess_update(H, it, col, cs, sn, hapend, cl);
 }
 
 // y = HH \ GRS (back substitution in GRS), once, by a single thread (it <= 100)
