@@ -624,19 +624,37 @@ __global__ __launch_bounds__(1024) void lu_rcond_kernel(const double *__restrict
         best = fabs(xs[i]);
         bi = i;
       }
-    rv[tid] = best;
-    ri[tid] = bi;
+    // first index of max |z|: wave shuffles, then wave 0 over the 16 wave winners
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      const double ov = __shfl_xor(best, o, 64);
+      const int oi = __shfl_xor(bi, o, 64);
+      if (ov > best || (ov == best && oi < bi)) {
+        best = ov;
+        bi = oi;
+      }
+    }
+    if ((tid & 63) == 0) {
+      rv[tid >> 6] = best;
+      ri[tid >> 6] = bi;
+    }
     __syncthreads();
-    for (int s = nt / 2; s > 0; s >>= 1) {
-      if (tid < s) {
-        if (rv[tid + s] > rv[tid] || (rv[tid + s] == rv[tid] && ri[tid + s] < ri[tid])) {
-          rv[tid] = rv[tid + s];
-          ri[tid] = ri[tid + s];
+    if (tid < 64) {
+      double b = tid < (nt >> 6) ? rv[tid] : -2.0;
+      int p = tid < (nt >> 6) ? ri[tid] : 0x7fffffff;
+#pragma unroll
+      for (int o = 8; o >= 1; o >>= 1) {
+        const double ob = __shfl_xor(b, o, 64);
+        const int op = __shfl_xor(p, o, 64);
+        if (ob > b || (ob == b && op < p)) {
+          b = ob;
+          p = op;
         }
       }
-      __syncthreads();
+      if (tid == 0) ri[32] = p;
     }
-    const int jn = ri[0];
+    __syncthreads();
+    const int jn = ri[32];
     __syncthreads();
     if (jn == jlast) break;
     jlast = jn;

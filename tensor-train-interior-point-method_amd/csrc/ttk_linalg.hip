@@ -2458,7 +2458,7 @@ int ttk_qr(void *stream, const double *A, int m, int n, double *Q, double *R, do
 }
 
 static int g_dense_block_min = 96;  // n at or above which Cholesky / TRSM take the blocked kernels
-static int g_lu_block_min = getenv("TTK_LU_BLOCK_MIN") ? atoi(getenv("TTK_LU_BLOCK_MIN")) : 96;  // LU / getrs
+static int g_lu_block_min = getenv("TTK_LU_BLOCK_MIN") ? atoi(getenv("TTK_LU_BLOCK_MIN")) : 32;  // LU / getrs
 
 int ttk_dense_set_block_min(int n) {
   const int old = g_dense_block_min;
