@@ -100,6 +100,15 @@ int ttk_mul_nd(void *stream, const double *src, const double *src2, double *dst,
                const int64_t *shape, const int64_t *sstride, const int64_t *s2stride,
                const int64_t *dstride, double alpha, double beta);
 int ttk_recip(void *stream, const double *src, double *dst, int64_t n);
+/* out (contiguous) = x / ||x||_2 on the device, no host round trip; bit-identical to
+ * ttk_dot_nd_sync + host sqrt/reciprocal + ttk_copy_nd (`v / np.linalg.norm(v)` of the eigen-ALS,
+ * src/tt_als.py:1002,1035).  A zero vector gives inf/nan instead of the host's ZeroDivisionError. */
+int ttk_normalize(void *stream, const double *x, double *out, int ndim, const int64_t *shape,
+                  const int64_t *xstride);
+/* ev = <v, Mv>; Mv <- Mv - ev v; res2 = ||Mv||^2, one launch and one host read (contiguous n);
+ * the residual of the step-size local solve (src/tt_als.py:1023-1030). */
+int ttk_rayleigh_tail_sync(void *stream, const double *v, double *Mv, int64_t n, double *ev_out,
+                           double *res2_out);
 /* dst = src * scales[i_axis] with the (<= 16) scales passed by value from the host: the per-block
  * column scaling / unscaling of the AMEn sweep (`src/tt_als.py:321-322,444-446`), no H2D copy. */
 int ttk_scale_axis(void *stream, const double *src, double *dst, int ndim, const int64_t *shape,

@@ -320,6 +320,49 @@ __global__ void add_diag_kernel(double *A, int n, int lda, double v) {
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) A[(int64_t)i * lda + i] += v;
 }
 
+// out = x / ||x|| without a host round trip: the sum of squares is formed exactly as dot_nd_kernel
+// forms <x, x> (same thread map and block reduction), then the host formula of dev.norm and
+// dev.scaled (sqrt(max(s, 0)), 1.0 / nrm, alpha * x), so results are bit-identical to the synced path
+__global__ void normalize_kernel(const double *__restrict__ x, ttk::NdDesc d, double *__restrict__ out) {
+  __shared__ double red[16];
+  double acc = 0.0;
+  for (int64_t i = threadIdx.x; i < d.total; i += blockDim.x) {
+    int64_t ox, oy, unused;
+    nd_offsets(d, i, ox, oy, unused);
+    acc += x[ox] * x[oy];
+  }
+  acc = ttk::block_sum(acc, red);
+  const double m = (0.0 > acc) ? 0.0 : acc;
+  const double inv = 1.0 / sqrt(m);
+  for (int64_t i = threadIdx.x; i < d.total; i += blockDim.x) {
+    int64_t ox, oy, od;
+    nd_offsets(d, i, ox, oy, od);
+    out[od] = inv * x[ox];
+  }
+}
+
+// Rayleigh tail of the step-size local solve: ev = <v, Mv>; Mv <- Mv - ev v; res2 = <Mv, Mv>
+// (contiguous vectors, one workgroup; the operations and their order of dot_nd / copy_nd)
+__global__ void rayleigh_tail_kernel(const double *__restrict__ v, double *__restrict__ Mv, int64_t n,
+                                     double *__restrict__ out2) {
+  __shared__ double red[16];
+  double acc = 0.0;
+  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) acc += v[i] * Mv[i];
+  const double ev = ttk::block_sum(acc, red);
+  const double a = -ev;
+  double acc2 = 0.0;
+  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+    const double w = a * v[i] + 1.0 * Mv[i];
+    Mv[i] = w;
+    acc2 += w * w;
+  }
+  acc2 = ttk::block_sum(acc2, red);
+  if (threadIdx.x == 0) {
+    out2[0] = ev;
+    out2[1] = acc2;
+  }
+}
+
 __global__ void dot_nd_kernel(const double *__restrict__ x, const double *__restrict__ y, ttk::NdDesc d,
                               double *out) {
   __shared__ double red[16];
@@ -648,6 +691,42 @@ int ttk_dot_nd_sync(void *stream, const double *x, const double *y, int ndim, co
   if (!h) return ttk_read_sync(stream, g_dev_scalar, result, 1);
   TTK_HIP(hipStreamSynchronize(TTK_STREAM(stream)));
   *result = h[0];
+  return TTK_OK;
+}
+
+int ttk_normalize(void *stream, const double *x, double *out, int ndim, const int64_t *shape,
+                  const int64_t *xstride) {
+  ttk::NdDesc d;
+  int64_t ost[ttk::MAXD];
+  if (ndim > ttk::MAXD || ndim < 0) {
+    ttk::set_error("ttk_normalize: ndim %d", ndim);
+    return TTK_ERR_ARG;
+  }
+  int64_t acc = 1;
+  for (int i = ndim - 1; i >= 0; --i) {
+    ost[i] = acc;
+    acc *= shape[i];
+  }
+  int st = make_nd(d, ndim, shape, xstride, xstride, ost);
+  if (st) return st;
+  if (d.total == 0) return TTK_OK;
+  hipLaunchKernelGGL(normalize_kernel, dim3(1), dim3(1024), 0, TTK_STREAM(stream), x, d, out);
+  TTK_LAUNCH_CHECK();
+  return TTK_OK;
+}
+
+int ttk_rayleigh_tail_sync(void *stream, const double *v, double *Mv, int64_t n, double *ev_out, double *res2_out) {
+  double *dev = nullptr;
+  double *h = ttk::mapped_stage(2, &dev);
+  if (!h) {
+    ttk::set_error("ttk_rayleigh_tail_sync: mapped allocation failed");
+    return TTK_ERR_HIP;
+  }
+  hipLaunchKernelGGL(rayleigh_tail_kernel, dim3(1), dim3(1024), 0, TTK_STREAM(stream), v, Mv, n, dev);
+  TTK_LAUNCH_CHECK();
+  TTK_HIP(hipStreamSynchronize(TTK_STREAM(stream)));
+  *ev_out = h[0];
+  *res2_out = h[1];
   return TTK_OK;
 }
 

@@ -177,6 +177,25 @@ def scale_axis(src, axis, scales, out=None):
     return out
 
 
+def normalized(src):
+    """src / ||src|| as a new contiguous tensor, computed on the device (no host sync)."""
+    out = empty(*src.shape)
+    nd = src.dim()
+    if nd == 0:
+        src, nd = src.reshape(1), 1
+    check(lib.ttk_normalize(_stream(), _p(src), _p(out), nd, _arr(src.shape), _arr(src.stride())), "normalize")
+    return out
+
+
+def rayleigh_tail_(v, Mv):
+    """ev = <v, Mv>; Mv -= ev v (in place); returns (ev, ||Mv||) with one host read."""
+    assert v.is_contiguous() and Mv.is_contiguous() and v.numel() == Mv.numel()
+    ev, r2 = ctypes.c_double(0.0), ctypes.c_double(0.0)
+    check(lib.ttk_rayleigh_tail_sync(_stream(), _p(v), _p(Mv), v.numel(), ctypes.byref(ev), ctypes.byref(r2)),
+          "rayleigh_tail")
+    return ev.value, float(np.sqrt(max(r2.value, 0.0)))
+
+
 def recip(src):
     src = src.contiguous()
     out = empty(*src.shape)
@@ -493,6 +512,6 @@ def syev_extreme(A, largest=False):
     return lam, buf[1:]
 
 
-__all__ = ["scale_axis", "syev_extreme", "einsum", "tensordot", "matmul", "copy_", "scaled", "clone", "mul_", "recip", "fill_", "add_diag_",
+__all__ = ["normalized", "rayleigh_tail_", "scale_axis", "syev_extreme", "einsum", "tensordot", "matmul", "copy_", "scaled", "clone", "mul_", "recip", "fill_", "add_diag_",
            "dot", "norm", "read", "svd", "qr", "rq", "cholesky_", "trsm_", "lu_", "lu_solve_", "syev", "empty",
            "zeros", "from_numpy", "to_numpy", "LinAlgError", "LinAlgWarning"]

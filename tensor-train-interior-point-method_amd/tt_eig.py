@@ -20,7 +20,9 @@ from .tt_als import compute_phi_bck_A, compute_phi_fwd_A
 TWO_SITE = "lsr,smnk,kptS,LSR->lmpLrntR"
 ONE_SITE = "lsr,smnS,LSR->lmLrnR"
 MAX_DENSE = 4096
-_DEBUG = bool(os.environ.get("TTIPM_EIG_DEBUG"))  # diagnostics: one line per local step-size solve
+_DEBUG = bool(os.environ.get("TTIPM_EIG_DEBUG"))
+# normalisation / Rayleigh residual on the device with one (or no) host read; same arithmetic
+_FUSED_TAIL = os.environ.get("TTIPM_EIG_FUSED_TAIL", "1") == "1"  # diagnostics: one line per local step-size solve
 
 
 def _sym(Mt, m):
@@ -56,12 +58,16 @@ def _rayleigh(Am, Dm, step, v):
     M = D.scaled(Am, 1.0 / step)
     D.copy_(M, Dm, 1.0, 1.0)
     Mv = D.matmul(M, v.view(-1, 1)).view(-1)
+    if _FUSED_TAIL and v.is_contiguous():
+        return D.rayleigh_tail_(v, Mv)
     ev = D.dot(v, Mv)
     D.copy_(Mv, v, -ev, 1.0)
     return ev, D.norm(Mv)
 
 
 def _normalise(v):
+    if _FUSED_TAIL:
+        return D.normalized(v)
     return D.scaled(v, 1.0 / D.norm(v))
 
 

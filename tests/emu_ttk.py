@@ -154,6 +154,25 @@ class EmuLib:
         _dv(dst, i_d.max() + 1)[i_d] = v
         return 0
 
+    def ttk_normalize(self, s, x, out, nd, shape, xs):
+        self.launches += 1
+        ix = _nd_index(nd, shape, xs)
+        if ix.size == 0:
+            return 0
+        v = _dv(x, ix.max() + 1)[ix].copy()
+        d = float(np.dot(v, v))
+        _dv(out, ix.size)[:] = (1.0 / np.sqrt(0.0 if 0.0 > d else d)) * v
+        return 0
+
+    def ttk_rayleigh_tail_sync(self, s, v, Mv, n, ev_out, r2_out):
+        self.launches += 1
+        a, b = _dv(v, n), _dv(Mv, n)
+        ev = float(np.dot(a, b))
+        b[:] = -ev * a + b
+        ev_out._obj.value = ev
+        r2_out._obj.value = float(np.dot(b, b))
+        return 0
+
     def ttk_recip(self, s, src, dst, n):
         _dv(dst, n)[:] = 1.0 / _dv(src, n)
         return 0
