@@ -119,6 +119,10 @@ int ttk_add_diag(void *stream, double *A, int n, int lda, double value);
 /* Reductions (strided up to 6-D), result copied to the host: sum(x*y), sum(x*x). */
 int ttk_dot_nd_sync(void *stream, const double *x, const double *y, int ndim, const int64_t *shape,
                     const int64_t *xstride, const int64_t *ystride, double *result);
+/* the same reduction into a device scalar, no host synchronisation (several norms of one sweep or
+ * local solve are read back together) */
+int ttk_dot_nd_dev(void *stream, const double *x, const double *y, int ndim, const int64_t *shape,
+                   const int64_t *xstride, const int64_t *ystride, double *out);
 /* batched sums of squares over `nb` contiguous slices of length n with stride `bstride`;
  * `out` is a device array of nb doubles (no sync). */
 int ttk_sumsq_batched(void *stream, const double *x, int64_t n, int nb, int64_t bstride, double *out);

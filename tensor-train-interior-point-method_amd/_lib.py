@@ -39,6 +39,7 @@ _SIGS = {
     "ttk_fill": (i32, [vp, vp, i64, f64]),
     "ttk_add_diag": (i32, [vp, vp, i32, i32, f64]),
     "ttk_dot_nd_sync": (i32, [vp, vp, vp, i32, c_i64p, c_i64p, c_i64p, c_dp]),
+    "ttk_dot_nd_dev": (i32, [vp, vp, vp, i32, c_i64p, c_i64p, c_i64p, vp]),
     "ttk_sumsq_batched": (i32, [vp, vp, i64, i32, i64, vp]),
     "ttk_read_sync": (i32, [vp, vp, c_dp, i64]),
     "ttk_svd_work": (i64, [i32, i32]),

@@ -694,6 +694,20 @@ int ttk_dot_nd_sync(void *stream, const double *x, const double *y, int ndim, co
   return TTK_OK;
 }
 
+int ttk_dot_nd_dev(void *stream, const double *x, const double *y, int ndim, const int64_t *shape,
+                   const int64_t *xstride, const int64_t *ystride, double *out) {
+  ttk::NdDesc d;
+  int st = make_nd(d, ndim, shape, xstride, ystride, nullptr);
+  if (st) return st;
+  if (d.total == 0) {
+    hipLaunchKernelGGL(fill_kernel, dim3(1), dim3(64), 0, TTK_STREAM(stream), out, (int64_t)1, 0.0);
+  } else {
+    hipLaunchKernelGGL(dot_nd_kernel, dim3(1), dim3(1024), 0, TTK_STREAM(stream), x, y, d, out);
+  }
+  TTK_LAUNCH_CHECK();
+  return TTK_OK;
+}
+
 int ttk_normalize(void *stream, const double *x, double *out, int ndim, const int64_t *shape,
                   const int64_t *xstride) {
   ttk::NdDesc d;

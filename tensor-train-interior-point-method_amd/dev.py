@@ -230,6 +230,21 @@ def norm(x):
     return float(np.sqrt(max(dot(x, x), 0.0)))
 
 
+def dot_into(x, y, out):
+    """sum(x*y) into the device scalar `out` (a 1-element view), no host synchronisation."""
+    assert tuple(x.shape) == tuple(y.shape)
+    nd = x.dim()
+    if nd == 0:
+        x, y, nd = x.reshape(1), y.reshape(1), 1
+    check(lib.ttk_dot_nd_dev(_stream(), _p(x), _p(y), nd, _arr(x.shape), _arr(x.stride()), _arr(y.stride()),
+                             _p(out)), "dot_into")
+
+
+def norm_of(d):
+    """dev.norm's host formula applied to a read-back <x, x>."""
+    return float(np.sqrt(max(float(d), 0.0)))
+
+
 def read(t):
     """Copy a (small) device tensor to a host numpy array (blocking)."""
     t = t.contiguous()
@@ -512,6 +527,6 @@ def syev_extreme(A, largest=False):
     return lam, buf[1:]
 
 
-__all__ = ["normalized", "rayleigh_tail_", "scale_axis", "syev_extreme", "einsum", "tensordot", "matmul", "copy_", "scaled", "clone", "mul_", "recip", "fill_", "add_diag_",
+__all__ = ["dot_into", "norm_of", "normalized", "rayleigh_tail_", "scale_axis", "syev_extreme", "einsum", "tensordot", "matmul", "copy_", "scaled", "clone", "mul_", "recip", "fill_", "add_diag_",
            "dot", "norm", "read", "svd", "qr", "rq", "cholesky_", "trsm_", "lu_", "lu_solve_", "syev", "empty",
            "zeros", "from_numpy", "to_numpy", "LinAlgError", "LinAlgWarning"]

@@ -263,6 +263,10 @@ def _sweep(c, backward, swp, last, dsf):
     amen = c.amen
     local_res = np.inf if swp == 0 else 0
     local_dx = np.inf if swp == 0 else 0
+    # ||sol - prev|| / ||sol|| per core: the dots stay on the device and are read once after the
+    # sweep (local_dx only feeds the stopping test after it); the host formula is applied in order
+    dx_buf = D.empty(2 * d) if (swp > 0 and not last) else None
+    dx_seq = []
     order = range(d - 1, -1, -1) if backward else range(d)
     for k in order:
         Ak = c.A[k]
@@ -277,9 +281,12 @@ def _sweep(c, backward, swp, last, dsf):
             if sol is not prev:
                 diff = D.clone(sol)
                 D.copy_(diff, prev, -1.0, 1.0)
-                local_dx = max(D.norm(diff) / D.norm(sol), local_dx)
+                j = sum(1 for t in dx_seq if t is not None)
+                D.dot_into(diff, diff, dx_buf[2 * j:2 * j + 1])
+                D.dot_into(sol, sol, dx_buf[2 * j + 1:2 * j + 2])
+                dx_seq.append(j)
             else:
-                local_dx = max(0.0, local_dx)
+                dx_seq.append(None)
             if amen:
                 zsh = (rz[k], B, N[k], rz[k + 1])
                 rz_ = D.zeros(*zsh)
@@ -437,6 +444,14 @@ def _sweep(c, backward, swp, last, dsf):
                            for ij, lt in Ak._transposes.items()})
                 c.ZAX[k + 1] = zz
                 c.Zb[k + 1] = {i: compute_phi_fwd_rhs(c.Zb[k][i], bk[i], z[k]) for i in bk}
+    if dx_seq:
+        n_used = sum(1 for j in dx_seq if j is not None)
+        vals = D.read(dx_buf[:2 * n_used]) if n_used else None
+        for j in dx_seq:
+            if j is None:
+                local_dx = max(0.0, local_dx)
+            else:
+                local_dx = max(D.norm_of(vals[2 * j]) / D.norm_of(vals[2 * j + 1]), local_dx)
     return local_res, local_dx, dsf
 
 

@@ -159,6 +159,18 @@ def _residual_norm(A_k, XAX_k, XAX_k1, x, rhs, nrhs):
     return D.norm(res) / nrhs
 
 
+def _rhs_and_residual_norms(A_k, XAX_k, XAX_k1, x, rhs):
+    """(max(||rhs||, 1e-10), ||A x - rhs|| / that) with ONE host read (both dots on the device)."""
+    buf = D.empty(2)
+    D.dot_into(rhs, rhs, buf[0:1])
+    res = D.scaled(rhs, -1.0)
+    A_k.block_local_product(XAX_k, XAX_k1, x, out=res)
+    D.dot_into(res, res, buf[1:2])
+    v = D.read(buf)
+    nrhs = max(D.norm_of(v[0]), 1e-10)
+    return nrhs, D.norm_of(v[1]) / nrhs
+
+
 def _assemble(XAX_k, A_k, XAX_k1, key, m):
     return einsum(ASSEMBLE, XAX_k[key], A_k[key], XAX_k1[key]).view(m, m)
 
@@ -185,9 +197,8 @@ def _ipm_local_solver(XAX_k, A_k, XAX_k1, Xb_k, b_k, Xb_k1, prev, size_limit, de
     r, n, R = xs[0], xs[2], xs[3]
     m = r * n * R
     rhs = _local_rhs(Xb_k, b_k, Xb_k1, xs, 3)
-    nrhs = max(D.norm(rhs), 1e-10)
     inv_I = D.recip(einsum(DIAG, XAX_k[1, 2], A_k[1, 2], XAX_k1[1, 2]))
-    res_old = _residual_norm(A_k, XAX_k, XAX_k1, prev, rhs, nrhs)
+    nrhs, res_old = _rhs_and_residual_norms(A_k, XAX_k, XAX_k1, prev, rhs)
     dense_solve = (np.sqrt(r * R) <= size_limit) and dense_solve and (res_old >= rtol)
     failed = not dense_solve
     sol = None
@@ -236,13 +247,17 @@ def _ipm_local_solver(XAX_k, A_k, XAX_k1, Xb_k, b_k, Xb_k1, prev, size_limit, de
         w = D.empty(r, n, R)
         D.mul_(w, inv_I, rhs[:, 1])
         einsum(APPLY, XAX_k[2, 2], A_k[2, 2], XAX_k1[2, 2], w, out=l1, alpha=-1.0, beta=1.0)
-        lnorm = D.norm(lrhs)
+        nb2 = D.empty(2)
+        D.dot_into(lrhs, lrhs, nb2[0:1])
         pv = D.empty(2 * m)
         D.copy_(pv.view(2, r, n, R), prev[:, :2].permute(1, 0, 2, 3))
         lvec = op.matvec(pv)
         diff = D.clone(lrhs)
         D.copy_(diff, lvec, -1.0, 1.0)
-        use_prev = D.norm(diff) < lnorm
+        D.dot_into(diff, diff, nb2[1:2])
+        nv = D.read(nb2)
+        lnorm = D.norm_of(nv[0])
+        use_prev = D.norm_of(nv[1]) < lnorm
         if use_prev:
             lrhs = diff
         it_fail = False
@@ -276,8 +291,7 @@ def _ipm_local_solver_ineq(XAX_k, A_k, XAX_k1, Xb_k, b_k, Xb_k1, prev, size_limi
     m = r * n * R
     rhs = _local_rhs(Xb_k, b_k, Xb_k1, xs, 4)
     inv_I = D.recip(einsum(DIAG, XAX_k[1, 2], A_k[1, 2], XAX_k1[1, 2]))
-    nrhs = max(D.norm(rhs), 1e-10)
-    res_old = _residual_norm(A_k, XAX_k, XAX_k1, prev, rhs, nrhs)
+    nrhs, res_old = _rhs_and_residual_norms(A_k, XAX_k, XAX_k1, prev, rhs)
     dense_solve = (np.sqrt(r * R) <= 0.95 * size_limit) and dense_solve and (res_old >= rtol)
     failed = not dense_solve
     sol = None

@@ -154,6 +154,13 @@ class EmuLib:
         _dv(dst, i_d.max() + 1)[i_d] = v
         return 0
 
+    def ttk_dot_nd_dev(self, s, x, y, nd, shape, xs, ys, out):
+        self.launches += 1
+        ix, iy = _nd_index(nd, shape, xs), _nd_index(nd, shape, ys)
+        v = 0.0 if ix.size == 0 else float(np.dot(_dv(x, ix.max() + 1)[ix], _dv(y, iy.max() + 1)[iy]))
+        _dv(out, 1)[0] = v
+        return 0
+
     def ttk_normalize(self, s, x, out, nd, shape, xs):
         self.launches += 1
         ix = _nd_index(nd, shape, xs)
