@@ -105,6 +105,10 @@ int ttk_recip(void *stream, const double *src, double *dst, int64_t n);
  * src/tt_als.py:1002,1035).  A zero vector gives inf/nan instead of the host's ZeroDivisionError. */
 int ttk_normalize(void *stream, const double *x, double *out, int ndim, const int64_t *shape,
                   const int64_t *xstride);
+/* dst = src * f(ss[i_axis]) with f = max(sqrt(ss), 1e-10) (invert = 0) or its reciprocal: the
+ * per-block scaling of the sweep from the device block sums of squares (no host read). */
+int ttk_scale_axis_ss(void *stream, const double *src, double *dst, int ndim, const int64_t *shape,
+                      const int64_t *sstride, const int64_t *dstride, int axis, const double *ss, int invert);
 /* ev = <v, Mv>; Mv <- Mv - ev v; res2 = ||Mv||^2, one launch and one host read (contiguous n);
  * the residual of the step-size local solve (src/tt_als.py:1023-1030). */
 int ttk_rayleigh_tail_sync(void *stream, const double *v, double *Mv, int64_t n, double *ev_out,

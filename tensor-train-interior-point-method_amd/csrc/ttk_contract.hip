@@ -306,6 +306,28 @@ __global__ void scale_axis_kernel(const double *__restrict__ src, double *__rest
   }
 }
 
+// the same scaling with per-block scales derived on the device from block sums of squares:
+// sc = max(sqrt(ss), 1e-10) (np.maximum(np.sqrt(ss), 1e-10)), factor sc or 1.0 / sc
+__global__ void scale_axis_ss_kernel(const double *__restrict__ src, double *__restrict__ dst, ttk::NdDesc d,
+                                     int axis, const double *__restrict__ ss, int invert) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < d.total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t lin = i, os = 0, od = 0, ca = 0;
+    for (int k = d.ndim - 1; k >= 0; --k) {
+      const int64_t e = d.shape[k];
+      const int64_t q = lin / e;
+      const int64_t r = lin - q * e;
+      lin = q;
+      os += r * d.s0[k];
+      od += r * d.s1[k];
+      if (k == axis) ca = r;
+    }
+    const double nr = sqrt(ss[ca]);
+    const double sc = nr > 1e-10 ? nr : 1e-10;
+    dst[od] = src[os] * (invert ? 1.0 / sc : sc);
+  }
+}
+
 __global__ void recip_kernel(const double *__restrict__ src, double *__restrict__ dst, int64_t n) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
     dst[i] = 1.0 / src[i];
@@ -648,6 +670,22 @@ int ttk_scale_axis(void *stream, const double *src, double *dst, int ndim, const
   for (int i = 0; i < 16; ++i) sc.v[i] = i < shape[axis] ? scales[i] : 0.0;
   hipLaunchKernelGGL(scale_axis_kernel, dim3(grid_for(d.total, 256)), dim3(256), 0, TTK_STREAM(stream), src, dst,
                      d, axis, sc);
+  TTK_LAUNCH_CHECK();
+  return TTK_OK;
+}
+
+int ttk_scale_axis_ss(void *stream, const double *src, double *dst, int ndim, const int64_t *shape,
+                      const int64_t *sstride, const int64_t *dstride, int axis, const double *ss, int invert) {
+  ttk::NdDesc d;
+  int st = make_nd(d, ndim, shape, sstride, dstride, nullptr);
+  if (st) return st;
+  if (axis < 0 || axis >= ndim) {
+    ttk::set_error("ttk_scale_axis_ss: axis %d out of range", axis);
+    return TTK_ERR_ARG;
+  }
+  if (d.total == 0) return TTK_OK;
+  hipLaunchKernelGGL(scale_axis_ss_kernel, dim3(grid_for(d.total, 256)), dim3(256), 0, TTK_STREAM(stream), src, dst,
+                     d, axis, ss, invert);
   TTK_LAUNCH_CHECK();
   return TTK_OK;
 }

@@ -177,6 +177,15 @@ def scale_axis(src, axis, scales, out=None):
     return out
 
 
+def scale_axis_ss(src, axis, ss, invert):
+    """src * max(sqrt(ss), 1e-10)[i] (or its reciprocal) along `axis`; ss = device sums of squares."""
+    out = empty(*src.shape)
+    nd = src.dim()
+    check(lib.ttk_scale_axis_ss(_stream(), _p(src), _p(out), nd, _arr(src.shape), _arr(src.stride()),
+                                _arr(out.stride()), int(axis), _p(ss), int(bool(invert))), "scale_axis_ss")
+    return out
+
+
 def normalized(src):
     """src / ||src|| as a new contiguous tensor, computed on the device (no host sync)."""
     out = empty(*src.shape)
@@ -401,9 +410,10 @@ _DUMP = {"min": int(os.environ.get("TTIPM_DUMP_SVD", "0")), "max": int(os.enviro
          "qmin": int(os.environ.get("TTIPM_DUMP_SVD_QMIN", "0")), "n": 0}
 
 
-def svd(A, defl=0.0):
+def svd(A, defl=0.0, host=True):
     """Thin SVD of a 2-D device matrix.  Returns (U, S, Vt, s_host).  `defl` > 0 lets the large-
-    matrix path deflate directions whose total Frobenius norm is <= defl (S = 0 there)."""
+    matrix path deflate directions whose total Frobenius norm is <= defl (S = 0 there).
+    host=False: no host copy of S (s_host None), so the call does not synchronise."""
     t0 = _tic() if OPSTATS is not None else 0
     A = A.contiguous()
     m, n = A.shape
@@ -416,7 +426,7 @@ def svd(A, defl=0.0):
     U, S, Vt = empty(m, k), empty(k), empty(k, n)
     work = empty(int(lib.ttk_svd_work(m, n)))
     check(lib.ttk_svd_tol(_stream(), _p(A), m, n, _p(U), _p(S), _p(Vt), _p(work), float(defl)), "svd")
-    sh = read(S)
+    sh = read(S) if host else None
     if OPSTATS is not None:
         _stat("svd", (m, n), t0, site_min=min(m, n) >= 64)
     return U, S, Vt, sh
@@ -527,6 +537,6 @@ def syev_extreme(A, largest=False):
     return lam, buf[1:]
 
 
-__all__ = ["dot_into", "norm_of", "normalized", "rayleigh_tail_", "scale_axis", "syev_extreme", "einsum", "tensordot", "matmul", "copy_", "scaled", "clone", "mul_", "recip", "fill_", "add_diag_",
+__all__ = ["scale_axis_ss", "dot_into", "norm_of", "normalized", "rayleigh_tail_", "scale_axis", "syev_extreme", "einsum", "tensordot", "matmul", "copy_", "scaled", "clone", "mul_", "recip", "fill_", "add_diag_",
            "dot", "norm", "read", "svd", "qr", "rq", "cholesky_", "trsm_", "lu_", "lu_solve_", "syev", "empty",
            "zeros", "from_numpy", "to_numpy", "LinAlgError", "LinAlgWarning"]

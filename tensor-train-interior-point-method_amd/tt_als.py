@@ -221,34 +221,35 @@ def compute_phi_fwd_rhs(P, b, x):
 
 def truncated_svd(m, k):
     """`src/tt_als.py:269-274`: returns (u[:, :k], s[:k] * v[:k])."""
-    U, S, Vt, _ = D.svd(D.contig(m))
+    U, S, Vt, _ = D.svd(D.contig(m), host=False)
     return U[:, :k], einsum("r,rj->rj", S[:k], Vt[:k])
 
 
-def _block_norms(sol):
-    """per-block norms of a (r, B, n, R) core -> host array (one kernel + one read)."""
+def _block_sumsq(sol):
+    """per-block sums of squares of a (r, B, n, R) core, left on the device (one kernel)."""
     B = sol.shape[1]
     perm = D.clone(sol.permute(1, 0, 2, 3))
     out = D.empty(B)
     n = perm[0].numel()
     D.check(D.lib.ttk_sumsq_batched(D._stream(), perm.data_ptr(), n, B, n, out.data_ptr()), "sumsq")
-    return np.sqrt(D.read(out))
+    return out
 
 
 def _scales(sol):
-    """`np.maximum([||sol[:, b]||], 1e-10)` and its reciprocal, as host arrays (`src/tt_als.py:321-322`)."""
-    sc = np.maximum(_block_norms(sol), 1e-10)
-    return sc, sc, 1.0 / sc
+    """`np.maximum([||sol[:, b]||], 1e-10)` (`src/tt_als.py:321-322`) as the device sums of squares
+    the scaling kernels turn into sc / 1/sc themselves (no host read)."""
+    ss = _block_sumsq(sol)
+    return ss, ss, ss
 
 
-def _scale_blocks(t, sc):
+def _scale_blocks(t, ss):
     """t * sc[b] along the block axis 1 of a (r, B, n, R) tensor -> new tensor."""
-    return D.scale_axis(t, 1, sc)
+    return D.scale_axis_ss(t, 1, ss, invert=False)
 
 
-def _div_blocks_bdim(t, inv, axis):
-    """t * inv[b] along the block axis `axis` (inv = 1 / scales, host)."""
-    return D.scale_axis(t, axis, inv)
+def _div_blocks_bdim(t, ss, axis):
+    """t * (1 / sc[b]) along the block axis `axis`."""
+    return D.scale_axis_ss(t, axis, ss, invert=True)
 
 
 class _Ctx:

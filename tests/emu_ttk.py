@@ -161,6 +161,18 @@ class EmuLib:
         _dv(out, 1)[0] = v
         return 0
 
+    def ttk_scale_axis_ss(self, s, src, dst, nd, shape, ss, ds, axis, sumsq, invert):
+        self.launches += 1
+        i_s, i_d = _nd_index(nd, shape, ss), _nd_index(nd, shape, ds)
+        if i_s.size == 0:
+            return 0
+        shp = [int(shape[i]) for i in range(nd)]
+        coord = np.indices(shp)[axis].reshape(-1)
+        sc = np.maximum(np.sqrt(_dv(sumsq, shp[axis]).copy()), 1e-10)
+        f = 1.0 / sc if invert else sc
+        _dv(dst, i_d.max() + 1)[i_d] = _dv(src, i_s.max() + 1)[i_s] * f[coord]
+        return 0
+
     def ttk_normalize(self, s, x, out, nd, shape, xs):
         self.launches += 1
         ix = _nd_index(nd, shape, xs)
