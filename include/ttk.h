@@ -206,7 +206,7 @@ int ttk_syev_extreme(void *stream, const double *A, int n, int which, double *ev
 
 /* Schur-reduced local KKT operator of the iterative local solve (`MatVecWrapper` /
  * `IneqMatVecWrapper`, cy_src/lgmres_cy.pyx:203-331,379-510) as a handle.  `descs`: 5 (ineq = 0)
- * or 7 block descriptors of 34 int64 words each, in ttk_einsum's format for the local apply
+ * or 7 block descriptors of 36 int64 words each, in ttk_einsum's format for the local apply
  * 'lsr,smnS,LSR,rnR->lmL' (4 operands: XAX_k, A_k, XAX_k1, x with any pointer; has_out = 0):
  * B00, B01, B21, B22, B01 (read as its transpose 'lsr,smnS,LSR,lmL->rnR') [, B31, B33].
  * inv_I: m device doubles.  *handle = 0 when a block exceeds the fused kernel's limits (the

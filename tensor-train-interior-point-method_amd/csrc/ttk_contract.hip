@@ -366,7 +366,7 @@ __global__ void normalize_kernel(const double *__restrict__ x, ttk::NdDesc d, do
 // Rayleigh tail of the step-size local solve: ev = <v, Mv>; Mv <- Mv - ev v; res2 = <Mv, Mv>
 // (contiguous vectors, one workgroup; the operations and their order of dot_nd / copy_nd)
 __global__ void rayleigh_tail_kernel(const double *__restrict__ v, double *__restrict__ Mv, int64_t n,
-                                     double *__restrict__ out2) {
+                                     double *__restrict__ out2, double beta) {
   __shared__ double red[16];
   double acc = 0.0;
   for (int64_t i = threadIdx.x; i < n; i += blockDim.x) acc += v[i] * Mv[i];
@@ -374,7 +374,8 @@ __global__ void rayleigh_tail_kernel(const double *__restrict__ v, double *__res
   const double a = -ev;
   double acc2 = 0.0;
   for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
-    const double w = a * v[i] + 1.0 * Mv[i];
+    const double vv = a * v[i];  // written as copy_nd_kernel writes it (same contraction by the compiler)
+    const double w = (beta == 0.0) ? vv : vv + beta * Mv[i];
     Mv[i] = w;
     acc2 += w * w;
   }
@@ -774,7 +775,7 @@ int ttk_rayleigh_tail_sync(void *stream, const double *v, double *Mv, int64_t n,
     ttk::set_error("ttk_rayleigh_tail_sync: mapped allocation failed");
     return TTK_ERR_HIP;
   }
-  hipLaunchKernelGGL(rayleigh_tail_kernel, dim3(1), dim3(1024), 0, TTK_STREAM(stream), v, Mv, n, dev);
+  hipLaunchKernelGGL(rayleigh_tail_kernel, dim3(1), dim3(1024), 0, TTK_STREAM(stream), v, Mv, n, dev, 1.0);
   TTK_LAUNCH_CHECK();
   TTK_HIP(hipStreamSynchronize(TTK_STREAM(stream)));
   *ev_out = h[0];

@@ -732,7 +732,7 @@ extern "C" {
 
 int ttk_schur_build(int ineq, int64_t m, const int64_t *descs, const double *inv_I, int64_t *handle) {
   *handle = 0;
-  constexpr int W = 34;  // words per block descriptor: 4 operand records (3/4/3/3-D) + has_out = 0
+  constexpr int W = 36;  // words per block descriptor: nops + 4 operand records (3/4/3/3-D) + has_out = 0
   const int nblk = ineq ? 7 : 5;
   ApplyArgs g[7];
   static const char *F = "lsr,smnS,LSR,rnR->lmL", *T = "lsr,smnS,LSR,lmL->rnR";

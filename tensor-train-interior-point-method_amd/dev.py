@@ -377,7 +377,7 @@ def _einsum_native(eq, *ops, out=None, alpha=1.0, beta=0.0, fused=False):
 
 def apply_desc(P, A, Q, xshape):
     """ttk_einsum descriptor of the local apply 'lsr,smnS,LSR,rnR->lmL' with operands P, A, Q and a
-    placeholder x of shape `xshape` (pointer patched per call by ttk_schur_apply); 34 words."""
+    placeholder x of shape `xshape` (pointer patched per call by ttk_schur_apply); 36 words."""
     d = [4 | 256]
     for o in (P, A, Q):
         d.append(o.data_ptr())

@@ -172,6 +172,94 @@ def _lgmres_case(dev, ci):
     _close(dev.read(x), xr, 1e-8)
 
 
+@pytest.mark.parametrize("ci", range(3))
+def test_schur_operator_handle_is_bit_identical(dev, ci):
+    """the native 2-launch Schur operator (ttk_schur_apply) reproduces the per-block fused applies
+    bit for bit (same operations in the same order)"""
+    from ttipm_amd import tt_ipm
+    x = dev.from_numpy(G[f"mv{ci}/x"])
+    op = _schur(dev, ci)
+    old = tt_ipm.SCHUR_OP
+    try:
+        tt_ipm.SCHUR_OP = False
+        ref = _schur(dev, ci)
+    finally:
+        tt_ipm.SCHUR_OP = old
+    assert ref.h == 0 and op.h != 0  # the golden operators are well inside the fused limits
+    assert np.array_equal(dev.read(op.matvec(x)), dev.read(ref.matvec(x)))
+
+
+@pytest.mark.parametrize("ci", range(3))
+def test_ineq_schur_operator_handle_is_bit_identical(dev, ci):
+    """the 3-block (inequality) operator through the native handle vs the per-block path"""
+    from ttipm_amd import tt_ipm
+    keys = [(0, 0), (0, 1), (2, 1), (2, 2)]
+    src = {(3, 1): (2, 1), (3, 3): (2, 2)}  # golden blocks reused as B31 / B33 (same shapes)
+    L = {k: dev.from_numpy(G[f"mv{ci}/L{k[0]}{k[1]}"]) for k in keys}
+    Am = {k: dev.from_numpy(G[f"mv{ci}/A{k[0]}{k[1]}"]) for k in keys}
+    R = {k: dev.from_numpy(G[f"mv{ci}/R{k[0]}{k[1]}"]) for k in keys}
+    for k, s_ in src.items():
+        L[k], Am[k], R[k] = L[s_], dev.scaled(Am[s_], 0.5), R[s_]
+    invI = G[f"mv{ci}/invI"]
+    x = dev.from_numpy(np.random.default_rng(ci).standard_normal(3 * invI.size))
+    op = tt_ipm.IneqMatVecWrapper(L, Am, R, dev.from_numpy(invI), invI.shape)
+    old = tt_ipm.SCHUR_OP
+    try:
+        tt_ipm.SCHUR_OP = False
+        ref = tt_ipm.IneqMatVecWrapper(L, Am, R, dev.from_numpy(invI), invI.shape)
+    finally:
+        tt_ipm.SCHUR_OP = old
+    assert ref.h == 0 and op.h != 0
+    assert np.array_equal(dev.read(op.matvec(x)), dev.read(ref.matvec(x)))
+
+
+@pytest.mark.parametrize("ci", range(3))
+def test_lgmres_chunked_syncs_are_exact(dev, ci):
+    """speculative Arnoldi chunks (one host read per chunk) give the step-by-step iterates exactly"""
+    from ttipm_amd import lgmres as LG
+    op = _schur(dev, ci)
+    b = dev.from_numpy(np.random.default_rng(10 + ci).standard_normal(G[f"mv{ci}/x"].size))
+    m = b.numel() // 2
+    restart = min(m, 100)
+    out = {}
+    for chunk in (1, 8):
+        old = LG.CHUNK
+        LG.CHUNK = chunk
+        try:
+            info = {}
+            x = LG.lgmres(op.matvec_into, b, rtol=1e-5, max_it=300, restart=restart,
+                          augment=max(restart // 10, 3), info=info)
+            out[chunk] = (dev.read(x), info["its"], info["reason"])
+        finally:
+            LG.CHUNK = old
+    assert out[1][1] == out[8][1] and out[1][2] == out[8][2]
+    assert np.array_equal(out[1][0], out[8][0])
+
+
+def test_sync_free_reductions_match_host_formulas(dev):
+    """device normalisation / Rayleigh tail / deferred dots / block scaling against the synced
+    host formulas they replace (bit-identical)"""
+    rng = np.random.default_rng(3)
+    v = dev.from_numpy(rng.standard_normal(517))
+    assert np.array_equal(dev.read(dev.normalized(v)), dev.read(dev.scaled(v, 1.0 / dev.norm(v))))
+    Mv = dev.from_numpy(rng.standard_normal(517))
+    Mv2 = dev.clone(Mv)
+    ev, rn = dev.rayleigh_tail_(v, Mv)
+    ev2 = dev.dot(v, Mv2)
+    dev.copy_(Mv2, v, -ev2, 1.0)
+    assert ev == ev2
+    assert np.array_equal(dev.read(Mv), dev.read(Mv2))
+    assert rn == dev.norm(Mv2)
+    buf = dev.empty(1)
+    dev.dot_into(v, Mv, buf)
+    assert dev.read(buf)[0] == dev.dot(v, Mv)
+    t = dev.from_numpy(rng.standard_normal((3, 4, 2, 5)))
+    ss = dev.from_numpy(np.array([4.0, 1e-30, 2.5, 9.0]))
+    sc = np.maximum(np.sqrt(dev.read(ss)), 1e-10)
+    assert np.array_equal(dev.read(dev.scale_axis_ss(t, 1, ss, invert=True)), dev.read(dev.scale_axis(t, 1, 1.0 / sc)))
+    assert np.array_equal(dev.read(dev.scale_axis_ss(t, 1, ss, invert=False)), dev.read(dev.scale_axis(t, 1, sc)))
+
+
 def test_normalise_rng_coupling(dev):
     from ttipm_amd import tt_ops as T
     np.random.seed(7)
