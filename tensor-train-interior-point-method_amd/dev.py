@@ -50,9 +50,14 @@ def _load_bind():
     paths = glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "_ttkbind*.so"))
     if not paths:
         return None
-    spec = importlib.util.spec_from_file_location("_ttkbind", paths[0])
-    mod = importlib.util.module_from_spec(spec)
-    spec.loader.exec_module(mod)
+    try:
+        spec = importlib.util.spec_from_file_location("_ttkbind", paths[0])
+        mod = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mod)
+    except Exception as e:  # same libttk calls through ctypes packing (slower host side)
+        import warnings
+        warnings.warn(f"_ttkbind not loadable ({e}); packing einsum/copy arguments in Python")
+        return None
     return mod
 
 
