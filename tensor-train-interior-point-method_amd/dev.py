@@ -55,8 +55,8 @@ def _load_bind():
         mod = importlib.util.module_from_spec(spec)
         spec.loader.exec_module(mod)
     except Exception as e:  # same libttk calls through ctypes packing (slower host side)
-        import warnings
-        warnings.warn(f"_ttkbind not loadable ({e}); packing einsum/copy arguments in Python")
+        import sys
+        print(f"ttipm_amd: _ttkbind not loadable ({e}); packing einsum/copy arguments in Python", file=sys.stderr)
         return None
     return mod
 
