@@ -132,6 +132,10 @@ int ttk_dot_nd_dev(void *stream, const double *x, const double *y, int ndim, con
 int ttk_sumsq_batched(void *stream, const double *x, int64_t n, int nb, int64_t bstride, double *out);
 /* copy `n` device doubles to the host (blocking) */
 int ttk_read_sync(void *stream, const double *src, double *host_dst, int64_t n);
+/* n doubles from pageable host memory to the device, asynchronously on the stream (staged through
+ * a ring of pinned slots; the host buffer may be reused on return).  The eigen-ALS / AMEn random
+ * draws (NumPy MT19937, `src/tt_als.py:534,580,1041-1053`) reach the device this way. */
+int ttk_upload(void *stream, const double *host, double *dev, int64_t n);
 
 /* ---------------------------------------------------------------------------------------
  * Small dense factorisations, one 256..1024-thread workgroup each (matrices staged in LDS

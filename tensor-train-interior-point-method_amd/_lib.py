@@ -43,6 +43,7 @@ _SIGS = {
     "ttk_dot_nd_dev": (i32, [vp, vp, vp, i32, c_i64p, c_i64p, c_i64p, vp]),
     "ttk_sumsq_batched": (i32, [vp, vp, i64, i32, i64, vp]),
     "ttk_read_sync": (i32, [vp, vp, c_dp, i64]),
+    "ttk_upload": (i32, [vp, vp, vp, i64]),
     "ttk_svd_work": (i64, [i32, i32]),
     "ttk_svd": (i32, [vp, vp, i32, i32, vp, vp, vp, vp]),
     "ttk_qr_work": (i64, [i32, i32]),

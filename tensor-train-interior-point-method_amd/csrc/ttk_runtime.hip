@@ -69,6 +69,18 @@ double *mapped_stage(size_t n, double **dev) {
   return g_mapped_h;
 }
 
+// host -> device uploads through a ring of pinned slots: the host copy lands in slot i, an async
+// H2D copy is queued on the stream and an event marks when the slot may be refilled
+struct UpSlot {
+  double *p = nullptr;
+  size_t n = 0;
+  hipEvent_t ev = nullptr;
+  bool pending = false;
+};
+constexpr int UP_SLOTS = 64;
+static UpSlot g_up[UP_SLOTS];
+static int g_up_next = 0;
+
 }  // namespace ttk
 
 namespace {
@@ -83,6 +95,30 @@ extern "C" {
 const char *ttk_last_error(void) { return ttk::g_err; }
 int ttk_version(void) { return 1; }
 long long ttk_launch_count(void) { return ttk::g_launches.load(); }
+
+int ttk_upload(void *stream, const double *host, double *dev, int64_t n) {
+  if (n <= 0) return TTK_OK;
+  ttk::UpSlot &sl = ttk::g_up[ttk::g_up_next];
+  ttk::g_up_next = (ttk::g_up_next + 1) % ttk::UP_SLOTS;
+  if (sl.pending) {
+    TTK_HIP(hipEventSynchronize(sl.ev));  // the slot's previous copy has left it (normally long ago)
+    sl.pending = false;
+  }
+  if (sl.n < (size_t)n) {
+    if (sl.p) (void)hipHostFree(sl.p);
+    sl.p = nullptr;
+    sl.n = 0;
+    const size_t want = (size_t)n < 4096 ? 4096 : (size_t)n;
+    TTK_HIP(hipHostMalloc(reinterpret_cast<void **>(&sl.p), want * sizeof(double), 0));
+    sl.n = want;
+  }
+  if (!sl.ev) TTK_HIP(hipEventCreateWithFlags(&sl.ev, hipEventDisableTiming));
+  std::memcpy(sl.p, host, (size_t)n * sizeof(double));
+  TTK_HIP(hipMemcpyAsync(dev, sl.p, (size_t)n * sizeof(double), hipMemcpyHostToDevice, TTK_STREAM(stream)));
+  TTK_HIP(hipEventRecord(sl.ev, TTK_STREAM(stream)));
+  sl.pending = true;
+  return TTK_OK;
+}
 
 static int g_mapped_reads = getenv("TTK_MAPPED_READS") ? atoi(getenv("TTK_MAPPED_READS")) : 1;
 

@@ -173,6 +173,10 @@ class EmuLib:
         _dv(dst, i_d.max() + 1)[i_d] = _dv(src, i_s.max() + 1)[i_s] * f[coord]
         return 0
 
+    def ttk_upload(self, s, host, dev, n):
+        _dv(dev, n)[:] = _dv(host, n)
+        return 0
+
     def ttk_normalize(self, s, x, out, nd, shape, xs):
         self.launches += 1
         ix = _nd_index(nd, shape, xs)
