@@ -553,6 +553,7 @@ int ttk_gemm_hist(int on, const char *dump_path) {
   return TTK_OK;
 }
 
+static int g_splitk_mink = getenv("TTK_SPLITK_MINK") ? atoi(getenv("TTK_SPLITK_MINK")) : 128;  // K per split
 static int g_gemm64_min = getenv("TTK_GEMM64_MIN") ? atoi(getenv("TTK_GEMM64_MIN")) : 64;
 static int g_gemm64_ks = getenv("TTK_GEMM64_KS") ? atoi(getenv("TTK_GEMM64_KS")) : 16;
 
@@ -576,8 +577,8 @@ int ttk_gemm_offs(void *stream, const double *A, const double *B, double *C, con
   // split-K when the tile grid cannot fill the chip and K is long: each split runs >= 256 of K
   const int64_t tiles = (int64_t)grid.x * grid.y * nb;
   int nsplit = 1;
-  if (g_splitk_on && tiles < 256 && K >= 512) {
-    nsplit = (int)(K / 256);
+  if (g_splitk_on && tiles < 256 && K >= 2 * g_splitk_mink) {
+    nsplit = (int)(K / g_splitk_mink);
     const int64_t cap = (512 + tiles - 1) / tiles;
     if (nsplit > cap) nsplit = (int)cap;
     if ((int64_t)nsplit * nb > 65535) nsplit = (int)(65535 / nb);
