@@ -209,7 +209,8 @@ def main():
             ach = tflops / (tms * 1e-3)
             roofline = {"bound": "mfma", "achieved": ach / 1e12, "peak": FP64_MATRIX_PEAK / 1e12,
                         "unit": "TFLOP/s", "frac": ach / FP64_MATRIX_PEAK, "traffic": _pmc_traffic(),
-                        "kernel": "gemm_offs_kernel (fp64 MFMA 16x16x4, offset-table batched GEMM)",
+                        "kernel": "contraction kernels: gemm_offs (fp64 MFMA 16x16x4 offset-table GEMM) + fused "
+                                  "local apply + Schur multi-task apply; traffic = per gemm_offs launch",
                         "flops_per_launch": tflops / max(tl, 1), "avg_launch_us": tms * 1e3 / max(tl, 1),
                         "launches_per_solve": int(tl), "kernel_ms_per_solve": tms}
 
