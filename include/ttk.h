@@ -100,6 +100,11 @@ int ttk_mul_nd(void *stream, const double *src, const double *src2, double *dst,
                const int64_t *shape, const int64_t *sstride, const int64_t *s2stride,
                const int64_t *dstride, double alpha, double beta);
 int ttk_recip(void *stream, const double *src, double *dst, int64_t n);
+/* dst = alpha * src + beta * (gamma * src2) in one launch, rounding like the two-step scaled +
+ * copy it replaces (eigen-ALS M = A / step + D and (M + M^T) / 2, src/tt_als.py:957-996). */
+int ttk_axpby_nd(void *stream, const double *src, const double *src2, double *dst, int ndim,
+                 const int64_t *shape, const int64_t *sstride, const int64_t *s2stride,
+                 const int64_t *dstride, double alpha, double beta, double gamma);
 /* out (contiguous) = x / ||x||_2 on the device, no host round trip; bit-identical to
  * ttk_dot_nd_sync + host sqrt/reciprocal + ttk_copy_nd (`v / np.linalg.norm(v)` of the eigen-ALS,
  * src/tt_als.py:1002,1035).  A zero vector gives inf/nan instead of the host's ZeroDivisionError. */

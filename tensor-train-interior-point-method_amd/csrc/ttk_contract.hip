@@ -283,6 +283,20 @@ __global__ void mul_nd_kernel(const double *__restrict__ s1, const double *__res
   }
 }
 
+// dst = alpha * src + beta * (gamma * src2), written in copy_nd_kernel's form so that it rounds like
+// the two-step dev.scaled(src2, gamma) + dev.copy_(dst, src, alpha, beta) it replaces
+__global__ void axpby_nd_kernel(const double *__restrict__ src, const double *__restrict__ src2,
+                                double *__restrict__ dst, ttk::NdDesc d, double alpha, double beta, double gamma) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < d.total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t o1, o2, od;
+    nd_offsets(d, i, o1, o2, od);
+    const double t = gamma * src2[o2];
+    const double v = alpha * src[o1];
+    dst[od] = (beta == 0.0) ? v : v + beta * t;
+  }
+}
+
 struct AxisScales {
   double v[16];
 };
@@ -653,6 +667,19 @@ int ttk_mul_nd(void *stream, const double *src, const double *src2, double *dst,
   if (d.total == 0) return TTK_OK;
   hipLaunchKernelGGL(mul_nd_kernel, dim3(grid_for(d.total, 256)), dim3(256), 0, TTK_STREAM(stream), src,
                      src2, dst, d, alpha, beta);
+  TTK_LAUNCH_CHECK();
+  return TTK_OK;
+}
+
+int ttk_axpby_nd(void *stream, const double *src, const double *src2, double *dst, int ndim, const int64_t *shape,
+                 const int64_t *sstride, const int64_t *s2stride, const int64_t *dstride, double alpha, double beta,
+                 double gamma) {
+  ttk::NdDesc d;
+  int st = make_nd(d, ndim, shape, sstride, s2stride, dstride);
+  if (st) return st;
+  if (d.total == 0) return TTK_OK;
+  hipLaunchKernelGGL(axpby_nd_kernel, dim3(grid_for(d.total, 256)), dim3(256), 0, TTK_STREAM(stream), src, src2, dst,
+                     d, alpha, beta, gamma);
   TTK_LAUNCH_CHECK();
   return TTK_OK;
 }

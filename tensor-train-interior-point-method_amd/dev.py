@@ -186,6 +186,16 @@ def scale_axis(src, axis, scales, out=None):
     return out
 
 
+def axpby(src, src2, alpha, beta, gamma, out=None):
+    """out = alpha * src + beta * (gamma * src2) (same shapes, any strides), one launch; rounds like
+    scaled(src2, gamma) followed by copy_(out, src, alpha, beta)."""
+    out = empty(*src.shape) if out is None else out
+    nd = src.dim()
+    check(lib.ttk_axpby_nd(_stream(), _p(src), _p(src2), _p(out), nd, _arr(src.shape), _arr(src.stride()),
+                           _arr(src2.stride()), _arr(out.stride()), float(alpha), float(beta), float(gamma)), "axpby")
+    return out
+
+
 def scale_axis_ss(src, axis, ss, invert):
     """src * max(sqrt(ss), 1e-10)[i] (or its reciprocal) along `axis`; ss = device sums of squares."""
     out = empty(*src.shape)
@@ -546,6 +556,6 @@ def syev_extreme(A, largest=False):
     return lam, buf[1:]
 
 
-__all__ = ["scale_axis_ss", "dot_into", "norm_of", "normalized", "rayleigh_tail_", "scale_axis", "syev_extreme", "einsum", "tensordot", "matmul", "copy_", "scaled", "clone", "mul_", "recip", "fill_", "add_diag_",
+__all__ = ["axpby", "scale_axis_ss", "dot_into", "norm_of", "normalized", "rayleigh_tail_", "scale_axis", "syev_extreme", "einsum", "tensordot", "matmul", "copy_", "scaled", "clone", "mul_", "recip", "fill_", "add_diag_",
            "dot", "norm", "read", "svd", "qr", "rq", "cholesky_", "trsm_", "lu_", "lu_solve_", "syev", "empty",
            "zeros", "from_numpy", "to_numpy", "LinAlgError", "LinAlgWarning"]

@@ -27,9 +27,20 @@ _FUSED_TAIL = os.environ.get("TTIPM_EIG_FUSED_TAIL", "1") == "1"  # diagnostics:
 
 def _sym(Mt, m):
     M = Mt.view(m, m)
+    if _FUSED_TAIL:  # (M + M^T) / 2 as clone + copy_(S, M^T, 0.5, 0.5), in one launch
+        return D.axpby(M.t(), M, 0.5, 0.5, 1.0)
     S = D.clone(M)
     D.copy_(S, M.t(), 0.5, 0.5)
     return S
+
+
+def _shifted(Am, Dm, step):
+    """M = A / step + D (scaled + copy_, one launch)."""
+    if _FUSED_TAIL:
+        return D.axpby(Dm, Am, 1.0, 1.0, 1.0 / step)
+    M = D.scaled(Am, 1.0 / step)
+    D.copy_(M, Dm, 1.0, 1.0)
+    return M
 
 
 def _min_eigpair(M):
@@ -55,8 +66,7 @@ def _gen_max_eig(Dm, Am):
 
 def _rayleigh(Am, Dm, step, v):
     """eig = v^T M v, res = ||M v - eig v|| for M = A/step + D."""
-    M = D.scaled(Am, 1.0 / step)
-    D.copy_(M, Dm, 1.0, 1.0)
+    M = _shifted(Am, Dm, step)
     Mv = D.matmul(M, v.view(-1, 1)).view(-1)
     if _FUSED_TAIL and v.is_contiguous():
         return D.rayleigh_tail_(v, Mv)
@@ -247,8 +257,7 @@ def lobpcg(A, x0, B=None, tol=1e-8, maxiter=20, largest=True, restart_control=20
 def _dense_step(prev, Am, Dm, step, eps, tag):
     """dense branch of the step-size local solves: M = A/step + D, smallest eigenpair; if negative,
     the largest lambda of -D v = lambda A v bounds the step (`src/tt_als.py:957-996,1060-1101`)."""
-    M = D.scaled(Am, 1.0 / step)
-    D.copy_(M, Dm, 1.0, 1.0)
+    M = _shifted(Am, Dm, step)
     ev, sol = _min_eigpair(M)
     step_in, branch = step, "keep"
     if tag == "two-site":

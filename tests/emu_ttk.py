@@ -161,6 +161,16 @@ class EmuLib:
         _dv(out, 1)[0] = v
         return 0
 
+    def ttk_axpby_nd(self, s, src, src2, dst, nd, shape, s1, s2, ds, alpha, beta, gamma):
+        self.launches += 1
+        i1, i2, idd = _nd_index(nd, shape, s1), _nd_index(nd, shape, s2), _nd_index(nd, shape, ds)
+        if i1.size == 0:
+            return 0
+        t = gamma * _dv(src2, i2.max() + 1)[i2]
+        v = alpha * _dv(src, i1.max() + 1)[i1]
+        _dv(dst, idd.max() + 1)[idd] = v if beta == 0.0 else v + beta * t
+        return 0
+
     def ttk_scale_axis_ss(self, s, src, dst, nd, shape, ss, ds, axis, sumsq, invert):
         self.launches += 1
         i_s, i_d = _nd_index(nd, shape, ss), _nd_index(nd, shape, ds)

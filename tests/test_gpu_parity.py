@@ -253,6 +253,13 @@ def test_sync_free_reductions_match_host_formulas(dev):
     buf = dev.empty(1)
     dev.dot_into(v, Mv, buf)
     assert dev.read(buf)[0] == dev.dot(v, Mv)
+    A, Dm = dev.from_numpy(rng.standard_normal((37, 37))), dev.from_numpy(rng.standard_normal((37, 37)))
+    M_ref = dev.scaled(A, 1.0 / 0.37)
+    dev.copy_(M_ref, Dm, 1.0, 1.0)
+    assert np.array_equal(dev.read(dev.axpby(Dm, A, 1.0, 1.0, 1.0 / 0.37)), dev.read(M_ref))
+    S_ref = dev.clone(A)
+    dev.copy_(S_ref, A.t(), 0.5, 0.5)
+    assert np.array_equal(dev.read(dev.axpby(A.t(), A, 0.5, 0.5, 1.0)), dev.read(S_ref))
     t = dev.from_numpy(rng.standard_normal((3, 4, 2, 5)))
     ss = dev.from_numpy(np.array([4.0, 1e-30, 2.5, 9.0]))
     sc = np.maximum(np.sqrt(dev.read(ss)), 1e-10)
