@@ -145,9 +145,11 @@ def main():
     import torch
     import torch.distributed as dist
     if torch.cuda.is_available():
-        torch.cuda.set_device(local)
+        # one process per GPU; more ranks than GPUs only in rehearsals (TTIPM_BENCH_BACKEND=gloo)
+        torch.cuda.set_device(local % torch.cuda.device_count())
     if world > 1:
-        dist.init_process_group("nccl" if torch.cuda.is_available() else "gloo")
+        backend = os.environ.get("TTIPM_BENCH_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
+        dist.init_process_group(backend)
     from ttipm_amd import shard
     from ttipm_amd._lib import lib
     from ttipm_amd.utils import solve as _solve
