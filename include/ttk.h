@@ -246,6 +246,11 @@ int ttk_lgmres_arnoldi_async(void *stream, double *V, int n, int it, double *hh,
                              double marker);
 /* Build the correction y = HH \ GRS (in place in GRS), temp = sum_j y_j basis_j where the
  * basis list is given as a device pointer array of `nvec` vectors; x += temp; aug_temp = temp. */
+/* k Arnoldi steps it0 .. it0+k-1 of a chunk with the native Schur operator `schur`
+ * (ttk_schur_build) as the matvec: V[it+1] = A V[it] then ttk_lgmres_arnoldi_async(slot q,
+ * marker marker0 + q) -- the host loop's chunk without a host round trip per step. */
+int ttk_lgmres_chunk(void *stream, int64_t schur, double *V, int n, int it0, int k, double *hh,
+                     int max_k, double haptol, double ttol, double divtol, double *ctl, double marker0);
 int ttk_lgmres_build(void *stream, double *hh, int max_k, int it, const double *const *basis,
                      int nvec, int n, double *x, double *aug_temp);
 /* A*aug = V (HES y) / nrm over it_total+1 basis vectors (LGMRES augmentation bookkeeping). */

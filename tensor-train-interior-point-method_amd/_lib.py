@@ -77,6 +77,7 @@ _SIGS = {
     "ttk_schur_apply": (i32, [vp, i64, vp, vp]),
     "ttk_schur_free": (i32, [i64]),
     "ttk_lgmres_arnoldi_async": (i32, [vp, vp, i32, i32, vp, i32, f64, f64, f64, vp, i32, f64]),
+    "ttk_lgmres_chunk": (i32, [vp, i64, vp, i32, i32, i32, vp, i32, f64, f64, f64, vp, f64]),
     "ttk_lgmres_build": (i32, [vp, vp, i32, i32, ctypes.POINTER(vp), i32, i32, vp, vp]),
     "ttk_lgmres_aug": (i32, [vp, vp, i32, i32, vp, i32, f64, vp, vp, vp]),
     "ttk_lgmres_set_mw_threshold": (i32, [i32]),

@@ -432,6 +432,18 @@ int ttk_lgmres_arnoldi_async(void *stream, double *V, int n, int it, double *hh,
   return arnoldi_launch(TTK_STREAM(stream), V, n, it, hh, max_k, haptol, cl, "ttk_lgmres_arnoldi_async");
 }
 
+int ttk_lgmres_chunk(void *stream, int64_t schur, double *V, int n, int it0, int k, double *hh, int max_k,
+                     double haptol, double ttol, double divtol, double *ctl, double marker0) {
+  for (int q = 0; q < k; ++q) {
+    const int it = it0 + q;
+    int rc = ttk_schur_apply(stream, schur, V + (int64_t)it * n, V + (int64_t)(it + 1) * n);
+    if (rc) return rc;
+    rc = ttk_lgmres_arnoldi_async(stream, V, n, it, hh, max_k, haptol, ttol, divtol, ctl, q, marker0 + q);
+    if (rc) return rc;
+  }
+  return TTK_OK;
+}
+
 int ttk_lgmres_build(void *stream, double *hh, int max_k, int it, const double *const *basis, int nvec, int n,
                      double *x, double *aug_temp) {
   if (nvec > MAXV || it + 1 > MAXV) {

@@ -40,8 +40,10 @@ def _grs_offset(max_k):
 
 
 def lgmres(matvec_into, b, rtol=1e-8, max_it=300, restart=30, augment=2, abstol=1e-50, dtol=1e5,
-           haptol=1e-30, info=None):
-    """Solve A x = b from x0 = 0.  `matvec_into(v, out)` writes A v into `out` (device, 1-D)."""
+           haptol=1e-30, info=None, native=0):
+    """Solve A x = b from x0 = 0.  `matvec_into(v, out)` writes A v into `out` (device, 1-D);
+    `native`: a ttk_schur_build handle of the same operator, so whole Arnoldi chunks run in one
+    native call (`ttk_lgmres_chunk`) instead of a Python loop per step."""
     n = b.numel()
     max_k = int(restart)
     aug_dim = int(augment)
@@ -117,11 +119,16 @@ def lgmres(matvec_into, b, rtol=1e-8, max_it=300, restart=30, augment=2, abstol=
                 recs = [(float(its + 1), resbuf[0], float(flags[0]), float(flags[1]), resbuf[1])]
             else:
                 ttol, divtol = state["ttol"], dtol * state["rnorm0"]
-                for q in range(kmax):
-                    _matvec_or_aug(loc_it + q)
-                    D.check(lib.ttk_lgmres_arnoldi_async(s, V.data_ptr(), n, loc_it + q, hh.data_ptr(), max_k,
-                                                         haptol, ttol, divtol, ctl.data_ptr(), q,
-                                                         float(its + q + 1)), "lgmres_arnoldi")
+                if native and loc_it + kmax <= it_arnoldi:  # whole chunk in one native call
+                    D.check(lib.ttk_lgmres_chunk(s, native, V.data_ptr(), n, loc_it, kmax, hh.data_ptr(), max_k,
+                                                 haptol, ttol, divtol, ctl.data_ptr(), float(its + 1)),
+                            "lgmres_chunk")
+                else:
+                    for q in range(kmax):
+                        _matvec_or_aug(loc_it + q)
+                        D.check(lib.ttk_lgmres_arnoldi_async(s, V.data_ptr(), n, loc_it + q, hh.data_ptr(), max_k,
+                                                             haptol, ttol, divtol, ctl.data_ptr(), q,
+                                                             float(its + q + 1)), "lgmres_arnoldi")
                 h = D.read(ctl[:1 + 5 * kmax])
                 recs = [tuple(h[1 + 5 * q:6 + 5 * q]) for q in range(kmax)]
             for q, (marker, r_, hap_, null_, diag_) in enumerate(recs):

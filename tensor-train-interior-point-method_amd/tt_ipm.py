@@ -188,7 +188,8 @@ _LOCAL_TRACE = bool(os.environ.get("TTIPM_LOCAL_TRACE"))  # diagnostics: one lin
 def _run_lgmres(op, rhs_flat, m, rtol):
     restart = min(m, 100)
     aug = max(restart // 10, 3)
-    return lgmres(op.matvec_into, rhs_flat, rtol=rtol, max_it=300, restart=restart, augment=aug)
+    return lgmres(op.matvec_into, rhs_flat, rtol=rtol, max_it=300, restart=restart, augment=aug,
+                  native=getattr(op, "h", 0))
 
 
 def _ipm_local_solver(XAX_k, A_k, XAX_k1, Xb_k, b_k, Xb_k1, prev, size_limit, dense_solve=True, rtol=1e-5):

@@ -232,8 +232,13 @@ def test_lgmres_chunked_syncs_are_exact(dev, ci):
             out[chunk] = (dev.read(x), info["its"], info["reason"])
         finally:
             LG.CHUNK = old
-    assert out[1][1] == out[8][1] and out[1][2] == out[8][2]
-    assert np.array_equal(out[1][0], out[8][0])
+    info = {}
+    x = LG.lgmres(op.matvec_into, b, rtol=1e-5, max_it=300, restart=restart, augment=max(restart // 10, 3),
+                  info=info, native=op.h)  # whole chunks in one native call
+    out["native"] = (dev.read(x), info["its"], info["reason"])
+    assert op.h != 0
+    assert out[1][1] == out[8][1] == out["native"][1] and out[1][2] == out[8][2] == out["native"][2]
+    assert np.array_equal(out[1][0], out[8][0]) and np.array_equal(out[1][0], out["native"][0])
 
 
 def test_sync_free_reductions_match_host_formulas(dev):
