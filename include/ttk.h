@@ -16,7 +16,11 @@
  *   - every function returns an int status (TTK_OK = 0); no C++ exception crosses the ABI;
  *     `ttk_last_error()` returns a thread-local message for the last failure;
  *   - functions whose name ends in `_sync` block on `stream` and return host scalars that drive
- *     host-side decisions (rank truncation, convergence tests).
+ *     host-side decisions (rank truncation, convergence tests);
+ *   - threading: one host thread and one stream per process (the reference's model, SURVEY.md
+ *     §8(b)); plan cache, split-K / LGMRES / Schur scratch, the upload ring and the mapped read
+ *     buffer are process-global and stream-ordered, so concurrent calls from several host
+ *     threads or on several streams are not supported.
  */
 #ifndef TTK_H
 #define TTK_H
