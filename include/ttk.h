@@ -104,6 +104,11 @@ int ttk_mul_nd(void *stream, const double *src, const double *src2, double *dst,
                const int64_t *shape, const int64_t *sstride, const int64_t *s2stride,
                const int64_t *dstride, double alpha, double beta);
 int ttk_recip(void *stream, const double *src, double *dst, int64_t n);
+/* tt_add core assembly (`_block_diag_tensor` / concatenation, cy_src/tt_ops_cy.pyx:228-258) in one
+ * launch from contiguous cores a (ra, mid, Ra), b (rb, mid, Rb): mode 0 block diagonal, 1 concat
+ * along the last axis (ra == rb), 2 along the first axis (Ra == Rb); out contiguous. */
+int ttk_tt_join(void *stream, const double *a, const double *b, double *out, int ra, int Ra, int rb,
+                int Rb, int64_t mid, int mode);
 /* dst = alpha * src + beta * (gamma * src2) in one launch, rounding like the two-step scaled +
  * copy it replaces (eigen-ALS M = A / step + D and (M + M^T) / 2, src/tt_als.py:957-996). */
 int ttk_axpby_nd(void *stream, const double *src, const double *src2, double *dst, int ndim,

@@ -33,6 +33,7 @@ _SIGS = {
     "ttk_copy_nd": (i32, [vp, vp, vp, i32, c_i64p, c_i64p, c_i64p, f64, f64]),
     "ttk_mul_nd": (i32, [vp, vp, vp, vp, i32, c_i64p, c_i64p, c_i64p, c_i64p, f64, f64]),
     "ttk_recip": (i32, [vp, vp, vp, i64]),
+    "ttk_tt_join": (i32, [vp, vp, vp, vp, i32, i32, i32, i32, i64, i32]),
     "ttk_axpby_nd": (i32, [vp, vp, vp, vp, i32, c_i64p, c_i64p, c_i64p, c_i64p, f64, f64, f64]),
     "ttk_scale_axis_ss": (i32, [vp, vp, vp, i32, c_i64p, c_i64p, c_i64p, i32, vp, i32]),
     "ttk_normalize": (i32, [vp, vp, vp, i32, c_i64p, c_i64p]),

@@ -297,6 +297,33 @@ __global__ void axpby_nd_kernel(const double *__restrict__ src, const double *__
   }
 }
 
+// TT-core assembly of the rank-additive sum (tt_add, cy_src/tt_ops_cy.pyx:228-258) in one launch:
+// out (ro, mid, Ro) from contiguous a (ra, mid, Ra) and b (rb, mid, Rb).
+//   mode 0: block diagonal (ro = ra + rb, Ro = Ra + Rb, zeros elsewhere)
+//   mode 1: concatenation along the last axis (ro = ra = rb, Ro = Ra + Rb)
+//   mode 2: concatenation along the first axis (ro = ra + rb, Ro = Ra = Rb)
+__global__ void tt_join_kernel(const double *__restrict__ a, const double *__restrict__ b, double *__restrict__ out,
+                               int ra, int Ra, int rb, int Rb, int64_t mid, int mode) {
+  const int ro = mode == 1 ? ra : ra + rb, Ro = mode == 2 ? Ra : Ra + Rb;
+  const int64_t total = (int64_t)ro * mid * Ro;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int j = (int)(e % Ro);
+    const int64_t t = e / Ro;
+    const int64_t m = t % mid;
+    const int i = (int)(t / mid);
+    double v = 0.0;
+    if (mode == 0) {
+      if (i < ra && j < Ra) v = a[((int64_t)i * mid + m) * Ra + j];
+      else if (i >= ra && j >= Ra) v = b[((int64_t)(i - ra) * mid + m) * Rb + (j - Ra)];
+    } else if (mode == 1) {
+      v = j < Ra ? a[((int64_t)i * mid + m) * Ra + j] : b[((int64_t)i * mid + m) * Rb + (j - Ra)];
+    } else {
+      v = i < ra ? a[((int64_t)i * mid + m) * Ra + j] : b[((int64_t)(i - ra) * mid + m) * Rb + j];
+    }
+    out[e] = v;
+  }
+}
+
 struct AxisScales {
   double v[16];
 };
@@ -680,6 +707,20 @@ int ttk_axpby_nd(void *stream, const double *src, const double *src2, double *ds
   if (d.total == 0) return TTK_OK;
   hipLaunchKernelGGL(axpby_nd_kernel, dim3(grid_for(d.total, 256)), dim3(256), 0, TTK_STREAM(stream), src, src2, dst,
                      d, alpha, beta, gamma);
+  TTK_LAUNCH_CHECK();
+  return TTK_OK;
+}
+
+int ttk_tt_join(void *stream, const double *a, const double *b, double *out, int ra, int Ra, int rb, int Rb,
+                int64_t mid, int mode) {
+  if (mode < 0 || mode > 2 || (mode == 1 && ra != rb) || (mode == 2 && Ra != Rb)) {
+    ttk::set_error("ttk_tt_join: bad mode %d / shapes", mode);
+    return TTK_ERR_ARG;
+  }
+  const int64_t total = (int64_t)(mode == 1 ? ra : ra + rb) * mid * (mode == 2 ? Ra : Ra + Rb);
+  if (total == 0) return TTK_OK;
+  hipLaunchKernelGGL(tt_join_kernel, dim3(grid_for(total, 256)), dim3(256), 0, TTK_STREAM(stream), a, b, out, ra, Ra,
+                     rb, Rb, mid, mode);
   TTK_LAUNCH_CHECK();
   return TTK_OK;
 }

@@ -89,8 +89,28 @@ def tt_scale(alpha, tt):
     return out
 
 
+DEV_JOIN = os.environ.get("TTIPM_DEV_JOIN", "1") == "1"
+
+
+def _join(a, b, mode):
+    """one-launch assembly (ttk_tt_join) for contiguous cores; None if not applicable."""
+    if DEV_JOIN and a.is_contiguous() and b.is_contiguous() and a.dim() >= 2 and a.shape[1:-1] == b.shape[1:-1]:
+        ra, Ra, rb, Rb = a.shape[0], a.shape[-1], b.shape[0], b.shape[-1]
+        if (mode == 1 and ra != rb) or (mode == 2 and Ra != Rb):
+            return None
+        mid = int(np.prod(a.shape[1:-1])) if a.dim() > 2 else 1
+        out = D.empty(ra if mode == 1 else ra + rb, *a.shape[1:-1], Ra if mode == 2 else Ra + Rb)
+        D.check(D.lib.ttk_tt_join(D._stream(), a.data_ptr(), b.data_ptr(), out.data_ptr(), ra, Ra, rb, Rb, mid,
+                                  mode), "tt_join")
+        return out
+    return None
+
+
 def _block_diag(a, b):
     """`cy_src/tt_ops_cy.pyx:228-241`"""
+    out = _join(a, b, 0)
+    if out is not None:
+        return out
     out = D.zeros(a.shape[0] + b.shape[0], *a.shape[1:-1], a.shape[-1] + b.shape[-1])
     D.copy_(out[:a.shape[0], ..., :a.shape[-1]], a)
     D.copy_(out[a.shape[0]:, ..., a.shape[-1]:], b)
@@ -98,6 +118,9 @@ def _block_diag(a, b):
 
 
 def _cat(a, b, axis):
+    out = _join(a, b, 2 if axis == 0 else 1)
+    if out is not None:
+        return out
     shp = list(a.shape)
     shp[axis] += b.shape[axis]
     out = D.empty(*shp)

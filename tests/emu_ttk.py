@@ -161,6 +161,21 @@ class EmuLib:
         _dv(out, 1)[0] = v
         return 0
 
+    def ttk_tt_join(self, s, a, b, out, ra, Ra, rb, Rb, mid, mode):
+        self.launches += 1
+        A = _dv(a, ra * mid * Ra).reshape(ra, mid, Ra)
+        B = _dv(b, rb * mid * Rb).reshape(rb, mid, Rb)
+        if mode == 0:
+            o = np.zeros((ra + rb, mid, Ra + Rb))
+            o[:ra, :, :Ra] = A
+            o[ra:, :, Ra:] = B
+        elif mode == 1:
+            o = np.concatenate([A, B], axis=2)
+        else:
+            o = np.concatenate([A, B], axis=0)
+        _dv(out, o.size)[:] = o.reshape(-1)
+        return 0
+
     def ttk_axpby_nd(self, s, src, src2, dst, nd, shape, s1, s2, ds, alpha, beta, gamma):
         self.launches += 1
         i1, i2, idd = _nd_index(nd, shape, s1), _nd_index(nd, shape, s2), _nd_index(nd, shape, ds)
