@@ -114,6 +114,7 @@ RUNS = [
     ("maxcut", "maxcut_10", 41, 1, True),
     ("corr_clust", "corr_clust_9", 764, 1, True),
     ("corr_clust", "corr_clust_9", 764, 1, False),
+    ("maxcut", "maxcut_12", 80, 2, True),  # made with OPENBLAS_NUM_THREADS=8 (~22 min)
 ]
 
 
