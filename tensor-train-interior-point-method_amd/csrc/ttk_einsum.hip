@@ -141,6 +141,7 @@ bool build_plan(const std::string &eq, int nops, const int *ndims, const int64_t
     return false;
   }
   int64_t ext[128];
+  bool seen[128] = {};
   for (int i = 0; i < 128; ++i) ext[i] = 1;
   std::vector<Operand> live;
   {
@@ -156,6 +157,12 @@ bool build_plan(const std::string &eq, int nops, const int *ndims, const int64_t
       std::memset(op.st, 0, sizeof(op.st));
       for (int d = 0; d < ndims[i]; ++d) {  // a repeated index (diagonal) adds its strides
         const unsigned char c = (unsigned char)ins[i][d];
+        if (seen[c] && ext[c] != shapes[o + d]) {  // operands disagree on a shared index
+          ttk::set_error("einsum: index '%c' has extents %lld and %lld in %s", (char)c, (long long)ext[c],
+                         (long long)shapes[o + d], eq.c_str());
+          return false;
+        }
+        seen[c] = true;
         ext[c] = shapes[o + d];
         op.st[c] += strides[o + d];
       }

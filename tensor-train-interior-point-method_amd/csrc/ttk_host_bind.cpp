@@ -81,6 +81,8 @@ at::Tensor einsum(const std::string &eq, const std::vector<at::Tensor> &ops, c10
   for (const auto &o : ops) {
     const int nd = (int)o.dim();
     TORCH_CHECK(nd <= 16, "einsum: operand rank ", nd);
+    TORCH_CHECK(o.scalar_type() == at::kDouble && o.device() == ops[0].device(),
+                "einsum: operands must be float64 on one device (", eq, ")");
     desc[pos++] = reinterpret_cast<int64_t>(o.data_ptr());
     desc[pos++] = nd;
     const auto sz = o.sizes();
@@ -92,6 +94,12 @@ at::Tensor einsum(const std::string &eq, const std::vector<at::Tensor> &ops, c10
   if (out.has_value()) {
     res = *out;
     const int nd = (int)res.dim();
+    TORCH_CHECK(res.scalar_type() == at::kDouble && res.device() == ops[0].device(), "einsum: out dtype/device");
+    const OutMap &m = out_map(eq);
+    TORCH_CHECK((size_t)nd == m.src.size(), "einsum: out rank ", nd, " for ", eq);
+    for (int i = 0; i < nd; ++i)
+      TORCH_CHECK(res.size(i) == ops[m.src[i].first].size(m.src[i].second), "einsum: out shape ", res.sizes(),
+                  " does not match ", eq);
     desc[pos++] = 1;
     desc[pos++] = nd;
     const auto st = res.strides();
@@ -131,6 +139,8 @@ at::Tensor copy_(at::Tensor dst, const at::Tensor &src, double alpha, double bet
 at::Tensor mul_(at::Tensor dst, const at::Tensor &a, const at::Tensor &b, double alpha, double beta) {
   const int nd = (int)dst.dim();
   TORCH_CHECK(nd >= 1 && nd <= 16 && a.dim() == nd && b.dim() == nd, "mul_: rank mismatch");
+  TORCH_CHECK(a.sizes() == dst.sizes() && b.sizes() == dst.sizes(), "mul_: shape mismatch ", a.sizes(), " ",
+              b.sizes(), " -> ", dst.sizes());
   int64_t shp[16], as[16], bs[16], ds[16];
   for (int i = 0; i < nd; ++i) {
     shp[i] = dst.size(i);

@@ -205,7 +205,6 @@ def _ipm_local_solver(XAX_k, A_k, XAX_k1, Xb_k, b_k, Xb_k1, prev, size_limit, de
     sol = None
     if dense_solve:
         try:
-            rp = rhs[:, 0].reshape(m, 1) if rhs[:, 0].is_contiguous() else D.clone(rhs[:, 0]).view(m, 1)
             rd = D.clone(rhs[:, 1]).view(m, 1)
             rc = D.clone(rhs[:, 2]).view(m, 1)
             rp = D.clone(rhs[:, 0]).view(m, 1)

@@ -49,8 +49,17 @@ PROBLEM_MOD = {"maxcut": "psd_system.maxcut.maxcut", "corr_clust": "psd_system.c
                "graphm": "psd_system.graphm.graphm", "max_stable_set": "psd_system.max_stable_set.max_stable_set"}
 
 
-def run_reference(problem, cfg_name, seed, rank, fixed_ineq=True):
-    """Mirror of `src/utils.py:245-321` (run_and_record) with a per-Newton-system trace hook."""
+class _Bounded(Exception):
+    """Raised by the trace hook once `max_assemblies` Newton systems have been assembled."""
+
+
+def run_reference(problem, cfg_name, seed, rank, fixed_ineq=True, max_assemblies=0):
+    """Mirror of `src/utils.py:245-321` (run_and_record) with a per-Newton-system trace hook.
+
+    `max_assemblies > 0` gives a BOUNDED trace (configs whose full reference run does not fit the
+    build container's budget): the run stops right after that many Newton-system assemblies and
+    records, besides the trace, every AMEn KKT solve (`tt_restarted_block_amen`: residual, solution
+    ranks) and every step-size pair (`_tt_get_step_sizes`) made before the stop."""
     import importlib
     import warnings
     rops, rals, ripm = _import_reference(fixed_ineq)
@@ -69,7 +78,34 @@ def run_reference(problem, cfg_name, seed, rank, fixed_ineq=True):
                       "ranksY": rops.tt_ranks(Y), "is_last_iter": bool(st.is_last_iter)})
         return out
 
-    ripm.tt_infeasible_newton_system = hooked
+    amen, steps = [], []
+    orig_amen, orig_steps = ripm.tt_restarted_block_amen, ripm._tt_get_step_sizes
+
+    def hooked_amen(*a, **k):
+        t0 = time.time()
+        sol, res = orig_amen(*a, **k)
+        amen.append({"res": float(res), "ranks": [int(c.shape[-1]) for c in sol[:-1]],
+                     "block_core": [int(i) for i, c in enumerate(sol) if c.ndim == 4][:1],
+                     "seconds": time.time() - t0})
+        return sol, res
+
+    def hooked_steps(*a, **k):
+        xs, zs = orig_steps(*a, **k)
+        steps.append([float(xs), float(zs)])
+        return xs, zs
+
+    def bounded(*a, **k):
+        out = hooked(*a, **k)
+        if max_assemblies and len(trace) >= max_assemblies:
+            raise _Bounded
+        return out
+
+    ripm.tt_infeasible_newton_system = bounded
+    ripm.tt_restarted_block_amen = hooked_amen
+    ripm._tt_get_step_sizes = hooked_steps
+    if max_assemblies:
+        return _run_bounded(ripm, rops, mod, config, problem, cfg_name, seed, rank, fixed_ineq, max_assemblies,
+                            trace, amen, steps)
     with warnings.catch_warnings():
         warnings.simplefilter("error")
         np.random.seed(seed)
@@ -101,11 +137,43 @@ def run_reference(problem, cfg_name, seed, rank, fixed_ineq=True):
             dr = rops.tt_rank_reduce(rops.tt_sub(dr, rops.tt_reshape(Tt, (4,))), eps=1e-12)
         dfeas = rops.tt_inner_prod(dr, dr)
     ripm.tt_infeasible_newton_system = orig
+    ripm.tt_restarted_block_amen, ripm._tt_get_step_sizes = orig_amen, orig_steps
     return {"problem": problem, "config": cfg_name, "seed": seed, "rank": rank, "fixed_ineq": fixed_ineq,
             "num_iters": int(info["num_iters"]), "runtime": t3 - t2,
             "sec_per_iter": (t3 - t2) / max(1, int(info["num_iters"])), "gap": float(gap), "feas": float(feas),
             "dual_feas": float(dfeas), "ranksX": info["ranksX"], "ranksY": info["ranksY"],
             "ranksZ": info["ranksZ"], "trace": trace, "blas_threads": os.environ.get("OPENBLAS_NUM_THREADS")}
+
+
+def _run_bounded(ripm, rops, mod, config, problem, cfg_name, seed, rank, fixed_ineq, n, trace, amen, steps):
+    import warnings
+    t2 = time.time()
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")
+        np.random.seed(seed)
+        prob = mod.create_problem(config["dim"], rank)
+        if len(prob) == 5:
+            C, L, b, mask, lag = prob
+        else:
+            C, L, b, lag_y = prob
+            mask = None
+            lag = {"y": lag_y}
+        lag = {k: rops.tt_reshape(v, (4, 4)) for k, v in lag.items()}
+        C = rops.tt_reshape(C, (4,))
+        b = rops.tt_reshape(b, (4,))
+        try:
+            ripm.tt_ipm(lag, C, L, b, ineq_mask=mask, max_iter=config["max_iter"], verbose=False,
+                        gap_tol=float(config["gap_tol"]), op_tol=float(config["op_tol"]),
+                        warm_up=config["warm_up"], abs_tol=float(config["abs_tol"]), aho_direction=False,
+                        mals_restarts=config["mals_restarts"], max_refinement=config["max_refinement"],
+                        lambdaStar=float(config.get("lambdaStar", 1)),
+                        lambdaStarIneq=float(config.get("lambdaStarIneq", 1)))
+            stopped = False
+        except _Bounded:
+            stopped = True
+    return {"problem": problem, "config": cfg_name, "seed": seed, "rank": rank, "fixed_ineq": fixed_ineq,
+            "bounded": n, "stopped": stopped, "seconds": time.time() - t2, "trace": trace, "amen": amen,
+            "steps": steps, "blas_threads": os.environ.get("OPENBLAS_NUM_THREADS")}
 
 
 RUNS = [
@@ -138,8 +206,9 @@ def make_runs(only=None):
 
 if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "one":
-        _, _, prob, cfg, seed, rank, fixed, tmp = sys.argv
-        json.dump(run_reference(prob, cfg, int(seed), int(rank), bool(int(fixed))), open(tmp, "w"))
+        _, _, prob, cfg, seed, rank, fixed, tmp = sys.argv[:8]
+        nmax = int(sys.argv[8]) if len(sys.argv) > 8 else 0
+        json.dump(run_reference(prob, cfg, int(seed), int(rank), bool(int(fixed)), nmax), open(tmp, "w"))
         sys.exit(0)
     what = sys.argv[1] if len(sys.argv) > 1 else "all"
     rest = sys.argv[2:]

@@ -1,0 +1,44 @@
+#!/bin/bash
+# One parametrised GPU job (run through gpurun from the repo root):
+#   gpurun --timeout 900 -- 'bash tools/gpu_run.sh TAG STEP [STEP ...]'
+# STEP is one of
+#   tests           pytest -m gpu (one process, per-test timeout)
+#   smoke           __graft_entry__.smoke()
+#   bench[:ARGS]    python bench.py ARGS (default --steps 5 --warmup 1), JSON line -> gpurun_out/TAG_bench.json
+#   stats[:ARGS]    rocprofv3 --kernel-trace --stats over bench.py ARGS -> gpurun_out/TAG_stats/
+#   pmc:CNTRS[:ARGS] one rocprofv3 --pmc pass (counters comma-separated) over bench.py ARGS
+#   py:SCRIPT[:ARGS] python SCRIPT ARGS
+# Steps run in order; the job stops at the first failing step.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-.}"
+export TMPDIR=/tmp
+tag=$1; shift
+mkdir -p gpurun_out
+for step in "$@"; do
+  kind=${step%%:*}; rest=${step#*:}; [ "$rest" = "$step" ] && rest=""
+  echo "== $tag $step $(date +%T)"
+  case $kind in
+    tests) timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+             > gpurun_out/${tag}_tests.log 2>&1 || { tail -30 gpurun_out/${tag}_tests.log; exit 1; }
+           tail -3 gpurun_out/${tag}_tests.log ;;
+    smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${tag}_smoke.log 2>&1 \
+             || { tail -20 gpurun_out/${tag}_smoke.log; exit 1; }
+           tail -2 gpurun_out/${tag}_smoke.log ;;
+    bench) args=${rest:-"--steps 5 --warmup 1"}
+           timeout -k 10 900 python bench.py $args > gpurun_out/${tag}_bench.json 2> gpurun_out/${tag}_bench.err \
+             || { tail -20 gpurun_out/${tag}_bench.err; exit 1; }
+           cut -c1-600 gpurun_out/${tag}_bench.json ;;
+    stats) args=${rest:-"--steps 5 --warmup 1 --no-cpu-baseline"}
+           timeout -k 10 900 rocprofv3 --kernel-trace --stats -d gpurun_out/${tag}_stats -o run -- \
+             python3 bench.py $args > gpurun_out/${tag}_stats.log 2>&1 || { tail -20 gpurun_out/${tag}_stats.log; exit 1; } ;;
+    pmc)   cn=${rest%%:*}; args=${rest#*:}; [ "$args" = "$rest" ] && args="--steps 1 --warmup 0 --no-cpu-baseline --no-roofline"
+           timeout -s KILL 300 rocprofv3 --pmc ${cn//,/ } -d gpurun_out/${tag}_pmc_${cn%%,*} -o run -- \
+             python3 bench.py $args > gpurun_out/${tag}_pmc_${cn%%,*}.log 2>&1 || { tail -20 gpurun_out/${tag}_pmc_${cn%%,*}.log; exit 1; } ;;
+    py)    script=${rest%%:*}; args=${rest#*:}; [ "$args" = "$rest" ] && args=""
+           timeout -k 10 900 python -u $script $args > gpurun_out/${tag}_$(basename $script .py).log 2>&1 \
+             || { tail -30 gpurun_out/${tag}_$(basename $script .py).log; exit 1; }
+           tail -15 gpurun_out/${tag}_$(basename $script .py).log ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo "== done $(date +%T)"
