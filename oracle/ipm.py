@@ -83,6 +83,11 @@ class SchurMatVec:
 
     def __init__(self, L, A, R, inv_I, shape):
         self.shape = shape
+        if T.ALGO is not None:  # one application = the chained local applies
+            sh = tuple(shape)
+            self.mv_flops = sum(T._path_and_flops(eq, (L[k].shape, A[k].shape, R[k].shape, sh))[1]
+                                for eq, k in [("lsr,smnS,LSR,rnR->lmL", k) for k in self.keys]
+                                + [("lsr,smnS,LSR,lmL->rnR", (0, 1))])
         self.ops = {k: _chain_operands(L[k], A[k], R[k]) for k in self.keys}
         self.ops_01T = _chain_operands_t(L[0, 1], A[0, 1], R[0, 1])
         r, n, RR = shape
@@ -97,7 +102,13 @@ class SchurMatVec:
         tmp = _chain(self.ops_01T, y, r, n, R)
         return tmp.reshape(R, n, r).transpose(2, 1, 0).reshape(r * n, R) * self.inv_I
 
+    def _count(self):
+        if T.ALGO is not None:
+            T.ALGO["flops"] += self.mv_flops
+            T.ALGO["calls"] += 1
+
     def matvec(self, v):
+        self._count()
         r, n, R = self.shape
         y, x = self._parts(v, 2)
         res0 = _chain(self.ops[0, 0], y, r, n, R)
@@ -115,6 +126,7 @@ class IneqSchurMatVec(SchurMatVec):
     def matvec(self, v):
         if INEQ_MATVEC_BUG:
             raise IneqMatvecBug("reference bug: IneqMatVecWrapper.matvec returns a memoryview")
+        self._count()
         r, n, R = self.shape
         y, x, t = self._parts(v, 3)
         res0 = _chain(self.ops[0, 0], y, r, n, R)

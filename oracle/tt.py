@@ -19,13 +19,27 @@ import scipy.linalg as sla
 
 
 @lru_cache(maxsize=4096)
-def _path(eq, shapes):
+def _path_and_flops(eq, shapes):
+    import re
     ops = [np.empty(s) for s in shapes]
-    return np.einsum_path(eq, *ops, optimize="greedy")[0]
+    path, txt = np.einsum_path(eq, *ops, optimize="greedy")
+    return path, float(re.search(r"Optimized FLOP count:\s*([0-9.eE+-]+)", txt).group(1))
+
+
+def _path(eq, shapes):
+    return _path_and_flops(eq, shapes)[0]
+
+
+# algorithmic contraction FLOP counter: einsum_path greedy convention per call
+ALGO = None
 
 
 def einsum(eq, *ops):
-    return np.einsum(eq, *ops, optimize=_path(eq, tuple(o.shape for o in ops)))
+    path, flops = _path_and_flops(eq, tuple(o.shape for o in ops))
+    if ALGO is not None:
+        ALGO["flops"] += flops
+        ALGO["calls"] += 1
+    return np.einsum(eq, *ops, optimize=path)
 
 
 # --------------------------------------------------------------------------------------------

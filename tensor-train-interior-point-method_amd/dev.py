@@ -354,10 +354,37 @@ def _einsum_checked(eq, ops, out, alpha, beta):
 _FUSED_ALL = os.environ.get("TTIPM_FUSED_ALL") == "1"  # experiment switch: every local apply fused
 
 
+# Algorithmic contraction FLOPs: when ALGO is a dict, every einsum call adds the
+# FLOP count NumPy's `einsum_path(..., optimize="greedy")` reports for its equation and shapes --
+# the convention the oracle's counter uses at the reference's call sites -- whatever plan (fused
+# launch, pairwise MFMA GEMMs) the device executes.  Operator applications made natively (Schur
+# handle, LGMRES chunks) are added by their callers with `count_algo`.
+ALGO = None
+_ALGO_CACHE = {}
+
+
+def algo_flops(eq, shapes):
+    f = _ALGO_CACHE.get((eq, shapes))
+    if f is None:
+        import re
+        txt = np.einsum_path(eq, *[np.empty(sh) for sh in shapes], optimize="greedy")[1]
+        f = float(re.search(r"Optimized FLOP count:\s*([0-9.eE+-]+)", txt).group(1))
+        _ALGO_CACHE[(eq, shapes)] = f
+    return f
+
+
+def count_algo(flops, calls=1):
+    if ALGO is not None:
+        ALGO["flops"] += flops
+        ALGO["calls"] += calls
+
+
 def einsum(eq, *ops, out=None, alpha=1.0, beta=0.0, fused=False):
     """`fused=True` lets the local-operator equations run as one fused launch (see ttk_einsum);
     call sites whose results feed noise-level decisions keep the pairwise plan.  `fused="env"`:
     a relabelled environment update (fused under a smaller FLOP limit)."""
+    if ALGO is not None:
+        count_algo(algo_flops(eq, tuple(tuple(o.shape) for o in ops)))
     fused = fused or _FUSED_ALL
     if _CHECK_FUSED and fused and eq in _FUSED_EQS:
         return _einsum_checked(eq, ops, out, alpha, beta)

@@ -63,6 +63,8 @@ def lgmres(matvec_into, b, rtol=1e-8, max_it=300, restart=30, augment=2, abstol=
     state = {}
     guess_zero = True
     res = 0.0
+    nmv_native = 0
+    nmv = 0  # operator applications the algorithm consumed (speculative chunk steps past a stop excluded)
     s = D._stream()
     resbuf = (ctypes.c_double * 2)()
     flags = (ctypes.c_int * 2)()
@@ -97,6 +99,7 @@ def lgmres(matvec_into, b, rtol=1e-8, max_it=300, restart=30, augment=2, abstol=
             D.copy_(V[0], b)
         else:
             matvec_into(x, V[0])
+            nmv += 1
             D.copy_(V[0], b, 1.0, -1.0)  # r = b - A x
         it_arnoldi = max_k - aug_dim
         it_total = it_arnoldi + aug_ct
@@ -112,6 +115,7 @@ def lgmres(matvec_into, b, rtol=1e-8, max_it=300, restart=30, augment=2, abstol=
         last_diag = 1.0
         while (not reason) and loc_it < it_total and its < max_it:
             kmax = min(CHUNK, it_total - loc_it, max_it - its)
+            in_native = False
             if kmax <= 1:
                 _matvec_or_aug(loc_it)
                 D.check(lib.ttk_lgmres_arnoldi_sync(s, V.data_ptr(), n, loc_it, hh.data_ptr(), max_k, haptol,
@@ -119,7 +123,8 @@ def lgmres(matvec_into, b, rtol=1e-8, max_it=300, restart=30, augment=2, abstol=
                 recs = [(float(its + 1), resbuf[0], float(flags[0]), float(flags[1]), resbuf[1])]
             else:
                 ttol, divtol = state["ttol"], dtol * state["rnorm0"]
-                if native and loc_it + kmax <= it_arnoldi:  # whole chunk in one native call
+                in_native = bool(native and loc_it + kmax <= it_arnoldi)
+                if in_native:  # whole chunk in one native call
                     D.check(lib.ttk_lgmres_chunk(s, native, V.data_ptr(), n, loc_it, kmax, hh.data_ptr(), max_k,
                                                  haptol, ttol, divtol, ctl.data_ptr(), float(its + 1)),
                             "lgmres_chunk")
@@ -141,6 +146,8 @@ def lgmres(matvec_into, b, rtol=1e-8, max_it=300, restart=30, augment=2, abstol=
                     break
                 res = r_
                 last_diag = diag_
+                nmv += loc_it < it_arnoldi
+                nmv_native += kmax > 1 and in_native
                 loc_it += 1
                 its += 1
                 reason = converged(its, res)
@@ -199,5 +206,5 @@ def lgmres(matvec_into, b, rtol=1e-8, max_it=300, restart=30, augment=2, abstol=
             break
         guess_zero = False
     if info is not None:
-        info.update(reason=reason, its=its, res=res)
+        info.update(reason=reason, its=its, res=res, matvecs=nmv, native_matvecs=nmv_native)
     return x

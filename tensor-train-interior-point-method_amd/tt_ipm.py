@@ -95,8 +95,19 @@ class MatVecWrapper:
         D.mul_(self.tmp, self.tmp, self.inv_I)
         return self.tmp
 
+    def mv_flops(self):
+        """Algorithmic FLOPs of one operator application (SURVEY.md §8(d) convention): the local
+        applies it chains (`cy_src/lgmres_cy.pyx:297-327`: 5 blocks; 7 for the 3-block operator)."""
+        if getattr(self, "_mvf", None) is None:
+            sh = tuple(self.shape)
+            blocks = [(APPLY, k) for k in self.keys] + [(APPLY_T, (0, 1))]
+            self._mvf = sum(D.algo_flops(eq, (tuple(self.L[k].shape), tuple(self.A[k].shape),
+                                              tuple(self.R[k].shape), sh)) for eq, k in blocks)
+        return self._mvf
+
     def matvec_into(self, v, out):
         if self.h:
+            D.count_algo(self.mv_flops() if D.ALGO is not None else 0.0)
             D.check(lib.ttk_schur_apply(D._stream(), self.h, v.data_ptr(), out.data_ptr()), "schur_apply")
             return out
         y, x = self._parts(v, 2)
@@ -121,6 +132,7 @@ class IneqMatVecWrapper(MatVecWrapper):
         if INEQ_MATVEC_BUG:
             raise IneqMatvecBug("reference bug: IneqMatVecWrapper.matvec returns a memoryview")
         if self.h:
+            D.count_algo(self.mv_flops() if D.ALGO is not None else 0.0)
             D.check(lib.ttk_schur_apply(D._stream(), self.h, v.data_ptr(), out.data_ptr()), "schur_apply")
             return out
         y, x, t = self._parts(v, 3)
@@ -188,8 +200,12 @@ _LOCAL_TRACE = bool(os.environ.get("TTIPM_LOCAL_TRACE"))  # diagnostics: one lin
 def _run_lgmres(op, rhs_flat, m, rtol):
     restart = min(m, 100)
     aug = max(restart // 10, 3)
-    return lgmres(op.matvec_into, rhs_flat, rtol=rtol, max_it=300, restart=restart, augment=aug,
-                  native=getattr(op, "h", 0))
+    info = {}
+    x = lgmres(op.matvec_into, rhs_flat, rtol=rtol, max_it=300, restart=restart, augment=aug,
+               native=getattr(op, "h", 0), info=info)
+    if D.ALGO is not None:  # applications made inside native chunks (the others counted themselves)
+        D.count_algo(info.get("native_matvecs", 0) * op.mv_flops(), info.get("native_matvecs", 0))
+    return x
 
 
 def _ipm_local_solver(XAX_k, A_k, XAX_k1, Xb_k, b_k, Xb_k1, prev, size_limit, dense_solve=True, rtol=1e-5):

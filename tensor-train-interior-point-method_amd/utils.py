@@ -109,19 +109,26 @@ def print_results_summary(config, results):
     print("=" * 80)
 
 
-def save_results_summary(config, cfg_path, rank, results, out_dir="results"):
-    """`src/utils.py:210-243` JSON keys (+ sec_per_iter)."""
+def save_results_summary(config, cfg_path, rank, results, out_dir="results", args=None):
+    """`src/utils.py:210-243`: the same JSON keys (`config_str`, `args_str`, per-seed arrays shaped
+    (num_ranks=1, num_seeds), `memory`) plus `sec_per_iter`; file name as the reference builds it
+    (`<config>_trackmem_<bool>_seeds_<s1-s2..>_ranks_<rank>.json`)."""
     os.makedirs(out_dir, exist_ok=True)
     seeds = "-".join(str(r["seed"]) for r in results)
-    name = re.sub(r"[^a-zA-Z0-9_.-]", "_", f"{os.path.basename(cfg_path)[:-5]}_seeds_{seeds}_ranks_{rank}.json")
-    data = {"config_str": str(config), "runtimes": [[r["runtime"] for r in results]],
+    track = bool(getattr(args, "track_mem", False))
+    stem = os.path.basename(cfg_path)[:-5] if cfg_path.endswith(".yaml") else os.path.basename(cfg_path)
+    name = re.sub(r"[^a-zA-Z0-9_.-]", "_", f"{stem}_trackmem_{track}_seeds_{seeds}_ranks_{'-'.join(str(rank))}.json")
+    data = {"config_str": str(config), "args_str": str(vars(args)) if args is not None else "{}",
+            "runtimes": [[r["runtime"] for r in results]],
             "problem_creation_times": [[r["creation_time"] for r in results]],
             "num_iters": [[r["num_iters"] for r in results]],
             "feasibility_errors": [[r["feas"] for r in results]],
             "dual_feasibility_errors": [[r["dual_feas"] for r in results]],
             "complementary_slackness": [[r["gap"] for r in results]],
             "ranksX": [[r["ranksX"] for r in results]], "ranksY": [[r["ranksY"] for r in results]],
-            "ranksZ": [[r["ranksZ"] for r in results]], "ranksT": [[r["ranksT"] for r in results]],
+            "ranksZ": [[r["ranksZ"] for r in results]],
+            "ranksT": [[r["ranksT"] for r in results]] if any(any(r["ranksT"]) for r in results) else [],
+            "memory": [[r.get("memory", 0.0) for r in results]],
             "sec_per_iter": [[r["sec_per_iter"] for r in results]]}
     path = os.path.join(out_dir, name)
     with open(path, "w") as f:
@@ -129,25 +136,73 @@ def save_results_summary(config, cfg_path, rank, results, out_dir="results"):
     return path
 
 
+def is_pathological(res):
+    """The reference runner's rule (`src/utils.py:67`): feasibility error or slackness > 1e-3."""
+    return res["feas"] > 1e-3 or res["gap"] > 1e-3
+
+
+def _run_tracked(prob, config, seed, rank, track_mem):
+    """`run_and_record` with `--track_mem`: the reference records the peak host RSS growth of the
+    solve (`memory_profiler`, `src/utils.py:292-296`, MB); here the solve's data lives in HBM, so
+    the recorded figure is the peak device allocation growth during the solve (MB)."""
+    if not track_mem or not torch.cuda.is_available():
+        return run_and_record(prob, config, seed, rank)
+    torch.cuda.synchronize()
+    base = torch.cuda.memory_allocated()
+    torch.cuda.reset_peak_memory_stats()
+    res = run_and_record(prob, config, seed, rank)
+    torch.cuda.synchronize()
+    res["memory"] = (torch.cuda.max_memory_allocated() - base) / 2 ** 20
+    return res
+
+
 def run_experiment(problem=None, argv=None):
-    """`run_experiment(create_problem_fn)` (`src/utils.py:13-101`): CLI --config/--rank."""
+    """`run_experiment(create_problem_fn)` (`src/utils.py:13-101`): CLI --config/--rank/--track_mem.
+
+    Pathological seeds (`is_pathological`) are replaced as the reference does (`src/utils.py:67-84`):
+    a new seed is drawn with `np.random.randint(0, 2**10)` from the global RNG as the previous solve
+    left it, skipping used seeds, and the solve is rerun in the same slot.  The reference also
+    rewrites the YAML file with the replacement; that happens here only with `--rewrite_config`
+    (the seed-sharded multi-GPU path never replaces seeds).  `--no_replace`
+    reports the config's seeds as they are."""
     ap = argparse.ArgumentParser(description="TT-IPM on MI355X")
     ap.add_argument("--problem", default=problem, choices=sorted(PROBLEMS))
     ap.add_argument("--config", required=True)
     ap.add_argument("--rank", type=int, default=1)
     ap.add_argument("--track_mem", action="store_true")
     ap.add_argument("--seeds", type=str, default=None, help="comma-separated override of the config seeds")
+    ap.add_argument("--no_replace", action="store_true", help="keep pathological seeds (no replacement)")
+    ap.add_argument("--rewrite_config", action="store_true", help="write replacement seeds back to the YAML")
     args = ap.parse_args(argv)
     with open(args.config) as f:
         config = yaml.safe_load(f)
     prob = args.problem or next(p for p in PROBLEMS if os.path.basename(args.config).startswith(p))
-    seeds = [int(s) for s in args.seeds.split(",")] if args.seeds else config["seeds"]
+    if args.seeds:
+        config["seeds"] = [int(s) for s in args.seeds.split(",")]
+    used = set(config["seeds"])
     results = []
-    for seed in seeds:
+    print(f"\n===== Processing Rank: {args.rank} =====")
+    for s_i, seed in enumerate(list(config["seeds"])):
         print(f"Running seed {seed}")
-        results.append(run_and_record(prob, config, seed, args.rank))
+        res = _run_tracked(prob, config, seed, args.rank, args.track_mem)
+        while not args.no_replace and is_pathological(res):
+            print(f"Seed {res['seed']} is pathological (feasibility error: {res['feas']:.2e}, slackness: "
+                  f"{res['gap']:.2e}). Suggesting a new seed.")
+            new_seed = np.random.randint(0, 2 ** 10)
+            while new_seed in used:
+                new_seed = np.random.randint(0, 2 ** 10)
+            print(f"New seed suggested: {new_seed}")
+            used.add(new_seed)
+            config["seeds"][s_i] = int(new_seed)
+            if args.rewrite_config:
+                with open(args.config, "w") as f:
+                    yaml.safe_dump(config, f)
+            res = _run_tracked(prob, config, int(new_seed), args.rank, args.track_mem)
+            print(f"Rerun with new seed {new_seed} complete. Feasibility error: {res['feas']:.2e}, "
+                  f"Slackness: {res['gap']:.2e}")
+        results.append(res)
     print_results_summary(config, results)
-    return save_results_summary(config, args.config, args.rank, results)
+    return save_results_summary(config, args.config, args.rank, results, args=args)
 
 
 if __name__ == "__main__":
