@@ -270,7 +270,7 @@ def main():
         st = (ctypes.c_double * 5)()
         lib.ttk_contract_stats(st, 1)
         lib.ttk_contract_timing(1)
-        D.ALGO = {"flops": 0.0, "calls": 0}
+        D.ALGO = {"flops": 0.0, "calls": 0, "by": {}}
         try:
             solve(shard.unpack(*packed[mine_seeds[0]]))
             sync()
@@ -289,7 +289,8 @@ def main():
                         "algorithmic_calls_per_solve": algo["calls"], "device_flops_per_solve": tflops,
                         "launches_per_solve": int(tl), "kernel_ms_per_solve": tms,
                         "avg_launch_us": tms * 1e3 / max(tl, 1),
-                        "algorithmic_flops_per_launch": algo["flops"] / max(tl, 1)}
+                        "algorithmic_flops_per_launch": algo["flops"] / max(tl, 1),
+                        "algorithmic_by_op": dict(sorted(algo["by"].items(), key=lambda kv: -kv[1][1])[:10])}
 
     cpu = None
     if do_cpu:

@@ -39,6 +39,10 @@ def einsum(eq, *ops):
     if ALGO is not None:
         ALGO["flops"] += flops
         ALGO["calls"] += 1
+        if "by_eq" in ALGO:
+            e = ALGO["by_eq"].setdefault(eq, [0, 0.0])
+            e[0] += 1
+            e[1] += flops
     return np.einsum(eq, *ops, optimize=path)
 
 

@@ -373,18 +373,27 @@ def algo_flops(eq, shapes):
     return f
 
 
-def count_algo(flops, calls=1):
+def count_algo(flops, calls=1, what=None):
     if ALGO is not None:
         ALGO["flops"] += flops
         ALGO["calls"] += calls
+        if what is not None and "by" in ALGO:
+            e = ALGO["by"].setdefault(what, [0, 0.0])
+            e[0] += calls
+            e[1] += flops
 
 
-def einsum(eq, *ops, out=None, alpha=1.0, beta=0.0, fused=False):
+def einsum(eq, *ops, out=None, alpha=1.0, beta=0.0, fused=False, algo=None):
     """`fused=True` lets the local-operator equations run as one fused launch (see ttk_einsum);
     call sites whose results feed noise-level decisions keep the pairwise plan.  `fused="env"`:
-    a relabelled environment update (fused under a smaller FLOP limit)."""
+    a relabelled environment update (fused under a smaller FLOP limit).  `algo=(eq, shapes)`: the
+    reference's own equation and operand shapes for a relabelled call, so the algorithmic count
+    follows the reference's contraction order."""
     if ALGO is not None:
-        count_algo(algo_flops(eq, tuple(tuple(o.shape) for o in ops)))
+        if algo is not None:
+            count_algo(algo_flops(*algo), what=algo[0])
+        else:
+            count_algo(algo_flops(eq, tuple(tuple(o.shape) for o in ops)), what=eq)
     fused = fused or _FUSED_ALL
     if _CHECK_FUSED and fused and eq in _FUSED_EQS:
         return _einsum_checked(eq, ops, out, alpha, beta)

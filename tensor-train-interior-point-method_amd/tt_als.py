@@ -195,17 +195,23 @@ FUSED_ENV = os.environ.get("TTIPM_FUSED_ENV", "1") == "1"
 _APPLY = "lsr,smnS,LSR,rnR->lmL"
 
 
+def _shapes(*ops):
+    return tuple(tuple(o.shape) for o in ops)
+
+
 def compute_phi_bck_A(P, xl, A, xr):
     """`src/tt_als.py:252-253`"""
     if FUSED_ENV:
-        return einsum(_APPLY, xl, A.permute(1, 0, 3, 2), xr, P, fused="env")
+        return einsum(_APPLY, xl, A.permute(1, 0, 3, 2), xr, P, fused="env",
+                      algo=("LSR,lML,sMNS,rNR->lsr", _shapes(P, xl, A, xr)))
     return einsum("LSR,lML,sMNS,rNR->lsr", P, xl, A, xr)
 
 
 def compute_phi_fwd_A(P, xl, A, xr):
     """`src/tt_als.py:256-257`"""
     if FUSED_ENV:
-        return einsum(_APPLY, xl.permute(2, 1, 0), A.permute(1, 3, 0, 2), xr.permute(2, 1, 0), P, fused="env")
+        return einsum(_APPLY, xl.permute(2, 1, 0), A.permute(1, 3, 0, 2), xr.permute(2, 1, 0), P, fused="env",
+                      algo=("lsr,lML,sMNS,rNR->LSR", _shapes(P, xl, A, xr)))
     return einsum("lsr,lML,sMNS,rNR->LSR", P, xl, A, xr)
 
 

@@ -107,7 +107,7 @@ class MatVecWrapper:
 
     def matvec_into(self, v, out):
         if self.h:
-            D.count_algo(self.mv_flops() if D.ALGO is not None else 0.0)
+            D.count_algo(self.mv_flops() if D.ALGO is not None else 0.0, what="schur_matvec")
             D.check(lib.ttk_schur_apply(D._stream(), self.h, v.data_ptr(), out.data_ptr()), "schur_apply")
             return out
         y, x = self._parts(v, 2)
@@ -132,7 +132,7 @@ class IneqMatVecWrapper(MatVecWrapper):
         if INEQ_MATVEC_BUG:
             raise IneqMatvecBug("reference bug: IneqMatVecWrapper.matvec returns a memoryview")
         if self.h:
-            D.count_algo(self.mv_flops() if D.ALGO is not None else 0.0)
+            D.count_algo(self.mv_flops() if D.ALGO is not None else 0.0, what="schur_matvec")
             D.check(lib.ttk_schur_apply(D._stream(), self.h, v.data_ptr(), out.data_ptr()), "schur_apply")
             return out
         y, x, t = self._parts(v, 3)
@@ -204,7 +204,7 @@ def _run_lgmres(op, rhs_flat, m, rtol):
     x = lgmres(op.matvec_into, rhs_flat, rtol=rtol, max_it=300, restart=restart, augment=aug,
                native=getattr(op, "h", 0), info=info)
     if D.ALGO is not None:  # applications made inside native chunks (the others counted themselves)
-        D.count_algo(info.get("native_matvecs", 0) * op.mv_flops(), info.get("native_matvecs", 0))
+        D.count_algo(info.get("native_matvecs", 0) * op.mv_flops(), info.get("native_matvecs", 0), "schur_matvec")
     return x
 
 

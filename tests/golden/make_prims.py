@@ -113,5 +113,47 @@ def main(import_reference):
     res = rops.tt_normalise(tt, radius=np.sqrt(10))
     out["norm/dense"] = _dense(res)
     out["norm/next_randint"] = np.array(np.random.randint(0, 1 << 30))
+    # ---- mask rounding (cy_src/tt_ops_cy.pyx:328-388): matrix TTs + a rank-2 0/1-ish mask TT
+    for ci, (d, r, eps) in enumerate([(5, 4, 5e-4), (6, 3, 1e-3), (4, 5, 1e-10)]):
+        tt = _rand_tt(rng, d, None, r, (2, 2))
+        for i in range(d):
+            tt[i][..., 1:] *= 1e-6
+        mask = _rand_tt(rng, d, None, 2, (2, 2))
+        _put_tt(out, f"mask{ci}/in", tt)
+        _put_tt(out, f"mask{ci}/mask", mask)
+        out[f"mask{ci}/eps"] = np.array(eps)
+        res = rops.tt_mask_rank_reduce([c.copy() for c in tt], [c.copy() for c in mask], eps)
+        out[f"mask{ci}/ranks"] = np.array(rops.tt_ranks(res))
+        out[f"mask{ci}/dense"] = _dense(res)
+    # ---- rank retraction (src/tt_ops.py:132-152) on a block TT (one (r, B, 4, R) core) and a plain TT
+    for ci, (d, r, B, up) in enumerate([(5, 6, 3, 3), (6, 9, 4, 4), (4, 5, 0, 2)]):
+        tt = _rand_tt(rng, d, None, r, (4,))
+        if B:
+            k = d // 2
+            tt[k] = rng.standard_normal((tt[k].shape[0], B, 4, tt[k].shape[-1]))
+        _put_tt(out, f"retract{ci}/in", tt)
+        out[f"retract{ci}/upper"] = np.array([up] * (d - 1))
+        res = rops.tt_rank_retraction([c.copy() for c in tt], [up] * (d - 1))
+        out[f"retract{ci}/ranks"] = np.array(rops.tt_ranks(res))
+        out[f"retract{ci}/dense"] = _dense(res)
+    # ---- 3-block (inequality) Schur-reduced KKT matvec, fixed mode (cy_src/lgmres_cy.pyx:379-510 with
+    #      :510 returning the array; the fixed module is what import_reference(True) loads)
+    for ci, (r, R, s) in enumerate([(2, 3, 2), (5, 4, 3), (7, 9, 5)]):
+        n = 4
+        keys = [(0, 0), (0, 1), (2, 1), (2, 2), (3, 1), (3, 3)]
+        Ls = {k: rng.standard_normal((r, s, r)) for k in keys}
+        As = {k: rng.standard_normal((s, n, n, s)) for k in keys}
+        Rs = {k: rng.standard_normal((R, s, R)) for k in keys}
+        invI = rng.uniform(0.5, 2.0, (r, n, R))
+        x = rng.standard_normal(3 * r * n * R)
+        mw = ripm.IneqMatVecWrapper(*[Ls[k] for k in keys], *[As[k] for k in keys], *[Rs[k] for k in keys],
+                                    invI, r, n, R)
+        for k in keys:
+            out[f"imv{ci}/L{k[0]}{k[1]}"] = Ls[k]
+            out[f"imv{ci}/A{k[0]}{k[1]}"] = As[k]
+            out[f"imv{ci}/R{k[0]}{k[1]}"] = Rs[k]
+        out[f"imv{ci}/invI"] = invI
+        out[f"imv{ci}/x"] = x
+        out[f"imv{ci}/y"] = np.array(mw.matvec(x), copy=True)
     np.savez_compressed(os.path.join(HERE, "prims.npz"), **out)
     print("wrote", len(out), "arrays to prims.npz")

@@ -82,6 +82,32 @@ def test_schur_matvec(ci):
     _close(y, G[f"mv{ci}/y"], 1e-13)
 
 
+@pytest.mark.parametrize("ci", range(3))
+def test_mask_rank_reduce(ci):
+    res = T.mask_rank_reduce(_tt(f"mask{ci}/in"), _tt(f"mask{ci}/mask"), float(G[f"mask{ci}/eps"]))
+    assert T.ranks(res) == list(G[f"mask{ci}/ranks"])
+    _close(_dense(res), G[f"mask{ci}/dense"])
+
+
+@pytest.mark.parametrize("ci", range(3))
+def test_rank_retraction(ci):
+    res = T.rank_retraction(_tt(f"retract{ci}/in"), [int(u) for u in G[f"retract{ci}/upper"]])
+    assert T.ranks(res) == list(G[f"retract{ci}/ranks"])
+    _close(_dense(res), G[f"retract{ci}/dense"])
+
+
+@pytest.mark.parametrize("ci", range(3))
+def test_ineq_schur_matvec(ci):
+    """3-block operator (`cy_src/lgmres_cy.pyx:490-510`, fixed mode) against the reference's output"""
+    keys = [(0, 0), (0, 1), (2, 1), (2, 2), (3, 1), (3, 3)]
+    L = {k: G[f"imv{ci}/L{k[0]}{k[1]}"] for k in keys}
+    Am = {k: G[f"imv{ci}/A{k[0]}{k[1]}"] for k in keys}
+    R = {k: G[f"imv{ci}/R{k[0]}{k[1]}"] for k in keys}
+    invI = G[f"imv{ci}/invI"]
+    op = I.IneqSchurMatVec(L, Am, R, invI, invI.shape)
+    _close(op.matvec(G[f"imv{ci}/x"]), G[f"imv{ci}/y"], 1e-13)
+
+
 def test_normalise_rng_coupling():
     np.random.seed(7)
     res = T.normalise(_tt("norm/in"), radius=np.sqrt(10))
@@ -115,6 +141,56 @@ def test_oracle_full_run_maxcut5():
     for a, b in zip(trace, g["trace"]):
         assert a["ranksX"] == b["ranksX"]
         assert abs(a["mu"] - b["mu"]) <= 1e-5 * abs(b["mu"])
+
+
+class _Bounded(Exception):
+    pass
+
+
+@pytest.mark.parametrize("key", sorted(k for k in RUNS if RUNS[k].get("bounded")))
+def test_oracle_bounded_trace(key):
+    """Bounded reference traces (fixed-mode inequality configs): the oracle's first Newton-system
+    assemblies, AMEn solution ranks and step sizes against the reference's."""
+    import yaml
+    from oracle.problems import run_and_record
+    g = RUNS[key]
+    n = int(g["bounded"])
+    amen, steps = [], []
+
+    class Trace(list):
+        def append(self, item):
+            super().append(item)
+            if len(self) >= n:
+                raise _Bounded
+
+    o_amen, o_steps = I.restarted_block_amen, I.step_sizes
+
+    def h_amen(*a, **k):
+        sol, res = o_amen(*a, **k)
+        amen.append([int(c.shape[-1]) for c in sol[:-1]])
+        return sol, res
+
+    def h_steps(*a, **k):
+        xs, zs = o_steps(*a, **k)
+        steps.append([float(xs), float(zs)])
+        return xs, zs
+
+    cfg = yaml.safe_load(open(os.path.join(HERE, "..", "configs", g["config"] + ".yaml")))
+    trace = Trace()
+    I.restarted_block_amen, I.step_sizes = h_amen, h_steps
+    try:
+        with pytest.raises(_Bounded):
+            run_and_record(g["problem"], cfg, g["seed"], g["rank"], trace=trace)
+    finally:
+        I.restarted_block_amen, I.step_sizes = o_amen, o_steps
+    for i, (a, b) in enumerate(zip(trace, g["trace"])):
+        assert a["ranksX"] == b["ranksX"], (i, a["ranksX"], b["ranksX"])
+        for k in ("mu", "primal_error", "dual_error", "centrality_error"):
+            assert abs(a[k] - b[k]) <= 1e-6 * abs(b[k]) + 1e-14, (i, k, a[k], b[k])
+    # the AMEn solutions' TT ranks may differ by directions carrying rounding-level energy (measured:
+    # solve 7 keeps [1,2,..,3] where the reference keeps [1,3,..,3]) without moving the iterates
+    assert len(amen) == len(g["amen"])
+    assert np.allclose(steps, g["steps"], rtol=1e-6, atol=1e-12)
 
 
 AP = np.load(os.path.join(HERE, "golden", "approx.npz"))
