@@ -18,32 +18,29 @@ import scipy.linalg as sla
 # --------------------------------------------------------------------------------------------
 
 
-@lru_cache(maxsize=4096)
+# opt_einsum 3.4.0 greedy semantics (`oracle/opt_einsum_greedy.py`): NumPy's own greedy planner caps
+# intermediates at the largest operand and then contracts the 4-operand local applies naively.
+from . import opt_einsum_greedy as _oe  # noqa: E402
+
+
 def _path_and_flops(eq, shapes):
-    import re
-    ops = [np.empty(s) for s in shapes]
-    path, txt = np.einsum_path(eq, *ops, optimize="greedy")
-    return path, float(re.search(r"Optimized FLOP count:\s*([0-9.eE+-]+)", txt).group(1))
+    return None, _oe.flops(eq, shapes)
 
 
-def _path(eq, shapes):
-    return _path_and_flops(eq, shapes)[0]
-
-
-# algorithmic contraction FLOP counter: einsum_path greedy convention per call
+# algorithmic contraction FLOP counter: opt_einsum greedy convention per call
 ALGO = None
 
 
 def einsum(eq, *ops):
-    path, flops = _path_and_flops(eq, tuple(o.shape for o in ops))
     if ALGO is not None:
+        flops = _oe.flops(eq, tuple(o.shape for o in ops))
         ALGO["flops"] += flops
         ALGO["calls"] += 1
         if "by_eq" in ALGO:
             e = ALGO["by_eq"].setdefault(eq, [0, 0.0])
             e[0] += 1
             e[1] += flops
-    return np.einsum(eq, *ops, optimize=path)
+    return _oe.contract(eq, *ops)
 
 
 # --------------------------------------------------------------------------------------------

@@ -355,9 +355,9 @@ _FUSED_ALL = os.environ.get("TTIPM_FUSED_ALL") == "1"  # experiment switch: ever
 
 
 # Algorithmic contraction FLOPs: when ALGO is a dict, every einsum call adds the
-# FLOP count NumPy's `einsum_path(..., optimize="greedy")` reports for its equation and shapes --
-# the convention the oracle's counter uses at the reference's call sites -- whatever plan (fused
-# launch, pairwise MFMA GEMMs) the device executes.  Operator applications made natively (Schur
+# FLOP count of the pairwise greedy path for its equation and shapes (opt_einsum's convention, which
+# the oracle's counter restates at the reference's call sites), whatever plan (fused launch, pairwise
+# MFMA GEMMs) the device executes.  Operator applications made natively (Schur
 # handle, LGMRES chunks) are added by their callers with `count_algo`.
 ALGO = None
 _ALGO_CACHE = {}
@@ -367,7 +367,9 @@ def algo_flops(eq, shapes):
     f = _ALGO_CACHE.get((eq, shapes))
     if f is None:
         import re
-        txt = np.einsum_path(eq, *[np.empty(sh) for sh in shapes], optimize="greedy")[1]
+        # pairwise greedy without NumPy's default intermediate-size cap (opt_einsum's greedy has none;
+        # the capped planner collapses 4-operand chains into one naive contraction)
+        txt = np.einsum_path(eq, *[np.empty(sh) for sh in shapes], optimize=("greedy", 1 << 62))[1]
         f = float(re.search(r"Optimized FLOP count:\s*([0-9.eE+-]+)", txt).group(1))
         _ALGO_CACHE[(eq, shapes)] = f
     return f

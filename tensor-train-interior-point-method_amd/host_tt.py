@@ -25,6 +25,20 @@ def _path(eq, shapes):
 
 
 def einsum(eq, *ops):
+    """As the reference's opt_einsum evaluates it: the creation code only contracts two operands over
+    one shared index, which opt_einsum 3.4.0 runs as `tensordot` + a transpose to the output order
+    (`contract.py::_core_contract`, `blas.can_blas`); anything else goes through numpy's planner."""
+    lhs, out = eq.split("->")
+    terms = lhs.split(",")
+    if len(terms) == 2:
+        a, b = terms
+        rm = [c for c in a if c in b and c not in out]
+        shared_ok = all((c in out) != (c in a and c in b) for c in set(a + b))  # blas.can_blas
+        if len(rm) == 1 and len(set(a)) == len(a) and len(set(b)) == len(b) and shared_ok:
+            c = rm[0]
+            res = "".join(x for x in a + b if x != c)
+            v = np.tensordot(ops[0], ops[1], axes=((a.find(c),), (b.find(c),)))
+            return v if res == out else v.transpose(tuple(map(res.index, out)))
     return np.einsum(eq, *ops, optimize=_path(eq, tuple(o.shape for o in ops)))
 
 

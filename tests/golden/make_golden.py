@@ -176,29 +176,53 @@ def _run_bounded(ripm, rops, mod, config, problem, cfg_name, seed, rank, fixed_i
             "steps": steps, "blas_threads": os.environ.get("OPENBLAS_NUM_THREADS")}
 
 
+# (problem, config, seed, rank, fixed_ineq, max_assemblies): max_assemblies > 0 = bounded trace
 RUNS = [
-    ("maxcut", "maxcut_5", 0, 1, True),
-    ("maxcut", "maxcut_5", 319, 1, True),
-    ("maxcut", "maxcut_10", 41, 1, True),
-    ("corr_clust", "corr_clust_9", 764, 1, True),
-    ("corr_clust", "corr_clust_9", 764, 1, False),
-    ("maxcut", "maxcut_12", 80, 2, True),  # made with OPENBLAS_NUM_THREADS=8 (~22 min)
+    ("maxcut", "maxcut_5", 0, 1, True, 0),
+    ("maxcut", "maxcut_5", 319, 1, True, 0),
+    ("maxcut", "maxcut_10", 41, 1, True, 0),
+    ("maxcut", "maxcut_10", 23, 1, True, 0),
+    ("maxcut", "maxcut_10", 235, 1, True, 0),
+    ("maxcut", "maxcut_10", 35, 1, True, 0),
+    ("maxcut", "maxcut_10", 14, 1, True, 0),
+    ("corr_clust", "corr_clust_9", 764, 1, True, 0),
+    ("corr_clust", "corr_clust_9", 764, 1, False, 0),
+    ("graphm", "graphm_3", 256, 2, True, 2),
+    ("maxcut", "maxcut_12", 80, 2, True, 0),
 ]
 
 
-def make_runs(only=None):
+def run_key(cfg, rank, seed, fixed, nmax):
+    return f"{cfg}_r{rank}_s{seed}" + ("" if fixed else "_shipped") + (f"_b{nmax}" if nmax else "")
+
+
+def make_runs(only=None, jobs=1):
+    """Each run in its own process (1 BLAS thread, PYTHONHASHSEED=0: opt_einsum's tensordot axis order
+    follows frozenset iteration, so the hash seed pins the summation order); `jobs` at a time."""
+    import subprocess
     path = os.path.join(HERE, "runs.json")
     out = json.load(open(path)) if os.path.exists(path) else {}
-    for prob, cfg, seed, rank, fixed in RUNS:
-        key = f"{cfg}_r{rank}_s{seed}" + ("" if fixed else "_shipped")
+    todo = []
+    for prob, cfg, seed, rank, fixed, nmax in RUNS:
+        key = run_key(cfg, rank, seed, fixed, nmax)
         if only and cfg not in only and key not in only:
             continue
-        print("running reference", key, flush=True)
-        import subprocess
-        tmp = os.path.join("/tmp", f"golden_{key}.json")
-        subprocess.check_call([sys.executable, __file__, "one", prob, cfg, str(seed), str(rank), str(int(fixed)), tmp])
+        todo.append((key, [sys.executable, __file__, "one", prob, cfg, str(seed), str(rank), str(int(fixed)),
+                           os.path.join("/tmp", f"golden_{key}.json"), str(nmax)]))
+    env = dict(os.environ, PYTHONHASHSEED="0", OPENBLAS_NUM_THREADS="1", OMP_NUM_THREADS="1")
+    running = []
+    while todo or running:
+        while todo and len(running) < jobs:
+            key, cmd = todo.pop(0)
+            print("running reference", key, flush=True)
+            running.append((key, cmd[-2], subprocess.Popen(cmd, env=env, stdout=subprocess.DEVNULL)))
+        key, tmp, p = running.pop(0)
+        if p.wait() != 0:
+            print(key, "FAILED", flush=True)
+            continue
         res = json.load(open(tmp))
-        print(key, {k: res[k] for k in ("num_iters", "gap", "feas", "dual_feas", "sec_per_iter")}, flush=True)
+        print(key, {k: res.get(k) for k in ("num_iters", "gap", "feas", "dual_feas", "sec_per_iter")}, flush=True)
+        out = json.load(open(path)) if os.path.exists(path) else {}
         out[key] = res
         with open(path, "w") as f:
             json.dump(out, f, indent=1)
@@ -208,12 +232,14 @@ if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "one":
         _, _, prob, cfg, seed, rank, fixed, tmp = sys.argv[:8]
         nmax = int(sys.argv[8]) if len(sys.argv) > 8 else 0
-        json.dump(run_reference(prob, cfg, int(seed), int(rank), bool(int(fixed)), nmax), open(tmp, "w"))
+        with open(tmp, "w") as f:
+            json.dump(run_reference(prob, cfg, int(seed), int(rank), bool(int(fixed)), nmax), f)
         sys.exit(0)
     what = sys.argv[1] if len(sys.argv) > 1 else "all"
-    rest = sys.argv[2:]
+    rest = [a for a in sys.argv[2:] if not a.startswith("-j")]
+    jobs = max([int(a[2:]) for a in sys.argv[2:] if a.startswith("-j")] or [1])
     if what in ("runs", "all"):
-        make_runs(rest or None)
+        make_runs(rest or None, jobs)
     if what in ("prims", "all"):
         from tests.golden import make_prims
         make_prims.main(_import_reference)
