@@ -70,6 +70,25 @@ int ttk_gemm_offs_grouped(void *stream, const double *const *Aptr, const double 
  * pairwise order + offset tables) are cached per (eq, shapes, strides); each pairwise step is one
  * ttk_gemm_offs launch. */
 int ttk_einsum(void *stream, const char *eq, const int64_t *desc, double *out, double alpha, double beta);
+
+/* Einsum batches: between begin and end, ttk_einsum records its steps (same plans, same fused-apply
+ * decisions, private intermediates) instead of launching them; end (or flush) launches them level
+ * by level -- a level is a set of steps without read/write conflicts -- as one grouped MFMA GEMM
+ * launch plus one grouped fused-apply launch per level.  Bit-identical to the unbatched calls.
+ * Used for one AMEn core step's environment updates (`src/tt_als.py:372-387,499-514`), the
+ * block local products and the rank loop's candidate products (`src/tt_als.py:334-346`).
+ * ttk_copy_nd / ttk_mul_nd flush pending steps first.  Nesting counts; only the outermost end
+ * launches.  stats: [flushes, recorded steps, launches]. */
+int ttk_einsum_batch_begin(void *stream);
+int ttk_einsum_batch_flush(void *stream);
+int ttk_einsum_batch_end(void *stream);
+int ttk_einsum_batch_stats(long long *out3);
+
+/* AMEn rank loop (`src/tt_als.py:334-346`, `:462-472`): res (n contiguous doubles) is updated
+ * res <- res - negs[q] for q = 0..nq-1 in order and <res, res> after each update is returned in
+ * host_out[q]; one launch and one host read for every candidate rank, with the same operations and
+ * reduction order as nq separate copy_nd + dot_nd_sync calls. */
+int ttk_rank_scan_sync(void *stream, double *res, const double *negs, int64_t n, int nq, double *host_out);
 /* calls that opt in (desc flag) route 'lsr,smnS,LSR,rnR->lmL' / 'lsr,smnS,LSR,lmL->rnR' (the local
  * operator, src/tt_als.py:190-200, cy_src/lgmres_cy.pyx:126-153) to a one-launch fused kernel when
  * its intermediates fit LDS; this switch disables it globally.  Returns the previous setting. */

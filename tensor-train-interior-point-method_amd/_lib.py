@@ -66,6 +66,11 @@ _SIGS = {
     "ttk_svd_tol": (i32, [vp, vp, i32, i32, vp, vp, vp, vp, f64]),
     "ttk_einsum": (i32, [vp, ctypes.c_char_p, vp, vp, f64, f64]),
     "ttk_einsum_stats": (i32, [vp]),
+    "ttk_einsum_batch_begin": (i32, [vp]),
+    "ttk_einsum_batch_flush": (i32, [vp]),
+    "ttk_einsum_batch_end": (i32, [vp]),
+    "ttk_einsum_batch_stats": (i32, [vp]),
+    "ttk_rank_scan_sync": (i32, [vp, vp, vp, i64, i32, vp]),
     "ttk_einsum_set_fused": (i32, [i32]),
     "ttk_qr_set_big_threshold": (i32, [i32]),
     "ttk_contract_timing": (i32, [i32]),

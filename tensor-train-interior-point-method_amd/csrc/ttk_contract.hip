@@ -16,10 +16,12 @@
 #include <array>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <map>
 #include <vector>
 
 #include "ttk_common.h"
+#include "ttk_internal.h"
 
 namespace {
 
@@ -246,6 +248,30 @@ __global__ __launch_bounds__(256) void gemm_offs_grouped_kernel(GemmArgs g, Grou
             nullptr);
 }
 
+// Independent problems of one einsum batch level in ONE launch: workgroup -> (problem, tile) through
+// the tile prefix; each tile runs gemm_tile exactly as gemm_offs_kernel would (same n/m/b tile
+// coordinates, same K order), so results are bit-identical to one launch per problem.
+constexpr int GROUP_MAX = 24;
+struct GemmGroup {
+  GemmArgs p[GROUP_MAX];
+  int tile0[GROUP_MAX + 1];
+  int n;
+};
+
+__global__ __launch_bounds__(256) void gemm_offs_group_kernel(GemmGroup G) {
+  const int bid = blockIdx.x;
+  int p = 0;
+  while (p + 1 < G.n && bid >= G.tile0[p + 1]) ++p;
+  const GemmArgs &g = G.p[p];
+  int t = bid - G.tile0[p];
+  const int ntn = (g.N + TN - 1) / TN, ntm = (g.M + TM - 1) / TM;
+  const int n0 = (t % ntn) * TN;
+  t /= ntn;
+  const int m0 = (t % ntm) * TM;
+  const int b = t / ntm;
+  gemm_tile(g.A, g.B, g.C, g.offs, g.nb, g.M, g.N, g.K, g.alpha, g.beta, b, m0, n0, 0, g.K, nullptr);
+}
+
 // ------------------------------------------------------------------ element-wise (N-D strided)
 __device__ __forceinline__ void nd_offsets(const ttk::NdDesc &d, int64_t lin, int64_t &o0,
                                            int64_t &o1, int64_t &o2) {
@@ -438,6 +464,27 @@ __global__ void dot_nd_kernel(const double *__restrict__ x, const double *__rest
   }
   acc = ttk::block_sum(acc, red);
   if (threadIdx.x == 0) out[0] = acc;
+}
+
+// The AMEn rank loop's residual updates (`src/tt_als.py:338-346`, `:466-472`): for q = 0..nq-1 in
+// order, res <- -1 * neg_q + res (copy_nd_kernel's operations with alpha = -1, beta = 1), then
+// <res, res> (dot_nd_kernel's thread map and block reduction) into out[q] -- every candidate rank's
+// residual norm in one launch and one host read, bit-identical to the one-candidate-at-a-time loop.
+__global__ __launch_bounds__(1024) void rank_scan_kernel(double *__restrict__ res, const double *__restrict__ negs,
+                                                         int64_t n, int nq, double *__restrict__ out) {
+  __shared__ double red[16];
+  for (int q = 0; q < nq; ++q) {
+    const double *ng = negs + (int64_t)q * n;
+    double acc = 0.0;
+    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+      const double v = -1.0 * ng[i];
+      const double w = v + 1.0 * res[i];
+      res[i] = w;
+      acc += w * w;
+    }
+    acc = ttk::block_sum(acc, red);
+    if (threadIdx.x == 0) out[q] = acc;
+  }
 }
 
 __global__ void sumsq_batched_kernel(const double *__restrict__ x, int64_t n, int64_t bstride, double *out) {
@@ -653,6 +700,46 @@ int ttk_gemm_offs(void *stream, const double *A, const double *B, double *C, con
   return TTK_OK;
 }
 
+}  // extern "C"
+
+namespace ttk {
+
+bool gemm_groupable(int nb, int M, int N, int K) {
+  if (nb <= 0 || M <= 0 || N <= 0 || K <= 0 || nb > 65535) return false;
+  const int64_t tiles = (int64_t)((N + TN - 1) / TN) * ((M + TM - 1) / TM) * nb;
+  if (g_splitk_on && tiles < 256 && K >= 2 * g_splitk_mink) return false;  // split-K path
+  if (M >= g_gemm64_min && N >= g_gemm64_min && K >= 64 &&
+      (int64_t)((M + BM - 1) / BM) * ((N + BN - 1) / BN) * nb >= 512)
+    return false;  // throughput variant: the problem fills the chip on its own
+  return tiles <= 4096;
+}
+
+int gemm_group(hipStream_t st, const GemmProblem *p, int n) {
+  for (int base = 0; base < n; base += GROUP_MAX) {
+    GemmGroup G;
+    G.n = n - base < GROUP_MAX ? n - base : GROUP_MAX;
+    G.tile0[0] = 0;
+    double flops = 0.0;
+    for (int i = 0; i < G.n; ++i) {
+      const GemmProblem &q = p[base + i];
+      G.p[i] = GemmArgs{q.A, q.B, q.C, q.offs, q.nb, q.M, q.N, q.K, q.alpha, q.beta};
+      G.tile0[i + 1] = G.tile0[i] + ((q.N + TN - 1) / TN) * ((q.M + TM - 1) / TM) * q.nb;
+      flops += 2.0 * q.M * q.N * (double)q.K * q.nb;
+    }
+    hipEvent_t e0, e1;
+    int rc = contract_events(&e0, &e1);
+    if (rc != TTK_OK) return rc;
+    hipExtLaunchKernelGGL(gemm_offs_group_kernel, dim3(G.tile0[G.n]), dim3(256), 0, st, e0, e1, 0, G);
+    TTK_LAUNCH_CHECK();
+    contract_count(flops);
+  }
+  return TTK_OK;
+}
+
+}  // namespace ttk
+
+extern "C" {
+
 int ttk_gemm_offs_grouped(void *stream, const double *const *Aptr, const double *const *Bptr,
                           double *const *Cptr, const int64_t *offs, int ngroups, int nb, int M,
                           int N, int K, double alpha, double beta) {
@@ -675,6 +762,7 @@ int ttk_gemm_offs_grouped(void *stream, const double *const *Aptr, const double 
 
 int ttk_copy_nd(void *stream, const double *src, double *dst, int ndim, const int64_t *shape,
                 const int64_t *sstride, const int64_t *dstride, double alpha, double beta) {
+  if (int rc = ttk::batch_barrier(stream)) return rc;
   ttk::NdDesc d;
   int st = make_nd(d, ndim, shape, sstride, dstride, nullptr);
   if (st) return st;
@@ -688,6 +776,7 @@ int ttk_copy_nd(void *stream, const double *src, double *dst, int ndim, const in
 int ttk_mul_nd(void *stream, const double *src, const double *src2, double *dst, int ndim,
                const int64_t *shape, const int64_t *sstride, const int64_t *s2stride,
                const int64_t *dstride, double alpha, double beta) {
+  if (int rc = ttk::batch_barrier(stream)) return rc;
   ttk::NdDesc d;
   int st = make_nd(d, ndim, shape, sstride, s2stride, dstride);
   if (st) return st;
@@ -856,6 +945,22 @@ int ttk_sumsq_batched(void *stream, const double *x, int64_t n, int nb, int64_t 
   if (nb <= 0) return TTK_OK;
   hipLaunchKernelGGL(sumsq_batched_kernel, dim3(nb), dim3(256), 0, TTK_STREAM(stream), x, n, bstride, out);
   TTK_LAUNCH_CHECK();
+  return TTK_OK;
+}
+
+int ttk_rank_scan_sync(void *stream, double *res, const double *negs, int64_t n, int nq, double *host_out) {
+  if (nq <= 0) return TTK_OK;
+  if (int rc = ttk::batch_barrier(stream)) return rc;
+  double *dev = nullptr;
+  double *h = ttk::mapped_stage((size_t)nq, &dev);
+  if (!h) {
+    ttk::set_error("ttk_rank_scan_sync: mapped buffer allocation failed");
+    return TTK_ERR_HIP;
+  }
+  hipLaunchKernelGGL(rank_scan_kernel, dim3(1), dim3(1024), 0, TTK_STREAM(stream), res, negs, n, nq, dev);
+  TTK_LAUNCH_CHECK();
+  TTK_HIP(hipStreamSynchronize(TTK_STREAM(stream)));
+  std::memcpy(host_out, h, (size_t)nq * sizeof(double));
   return TTK_OK;
 }
 

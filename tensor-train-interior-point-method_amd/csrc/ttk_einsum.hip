@@ -23,6 +23,7 @@
 #include <vector>
 
 #include "ttk_common.h"
+#include "ttk_internal.h"
 
 extern "C" int ttk_gemm_offs(void *stream, const double *A, const double *B, double *C, const int64_t *offs, int nb,
                              int M, int N, int K, double alpha, double beta);
@@ -36,14 +37,16 @@ constexpr int MAX_IDX = 52;
 struct Step {
   int a, b, out;  // operand slots: >= 0 input, < 0 intermediate -(k+1); b may be SLOT_ONES
   int nb, M, N, K;
-  int64_t offs;  // element offset of this step's tables inside the plan's table block
-  int64_t tmp;   // element offset of this step's result inside the scratch (intermediates)
+  int64_t offs;   // element offset of this step's tables inside the plan's table block
+  int64_t tmp;    // element offset of this step's result inside the scratch (intermediates)
+  int64_t tmp_n;  // elements of that intermediate
 };
 
 struct Plan {
   std::vector<Step> steps;
   int64_t *dtab = nullptr;  // device tables
   int64_t scratch = 0;      // doubles of scratch needed
+  std::vector<int64_t> out_ext, out_st;  // output extents and element strides (batch dependency spans)
 };
 
 struct Arena {  // device bump allocator for offset tables (freed only on a full cache reset)
@@ -306,10 +309,12 @@ bool build_plan(const std::string &eq, int nops, const int *ndims, const int64_t
     if (last) {
       st.out = SLOT_FINAL;
       st.tmp = 0;
+      st.tmp_n = 0;
     } else {
       st.out = -(ntmp + 1);
       ++ntmp;
       st.tmp = scratch;
+      st.tmp_n = extent_of(ext, R.idx);
       scratch += (extent_of(ext, R.idx) + 31) / 32 * 32;
       R.slot = st.out;
       live.push_back(R);
@@ -317,6 +322,10 @@ bool build_plan(const std::string &eq, int nops, const int *ndims, const int64_t
     pl.steps.push_back(st);
   }
   pl.scratch = scratch;
+  for (char c : out) {
+    pl.out_ext.push_back(ext[(unsigned char)c]);
+    pl.out_st.push_back(out_st[(unsigned char)c]);
+  }
   pl.dtab = static_cast<int64_t *>(g_eng.arena.take(tabs.size() * sizeof(int64_t)));
   if (!pl.dtab) {
     ttk::set_error("einsum: table allocation failed");
@@ -333,6 +342,16 @@ bool build_plan(const std::string &eq, int nops, const int *ndims, const int64_t
 
 int fused_apply_try(void *stream, const char *eq, const int64_t *desc, double *out, double alpha, double beta);
 static int g_fused_apply = 1;
+
+// einsum batches (defined at the end of this file)
+struct Span {
+  uintptr_t lo = 0, hi = 0;  // [lo, hi) bytes; empty when lo == hi
+};
+Span span_of(const void *p, int nd, const int64_t *shape, const int64_t *stride);
+bool batch_on();
+double *batch_scratch(int64_t n);
+int batch_add_gemm(const ttk::GemmProblem &g, const Span *rd, int nrd, Span wr);
+int batch_flush(hipStream_t st);
 
 extern "C" {
 
@@ -387,6 +406,8 @@ int ttk_einsum(void *stream, const char *eq, const int64_t *desc, double *out, d
   auto it = g_eng.plans.find(key);
   if (it == g_eng.plans.end()) {
     if (g_eng.plans.size() >= 200000) {  // bounded cache: drain the stream, then start over
+      const int rc = batch_flush(TTK_STREAM(stream));  // recorded steps point into the tables
+      if (rc != TTK_OK) return rc;
       if (hipStreamSynchronize(TTK_STREAM(stream)) != hipSuccess) return TTK_ERR_HIP;
       g_eng.plans.clear();
       g_eng.arena.reset();
@@ -399,7 +420,12 @@ int ttk_einsum(void *stream, const char *eq, const int64_t *desc, double *out, d
     ++g_eng.hits;
   }
   const Plan &pl = it->second;
-  if (pl.scratch > g_eng.scratch_n) {
+  const bool rec = batch_on();
+  double *scr = g_eng.scratch;
+  if (rec) {  // each recorded call gets its own intermediates (the batch's steps run out of order)
+    scr = batch_scratch(pl.scratch);
+    if (!scr && pl.scratch > 0) return TTK_ERR_HIP;
+  } else if (pl.scratch > g_eng.scratch_n) {
     // growing the shared scratch: earlier calls may still be using the old buffer on the stream
     if (g_eng.scratch) {
       TTK_HIP(hipStreamSynchronize(TTK_STREAM(stream)));
@@ -408,15 +434,27 @@ int ttk_einsum(void *stream, const char *eq, const int64_t *desc, double *out, d
     int64_t want = pl.scratch * 2 > (1 << 20) ? pl.scratch * 2 : (1 << 20);
     TTK_HIP(hipMalloc(reinterpret_cast<void **>(&g_eng.scratch), want * sizeof(double)));
     g_eng.scratch_n = want;
+    scr = g_eng.scratch;
   }
   if (!g_eng.ones) {
     TTK_HIP(hipMalloc(reinterpret_cast<void **>(&g_eng.ones), 64 * sizeof(double)));
     const double one[1] = {1.0};
     TTK_HIP(hipMemcpy(g_eng.ones, one, sizeof(double), hipMemcpyHostToDevice));
   }
+  Span in_sp[8], out_sp;
+  if (rec) {
+    for (int i = 0, o = 0; i < nops; o += ndims[i], ++i) in_sp[i] = span_of(ptrs[i], ndims[i], shapes + o, strides + o);
+    out_sp = span_of(out, (int)pl.out_ext.size(), pl.out_ext.data(), pl.out_st.data());
+  }
+  auto tmp_span = [&](const Step &t) {
+    Span sp;
+    sp.lo = reinterpret_cast<uintptr_t>(scr + t.tmp);
+    sp.hi = sp.lo + (uintptr_t)t.tmp_n * sizeof(double);
+    return sp;
+  };
   for (const Step &st : pl.steps) {
-    const double *A = st.a >= 0 ? ptrs[st.a] : g_eng.scratch + pl.steps[-st.a - 1].tmp;
-    const double *B = st.b == SLOT_ONES ? g_eng.ones : (st.b >= 0 ? ptrs[st.b] : g_eng.scratch + pl.steps[-st.b - 1].tmp);
+    const double *A = st.a >= 0 ? ptrs[st.a] : scr + pl.steps[-st.a - 1].tmp;
+    const double *B = st.b == SLOT_ONES ? g_eng.ones : (st.b >= 0 ? ptrs[st.b] : scr + pl.steps[-st.b - 1].tmp);
     double *C;
     double al = 1.0, be = 0.0;
     if (st.out == SLOT_FINAL) {
@@ -424,9 +462,19 @@ int ttk_einsum(void *stream, const char *eq, const int64_t *desc, double *out, d
       al = alpha;
       be = beta;
     } else {
-      C = g_eng.scratch + st.tmp;
+      C = scr + st.tmp;
     }
-    int rc = ttk_gemm_offs(stream, A, B, C, pl.dtab + st.offs, st.nb, st.M, st.N, st.K, al, be);
+    int rc;
+    if (rec) {
+      Span rd[2];
+      int nrd = 0;
+      rd[nrd++] = st.a >= 0 ? in_sp[st.a] : tmp_span(pl.steps[-st.a - 1]);
+      if (st.b != SLOT_ONES) rd[nrd++] = st.b >= 0 ? in_sp[st.b] : tmp_span(pl.steps[-st.b - 1]);
+      const ttk::GemmProblem g{A, B, C, pl.dtab + st.offs, st.nb, st.M, st.N, st.K, al, be};
+      rc = batch_add_gemm(g, rd, nrd, st.out == SLOT_FINAL ? out_sp : tmp_span(st));
+    } else {
+      rc = ttk_gemm_offs(stream, A, B, C, pl.dtab + st.offs, st.nb, st.M, st.N, st.K, al, be);
+    }
     if (rc != TTK_OK) return rc;
   }
   return TTK_OK;
@@ -659,6 +707,8 @@ static int apply_args(const char *eq, const int64_t *desc, double *out, double a
   return 1;
 }
 
+static int batch_add_fused(const ApplyArgs &g, int64_t lds_doubles);
+
 int fused_apply_try(void *stream, const char *eq, const int64_t *desc, double *out, double alpha, double beta) {
   if (!(desc[0] & 256)) return 0;  // caller did not opt in
   ApplyArgs g;
@@ -675,6 +725,7 @@ int fused_apply_try(void *stream, const char *eq, const int64_t *desc, double *o
   static const double env_max_flops =
       getenv("TTK_FUSED_ENV_MAX_FLOPS") ? atof(getenv("TTK_FUSED_ENV_MAX_FLOPS")) : 1e6;
   if (flops > ((desc[0] & 512) ? env_max_flops : max_flops)) return 0;
+  if (batch_on()) return batch_add_fused(g, need) == TTK_OK ? 1 : -1;
   const size_t shm = need * sizeof(double);
   if (shm > 65536)
     (void)hipFuncSetAttribute(reinterpret_cast<const void *>(fused_apply_kernel),
@@ -844,6 +895,246 @@ int ttk_schur_apply(void *stream, int64_t handle, const double *v, double *out) 
 
 int ttk_schur_free(int64_t handle) {
   if (handle >= 1 && handle <= (int64_t)g_schur.size()) g_schur[handle - 1].used = false;
+  return TTK_OK;
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------------ einsum batches
+// `ttk_einsum_batch_begin` .. `ttk_einsum_batch_end`: einsum calls are recorded instead of launched
+// (plans, offset tables and fused-apply decisions exactly as for a direct call; each call gets its
+// own intermediates).  Every recorded step is a node with the byte spans it reads and writes; a
+// node's level is one past the deepest earlier node it conflicts with (read-after-write,
+// write-after-read, write-after-write -- so accumulations into one output keep their order).  At
+// the end each level is launched as one grouped MFMA GEMM launch (problems that would take the
+// split-K or 64x64 path alone are launched alone) plus one grouped fused-apply launch, so a core
+// step's environment updates or a rank loop's candidate products cost a handful of launches
+// instead of one per pairwise step.  Results are bit-identical to the unbatched calls (same
+// kernels' per-element operations, same order per output element).  Any other libttk launch made
+// while a batch is open flushes the pending nodes first (ttk::batch_barrier), so stream order holds.
+namespace {
+
+struct BNode {
+  int kind;  // 0 gemm, 1 fused apply
+  ttk::GemmProblem g;
+  ApplyArgs f;
+  int64_t lds;
+  Span rd[4];
+  int nrd;
+  Span wr;
+  int level;
+};
+
+struct Batch {
+  int depth = 0;
+  std::vector<BNode> nodes;
+  std::vector<std::pair<double *, int64_t>> chunks;  // intermediates; kept across batches
+  size_t chunk = 0;
+  int64_t used = 0;
+  int max_level = -1;
+  long long flushes = 0, nodes_total = 0, launches = 0;
+};
+Batch g_batch;
+
+constexpr int FGROUP_MAX = 12;
+struct FusedGroup {
+  ApplyArgs t[FGROUP_MAX];
+  int off[FGROUP_MAX + 1];
+  int n;
+};
+
+__global__ __launch_bounds__(256) void fused_apply_group_kernel(FusedGroup G) {
+  extern __shared__ double sm[];
+  int t = 0;
+  while (t + 1 < G.n && (int)blockIdx.x >= G.off[t + 1]) ++t;
+  apply_row<true>(G.t[t], (int)blockIdx.x - G.off[t], sm, nullptr);
+}
+
+inline bool overlap(const Span &a, const Span &b) { return a.lo < b.hi && b.lo < a.hi; }
+
+bool conflict(const BNode &x, const BNode &y) {
+  if (overlap(x.wr, y.wr)) return true;
+  for (int i = 0; i < y.nrd; ++i)
+    if (overlap(x.wr, y.rd[i])) return true;
+  for (int i = 0; i < x.nrd; ++i)
+    if (overlap(x.rd[i], y.wr)) return true;
+  return false;
+}
+
+int add_node(BNode &n) {
+  n.level = 0;
+  for (const BNode &e : g_batch.nodes)
+    if (e.level >= n.level && conflict(e, n)) n.level = e.level + 1;
+  if (n.level > g_batch.max_level) g_batch.max_level = n.level;
+  g_batch.nodes.push_back(n);
+  return TTK_OK;
+}
+
+Span apply_span(const double *p, int n0, int64_t s0, int n1, int64_t s1, int n2, int64_t s2, int n3 = 1,
+                int64_t s3 = 0) {
+  const int64_t sh[4] = {n0, n1, n2, n3}, st[4] = {s0, s1, s2, s3};
+  return span_of(p, 4, sh, st);
+}
+
+int launch_fused_group(hipStream_t st, const std::vector<const BNode *> &v) {
+  for (size_t base = 0; base < v.size(); base += FGROUP_MAX) {
+    FusedGroup G;
+    G.n = (int)(v.size() - base < (size_t)FGROUP_MAX ? v.size() - base : FGROUP_MAX);
+    G.off[0] = 0;
+    int64_t lds = 0;
+    double flops = 0.0;
+    for (int i = 0; i < G.n; ++i) {
+      const BNode &n = *v[base + i];
+      G.t[i] = n.f;
+      G.off[i + 1] = G.off[i] + n.f.na;
+      lds = n.lds > lds ? n.lds : lds;
+      flops += term_flops(n.f);
+    }
+    const size_t shm = (size_t)lds * sizeof(double);
+    if (shm > 65536)
+      (void)hipFuncSetAttribute(reinterpret_cast<const void *>(fused_apply_group_kernel),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+    hipEvent_t e0, e1;
+    if (ttk::contract_events_ext(&e0, &e1) != TTK_OK) return TTK_ERR_HIP;
+    hipExtLaunchKernelGGL(fused_apply_group_kernel, dim3(G.off[G.n]), dim3(256), shm, st, e0, e1, 0, G);
+    TTK_LAUNCH_CHECK();
+    ttk::contract_count_ext(flops);
+    ++g_batch.launches;
+  }
+  return TTK_OK;
+}
+
+}  // namespace
+
+Span span_of(const void *p, int nd, const int64_t *shape, const int64_t *stride) {
+  Span s;
+  int64_t lo = 0, hi = 0;
+  for (int i = 0; i < nd; ++i) {
+    if (shape[i] <= 0) return s;
+    const int64_t e = (shape[i] - 1) * stride[i];
+    if (e < 0) lo += e;
+    else hi += e;
+  }
+  s.lo = reinterpret_cast<uintptr_t>(p) + lo * (int64_t)sizeof(double);
+  s.hi = reinterpret_cast<uintptr_t>(p) + (hi + 1) * (int64_t)sizeof(double);
+  return s;
+}
+
+bool batch_on() { return g_batch.depth > 0; }
+
+double *batch_scratch(int64_t n) {
+  if (n <= 0) return nullptr;
+  n = (n + 31) / 32 * 32;
+  while (true) {
+    if (g_batch.chunk < g_batch.chunks.size()) {
+      auto &c = g_batch.chunks[g_batch.chunk];
+      if (g_batch.used + n <= c.second) {
+        double *p = c.first + g_batch.used;
+        g_batch.used += n;
+        return p;
+      }
+      ++g_batch.chunk;
+      g_batch.used = 0;
+      continue;
+    }
+    const int64_t want = n > (int64_t(1) << 22) ? n : (int64_t(1) << 22);  // 32 MiB chunks
+    double *p = nullptr;
+    if (hipMalloc(reinterpret_cast<void **>(&p), want * sizeof(double)) != hipSuccess) {
+      ttk::set_error("einsum batch: scratch allocation failed");
+      return nullptr;
+    }
+    g_batch.chunks.push_back({p, want});
+  }
+}
+
+int batch_add_gemm(const ttk::GemmProblem &g, const Span *rd, int nrd, Span wr) {
+  if (g.nb <= 0 || g.M <= 0 || g.N <= 0) return TTK_OK;
+  BNode n{};
+  n.kind = 0;
+  n.g = g;
+  n.nrd = nrd;
+  for (int i = 0; i < nrd; ++i) n.rd[i] = rd[i];
+  n.wr = wr;
+  return add_node(n);
+}
+
+static int batch_add_fused(const ApplyArgs &g, int64_t lds_doubles) {
+  BNode n{};
+  n.kind = 1;
+  n.f = g;
+  n.lds = lds_doubles;
+  n.nrd = 4;
+  n.rd[0] = apply_span(g.P, g.na, g.ps[0], g.ns, g.ps[1], g.nb, g.ps[2]);
+  n.rd[1] = apply_span(g.A, g.ns, g.as[0], g.ni, g.as[1], g.nj, g.as[2], g.nS, g.as[3]);
+  n.rd[2] = apply_span(g.Q, g.nc, g.qs[0], g.nS, g.qs[1], g.nd, g.qs[2]);
+  n.rd[3] = apply_span(g.x, g.nb, g.xs[0], g.nj, g.xs[1], g.nd, g.xs[2]);
+  n.wr = apply_span(g.out, g.na, g.os[0], g.ni, g.os[1], g.nc, g.os[2]);
+  return add_node(n);
+}
+
+int batch_flush(hipStream_t st) {
+  if (g_batch.nodes.empty()) return TTK_OK;
+  std::vector<ttk::GemmProblem> grp;
+  std::vector<const BNode *> fused;
+  int rc = TTK_OK;
+  for (int lv = 0; lv <= g_batch.max_level && rc == TTK_OK; ++lv) {
+    grp.clear();
+    fused.clear();
+    for (const BNode &n : g_batch.nodes) {
+      if (n.level != lv) continue;
+      if (n.kind == 1) {
+        fused.push_back(&n);
+      } else if (ttk::gemm_groupable(n.g.nb, n.g.M, n.g.N, n.g.K)) {
+        grp.push_back(n.g);
+      } else {
+        rc = ttk_gemm_offs(st, n.g.A, n.g.B, n.g.C, n.g.offs, n.g.nb, n.g.M, n.g.N, n.g.K, n.g.alpha, n.g.beta);
+        ++g_batch.launches;
+        if (rc != TTK_OK) break;
+      }
+    }
+    if (rc == TTK_OK && !grp.empty()) {
+      rc = ttk::gemm_group(st, grp.data(), (int)grp.size());
+      g_batch.launches += (long long)(grp.size() + 23) / 24;
+    }
+    if (rc == TTK_OK && !fused.empty()) rc = launch_fused_group(st, fused);
+  }
+  g_batch.nodes_total += (long long)g_batch.nodes.size();
+  ++g_batch.flushes;
+  g_batch.nodes.clear();
+  g_batch.max_level = -1;
+  g_batch.chunk = 0;
+  g_batch.used = 0;
+  return rc;
+}
+
+namespace ttk {
+int batch_barrier(void *stream) { return batch_flush(TTK_STREAM(stream)); }
+}  // namespace ttk
+
+extern "C" {
+
+int ttk_einsum_batch_begin(void *stream) {
+  (void)stream;
+  ++g_batch.depth;
+  return TTK_OK;
+}
+
+int ttk_einsum_batch_flush(void *stream) { return batch_flush(TTK_STREAM(stream)); }
+
+int ttk_einsum_batch_end(void *stream) {
+  if (g_batch.depth <= 0) {
+    ttk::set_error("ttk_einsum_batch_end without begin");
+    return TTK_ERR_ARG;
+  }
+  const int rc = batch_flush(TTK_STREAM(stream));
+  --g_batch.depth;
+  return rc;
+}
+
+int ttk_einsum_batch_stats(long long *out) {
+  out[0] = g_batch.flushes;
+  out[1] = g_batch.nodes_total;
+  out[2] = g_batch.launches;
   return TTK_OK;
 }
 

@@ -28,12 +28,43 @@ _vp = ctypes.c_void_p
 _STREAM = []
 
 
+_BATCH = [0]  # open einsum batches (dev.einsum_batch)
+# operands of recorded (not yet launched) einsum steps: held until the flush so that the caching
+# allocator cannot hand their memory to an allocation whose kernels run before the recorded steps
+_KEEP = []
+
+
 def _stream():
     """The launch stream (the device's current stream when first used; the path never switches
     streams, and torch.cuda.current_stream() costs ~10 us per call)."""
     if not _STREAM:
         _STREAM.append(torch.cuda.current_stream().cuda_stream if DEV.type == "cuda" else None)
+    if _BATCH[0]:  # any launch other than an einsum first flushes the recorded steps (stream order)
+        check(lib.ttk_einsum_batch_flush(_STREAM[0]), "einsum_batch_flush")
+        _KEEP.clear()
     return _STREAM[0]
+
+
+class einsum_batch:
+    """`with dev.einsum_batch(): ...` -- the einsum calls inside are recorded and launched at the end
+    as grouped launches, one per dependency level (ttk_einsum_batch_*, bit-identical results).
+    Other device operations inside the block stay correct (they flush the pending steps first) but
+    split the batch, so keep batch bodies to einsums and fresh allocations."""
+
+    def __enter__(self):
+        if DEV.type == "cuda":
+            _stream()
+            check(lib.ttk_einsum_batch_begin(_STREAM[0]), "einsum_batch_begin")
+            _BATCH[0] += 1
+        return self
+
+    def __exit__(self, *exc):
+        if DEV.type == "cuda":
+            _BATCH[0] -= 1
+            check(lib.ttk_einsum_batch_end(_STREAM[0]), "einsum_batch_end")
+            if not _BATCH[0]:
+                _KEEP.clear()
+        return False
 
 
 def _p(t):
@@ -268,6 +299,18 @@ def dot_into(x, y, out):
                              _p(out)), "dot_into")
 
 
+def rank_scan(res, negs):
+    """res <- res - negs[q] for q in order, <res, res> after each (one launch, one read); the
+    per-candidate copy_(res, neg, -1, 1) + dot(res, res) of the rank loop, bit for bit."""
+    assert res.is_contiguous() and negs.is_contiguous() and tuple(negs.shape[1:]) == tuple(res.shape)
+    nq = negs.shape[0]
+    out = np.empty(nq)
+    if nq:
+        check(lib.ttk_rank_scan_sync(_stream(), _p(res), _p(negs), res.numel(), nq, out.ctypes.data_as(c_dp)),
+              "rank_scan")
+    return out
+
+
 def norm_of(d):
     """dev.norm's host formula applied to a read-back <x, x>."""
     return float(np.sqrt(max(float(d), 0.0)))
@@ -397,9 +440,18 @@ def einsum(eq, *ops, out=None, alpha=1.0, beta=0.0, fused=False, algo=None):
         else:
             count_algo(algo_flops(eq, tuple(tuple(o.shape) for o in ops)), what=eq)
     fused = fused or _FUSED_ALL
+    if _BATCH[0]:
+        if out is None:
+            out = _new_out(eq, ops)
+            beta = 0.0
+        _KEEP.append((ops, out))
     if _CHECK_FUSED and fused and eq in _FUSED_EQS:
         return _einsum_checked(eq, ops, out, alpha, beta)
     return _einsum_native(eq, *ops, out=out, alpha=alpha, beta=beta, fused=fused)
+
+
+def _new_out(eq, ops):
+    return empty(*_out_shape(eq, tuple(tuple(o.shape) for o in ops)))
 
 
 def _einsum_native(eq, *ops, out=None, alpha=1.0, beta=0.0, fused=False):
@@ -427,7 +479,8 @@ def _einsum_native(eq, *ops, out=None, alpha=1.0, beta=0.0, fused=False):
         desc.append(1)
         desc.append(out.dim())
         desc.extend(out.stride())
-    check(lib.ttk_einsum(_stream(), _eq_bytes(eq), (ctypes.c_int64 * len(desc))(*desc), out.data_ptr(),
+    _stream() if not _STREAM else None
+    check(lib.ttk_einsum(_STREAM[0], _eq_bytes(eq), (ctypes.c_int64 * len(desc))(*desc), out.data_ptr(),
                          float(alpha), float(beta)), "einsum")
     return out
 

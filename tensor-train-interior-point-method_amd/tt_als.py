@@ -141,9 +141,14 @@ class TTBlockMatrixView:
         return self.bm._data.keys()
 
     def block_local_product(self, L, R, x, out=None):
-        """`block_local_product` (`:190-200`); accumulates into `out` when given."""
+        """`block_local_product` (`:190-200`); accumulates into `out` when given.  The block applies
+        run as one einsum batch (grouped launches per dependency level)."""
         if out is None:
             out = D.zeros(*x.shape)
+        with D.einsum_batch():
+            return self._block_local_product(L, R, x, out)
+
+    def _block_local_product(self, L, R, x, out):
         for (i, j) in self.bm._data:
             A = self[i, j]
             einsum(APPLY, L[i, j], A, R[i, j], x[:, j], out=out[:, i], beta=1.0)
@@ -156,6 +161,10 @@ class TTBlockMatrixView:
         return out
 
     def _compressed(self, L, R, x, out, teq, tL, tR):
+        with D.einsum_batch():
+            return self._compressed_body(L, R, x, out, teq, tL, tR)
+
+    def _compressed_body(self, L, R, x, out, teq, tL, tR):
         for (i, j) in self.bm._data:
             A = self[i, j]
             einsum(APPLY, L[i, j], A, R[i, j], x[:, j], out=out[:, i], beta=1.0)
@@ -182,8 +191,9 @@ class TTBlockMatrixView:
 
 def rhs_local_product(bcore, L, R, out, alpha=1.0):
     """`TTBlockVectorView.block_local_product` (`src/tt_als.py:79-83`), accumulated into out."""
-    for i, c in bcore.items():
-        einsum("br,bnB,BR->rnR", L[i], c, R[i], out=out[:, i], alpha=alpha, beta=1.0)
+    with D.einsum_batch():
+        for i, c in bcore.items():
+            einsum("br,bnB,BR->rnR", L[i], c, R[i], out=out[:, i], alpha=alpha, beta=1.0)
     return out
 
 
@@ -349,16 +359,23 @@ def _sweep(c, backward, swp, last, dsf):
             res = D.scaled(rhs, -1.0)
             Ak.block_local_product(c.XAX[k], c.XAX[k + 1], cur, out=res)
             r = r0
-            for r in range(r0 - 1, 0, -1):
-                if backward:
-                    piece = einsum("i,j->ji", U[:, r], v[r]).view(rx[k], B, N[k], rx[k + 1])
-                else:
-                    piece = einsum("rb,dk->rdbk", u3[:, :, r], v3[r])
-                neg = D.zeros(*piece.shape)
-                Ak.block_local_product(c.XAX[k], c.XAX[k + 1], piece, out=neg)
-                D.copy_(res, neg, -1.0, 1.0)
-                if D.norm(res) / nrhs > trunc_lim:
-                    break
+            # every candidate's product in one einsum batch, then the sequential residual updates and
+            # norms in one scan (one host read); the break rule is replayed on the host unchanged
+            cands = list(range(r0 - 1, 0, -1))
+            if cands:
+                negs = D.zeros(len(cands), *res.shape)
+                with D.einsum_batch():
+                    for q, rr in enumerate(cands):
+                        if backward:
+                            piece = einsum("i,j->ji", U[:, rr], v[rr]).view(rx[k], B, N[k], rx[k + 1])
+                        else:
+                            piece = einsum("rb,dk->rdbk", u3[:, :, rr], v3[rr])
+                        Ak._block_local_product(c.XAX[k], c.XAX[k + 1], piece, negs[q])
+                ss = D.rank_scan(res, negs)
+                for q, rr in enumerate(cands):
+                    r = rr
+                    if D.norm_of(ss[q]) / nrhs > trunc_lim:
+                        break
             r += 1
             if backward:
                 u_new = D.clone(U[:, :r].t()).view(r, N[k], rx[k + 1])
@@ -416,16 +433,13 @@ def _sweep(c, backward, swp, last, dsf):
             x[k] = D.contig(u)
             x[k - 1] = _div_blocks_bdim(einsum("rdc,cbR->rbdR", x[k - 1], vv), inv, 1)
             rx[k] = r
-            c.XAX[k] = {key: compute_phi_bck_A(c.XAX[k + 1][key], x[k], Ak[key], x[k]) for key in Ak.keys()}
-            c.Xb[k] = {i: compute_phi_bck_rhs(c.Xb[k + 1][i], bk[i], x[k]) for i in bk}
         else:
             nv = einsum("rbR,Rdk->rbdk", vv, x[k + 1])
             x[k] = D.contig(u)
             x[k + 1] = _div_blocks_bdim(nv.view(r, B, N[k + 1], rx[k + 2]), inv, 1)
             rx[k + 1] = r
-            c.XAX[k + 1] = {key: compute_phi_fwd_A(c.XAX[k][key], x[k], Ak[key], x[k]) for key in Ak.keys()}
-            c.Xb[k + 1] = {i: compute_phi_fwd_rhs(c.Xb[k][i], bk[i], x[k]) for i in bk}
 
+        zk = None
         if amen and not last:
             kr = min(c.kick_rank, *resz.shape)
             uz, vz = truncated_svd(resz, kr)
@@ -435,22 +449,34 @@ def _sweep(c, backward, swp, last, dsf):
                 z[k] = uzc
                 z[k - 1] = _div_blocks_bdim(einsum("rdc,cbR->rbdR", z[k - 1], vzc), inv, 1)
                 rz[k] = kr
-                zz = {key: compute_phi_bck_A(c.ZAX[k + 1][key], z[k], Ak[key], x[k]) for key in Ak.keys()}
-                zz.update({lt: compute_phi_bck_A(c.ZAX[k + 1][lt], z[k], Ak[ij].transpose(1, 2), x[k])
-                           for ij, lt in Ak._transposes.items()})
-                c.ZAX[k] = zz
-                c.Zb[k] = {i: compute_phi_bck_rhs(c.Zb[k + 1][i], bk[i], z[k]) for i in bk}
             else:
                 uzc = D.contig(uz).view(rz[k], N[k], kr)
                 vzc = D.contig(vz).view(kr, B, rz[k + 1])
                 z[k] = uzc
                 z[k + 1] = _div_blocks_bdim(einsum("rbR,Rdk->rbdk", vzc, z[k + 1]), inv, 1)
                 rz[k + 1] = kr
-                zz = {key: compute_phi_fwd_A(c.ZAX[k][key], z[k], Ak[key], x[k]) for key in Ak.keys()}
-                zz.update({lt: compute_phi_fwd_A(c.ZAX[k][lt], z[k], Ak[ij].transpose(1, 2), x[k])
-                           for ij, lt in Ak._transposes.items()})
-                c.ZAX[k + 1] = zz
-                c.Zb[k + 1] = {i: compute_phi_fwd_rhs(c.Zb[k][i], bk[i], z[k]) for i in bk}
+            zk = z[k]
+        # every environment of the core step (XAX/Xb and, for AMEn, ZAX/Zb; src/tt_als.py:372-387,
+        # 499-514) in one einsum batch: grouped launches instead of one launch per block
+        with D.einsum_batch():
+            if backward:
+                c.XAX[k] = {key: compute_phi_bck_A(c.XAX[k + 1][key], x[k], Ak[key], x[k]) for key in Ak.keys()}
+                c.Xb[k] = {i: compute_phi_bck_rhs(c.Xb[k + 1][i], bk[i], x[k]) for i in bk}
+                if zk is not None:
+                    zz = {key: compute_phi_bck_A(c.ZAX[k + 1][key], zk, Ak[key], x[k]) for key in Ak.keys()}
+                    zz.update({lt: compute_phi_bck_A(c.ZAX[k + 1][lt], zk, Ak[ij].transpose(1, 2), x[k])
+                               for ij, lt in Ak._transposes.items()})
+                    c.ZAX[k] = zz
+                    c.Zb[k] = {i: compute_phi_bck_rhs(c.Zb[k + 1][i], bk[i], zk) for i in bk}
+            else:
+                c.XAX[k + 1] = {key: compute_phi_fwd_A(c.XAX[k][key], x[k], Ak[key], x[k]) for key in Ak.keys()}
+                c.Xb[k + 1] = {i: compute_phi_fwd_rhs(c.Xb[k][i], bk[i], x[k]) for i in bk}
+                if zk is not None:
+                    zz = {key: compute_phi_fwd_A(c.ZAX[k][key], zk, Ak[key], x[k]) for key in Ak.keys()}
+                    zz.update({lt: compute_phi_fwd_A(c.ZAX[k][lt], zk, Ak[ij].transpose(1, 2), x[k])
+                               for ij, lt in Ak._transposes.items()})
+                    c.ZAX[k + 1] = zz
+                    c.Zb[k + 1] = {i: compute_phi_fwd_rhs(c.Zb[k][i], bk[i], zk) for i in bk}
     if dx_seq:
         n_used = sum(1 for j in dx_seq if j is not None)
         vals = D.read(dx_buf[:2 * n_used]) if n_used else None

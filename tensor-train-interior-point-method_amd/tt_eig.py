@@ -420,8 +420,9 @@ def tt_max_generalised_eigen(A, Delta, x0=None, nswp=10, tol=1e-8, size_limit=25
                 x[k] = D.clone(U[:, :r]).view(rx[k], N[k], r)
                 x[k + 1] = einsum("ij,jkl->ikl", v[:r], x[k + 1])
                 rx[k + 1] = r
-                XAX[k + 1] = compute_phi_fwd_A(XAX[k], x[k], A[k], x[k])
-                XDX[k + 1] = compute_phi_fwd_A(XDX[k], x[k], Delta[k], x[k])
+                with D.einsum_batch():
+                    XAX[k + 1] = compute_phi_fwd_A(XAX[k], x[k], A[k], x[k])
+                    XDX[k + 1] = compute_phi_fwd_A(XDX[k], x[k], Delta[k], x[k])
             else:
                 x[k] = D.contig(sol).view(rx[k], N[k], rx[k + 1])
 
@@ -438,8 +439,9 @@ def tt_max_generalised_eigen(A, Delta, x0=None, nswp=10, tol=1e-8, size_limit=25
                 x[k] = D.clone(U[:, :r].t()).view(r, N[k], rx[k + 1])
                 x[k - 1] = einsum("rdc,Rc->rdR", x[k - 1], v[:r])
                 rx[k] = r
-                XAX[k] = compute_phi_bck_A(XAX[k + 1], x[k], A[k], x[k])
-                XDX[k] = compute_phi_bck_A(XDX[k + 1], x[k], Delta[k], x[k])
+                with D.einsum_batch():
+                    XAX[k] = compute_phi_bck_A(XAX[k + 1], x[k], A[k], x[k])
+                    XDX[k] = compute_phi_bck_A(XDX[k + 1], x[k], Delta[k], x[k])
             else:
                 x[k] = D.contig(sol).view(rx[k], N[k], rx[k + 1])
 

@@ -240,6 +240,27 @@ class EmuLib:
         out._obj.value = val
         return 0
 
+    def ttk_einsum_batch_begin(self, s):
+        return 0
+
+    def ttk_einsum_batch_flush(self, s):
+        return 0
+
+    def ttk_einsum_batch_end(self, s):
+        return 0
+
+    def ttk_einsum_batch_stats(self, out):
+        return 0
+
+    def ttk_rank_scan_sync(self, s, res, negs, n, nq, out):
+        r = _dv(res, n)
+        ng = _dv(negs, n * nq).reshape(nq, n)
+        o = np.ctypeslib.as_array((ctypes.c_double * int(nq)).from_address(ctypes.cast(out, ctypes.c_void_p).value))
+        for q in range(nq):
+            r[:] = -1.0 * ng[q] + r
+            o[q] = float(np.dot(r, r))
+        return 0
+
     def ttk_sumsq_batched(self, s, x, n, nb, bstride, out):
         xv = _dv(x, (nb - 1) * bstride + n)
         o = _dv(out, nb)

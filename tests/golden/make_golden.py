@@ -188,12 +188,17 @@ RUNS = [
     ("corr_clust", "corr_clust_9", 764, 1, True, 0),
     ("corr_clust", "corr_clust_9", 764, 1, False, 0),
     ("graphm", "graphm_3", 256, 2, True, 2),
+    ("graphm", "graphm_3", 256, 2, True, 0),
     ("maxcut", "maxcut_12", 80, 2, True, 0),
 ]
 
 
+THREADS = int(os.environ.get("GOLDEN_THREADS", "1"))  # >1: the thread-spread runs (key suffix _t<N>)
+
+
 def run_key(cfg, rank, seed, fixed, nmax):
-    return f"{cfg}_r{rank}_s{seed}" + ("" if fixed else "_shipped") + (f"_b{nmax}" if nmax else "")
+    return f"{cfg}_r{rank}_s{seed}" + ("" if fixed else "_shipped") + (f"_b{nmax}" if nmax else "") + \
+        (f"_t{THREADS}" if THREADS > 1 else "")
 
 
 def make_runs(only=None, jobs=1):
@@ -209,7 +214,7 @@ def make_runs(only=None, jobs=1):
             continue
         todo.append((key, [sys.executable, __file__, "one", prob, cfg, str(seed), str(rank), str(int(fixed)),
                            os.path.join("/tmp", f"golden_{key}.json"), str(nmax)]))
-    env = dict(os.environ, PYTHONHASHSEED="0", OPENBLAS_NUM_THREADS="1", OMP_NUM_THREADS="1")
+    env = dict(os.environ, PYTHONHASHSEED="0", OPENBLAS_NUM_THREADS=str(THREADS), OMP_NUM_THREADS=str(THREADS))
     running = []
     while todo or running:
         while todo and len(running) < jobs:

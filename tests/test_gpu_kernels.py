@@ -436,3 +436,74 @@ def test_elementwise_and_reductions(dev):
     assert np.allclose(dev.read(out), 2 * np.swapaxes(a, 1, 2) + np.swapaxes(a * b, 1, 2))
     r = dev.recip(dev.from_numpy(np.array([2.0, 4.0])))
     assert np.allclose(dev.read(r), [0.5, 0.25])
+
+
+def test_einsum_batch_is_bit_identical(dev):
+    """recorded + grouped launches (ttk_einsum_batch_*) give the same bits as one call at a time:
+    environment updates (fused and pairwise), accumulation into one output, dependent chains"""
+    import ctypes
+    from ttipm_amd._lib import lib
+    from ttipm_amd.tt_als import compute_phi_bck_A, compute_phi_fwd_A
+    rng = _rng(11)
+    ops = []
+    for (r, s, R) in [(3, 2, 4), (7, 5, 6), (13, 10, 13), (5, 3, 5)]:
+        ops.append(dict(P=dev.from_numpy(rng.standard_normal((r, s, r))),
+                        Q=dev.from_numpy(rng.standard_normal((R, s, R))),
+                        xl=dev.from_numpy(rng.standard_normal((r, 4, R))),
+                        A=dev.from_numpy(rng.standard_normal((s, 4, 4, s))),
+                        v=dev.from_numpy(rng.standard_normal((r, 4, R)))))
+    big = [dev.from_numpy(rng.standard_normal((70, 45))), dev.from_numpy(rng.standard_normal((45, 33)))]
+
+    def work():
+        outs = []
+        for o in ops:
+            outs.append(compute_phi_fwd_A(o["P"], o["xl"], o["A"], o["xl"]))
+            outs.append(compute_phi_bck_A(o["Q"], o["xl"], o["A"], o["xl"]))
+            acc = dev.zeros(*o["v"].shape)
+            dev.einsum("lsr,smnS,LSR,rnR->lmL", o["P"], o["A"], o["Q"], o["v"], out=acc, beta=1.0)
+            dev.einsum("lsr,smnS,LSR,rnR->lmL", o["P"], o["A"], o["Q"], o["v"], out=acc, alpha=-0.5, beta=1.0)
+            outs.append(acc)
+            t = dev.einsum("ik,kj->ij", big[0], big[1])
+            outs.append(dev.einsum("ij,kj->ik", t, big[1]))  # depends on t inside the batch
+        return [dev.read(x) for x in outs]
+
+    ref = work()
+    st0 = (ctypes.c_longlong * 3)()
+    lib.ttk_einsum_batch_stats(st0)
+    l0 = lib.ttk_launch_count()
+    outs = []  # recorded without reads inside the block (a read would flush it early)
+    with dev.einsum_batch():
+        for o in ops:
+            outs.append(compute_phi_fwd_A(o["P"], o["xl"], o["A"], o["xl"]))
+            outs.append(compute_phi_bck_A(o["Q"], o["xl"], o["A"], o["xl"]))
+            acc = dev.zeros(*o["v"].shape)
+            dev.einsum("lsr,smnS,LSR,rnR->lmL", o["P"], o["A"], o["Q"], o["v"], out=acc, beta=1.0)
+            dev.einsum("lsr,smnS,LSR,rnR->lmL", o["P"], o["A"], o["Q"], o["v"], out=acc, alpha=-0.5, beta=1.0)
+            outs.append(acc)
+            t = dev.einsum("ik,kj->ij", big[0], big[1])
+            outs.append(dev.einsum("ij,kj->ik", t, big[1]))
+    launches = lib.ttk_launch_count() - l0
+    st1 = (ctypes.c_longlong * 3)()
+    lib.ttk_einsum_batch_stats(st1)
+    assert st1[1] > st0[1]  # steps were recorded
+    got = [dev.read(x) for x in outs]
+    assert len(got) == len(ref)
+    for a, b in zip(got, ref):
+        assert np.array_equal(a, b)
+    assert launches < 4 * len(ops) * 3  # grouped: far fewer launches than steps
+
+
+def test_rank_scan_matches_sequential_updates(dev):
+    """ttk_rank_scan_sync == the loop of copy_(res, neg, -1, 1) + dot(res, res), bit for bit"""
+    rng = _rng(12)
+    res0 = rng.standard_normal((5, 3, 4, 6))
+    negs = rng.standard_normal((7, 5, 3, 4, 6)) * 1e-3
+    r1 = dev.from_numpy(res0)
+    ss_ref = []
+    for q in range(7):
+        dev.copy_(r1, dev.from_numpy(negs[q]), -1.0, 1.0)
+        ss_ref.append(dev.dot(r1, r1))
+    r2 = dev.from_numpy(res0)
+    ss = dev.rank_scan(r2, dev.from_numpy(negs))
+    assert list(ss) == ss_ref
+    assert np.array_equal(dev.read(r1), dev.read(r2))

@@ -348,8 +348,11 @@ TRAJ_RTOL = 1e-4
 FINAL_RTOL = 1e-2
 
 
-@pytest.mark.parametrize("key", ["maxcut_5_r1_s0", "maxcut_5_r1_s319", "maxcut_10_r1_s41",
-                                 "corr_clust_9_r1_s764_shipped"])
+FULL_KEYS = sorted(k for k, v in RUNS.items() if not v.get("bounded") and not k.startswith("maxcut_12")
+                   and "_t" not in k.rsplit("_s", 1)[-1])
+
+
+@pytest.mark.parametrize("key", FULL_KEYS)
 def test_full_solve_matches_reference(dev, key):
     from ttipm_amd._lib import lib
     l0 = lib.ttk_launch_count()
