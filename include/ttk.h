@@ -17,10 +17,9 @@
  *     `ttk_last_error()` returns a thread-local message for the last failure;
  *   - functions whose name ends in `_sync` block on `stream` and return host scalars that drive
  *     host-side decisions (rank truncation, convergence tests);
- *   - threading: one host thread and one stream per process (the reference's model, SURVEY.md
- *     §8(b)); plan cache, split-K / LGMRES / Schur scratch, the upload ring and the mapped read
- *     buffer are process-global and stream-ordered, so concurrent calls from several host
- *     threads or on several streams are not supported.
+ *   - threading: one host thread per context (ttk_ctx below); all scratch, staging and handle
+ *     state is per context, the einsum plan cache is shared and lock-protected.  The roofline
+ *     statistics (ttk_contract_stats / _timing) are process-wide.
  */
 #ifndef TTK_H
 #define TTK_H
@@ -39,6 +38,22 @@ enum ttk_status {
   TTK_ERR_SINGULAR = 4,     /* LU / triangular: exact zero pivot (scipy LinAlgError) */
   TTK_ERR_NOT_CONVERGED = 5 /* iterative kernel hit its sweep cap */
 };
+
+/* ---------------------------------------------------------------------------------------
+ * Contexts.  A context owns every piece of mutable library state between calls -- einsum
+ * intermediates and batch recorder, split-K slabs, LGMRES partials, Schur operator handles,
+ * factorisation status words, the pinned upload ring and the host-coherent read buffer -- and
+ * the HIP stream its work goes to.  Entry points taking a ttk_ctx run on that context; the older
+ * entry points (taking a stream) run on the calling thread's bound context (ttk_ctx_bind), or on
+ * the process default context when none is bound.  Two contexts driven by two host threads on two
+ * streams of one GPU share only the (lock-protected, immutable-once-built) einsum plan cache, so
+ * several seeds can be solved concurrently on one device.  Schur handles are per context.
+ * ------------------------------------------------------------------------------------- */
+typedef struct ttk_ctx_s *ttk_ctx;
+int ttk_ctx_create(void *stream, ttk_ctx *out);
+int ttk_ctx_destroy(ttk_ctx ctx);      /* synchronises the context's stream, frees its buffers */
+int ttk_ctx_bind(ttk_ctx ctx);         /* make ctx current for the calling thread (NULL: default) */
+void *ttk_ctx_stream(ttk_ctx ctx);
 
 const char *ttk_last_error(void);
 int ttk_version(void);
@@ -83,6 +98,25 @@ int ttk_einsum_batch_begin(void *stream);
 int ttk_einsum_batch_flush(void *stream);
 int ttk_einsum_batch_end(void *stream);
 int ttk_einsum_batch_stats(long long *out3);
+
+/* Environment (interface) updates of one AMEn / ALS core step, every block in one call
+ * (`compute_phi_fwd_A` / `compute_phi_bck_A`, `src/tt_als.py:252-257`, applied to all blocks of the
+ * step, `src/tt_als.py:372-387,499-514`):
+ *   forward   out[L,S,R] = sum phi[l,s,r] x[l,M,L] A[s,M,N,S] y[r,N,R]
+ *   backward  out[l,s,r] = sum phi[L,S,R] x[l,M,L] A[s,M,N,S] y[r,N,R]
+ * phi, x, y, out contiguous; A through a_strides (a transposed operator block is a stride swap).
+ * Recorded as one einsum batch on the context's stream (grouped launches), so the results equal
+ * nblocks separate relabelled local applies bit for bit. */
+typedef struct {
+  const double *phi;
+  const double *x;
+  const double *A;
+  const double *y;
+  double *out;
+  int64_t phi_shape[3], x_shape[3], A_shape[4], y_shape[3];
+  int64_t a_strides[4];
+} ttk_env_block;
+int ttk_env_update(ttk_ctx ctx, int backward, int nblocks, const ttk_env_block *blocks);
 
 /* AMEn rank loop (`src/tt_als.py:334-346`, `:462-472`): res (n contiguous doubles) is updated
  * res <- res - negs[q] for q = 0..nq-1 in order and <res, res> after each update is returned in
@@ -289,6 +323,22 @@ int ttk_lgmres_aug(void *stream, const double *hh, int max_k, int it_total, cons
  * kernels (default 16384 elements); 0 forces them everywhere, INT_MAX disables them (tests).
  * Returns the previous threshold. */
 int ttk_lgmres_set_mw_threshold(int elems);
+
+/* Whole local KKT solve by LGMRES (PETSc KSPLGMRES semantics, `src/tt_ipm.py:101-162,249-266`):
+ * solves A x = b from x0 = 0 with A the Schur operator `schur` (ttk_schur_build, the context's
+ * handle table), restart/augment/rtol/max_it as the reference sets them (`src/tt_ipm.py:249-251`),
+ * Arnoldi steps enqueued in speculative chunks of `chunk` steps with one host read per chunk.
+ * info: PETSc convergence reason (2 rtol, 3 atol, -3 its, -2 null, -5 breakdown, -4 dtol, -9 nan),
+ * iterations, last residual estimate, operator applications.  TTK_ERR_NOT_CONVERGED: HH(it,it) = 0
+ * (PETSC_ERR_CONV_FAILED, the reference's exception path). */
+typedef struct {
+  int reason;
+  int its;
+  double res;
+  int matvecs;
+} ttk_lgmres_info;
+int ttk_lgmres(ttk_ctx ctx, int64_t schur, const double *b, double *x, int64_t n, int restart, int augment,
+               double rtol, int max_it, int chunk, ttk_lgmres_info *info);
 
 #ifdef __cplusplus
 }

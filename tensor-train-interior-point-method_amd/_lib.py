@@ -71,6 +71,12 @@ _SIGS = {
     "ttk_einsum_batch_end": (i32, [vp]),
     "ttk_einsum_batch_stats": (i32, [vp]),
     "ttk_rank_scan_sync": (i32, [vp, vp, vp, i64, i32, vp]),
+    "ttk_ctx_create": (i32, [vp, vp]),
+    "ttk_ctx_destroy": (i32, [vp]),
+    "ttk_ctx_bind": (i32, [vp]),
+    "ttk_ctx_stream": (vp, [vp]),
+    "ttk_lgmres": (i32, [vp, i64, vp, vp, i64, i32, i32, f64, i32, i32, vp]),
+    "ttk_env_update": (i32, [vp, i32, i32, vp]),
     "ttk_einsum_set_fused": (i32, [i32]),
     "ttk_qr_set_big_threshold": (i32, [i32]),
     "ttk_contract_timing": (i32, [i32]),

@@ -78,8 +78,29 @@ def build_bind(force=False, verbose=False):
     return BIND_OUT
 
 
+CTEST_SRC = os.path.join(HERE, "..", "tests", "c", "test_abi.cpp")
+CTEST_OUT = os.path.join(HERE, "..", "tests", "c", "test_abi")
+
+
+def build_ctest(force=False, verbose=False):
+    """The C-ABI test program (tests/c/test_abi.cpp): host code only, linked against libttk.so and
+    the HIP runtime, rpath'd to the in-tree library."""
+    if not os.path.exists(CTEST_SRC):
+        return None
+    deps = [CTEST_SRC, OUT, os.path.join(HERE, "..", "include", "ttk.h")]
+    if not force and os.path.exists(CTEST_OUT) and all(os.path.getmtime(CTEST_OUT) >= os.path.getmtime(d) for d in deps):
+        return CTEST_OUT
+    cmd = ["hipcc", "-O2", "-std=c++17", "-o", CTEST_OUT, CTEST_SRC, "-L" + HERE, "-lttk", "-lpthread",
+           "-Wl,-rpath,$ORIGIN/../../tensor-train-interior-point-method_amd"]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.check_call(cmd, cwd=HERE)
+    return CTEST_OUT
+
+
 if __name__ == "__main__":
     defs = [a[2:] for a in sys.argv[1:] if a.startswith("-D")]
     outs = [a[6:] for a in sys.argv[1:] if a.startswith("--out=")]
     print(build(force="--force" in sys.argv, verbose=True, out=outs[0] if outs else OUT, defines=defs))
     print(build_bind(force="--force" in sys.argv, verbose=True))
+    print(build_ctest(force="--force" in sys.argv, verbose=True))

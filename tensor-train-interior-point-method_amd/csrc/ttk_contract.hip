@@ -521,7 +521,6 @@ inline int grid_for(int64_t n, int block) {
   return static_cast<int>(g);
 }
 
-double *g_dev_scalar = nullptr;
 
 // Contraction-kernel accounting (bench.py roofline): algorithmic FLOPs (2*M*N*K per GEMM step,
 // the opt_einsum convention of SURVEY.md 8(d)) are always counted; with timing on, every
@@ -594,23 +593,23 @@ extern "C" {
 namespace {
 bool g_splitk_on = true;
 
-double *splitk_scratch(int64_t n) {  // partial-sum slabs (grown, never shrunk; one stream)
-  static double *p = nullptr;
-  static int64_t cap = 0;
-  if (n > cap) {
-    if (p) {
-      (void)hipDeviceSynchronize();  // earlier split-K launches may still read the old slab
-      (void)hipFree(p);
+double *splitk_scratch(int64_t n) {  // partial-sum slabs of the current context (grown, never shrunk)
+  ttk::Ctx &c = ttk::ctx();
+  if (n > c.splitk_n) {
+    if (c.splitk) {
+      // earlier split-K launches may still read the old slab
+      (void)(c.stream ? hipStreamSynchronize(c.stream) : hipDeviceSynchronize());
+      (void)hipFree(c.splitk);
     }
     const int64_t want = n < (1 << 20) ? (1 << 20) : 2 * n;
-    if (hipMalloc(reinterpret_cast<void **>(&p), want * sizeof(double)) != hipSuccess) {
-      p = nullptr;
-      cap = 0;
+    if (hipMalloc(reinterpret_cast<void **>(&c.splitk), want * sizeof(double)) != hipSuccess) {
+      c.splitk = nullptr;
+      c.splitk_n = 0;
       return nullptr;
     }
-    cap = want;
+    c.splitk_n = want;
   }
-  return p;
+  return c.splitk;
 }
 
 // diagnostics: launch-shape histogram of the GEMM steps (ttk_gemm_hist)
@@ -875,7 +874,7 @@ int ttk_dot_nd_sync(void *stream, const double *x, const double *y, int ndim, co
   ttk::NdDesc d;
   int st = make_nd(d, ndim, shape, xstride, ystride, nullptr);
   if (st) return st;
-  if (!g_dev_scalar) TTK_HIP(hipMalloc(reinterpret_cast<void **>(&g_dev_scalar), 64 * sizeof(double)));
+  if (!ttk::ctx().dev_scalar) TTK_HIP(hipMalloc(reinterpret_cast<void **>(&ttk::ctx().dev_scalar), 64 * sizeof(double)));
   if (d.total == 0) {
     *result = 0.0;
     return TTK_OK;
@@ -883,9 +882,9 @@ int ttk_dot_nd_sync(void *stream, const double *x, const double *y, int ndim, co
   static const int mapped = getenv("TTK_MAPPED_READS") ? atoi(getenv("TTK_MAPPED_READS")) : 1;
   double *dev = nullptr;
   double *h = mapped ? ttk::mapped_stage(1, &dev) : nullptr;  // the reduction writes to host-coherent memory
-  hipLaunchKernelGGL(dot_nd_kernel, dim3(1), dim3(1024), 0, TTK_STREAM(stream), x, y, d, h ? dev : g_dev_scalar);
+  hipLaunchKernelGGL(dot_nd_kernel, dim3(1), dim3(1024), 0, TTK_STREAM(stream), x, y, d, h ? dev : ttk::ctx().dev_scalar);
   TTK_LAUNCH_CHECK();
-  if (!h) return ttk_read_sync(stream, g_dev_scalar, result, 1);
+  if (!h) return ttk_read_sync(stream, ttk::ctx().dev_scalar, result, 1);
   TTK_HIP(hipStreamSynchronize(TTK_STREAM(stream)));
   *result = h[0];
   return TTK_OK;

@@ -18,6 +18,7 @@
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -76,13 +77,12 @@ struct Arena {  // device bump allocator for offset tables (freed only on a full
   }
 };
 
-struct Engine {
+struct Engine {  // shared by all contexts: plans are immutable once built
   std::unordered_map<std::string, Plan> plans;
   Arena arena;
-  double *scratch = nullptr;
-  int64_t scratch_n = 0;
   double *ones = nullptr;
   long long hits = 0, misses = 0;
+  std::mutex mu;
 };
 Engine g_eng;
 
@@ -403,12 +403,13 @@ int ttk_einsum(void *stream, const char *eq, const int64_t *desc, double *out, d
   } else {
     key.push_back('c');
   }
+  std::unique_lock<std::mutex> lock(g_eng.mu);
   auto it = g_eng.plans.find(key);
   if (it == g_eng.plans.end()) {
-    if (g_eng.plans.size() >= 200000) {  // bounded cache: drain the stream, then start over
+    if (g_eng.plans.size() >= 200000) {  // bounded cache: drain the device, then start over
       const int rc = batch_flush(TTK_STREAM(stream));  // recorded steps point into the tables
       if (rc != TTK_OK) return rc;
-      if (hipStreamSynchronize(TTK_STREAM(stream)) != hipSuccess) return TTK_ERR_HIP;
+      if (hipDeviceSynchronize() != hipSuccess) return TTK_ERR_HIP;
       g_eng.plans.clear();
       g_eng.arena.reset();
     }
@@ -419,27 +420,29 @@ int ttk_einsum(void *stream, const char *eq, const int64_t *desc, double *out, d
   } else {
     ++g_eng.hits;
   }
-  const Plan &pl = it->second;
-  const bool rec = batch_on();
-  double *scr = g_eng.scratch;
-  if (rec) {  // each recorded call gets its own intermediates (the batch's steps run out of order)
-    scr = batch_scratch(pl.scratch);
-    if (!scr && pl.scratch > 0) return TTK_ERR_HIP;
-  } else if (pl.scratch > g_eng.scratch_n) {
-    // growing the shared scratch: earlier calls may still be using the old buffer on the stream
-    if (g_eng.scratch) {
-      TTK_HIP(hipStreamSynchronize(TTK_STREAM(stream)));
-      TTK_HIP(hipFree(g_eng.scratch));
-    }
-    int64_t want = pl.scratch * 2 > (1 << 20) ? pl.scratch * 2 : (1 << 20);
-    TTK_HIP(hipMalloc(reinterpret_cast<void **>(&g_eng.scratch), want * sizeof(double)));
-    g_eng.scratch_n = want;
-    scr = g_eng.scratch;
-  }
   if (!g_eng.ones) {
     TTK_HIP(hipMalloc(reinterpret_cast<void **>(&g_eng.ones), 64 * sizeof(double)));
     const double one[1] = {1.0};
     TTK_HIP(hipMemcpy(g_eng.ones, one, sizeof(double), hipMemcpyHostToDevice));
+  }
+  const Plan &pl = it->second;  // stable: the map only grows while plans are in use
+  lock.unlock();
+  ttk::Ctx &cx = ttk::ctx();
+  const bool rec = batch_on();
+  double *scr = cx.scratch;
+  if (rec) {  // each recorded call gets its own intermediates (the batch's steps run out of order)
+    scr = batch_scratch(pl.scratch);
+    if (!scr && pl.scratch > 0) return TTK_ERR_HIP;
+  } else if (pl.scratch > cx.scratch_n) {
+    // growing the context's scratch: earlier calls may still be using the old buffer on the stream
+    if (cx.scratch) {
+      TTK_HIP(hipStreamSynchronize(TTK_STREAM(stream)));
+      TTK_HIP(hipFree(cx.scratch));
+    }
+    int64_t want = pl.scratch * 2 > (1 << 20) ? pl.scratch * 2 : (1 << 20);
+    TTK_HIP(hipMalloc(reinterpret_cast<void **>(&cx.scratch), want * sizeof(double)));
+    cx.scratch_n = want;
+    scr = cx.scratch;
   }
   Span in_sp[8], out_sp;
   if (rec) {
@@ -757,9 +760,11 @@ struct SchurOp {
   double flops;
   bool used;
 };
-std::vector<SchurOp> g_schur;
-double *g_schur_w = nullptr;
-int64_t g_schur_wcap = 0;
+std::vector<SchurOp> &schur_ops() {  // the current context's handle table
+  ttk::Ctx &c = ttk::ctx();
+  if (!c.schur) c.schur = new std::vector<SchurOp>();
+  return *static_cast<std::vector<SchurOp> *>(c.schur);
+}
 
 size_t multi_lds(const ApplyLaunch &L) {
   int64_t mx = 0;
@@ -845,32 +850,39 @@ int ttk_schur_build(int ineq, int64_t m, const int64_t *descs, const double *inv
     op.shm[s] = multi_lds(L);
     if (op.shm[s] > (size_t)APPLY_LDS_DOUBLES * sizeof(double)) return TTK_OK;
   }
-  if (m > g_schur_wcap) {
-    if (g_schur_w) (void)hipFree(g_schur_w);
-    g_schur_w = nullptr;
-    g_schur_wcap = 0;
+  ttk::Ctx &cx = ttk::ctx();
+  if (m > cx.schur_wcap) {
+    if (cx.schur_w) {
+      TTK_HIP(cx.stream ? hipStreamSynchronize(cx.stream) : hipDeviceSynchronize());
+      (void)hipFree(cx.schur_w);
+    }
+    cx.schur_w = nullptr;
+    cx.schur_wcap = 0;
     const int64_t want = m < 65536 ? 65536 : m;
-    TTK_HIP(hipMalloc(reinterpret_cast<void **>(&g_schur_w), want * sizeof(double)));
-    g_schur_wcap = want;
+    TTK_HIP(hipMalloc(reinterpret_cast<void **>(&cx.schur_w), want * sizeof(double)));
+    cx.schur_wcap = want;
   }
   op.used = true;
+  std::vector<SchurOp> &ops = schur_ops();
   size_t slot = 0;
-  while (slot < g_schur.size() && g_schur[slot].used) ++slot;
-  if (slot == g_schur.size()) g_schur.push_back(op);
-  else g_schur[slot] = op;
+  while (slot < ops.size() && ops[slot].used) ++slot;
+  if (slot == ops.size()) ops.push_back(op);
+  else ops[slot] = op;
   *handle = (int64_t)slot + 1;
   return TTK_OK;
 }
 
 int ttk_schur_apply(void *stream, int64_t handle, const double *v, double *out) {
-  if (handle < 1 || handle > (int64_t)g_schur.size() || !g_schur[handle - 1].used) {
+  std::vector<SchurOp> &ops = schur_ops();
+  if (handle < 1 || handle > (int64_t)ops.size() || !ops[handle - 1].used) {
     ttk::set_error("ttk_schur_apply: bad handle %lld", (long long)handle);
     return TTK_ERR_ARG;
   }
-  SchurOp &op = g_schur[handle - 1];
+  SchurOp &op = ops[handle - 1];
   const int64_t m = op.m;
-  const double *in[4] = {v, v + m, v + 2 * m, g_schur_w};
-  double *o[4] = {out, out + m, out + 2 * m, g_schur_w};
+  double *w = ttk::ctx().schur_w;
+  const double *in[4] = {v, v + m, v + 2 * m, w};
+  double *o[4] = {out, out + m, out + 2 * m, w};
   for (int s = 0; s < 2; ++s) {
     ApplyLaunch L = op.st[s];
     for (int t = 0; t < L.ntask; ++t) {
@@ -894,7 +906,8 @@ int ttk_schur_apply(void *stream, int64_t handle, const double *v, double *out) 
 }
 
 int ttk_schur_free(int64_t handle) {
-  if (handle >= 1 && handle <= (int64_t)g_schur.size()) g_schur[handle - 1].used = false;
+  std::vector<SchurOp> &ops = schur_ops();
+  if (handle >= 1 && handle <= (int64_t)ops.size()) ops[handle - 1].used = false;
   return TTK_OK;
 }
 
@@ -934,7 +947,11 @@ struct Batch {
   int max_level = -1;
   long long flushes = 0, nodes_total = 0, launches = 0;
 };
-Batch g_batch;
+Batch &cur_batch() {  // the current context's recorder
+  ttk::Ctx &c = ttk::ctx();
+  if (!c.batch) c.batch = new Batch();
+  return *static_cast<Batch *>(c.batch);
+}
 
 constexpr int FGROUP_MAX = 12;
 struct FusedGroup {
@@ -963,10 +980,10 @@ bool conflict(const BNode &x, const BNode &y) {
 
 int add_node(BNode &n) {
   n.level = 0;
-  for (const BNode &e : g_batch.nodes)
+  for (const BNode &e : cur_batch().nodes)
     if (e.level >= n.level && conflict(e, n)) n.level = e.level + 1;
-  if (n.level > g_batch.max_level) g_batch.max_level = n.level;
-  g_batch.nodes.push_back(n);
+  if (n.level > cur_batch().max_level) cur_batch().max_level = n.level;
+  cur_batch().nodes.push_back(n);
   return TTK_OK;
 }
 
@@ -999,7 +1016,7 @@ int launch_fused_group(hipStream_t st, const std::vector<const BNode *> &v) {
     hipExtLaunchKernelGGL(fused_apply_group_kernel, dim3(G.off[G.n]), dim3(256), shm, st, e0, e1, 0, G);
     TTK_LAUNCH_CHECK();
     ttk::contract_count_ext(flops);
-    ++g_batch.launches;
+    ++cur_batch().launches;
   }
   return TTK_OK;
 }
@@ -1020,21 +1037,21 @@ Span span_of(const void *p, int nd, const int64_t *shape, const int64_t *stride)
   return s;
 }
 
-bool batch_on() { return g_batch.depth > 0; }
+bool batch_on() { return cur_batch().depth > 0; }
 
 double *batch_scratch(int64_t n) {
   if (n <= 0) return nullptr;
   n = (n + 31) / 32 * 32;
   while (true) {
-    if (g_batch.chunk < g_batch.chunks.size()) {
-      auto &c = g_batch.chunks[g_batch.chunk];
-      if (g_batch.used + n <= c.second) {
-        double *p = c.first + g_batch.used;
-        g_batch.used += n;
+    if (cur_batch().chunk < cur_batch().chunks.size()) {
+      auto &c = cur_batch().chunks[cur_batch().chunk];
+      if (cur_batch().used + n <= c.second) {
+        double *p = c.first + cur_batch().used;
+        cur_batch().used += n;
         return p;
       }
-      ++g_batch.chunk;
-      g_batch.used = 0;
+      ++cur_batch().chunk;
+      cur_batch().used = 0;
       continue;
     }
     const int64_t want = n > (int64_t(1) << 22) ? n : (int64_t(1) << 22);  // 32 MiB chunks
@@ -1043,7 +1060,7 @@ double *batch_scratch(int64_t n) {
       ttk::set_error("einsum batch: scratch allocation failed");
       return nullptr;
     }
-    g_batch.chunks.push_back({p, want});
+    cur_batch().chunks.push_back({p, want});
   }
 }
 
@@ -1073,14 +1090,14 @@ static int batch_add_fused(const ApplyArgs &g, int64_t lds_doubles) {
 }
 
 int batch_flush(hipStream_t st) {
-  if (g_batch.nodes.empty()) return TTK_OK;
+  if (cur_batch().nodes.empty()) return TTK_OK;
   std::vector<ttk::GemmProblem> grp;
   std::vector<const BNode *> fused;
   int rc = TTK_OK;
-  for (int lv = 0; lv <= g_batch.max_level && rc == TTK_OK; ++lv) {
+  for (int lv = 0; lv <= cur_batch().max_level && rc == TTK_OK; ++lv) {
     grp.clear();
     fused.clear();
-    for (const BNode &n : g_batch.nodes) {
+    for (const BNode &n : cur_batch().nodes) {
       if (n.level != lv) continue;
       if (n.kind == 1) {
         fused.push_back(&n);
@@ -1088,53 +1105,111 @@ int batch_flush(hipStream_t st) {
         grp.push_back(n.g);
       } else {
         rc = ttk_gemm_offs(st, n.g.A, n.g.B, n.g.C, n.g.offs, n.g.nb, n.g.M, n.g.N, n.g.K, n.g.alpha, n.g.beta);
-        ++g_batch.launches;
+        ++cur_batch().launches;
         if (rc != TTK_OK) break;
       }
     }
     if (rc == TTK_OK && !grp.empty()) {
       rc = ttk::gemm_group(st, grp.data(), (int)grp.size());
-      g_batch.launches += (long long)(grp.size() + 23) / 24;
+      cur_batch().launches += (long long)(grp.size() + 23) / 24;
     }
     if (rc == TTK_OK && !fused.empty()) rc = launch_fused_group(st, fused);
   }
-  g_batch.nodes_total += (long long)g_batch.nodes.size();
-  ++g_batch.flushes;
-  g_batch.nodes.clear();
-  g_batch.max_level = -1;
-  g_batch.chunk = 0;
-  g_batch.used = 0;
+  cur_batch().nodes_total += (long long)cur_batch().nodes.size();
+  ++cur_batch().flushes;
+  cur_batch().nodes.clear();
+  cur_batch().max_level = -1;
+  cur_batch().chunk = 0;
+  cur_batch().used = 0;
   return rc;
 }
 
 namespace ttk {
 int batch_barrier(void *stream) { return batch_flush(TTK_STREAM(stream)); }
+
+void ctx_free_einsum(Ctx &c) {
+  if (c.batch) {
+    Batch *b = static_cast<Batch *>(c.batch);
+    for (auto &ch : b->chunks) (void)hipFree(ch.first);
+    delete b;
+    c.batch = nullptr;
+  }
+  if (c.schur) {
+    delete static_cast<std::vector<SchurOp> *>(c.schur);
+    c.schur = nullptr;
+  }
+}
 }  // namespace ttk
 
 extern "C" {
 
 int ttk_einsum_batch_begin(void *stream) {
   (void)stream;
-  ++g_batch.depth;
+  ++cur_batch().depth;
   return TTK_OK;
 }
 
 int ttk_einsum_batch_flush(void *stream) { return batch_flush(TTK_STREAM(stream)); }
 
 int ttk_einsum_batch_end(void *stream) {
-  if (g_batch.depth <= 0) {
+  if (cur_batch().depth <= 0) {
     ttk::set_error("ttk_einsum_batch_end without begin");
     return TTK_ERR_ARG;
   }
   const int rc = batch_flush(TTK_STREAM(stream));
-  --g_batch.depth;
+  --cur_batch().depth;
   return rc;
 }
 
+// AMEn / ALS environment updates of one core step in one call (`compute_phi_fwd_A` / `_bck_A`,
+// src/tt_als.py:252-257, for every block of the step: src/tt_als.py:372-387,499-514).  Each block is
+// the relabelled local apply the Python host uses (fused under the environment FLOP limit, the
+// pairwise MFMA plan above it), recorded into one batch and launched as grouped launches.
+int ttk_env_update(ttk_ctx ctx, int backward, int nblocks, const ttk_env_block *blk) {
+  ttk::CtxScope scope(ctx);
+  void *stream = reinterpret_cast<void *>(ttk::ctx().stream);
+  static const char *APPLY = "lsr,smnS,LSR,rnR->lmL";
+  int rc = ttk_einsum_batch_begin(stream);
+  if (rc) return rc;
+  for (int b = 0; b < nblocks && rc == TTK_OK; ++b) {
+    const ttk_env_block &e = blk[b];
+    const int64_t *xs = e.x_shape, *ys = e.y_shape, *as = e.A_shape, *ps = e.phi_shape, *ast = e.a_strides;
+    const int64_t xst[3] = {xs[1] * xs[2], xs[2], 1}, yst[3] = {ys[1] * ys[2], ys[2], 1};
+    const int64_t pst[3] = {ps[1] * ps[2], ps[2], 1};
+    int64_t d[1 + 4 * 10 + 1];
+    int64_t k = 0;
+    d[k++] = 4 | 256 | 512;
+    auto put = [&](const void *p, int nd, const int64_t *sh, const int64_t *st) {
+      d[k++] = reinterpret_cast<int64_t>(p);
+      d[k++] = nd;
+      for (int i = 0; i < nd; ++i) d[k++] = sh[i];
+      for (int i = 0; i < nd; ++i) d[k++] = st[i];
+    };
+    if (backward) {  // einsum(APPLY, x, A.permute(1,0,3,2), y, Phi)
+      const int64_t ash[4] = {as[1], as[0], as[3], as[2]}, asd[4] = {ast[1], ast[0], ast[3], ast[2]};
+      put(e.x, 3, xs, xst);
+      put(e.A, 4, ash, asd);
+      put(e.y, 3, ys, yst);
+    } else {  // einsum(APPLY, x.permute(2,1,0), A.permute(1,3,0,2), y.permute(2,1,0), Phi)
+      const int64_t xsh[3] = {xs[2], xs[1], xs[0]}, xsd[3] = {xst[2], xst[1], xst[0]};
+      const int64_t ysh[3] = {ys[2], ys[1], ys[0]}, ysd[3] = {yst[2], yst[1], yst[0]};
+      const int64_t ash[4] = {as[1], as[3], as[0], as[2]}, asd[4] = {ast[1], ast[3], ast[0], ast[2]};
+      put(e.x, 3, xsh, xsd);
+      put(e.A, 4, ash, asd);
+      put(e.y, 3, ysh, ysd);
+    }
+    put(e.phi, 3, ps, pst);
+    d[k++] = 0;  // contiguous output
+    rc = ttk_einsum(stream, APPLY, d, e.out, 1.0, 0.0);
+  }
+  const int rc2 = ttk_einsum_batch_end(stream);
+  return rc ? rc : rc2;
+}
+
 int ttk_einsum_batch_stats(long long *out) {
-  out[0] = g_batch.flushes;
-  out[1] = g_batch.nodes_total;
-  out[2] = g_batch.launches;
+  out[0] = cur_batch().flushes;
+  out[1] = cur_batch().nodes_total;
+  out[2] = cur_batch().launches;
   return TTK_OK;
 }
 

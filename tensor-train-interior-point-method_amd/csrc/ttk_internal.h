@@ -4,7 +4,64 @@
 
 #include <hip/hip_runtime.h>
 
+#include "../../include/ttk.h"
+
 namespace ttk {
+// Per-context state (`ttk_ctx`): every scratch buffer, staging ring and handle table the library
+// keeps between calls lives in a context, so two contexts (each with its own stream, driven by its
+// own host thread) never share mutable state.  The plan cache (immutable plans + their offset
+// tables) is shared and lock-protected.  ctx() is the calling thread's bound context, or the
+// process default context when none is bound (the Python host layer's single-stream model).
+struct UpSlot {
+  double *p = nullptr;
+  size_t n = 0;
+  hipEvent_t ev = nullptr;
+  bool pending = false;
+};
+constexpr int UP_SLOTS = 64;
+
+struct Ctx {
+  hipStream_t stream = nullptr;
+  double *scratch = nullptr;  // einsum intermediates (unbatched calls)
+  int64_t scratch_n = 0;
+  void *batch = nullptr;      // einsum batch recorder (ttk_einsum.hip)
+  double *splitk = nullptr;   // split-K partial slabs
+  int64_t splitk_n = 0;
+  double *dev_scalar = nullptr;
+  void *schur = nullptr;      // Schur operator handle table (ttk_einsum.hip)
+  double *schur_w = nullptr;
+  int64_t schur_wcap = 0;
+  double *lgmres = nullptr;   // LGMRES partial sums
+  int64_t lgmres_n = 0;
+  int *status = nullptr;      // dense factorisation status words
+  double *rcond = nullptr;
+  double *mapped_h = nullptr, *mapped_d = nullptr;  // host-coherent read buffer
+  size_t mapped_n = 0;
+  UpSlot up[UP_SLOTS];        // pinned upload ring
+  int up_next = 0;
+};
+Ctx &ctx();
+Ctx *ctx_swap(Ctx *c);  // bind c to the calling thread, return the previous binding
+}  // namespace ttk
+
+struct ttk_ctx_s {
+  ttk::Ctx c;
+};
+
+namespace ttk {
+// binds an ABI context for the duration of a call (NULL: keep the thread's current context)
+struct CtxScope {
+  Ctx *prev;
+  bool on;
+  explicit CtxScope(ttk_ctx_s *h) : prev(nullptr), on(h != nullptr) {
+    if (on) prev = ctx_swap(&h->c);
+  }
+  ~CtxScope() {
+    if (on) ctx_swap(prev);
+  }
+};
+void ctx_free_einsum(Ctx &c);  // ttk_einsum.hip: batch + Schur tables of a context being destroyed
+
 // ttk_dense.hip: blocked multi-workgroup Cholesky (status = LAPACK info, device int) and
 // triangular solve op(L) X = B; both enqueue on `st` without synchronising.
 int cholesky_blocked(hipStream_t st, double *A, int n, int *status);

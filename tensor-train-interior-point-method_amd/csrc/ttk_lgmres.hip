@@ -10,6 +10,8 @@
 #include <math.h>
 
 #include "ttk_common.h"
+#include <vector>
+#include "ttk_internal.h"
 
 namespace {
 
@@ -356,20 +358,22 @@ __global__ __launch_bounds__(256) void aug_apply_kernel(const double *base_c, in
   a_augvec[i] = t * inv;
 }
 
-double *lgmres_scratch(int64_t n) {  // partials / norm parts (grown, never shrunk; one stream)
-  static double *p = nullptr;
-  static int64_t cap = 0;
-  if (n > cap) {
-    if (p) (void)hipFree(p);
+double *lgmres_scratch(int64_t n) {  // partials / norm parts of the current context (grown, never shrunk)
+  ttk::Ctx &c = ttk::ctx();
+  if (n > c.lgmres_n) {
+    if (c.lgmres) {
+      (void)(c.stream ? hipStreamSynchronize(c.stream) : hipDeviceSynchronize());
+      (void)hipFree(c.lgmres);
+    }
     const int64_t want = n < 65536 ? 65536 : n;
-    if (hipMalloc(reinterpret_cast<void **>(&p), want * sizeof(double)) != hipSuccess) {
-      p = nullptr;
-      cap = 0;
+    if (hipMalloc(reinterpret_cast<void **>(&c.lgmres), want * sizeof(double)) != hipSuccess) {
+      c.lgmres = nullptr;
+      c.lgmres_n = 0;
       return nullptr;
     }
-    cap = want;
+    c.lgmres_n = want;
   }
-  return p;
+  return c.lgmres;
 }
 
 int g_lgmres_mw_min = 16384;  // (it+1)*n at or above which the multi-workgroup kernels run
@@ -486,6 +490,236 @@ int ttk_lgmres_aug(void *stream, const double *hh, int max_k, int it_total, cons
                        augvec, a_augvec);
   }
   TTK_LAUNCH_CHECK();
+  return TTK_OK;
+}
+
+// ---------------------------------------------------------------- whole LGMRES solve (one call)
+// PETSc KSPLGMRES (`src/tt_ipm.py:101-162`; restated in oracle/petsc_lgmres.py) on a Schur operator
+// handle: the host bookkeeping of tensor-train-interior-point-method_amd/lgmres.py (restart cycles,
+// augmentation order, KSPConvergedDefault replayed on the speculative chunks' records) in C++, so a
+// local KKT solve is one library call.  The kernel sequence is that of the Python driver with the
+// native operator, hence the iterates are bit-identical to it.
+namespace {
+
+int64_t hh_size(int max_k) {
+  const int64_t ld = max_k + 1;
+  return 2 * (int64_t)(max_k + 2) * ld + (max_k + 2) + 2 * ld + 8;
+}
+
+int lg_converged(int k, double rnorm, double rtol, double abstol, double dtol, double &rnorm0, double &ttol) {
+  if (k == 0) {
+    rnorm0 = rnorm;
+    ttol = fmax(rtol * rnorm, abstol);
+  }
+  if (rnorm != rnorm || isinf(rnorm)) return -9;             // DIVERGED_NANORINF
+  if (rnorm <= ttol) return rnorm < abstol ? 3 : 2;           // CONVERGED_ATOL / _RTOL
+  if (rnorm >= dtol * rnorm0) return -4;                      // DIVERGED_DTOL
+  return 0;
+}
+
+}  // namespace
+
+int ttk_lgmres(ttk_ctx ctx, int64_t schur, const double *b, double *x, int64_t n64, int restart, int augment,
+               double rtol, int max_it, int chunk, ttk_lgmres_info *info) {
+  ttk::CtxScope scope(ctx);
+  ttk::Ctx &cx = ttk::ctx();
+  void *stream = reinterpret_cast<void *>(cx.stream);
+  const int n = (int)n64;
+  const int max_k = restart, aug_dim = augment;
+  const double abstol = 1e-50, dtol = 1e5, haptol = 1e-30;
+  const int nd = aug_dim > 1 ? aug_dim : 1;
+  chunk = chunk > 0 ? chunk : 1;
+  if (n <= 0 || max_k < 1 || max_k + 1 > MAXV) {
+    ttk::set_error("ttk_lgmres: bad size n=%d restart=%d", n, max_k);
+    return TTK_ERR_ARG;
+  }
+  // workspace: V | hh | augvecs | a_augvecs | aug_temp | ctl
+  const int64_t nV = (int64_t)(max_k + 1) * n, nH = hh_size(max_k), nA = (int64_t)nd * n, nC = 1 + 5 * (int64_t)chunk;
+  const int64_t need = nV + nH + 2 * nA + n + nC + 64;
+  double *ws = lgmres_scratch(need + 1 + 65536);  // the first 65536 doubles stay the partials slab
+  if (!ws) {
+    ttk::set_error("ttk_lgmres: workspace allocation failed");
+    return TTK_ERR_HIP;
+  }
+  ws += 65536;
+  double *V = ws, *hh = V + nV, *augvecs = hh + nH, *a_augvecs = augvecs + nA, *aug_temp = a_augvecs + nA,
+         *ctl = aug_temp + n;
+  const int64_t grs_off = 2 * (int64_t)(max_k + 2) * (max_k + 1);
+  int rc;
+  if ((rc = ttk_fill(stream, x, n, 0.0)) || (rc = ttk_fill(stream, hh, nH, 0.0)) || (rc = ttk_fill(stream, ctl, nC, 0.0)))
+    return rc;
+  std::vector<int64_t> aug_order(nd, 0);
+  int aug_ct = 0, its = 0, itcount = 0, reason = 0, nmv = 0;
+  bool guess_zero = true;
+  double res = 0.0, rnorm0 = 0.0, ttol = 0.0;
+  const int64_t one_shape[1] = {n}, unit[1] = {1};
+  auto copy = [&](double *dst, const double *src, double al, double be) {
+    return ttk_copy_nd(stream, src, dst, 1, one_shape, unit, unit, al, be);
+  };
+  auto norm = [&](const double *v, double &out) {
+    double d = 0.0;
+    int r = ttk_dot_nd_sync(stream, v, v, 1, one_shape, unit, unit, &d);
+    out = sqrt(fmax(d, 0.0));
+    return r;
+  };
+  int it_arnoldi = max_k - aug_dim;
+  auto matvec_or_aug = [&](int li) {
+    if (li < it_arnoldi) return ttk_schur_apply(stream, schur, V + (int64_t)li * n, V + (int64_t)(li + 1) * n);
+    const int64_t order = li - it_arnoldi + 1;
+    int spot = 0;
+    for (int ii = 0; ii < aug_dim; ++ii)
+      if (aug_order[ii] == order) {
+        spot = ii;
+        break;
+      }
+    return copy(V + (int64_t)(li + 1) * n, a_augvecs + (int64_t)spot * n, 1.0, 0.0);
+  };
+  while (!reason) {
+    if (guess_zero) {
+      if ((rc = copy(V, b, 1.0, 0.0))) return rc;
+    } else {
+      if ((rc = ttk_schur_apply(stream, schur, x, V))) return rc;
+      ++nmv;
+      if ((rc = copy(V, b, 1.0, -1.0))) return rc;  // r = b - A x
+    }
+    it_arnoldi = max_k - aug_dim;
+    const int it_total = it_arnoldi + aug_ct;
+    if ((rc = norm(V, res))) return rc;
+    if ((rc = ttk_fill(stream, hh + grs_off, 1, res))) return rc;
+    if (res == 0.0) {
+      reason = 3;
+      break;
+    }
+    if ((rc = copy(V, V, 1.0 / res, 0.0))) return rc;
+    reason = lg_converged(its, res, rtol, abstol, dtol, rnorm0, ttol);
+    int loc_it = 0;
+    bool hapend = false;
+    double last_diag = 1.0;
+    while (!reason && loc_it < it_total && its < max_it) {
+      int kmax = chunk;
+      if (it_total - loc_it < kmax) kmax = it_total - loc_it;
+      if (max_it - its < kmax) kmax = max_it - its;
+      double recs[5 * 64 + 1];
+      int nrec;
+      if (kmax <= 1) {
+        if ((rc = matvec_or_aug(loc_it))) return rc;
+        double rb[2];
+        int fl[2];
+        if ((rc = ttk_lgmres_arnoldi_sync(stream, V, n, loc_it, hh, max_k, haptol, rb, fl))) return rc;
+        recs[0] = its + 1;
+        recs[1] = rb[0];
+        recs[2] = fl[0];
+        recs[3] = fl[1];
+        recs[4] = rb[1];
+        nrec = 1;
+      } else {
+        if (kmax > 64) kmax = 64;
+        const double divtol = dtol * rnorm0;
+        const bool in_native = loc_it + kmax <= it_arnoldi;
+        if (in_native) {
+          if ((rc = ttk_lgmres_chunk(stream, schur, V, n, loc_it, kmax, hh, max_k, haptol, ttol, divtol, ctl,
+                                     (double)(its + 1))))
+            return rc;
+        } else {
+          for (int q = 0; q < kmax; ++q) {
+            if ((rc = matvec_or_aug(loc_it + q))) return rc;
+            if ((rc = ttk_lgmres_arnoldi_async(stream, V, n, loc_it + q, hh, max_k, haptol, ttol, divtol, ctl, q,
+                                               (double)(its + q + 1))))
+              return rc;
+          }
+        }
+        double h[1 + 5 * 64];
+        if ((rc = ttk_read_sync(stream, ctl, h, 1 + 5 * kmax))) return rc;
+        for (int q = 0; q < 5 * kmax; ++q) recs[q] = h[1 + q];
+        nrec = kmax;
+      }
+      for (int q = 0; q < nrec; ++q) {
+        const double *r = recs + 5 * q;
+        if (r[0] != its + 1) {
+          ttk::set_error("ttk_lgmres: device stopped the Arnoldi chunk at step %d without a host-side stop reason",
+                         its);
+          return TTK_ERR_ARG;
+        }
+        hapend = r[2] != 0.0;
+        if (r[3] != 0.0) {
+          reason = -2;  // DIVERGED_NULL
+          break;
+        }
+        res = r[1];
+        last_diag = r[4];
+        nmv += loc_it < it_arnoldi;
+        ++loc_it;
+        ++its;
+        reason = lg_converged(its, res, rtol, abstol, dtol, rnorm0, ttol);
+        if (hapend && !reason) {
+          reason = -5;  // DIVERGED_BREAKDOWN
+          break;
+        }
+        if (reason) break;
+      }
+      if (reason == -2 || reason == -5) break;
+    }
+    const int cycle_its = loc_it;
+    const int it = loc_it - 1;
+    bool built = false;
+    if (it >= 0) {
+      int ita = max_k - aug_dim, it_aug;
+      if (ita >= it + 1) {
+        it_aug = 0;
+        ita = it + 1;
+      } else {
+        it_aug = (it + 1) - ita;
+      }
+      if (last_diag == 0.0) {
+        ttk::set_error("ttk_lgmres: HH(it,it) is identically zero; it = %d (PETSC_ERR_CONV_FAILED)", it);
+        return TTK_ERR_NOT_CONVERGED;
+      }
+      std::vector<const double *> ptrs;
+      for (int j = 0; j < ita; ++j) ptrs.push_back(V + (int64_t)j * n);
+      for (int ii = 0; ii < it_aug; ++ii) {
+        int spot = 0;
+        for (int jj = 0; jj < aug_dim; ++jj)
+          if (aug_order[jj] == ii + 1) {
+            spot = jj;
+            break;
+          }
+        ptrs.push_back(augvecs + (int64_t)spot * n);
+      }
+      if ((rc = ttk_lgmres_build(stream, hh, max_k, it, ptrs.data(), (int)ptrs.size(), n, x, aug_temp))) return rc;
+      built = true;
+    }
+    if (!reason && its < max_it && aug_dim > 0 && built) {
+      int spot = 0;
+      if (aug_ct == 0) {
+        spot = 0;
+        ++aug_ct;
+      } else if (aug_ct < aug_dim) {
+        spot = aug_ct;
+        ++aug_ct;
+      } else {
+        spot = 0;
+        for (int ii = 0; ii < aug_dim; ++ii)
+          if (aug_order[ii] == aug_dim) spot = ii;
+      }
+      for (int ii = 0; ii < aug_dim; ++ii) aug_order[ii] += 1;
+      aug_order[spot] = 1;
+      if ((rc = ttk_lgmres_aug(stream, hh, max_k, it_total, V, n, 0.0, aug_temp, augvecs + (int64_t)spot * n,
+                               a_augvecs + (int64_t)spot * n)))
+        return rc;
+    }
+    itcount += cycle_its;
+    if (itcount >= max_it) {
+      if (!reason) reason = -3;  // DIVERGED_ITS
+      break;
+    }
+    guess_zero = false;
+  }
+  if (info) {
+    info->reason = reason;
+    info->its = its;
+    info->res = res;
+    info->matvecs = nmv;
+  }
   return TTK_OK;
 }
 

@@ -2231,13 +2231,11 @@ int qrb_apply_q(hipStream_t st, const double *W, int m, int k, const double *Tal
   return TTK_OK;
 }
 
-int *g_status = nullptr;
-double *g_rcond = nullptr;
-
-int ensure_status() {
-  if (!g_status) {
-    if (hipMalloc(reinterpret_cast<void **>(&g_status), 16 * sizeof(int)) != hipSuccess) return TTK_ERR_HIP;
-    if (hipMalloc(reinterpret_cast<void **>(&g_rcond), 16 * sizeof(double)) != hipSuccess) return TTK_ERR_HIP;
+int ensure_status() {  // the current context's device status words
+  ttk::Ctx &c = ttk::ctx();
+  if (!c.status) {
+    if (hipMalloc(reinterpret_cast<void **>(&c.status), 16 * sizeof(int)) != hipSuccess) return TTK_ERR_HIP;
+    if (hipMalloc(reinterpret_cast<void **>(&c.rcond), 16 * sizeof(double)) != hipSuccess) return TTK_ERR_HIP;
   }
   return TTK_OK;
 }
@@ -2283,8 +2281,8 @@ static int svd_big(void *stream, const double *A, int m, int n, double *U, doubl
   int *perm = reinterpret_cast<int *>(sig + 2 * p);  // p ints
   double *Tall = sig + 3 * p;                        // npan * QB * QB
   double *Z = Tall + (int64_t)npan * QB * QB;        // QB * p
-  int *ctl = g_status + 10;                          // [0] k_eff, [1] stopped
-  int *flag = g_status + 8;
+  int *ctl = ttk::ctx().status + 10;                          // [0] k_eff, [1] stopped
+  int *flag = ttk::ctx().status + 8;
   hipStream_t st = TTK_STREAM(stream);
   if (tall)
     hipLaunchKernelGGL(rm_to_cm_kernel, dim3(grid_for((int64_t)q * p)), dim3(256), 0, st, A, m, n, W);
@@ -2472,14 +2470,14 @@ int ttk_cholesky_sync(void *stream, double *A, int n) {
     return TTK_ERR_HIP;
   }
   if (n >= g_dense_block_min) {
-    const int rc = ttk::cholesky_blocked(TTK_STREAM(stream), A, n, g_status);
+    const int rc = ttk::cholesky_blocked(TTK_STREAM(stream), A, n, ttk::ctx().status);
     if (rc) return rc;
   } else {
-    hipLaunchKernelGGL(chol_kernel, dim3(1), dim3(1024), 0, TTK_STREAM(stream), A, n, g_status);
+    hipLaunchKernelGGL(chol_kernel, dim3(1), dim3(1024), 0, TTK_STREAM(stream), A, n, ttk::ctx().status);
     TTK_LAUNCH_CHECK();
   }
   int st = 0;
-  TTK_HIP(hipMemcpyAsync(&st, g_status, sizeof(int), hipMemcpyDeviceToHost, TTK_STREAM(stream)));
+  TTK_HIP(hipMemcpyAsync(&st, ttk::ctx().status, sizeof(int), hipMemcpyDeviceToHost, TTK_STREAM(stream)));
   TTK_HIP(hipStreamSynchronize(TTK_STREAM(stream)));
   if (st) {
     ttk::set_error("%d-th leading minor of the array is not positive definite", st);
@@ -2502,15 +2500,15 @@ int ttk_lu_sync(void *stream, double *A, int n, int *piv, double *work, double *
     return TTK_ERR_HIP;
   }
   if (n >= g_lu_block_min && n <= 7000) {
-    const int rc = ttk::lu_blocked(TTK_STREAM(stream), A, n, piv, work, g_status, g_rcond, 1);
+    const int rc = ttk::lu_blocked(TTK_STREAM(stream), A, n, piv, work, ttk::ctx().status, ttk::ctx().rcond, 1);
     if (rc) return rc;
   } else {
-    hipLaunchKernelGGL(lu_kernel, dim3(1), dim3(1024), 0, TTK_STREAM(stream), A, n, piv, work, g_status, g_rcond);
+    hipLaunchKernelGGL(lu_kernel, dim3(1), dim3(1024), 0, TTK_STREAM(stream), A, n, piv, work, ttk::ctx().status, ttk::ctx().rcond);
     TTK_LAUNCH_CHECK();
   }
   int st = 0;
-  TTK_HIP(hipMemcpyAsync(&st, g_status, sizeof(int), hipMemcpyDeviceToHost, TTK_STREAM(stream)));
-  TTK_HIP(hipMemcpyAsync(rcond_out, g_rcond, sizeof(double), hipMemcpyDeviceToHost, TTK_STREAM(stream)));
+  TTK_HIP(hipMemcpyAsync(&st, ttk::ctx().status, sizeof(int), hipMemcpyDeviceToHost, TTK_STREAM(stream)));
+  TTK_HIP(hipMemcpyAsync(rcond_out, ttk::ctx().rcond, sizeof(double), hipMemcpyDeviceToHost, TTK_STREAM(stream)));
   TTK_HIP(hipStreamSynchronize(TTK_STREAM(stream)));
   if (st) {
     ttk::set_error("Matrix is singular (zero pivot at %d).", st);

@@ -4,8 +4,10 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <new>
 
 #include "ttk_common.h"
+#include "ttk_internal.h"
 
 namespace ttk {
 
@@ -44,42 +46,32 @@ double *pinned_stage(size_t n) {
   return g_stage.p;
 }
 
-// host-coherent mapped buffer: small results are written there by a kernel and read by the host
-// after the stream synchronises (no runtime blit + staging copy per read)
-static double *g_mapped_h = nullptr, *g_mapped_d = nullptr;
-static size_t g_mapped_n = 0;
-
+// host-coherent mapped buffer (per context): small results are written there by a kernel and read
+// by the host after the stream synchronises (no runtime blit + staging copy per read)
 double *mapped_stage(size_t n, double **dev) {
-  if (g_mapped_n < n) {
-    if (g_mapped_h) (void)hipHostFree(g_mapped_h);
-    g_mapped_h = g_mapped_d = nullptr;
-    g_mapped_n = 0;
+  Ctx &c = ctx();
+  if (c.mapped_n < n) {
+    if (c.mapped_h) (void)hipHostFree(c.mapped_h);
+    c.mapped_h = c.mapped_d = nullptr;
+    c.mapped_n = 0;
     const size_t want = n < 8192 ? 8192 : n;
-    if (hipHostMalloc(reinterpret_cast<void **>(&g_mapped_h), want * sizeof(double),
+    if (hipHostMalloc(reinterpret_cast<void **>(&c.mapped_h), want * sizeof(double),
                       hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
       return nullptr;
-    if (hipHostGetDevicePointer(reinterpret_cast<void **>(&g_mapped_d), g_mapped_h, 0) != hipSuccess) {
-      (void)hipHostFree(g_mapped_h);
-      g_mapped_h = nullptr;
+    if (hipHostGetDevicePointer(reinterpret_cast<void **>(&c.mapped_d), c.mapped_h, 0) != hipSuccess) {
+      (void)hipHostFree(c.mapped_h);
+      c.mapped_h = nullptr;
       return nullptr;
     }
-    g_mapped_n = want;
+    c.mapped_n = want;
   }
-  *dev = g_mapped_d;
-  return g_mapped_h;
+  *dev = c.mapped_d;
+  return c.mapped_h;
 }
 
-// host -> device uploads through a ring of pinned slots: the host copy lands in slot i, an async
-// H2D copy is queued on the stream and an event marks when the slot may be refilled
-struct UpSlot {
-  double *p = nullptr;
-  size_t n = 0;
-  hipEvent_t ev = nullptr;
-  bool pending = false;
-};
-constexpr int UP_SLOTS = 64;
-static UpSlot g_up[UP_SLOTS];
-static int g_up_next = 0;
+static Ctx g_default_ctx;
+static thread_local Ctx *g_cur_ctx = nullptr;
+Ctx &ctx() { return g_cur_ctx ? *g_cur_ctx : g_default_ctx; }
 
 }  // namespace ttk
 
@@ -98,8 +90,9 @@ long long ttk_launch_count(void) { return ttk::g_launches.load(); }
 
 int ttk_upload(void *stream, const double *host, double *dev, int64_t n) {
   if (n <= 0) return TTK_OK;
-  ttk::UpSlot &sl = ttk::g_up[ttk::g_up_next];
-  ttk::g_up_next = (ttk::g_up_next + 1) % ttk::UP_SLOTS;
+  ttk::Ctx &c = ttk::ctx();  // host -> device through the context's ring of pinned slots
+  ttk::UpSlot &sl = c.up[c.up_next];
+  c.up_next = (c.up_next + 1) % ttk::UP_SLOTS;
   if (sl.pending) {
     TTK_HIP(hipEventSynchronize(sl.ev));  // the slot's previous copy has left it (normally long ago)
     sl.pending = false;
@@ -144,6 +137,58 @@ int ttk_read_sync(void *stream, const double *src, double *host_dst, int64_t n) 
   TTK_HIP(hipMemcpyAsync(st, src, n * sizeof(double), hipMemcpyDeviceToHost, TTK_STREAM(stream)));
   TTK_HIP(hipStreamSynchronize(TTK_STREAM(stream)));
   std::memcpy(host_dst, st, n * sizeof(double));
+  return TTK_OK;
+}
+
+}  // extern "C"
+
+// ---- contexts
+namespace ttk {
+void ctx_bind(Ctx *c) { g_cur_ctx = c; }
+Ctx *ctx_swap(Ctx *c) {
+  Ctx *p = g_cur_ctx;
+  g_cur_ctx = c;
+  return p;
+}
+}  // namespace ttk
+
+extern "C" {
+
+int ttk_ctx_create(void *stream, ttk_ctx *out) {
+  *out = nullptr;
+  ttk_ctx_s *h = new (std::nothrow) ttk_ctx_s();
+  if (!h) {
+    ttk::set_error("ttk_ctx_create: out of host memory");
+    return TTK_ERR_ARG;
+  }
+  h->c.stream = TTK_STREAM(stream);
+  *out = h;
+  return TTK_OK;
+}
+
+void *ttk_ctx_stream(ttk_ctx h) { return h ? reinterpret_cast<void *>(h->c.stream) : nullptr; }
+
+int ttk_ctx_bind(ttk_ctx h) {
+  ttk::ctx_bind(h ? &h->c : nullptr);
+  return TTK_OK;
+}
+
+int ttk_ctx_destroy(ttk_ctx h) {
+  if (!h) return TTK_OK;
+  ttk::Ctx &c = h->c;
+  TTK_HIP(hipStreamSynchronize(c.stream));
+  ttk::Ctx *prev = ttk::g_cur_ctx;
+  ttk::g_cur_ctx = &c;
+  ttk::ctx_free_einsum(c);
+  ttk::g_cur_ctx = prev == &c ? nullptr : prev;
+  for (double *p : {c.scratch, c.splitk, c.dev_scalar, c.schur_w, c.lgmres, c.rcond}) if (p) (void)hipFree(p);
+  if (c.status) (void)hipFree(c.status);
+  if (c.mapped_h) (void)hipHostFree(c.mapped_h);
+  for (ttk::UpSlot &u : c.up) {
+    if (u.p) (void)hipHostFree(u.p);
+    if (u.ev) (void)hipEventDestroy(u.ev);
+  }
+  delete h;
   return TTK_OK;
 }
 

@@ -28,6 +28,7 @@ _vp = ctypes.c_void_p
 _STREAM = []
 
 
+CTX = []  # the ttk_ctx bound to the host thread that drives the path (created with the stream)
 _BATCH = [0]  # open einsum batches (dev.einsum_batch)
 # operands of recorded (not yet launched) einsum steps: held until the flush so that the caching
 # allocator cannot hand their memory to an allocation whose kernels run before the recorded steps
@@ -39,6 +40,11 @@ def _stream():
     streams, and torch.cuda.current_stream() costs ~10 us per call)."""
     if not _STREAM:
         _STREAM.append(torch.cuda.current_stream().cuda_stream if DEV.type == "cuda" else None)
+        if DEV.type == "cuda":  # this process's libttk context: the launch stream + all scratch state
+            h = ctypes.c_void_p(0)
+            check(lib.ttk_ctx_create(_STREAM[0], ctypes.byref(h)), "ctx_create")
+            CTX.append(h)
+            check(lib.ttk_ctx_bind(h), "ctx_bind")
     if _BATCH[0]:  # any launch other than an einsum first flushes the recorded steps (stream order)
         check(lib.ttk_einsum_batch_flush(_STREAM[0]), "einsum_batch_flush")
         _KEEP.clear()

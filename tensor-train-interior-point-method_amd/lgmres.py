@@ -29,6 +29,33 @@ class PetscConvFailed(RuntimeError):
     """KSPLGMRESBuildSoln: HH(it,it) is identically zero (PETSC_ERR_CONV_FAILED)."""
 
 
+# with a native Schur operator the whole solve is one library call (ttk_lgmres: the same kernel
+# sequence as the loop below, host bookkeeping in C++)
+NATIVE_SOLVE = os.environ.get("TTIPM_LGMRES_NATIVE", "1") == "1"
+
+
+class _Info(ctypes.Structure):
+    _fields_ = [("reason", ctypes.c_int), ("its", ctypes.c_int), ("res", ctypes.c_double), ("matvecs", ctypes.c_int)]
+
+
+def _lgmres_native(handle, b, rtol, max_it, max_k, aug_dim, info):
+    from ._lib import TTK_ERR_NOT_CONVERGED
+    b = D.contig(b)
+    n = b.numel()
+    x = D.empty(n)
+    st = _Info()
+    s = D._stream()
+    rc = lib.ttk_lgmres(D.CTX[0] if D.CTX else None, int(handle), b.data_ptr(), x.data_ptr(), n, max_k, aug_dim,
+                        float(rtol), int(max_it), CHUNK, ctypes.byref(st))
+    if rc == TTK_ERR_NOT_CONVERGED:
+        raise PetscConvFailed(lib.ttk_last_error().decode())
+    D.check(rc, "lgmres")
+    del s
+    if info is not None:
+        info.update(reason=st.reason, its=st.its, res=st.res, matvecs=st.matvecs, native_matvecs=st.matvecs)
+    return x
+
+
 def _hh_size(max_k):
     ld = max_k + 1
     return 2 * (max_k + 2) * ld + (max_k + 2) + 2 * ld + 8
@@ -47,6 +74,8 @@ def lgmres(matvec_into, b, rtol=1e-8, max_it=300, restart=30, augment=2, abstol=
     n = b.numel()
     max_k = int(restart)
     aug_dim = int(augment)
+    if native and NATIVE_SOLVE and abstol == 1e-50 and dtol == 1e5 and haptol == 1e-30:
+        return _lgmres_native(native, b, rtol, max_it, max_k, aug_dim, info)
     x = D.zeros(n)
     V = D.empty(max_k + 1, n)
     hh = D.zeros(_hh_size(max_k))

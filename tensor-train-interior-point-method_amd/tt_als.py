@@ -7,6 +7,7 @@ its compressed variants) are the core-contraction kernels of the path: each is a
 whose pairwise steps run on the fp64-MFMA offset-table GEMM."""
 import time
 
+import ctypes
 import os
 
 import numpy as np
@@ -223,6 +224,42 @@ def compute_phi_fwd_A(P, xl, A, xr):
         return einsum(_APPLY, xl.permute(2, 1, 0), A.permute(1, 3, 0, 2), xr.permute(2, 1, 0), P, fused="env",
                       algo=("lsr,lML,sMNS,rNR->LSR", _shapes(P, xl, A, xr)))
     return einsum("lsr,lML,sMNS,rNR->LSR", P, xl, A, xr)
+
+
+class _EnvBlock(ctypes.Structure):
+    _fields_ = [("phi", ctypes.c_void_p), ("x", ctypes.c_void_p), ("A", ctypes.c_void_p), ("y", ctypes.c_void_p),
+                ("out", ctypes.c_void_p), ("phi_shape", ctypes.c_int64 * 3), ("x_shape", ctypes.c_int64 * 3),
+                ("A_shape", ctypes.c_int64 * 4), ("y_shape", ctypes.c_int64 * 3), ("a_strides", ctypes.c_int64 * 4)]
+
+
+NATIVE_ENV = os.environ.get("TTIPM_NATIVE_ENV", "1") == "1"
+
+
+def env_update_many(backward, items):
+    """All environment updates of one core step in ONE library call (`ttk_env_update`; the same
+    relabelled fused applies as compute_phi_*_A, recorded into one einsum batch).  items: list of
+    (P, x, A, y) with P, x, y contiguous; returns the new environments in order."""
+    if not (NATIVE_ENV and FUSED_ENV and D.DEV.type == "cuda") or \
+            not all(P.is_contiguous() and x.is_contiguous() and y.is_contiguous() for P, x, A, y in items):
+        f = compute_phi_bck_A if backward else compute_phi_fwd_A
+        return [f(P, x, A, y) for P, x, A, y in items]
+    arr = (_EnvBlock * len(items))()
+    outs = []
+    for e, (P, x, A, y) in zip(arr, items):
+        o = D.empty(*((x.shape[0], A.shape[0], y.shape[0]) if backward else (x.shape[2], A.shape[3], y.shape[2])))
+        outs.append(o)
+        e.phi, e.x, e.A, e.y, e.out = P.data_ptr(), x.data_ptr(), A.data_ptr(), y.data_ptr(), o.data_ptr()
+        e.phi_shape[:] = tuple(P.shape)
+        e.x_shape[:] = tuple(x.shape)
+        e.A_shape[:] = tuple(A.shape)
+        e.y_shape[:] = tuple(y.shape)
+        e.a_strides[:] = tuple(A.stride())
+        if D.ALGO is not None:
+            eq = "LSR,lML,sMNS,rNR->lsr" if backward else "lsr,lML,sMNS,rNR->LSR"
+            D.count_algo(D.algo_flops(eq, _shapes(P, x, A, y)), what=eq)
+    D._stream()
+    D.check(D.lib.ttk_env_update(D.CTX[0], int(backward), len(items), arr), "env_update")
+    return outs
 
 
 def compute_phi_bck_rhs(P, b, x):
@@ -458,25 +495,23 @@ def _sweep(c, backward, swp, last, dsf):
             zk = z[k]
         # every environment of the core step (XAX/Xb and, for AMEn, ZAX/Zb; src/tt_als.py:372-387,
         # 499-514) in one einsum batch: grouped launches instead of one launch per block
+        src, dst = (k + 1, k) if backward else (k, k + 1)
+        keys = list(Ak.keys())
+        items = [(c.XAX[src][key], x[k], Ak[key], x[k]) for key in keys]
+        zkeys = []
+        if zk is not None:
+            zkeys = keys + [lt for ij, lt in Ak._transposes.items()]
+            items += [(c.ZAX[src][key], zk, Ak[key], x[k]) for key in keys]
+            items += [(c.ZAX[src][lt], zk, Ak[ij].transpose(1, 2), x[k]) for ij, lt in Ak._transposes.items()]
+        envs = env_update_many(backward, items)
+        c.XAX[dst] = dict(zip(keys, envs[:len(keys)]))
+        if zk is not None:
+            c.ZAX[dst] = dict(zip(zkeys, envs[len(keys):]))
+        rhs_env = compute_phi_bck_rhs if backward else compute_phi_fwd_rhs
         with D.einsum_batch():
-            if backward:
-                c.XAX[k] = {key: compute_phi_bck_A(c.XAX[k + 1][key], x[k], Ak[key], x[k]) for key in Ak.keys()}
-                c.Xb[k] = {i: compute_phi_bck_rhs(c.Xb[k + 1][i], bk[i], x[k]) for i in bk}
-                if zk is not None:
-                    zz = {key: compute_phi_bck_A(c.ZAX[k + 1][key], zk, Ak[key], x[k]) for key in Ak.keys()}
-                    zz.update({lt: compute_phi_bck_A(c.ZAX[k + 1][lt], zk, Ak[ij].transpose(1, 2), x[k])
-                               for ij, lt in Ak._transposes.items()})
-                    c.ZAX[k] = zz
-                    c.Zb[k] = {i: compute_phi_bck_rhs(c.Zb[k + 1][i], bk[i], zk) for i in bk}
-            else:
-                c.XAX[k + 1] = {key: compute_phi_fwd_A(c.XAX[k][key], x[k], Ak[key], x[k]) for key in Ak.keys()}
-                c.Xb[k + 1] = {i: compute_phi_fwd_rhs(c.Xb[k][i], bk[i], x[k]) for i in bk}
-                if zk is not None:
-                    zz = {key: compute_phi_fwd_A(c.ZAX[k][key], zk, Ak[key], x[k]) for key in Ak.keys()}
-                    zz.update({lt: compute_phi_fwd_A(c.ZAX[k][lt], zk, Ak[ij].transpose(1, 2), x[k])
-                               for ij, lt in Ak._transposes.items()})
-                    c.ZAX[k + 1] = zz
-                    c.Zb[k + 1] = {i: compute_phi_fwd_rhs(c.Zb[k][i], bk[i], zk) for i in bk}
+            c.Xb[dst] = {i: rhs_env(c.Xb[src][i], bk[i], x[k]) for i in bk}
+            if zk is not None:
+                c.Zb[dst] = {i: rhs_env(c.Zb[src][i], bk[i], zk) for i in bk}
     if dx_seq:
         n_used = sum(1 for j in dx_seq if j is not None)
         vals = D.read(dx_buf[:2 * n_used]) if n_used else None

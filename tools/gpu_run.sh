@@ -29,11 +29,16 @@ for step in "$@"; do
              || { tail -20 gpurun_out/${tag}_bench.err; exit 1; }
            cut -c1-600 gpurun_out/${tag}_bench.json ;;
     stats) args=${rest:-"--steps 5 --warmup 1 --no-cpu-baseline"}
-           timeout -k 10 900 rocprofv3 --kernel-trace --stats -d gpurun_out/${tag}_stats -o run -- \
-             python3 bench.py $args > gpurun_out/${tag}_stats.log 2>&1 || { tail -20 gpurun_out/${tag}_stats.log; exit 1; } ;;
+           timeout -k 10 900 rocprofv3 --kernel-trace --stats -d /tmp/${tag}_stats -o run -- \
+             python3 bench.py $args > gpurun_out/${tag}_stats.log 2>&1 || { tail -20 gpurun_out/${tag}_stats.log; exit 1; }
+           # keep the summaries only (the full kernel trace exceeds what gpurun copies back)
+           for f in $(find /tmp/${tag}_stats -name "*stats.csv"); do cp $f gpurun_out/${tag}_$(basename $f); done
+           ls gpurun_out/ | grep "^${tag}_" ;;
     pmc)   cn=${rest%%:*}; args=${rest#*:}; [ "$args" = "$rest" ] && args="--steps 1 --warmup 0 --no-cpu-baseline --no-roofline"
-           timeout -s KILL 300 rocprofv3 --pmc ${cn//,/ } -d gpurun_out/${tag}_pmc_${cn%%,*} -o run -- \
-             python3 bench.py $args > gpurun_out/${tag}_pmc_${cn%%,*}.log 2>&1 || { tail -20 gpurun_out/${tag}_pmc_${cn%%,*}.log; exit 1; } ;;
+           timeout -s KILL 300 rocprofv3 --pmc ${cn//,/ } -d /tmp/${tag}_pmc_${cn%%,*} -o run -- \
+             python3 bench.py $args > gpurun_out/${tag}_pmc_${cn%%,*}.log 2>&1 || { tail -20 gpurun_out/${tag}_pmc_${cn%%,*}.log; exit 1; }
+           for f in $(find /tmp/${tag}_pmc_${cn%%,*} -name "*counter_collection*.csv" -o -name "*stats.csv"); do
+             cp $f gpurun_out/${tag}_pmc_${cn%%,*}_$(basename $f); done ;;
     py)    script=${rest%%:*}; args=${rest#*:}; [ "$args" = "$rest" ] && args=""
            timeout -k 10 900 python -u $script $args > gpurun_out/${tag}_$(basename $script .py).log 2>&1 \
              || { tail -30 gpurun_out/${tag}_$(basename $script .py).log; exit 1; }
