@@ -759,6 +759,12 @@ struct SchurOp {
   int ineq;
   double flops;
   bool used;
+  // blocks beyond the fused kernel's limits (graphm-sized ranks): the operator is applied as the
+  // per-block local applies on the pairwise MFMA plan, recorded into two einsum batches
+  bool pairwise;
+  std::vector<int64_t> desc;  // nblk x 36 words (ttk_einsum descriptors, x pointer patched per call)
+  const double *inv_I;
+  int64_t r, n, R;
 };
 std::vector<SchurOp> &schur_ops() {  // the current context's handle table
   ttk::Ctx &c = ttk::ctx();
@@ -791,6 +797,76 @@ double term_flops(const ApplyArgs &g) {
 
 }  // namespace
 
+static int schur_store(SchurOp &op, int64_t m, int64_t *handle) {
+  return schur_store(op, m, handle);
+}
+
+// descriptor words: [0] nops|flags, P record 1..8, A record 9..18, Q record 19..26, x record 27..34
+// ([27] pointer, [28] ndim 3, [29..31] r n R, [32..34] strides), [35] has_out = 0
+static constexpr int SW = 36, SX = 27;
+
+static int schur_build_pairwise(int ineq, int64_t m, const int64_t *descs, const double *inv_I, int64_t *handle) {
+  const int nblk = ineq ? 7 : 5;
+  for (int b = 0; b < nblk; ++b) {
+    const int64_t *d = descs + (int64_t)b * SW;
+    if ((d[0] & 255) != 4 || d[2] != 3 || d[10] != 4 || d[20] != 3 || d[SX + 1] != 3 || d[35] != 0) return TTK_OK;
+    if (d[SX + 2] * d[SX + 3] * d[SX + 4] != m) return TTK_OK;
+  }
+  SchurOp op{};
+  op.m = m;
+  op.ineq = ineq;
+  op.pairwise = true;
+  op.desc.assign(descs, descs + (int64_t)nblk * SW);
+  op.inv_I = inv_I;
+  op.r = descs[SX + 2];
+  op.n = descs[SX + 3];
+  op.R = descs[SX + 4];
+  op.flops = 0.0;
+  return schur_store(op, m, handle);
+}
+
+// the per-block sequence of MatVecWrapper.matvec_into / IneqMatVecWrapper.matvec_into
+// (tensor-train-interior-point-method_amd/tt_ipm.py; cy_src/lgmres_cy.pyx:297-327,490-508), same
+// einsum calls in the same order, the independent ones recorded into one batch
+static int schur_apply_pairwise(void *stream, const SchurOp &op, const double *v, double *out) {
+  static const char *F = "lsr,smnS,LSR,rnR->lmL", *T = "lsr,smnS,LSR,lmL->rnR";
+  const int64_t m = op.m;
+  double *w = ttk::ctx().schur_w;
+  const double *y = v, *x = v + m, *t = v + 2 * m;
+  double *o0 = out, *o1 = out + m, *o2 = out + 2 * m;
+  auto apply = [&](int blk, const double *xin, double *o, double alpha, double beta) {
+    int64_t d[SW + 5];
+    std::memcpy(d, op.desc.data() + (int64_t)blk * SW, (SW - 1) * sizeof(int64_t));
+    d[SX] = reinterpret_cast<int64_t>(xin);
+    d[SW - 1] = 1;  // output strides: contiguous (r, n, R)
+    d[SW] = 3;
+    d[SW + 1] = op.n * op.R;
+    d[SW + 2] = op.R;
+    d[SW + 3] = 1;
+    return ttk_einsum(stream, blk == 4 ? T : F, d, o, alpha, beta);
+  };
+  const int64_t shp[3] = {op.r, op.n, op.R}, st[3] = {op.n * op.R, op.R, 1};
+  int rc = ttk_einsum_batch_begin(stream);
+  if (rc) return rc;
+  if (!rc) rc = apply(0, y, o0, 1.0, 0.0);   // B00 y
+  if (!rc) rc = apply(1, x, o0, 1.0, 1.0);   // + B01 x
+  if (!rc) rc = apply(2, x, o1, 1.0, 0.0);   // B21 x
+  if (!rc) rc = apply(4, y, w, 1.0, 0.0);    // B01^T y
+  int rc2 = ttk_einsum_batch_end(stream);
+  if (rc || rc2) return rc ? rc : rc2;
+  if ((rc = ttk_mul_nd(stream, w, op.inv_I, w, 3, shp, st, st, st, 1.0, 0.0))) return rc;  // inv_I o B01^T y
+  if (op.ineq && (rc = ttk_copy_nd(stream, t, w, 3, shp, st, st, 1.0, 1.0))) return rc;    // + t
+  if ((rc = apply(3, w, o1, -1.0, 1.0))) return rc;                                      // - B22 w
+  if (op.ineq) {
+    if ((rc = ttk_einsum_batch_begin(stream))) return rc;
+    if (!rc) rc = apply(5, x, o2, 1.0, 0.0);  // B31 x
+    if (!rc) rc = apply(6, t, o2, 1.0, 1.0);  // + B33 t
+    rc2 = ttk_einsum_batch_end(stream);
+    if (rc || rc2) return rc ? rc : rc2;
+  }
+  return TTK_OK;
+}
+
 extern "C" {
 
 int ttk_schur_build(int ineq, int64_t m, const int64_t *descs, const double *inv_I, int64_t *handle) {
@@ -799,14 +875,17 @@ int ttk_schur_build(int ineq, int64_t m, const int64_t *descs, const double *inv
   const int nblk = ineq ? 7 : 5;
   ApplyArgs g[7];
   static const char *F = "lsr,smnS,LSR,rnR->lmL", *T = "lsr,smnS,LSR,lmL->rnR";
-  for (int b = 0; b < nblk; ++b) {
-    if (!apply_args(b == 4 ? T : F, descs + (int64_t)b * W, nullptr, 1.0, 0.0, g[b])) return TTK_OK;
-    if ((int64_t)g[b].na * g[b].ni * g[b].nc != m) return TTK_OK;
-    if (term_flops(g[b]) > fused_max_flops()) return TTK_OK;  // the pairwise MFMA plan is faster there
+  bool fused_ok = true;
+  for (int b = 0; b < nblk && fused_ok; ++b) {
+    if (!apply_args(b == 4 ? T : F, descs + (int64_t)b * W, nullptr, 1.0, 0.0, g[b])) fused_ok = false;
+    else if ((int64_t)g[b].na * g[b].ni * g[b].nc != m) return TTK_OK;
+    else if (term_flops(g[b]) > fused_max_flops()) fused_ok = false;  // the pairwise MFMA plan is faster there
   }
+  if (!fused_ok) return schur_build_pairwise(ineq, m, descs, inv_I, handle);
   SchurOp op{};
   op.m = m;
   op.ineq = ineq;
+  op.pairwise = false;
   // stage 1
   ApplyLaunch &L1 = op.st[0];
   L1.ntask = ineq ? 3 : 2;
@@ -850,26 +929,7 @@ int ttk_schur_build(int ineq, int64_t m, const int64_t *descs, const double *inv
     op.shm[s] = multi_lds(L);
     if (op.shm[s] > (size_t)APPLY_LDS_DOUBLES * sizeof(double)) return TTK_OK;
   }
-  ttk::Ctx &cx = ttk::ctx();
-  if (m > cx.schur_wcap) {
-    if (cx.schur_w) {
-      TTK_HIP(cx.stream ? hipStreamSynchronize(cx.stream) : hipDeviceSynchronize());
-      (void)hipFree(cx.schur_w);
-    }
-    cx.schur_w = nullptr;
-    cx.schur_wcap = 0;
-    const int64_t want = m < 65536 ? 65536 : m;
-    TTK_HIP(hipMalloc(reinterpret_cast<void **>(&cx.schur_w), want * sizeof(double)));
-    cx.schur_wcap = want;
-  }
-  op.used = true;
-  std::vector<SchurOp> &ops = schur_ops();
-  size_t slot = 0;
-  while (slot < ops.size() && ops[slot].used) ++slot;
-  if (slot == ops.size()) ops.push_back(op);
-  else ops[slot] = op;
-  *handle = (int64_t)slot + 1;
-  return TTK_OK;
+  return schur_store(op, m, handle);
 }
 
 int ttk_schur_apply(void *stream, int64_t handle, const double *v, double *out) {
@@ -879,6 +939,7 @@ int ttk_schur_apply(void *stream, int64_t handle, const double *v, double *out) 
     return TTK_ERR_ARG;
   }
   SchurOp &op = ops[handle - 1];
+  if (op.pairwise) return schur_apply_pairwise(stream, op, v, out);
   const int64_t m = op.m;
   double *w = ttk::ctx().schur_w;
   const double *in[4] = {v, v + m, v + 2 * m, w};

@@ -253,6 +253,45 @@ def test_ineq_schur_operator_handle_is_bit_identical(dev, ci):
     assert np.array_equal(dev.read(op.matvec(x)), dev.read(ref.matvec(x)))
 
 
+@pytest.mark.parametrize("ineq", [False, True])
+def test_pairwise_schur_handle_is_bit_identical(dev, ineq):
+    """graphm-sized blocks (beyond the fused kernel): the native handle applies the operator as the
+    per-block pairwise-plan applies in two einsum batches -- same bits as the Python per-block path,
+    and the whole native LGMRES solve equals the Python-driven one"""
+    from ttipm_amd import lgmres as LG
+    from ttipm_amd import tt_ipm
+    rng = np.random.default_rng(5)
+    r, R, s, n = 24, 22, 12, 4
+    keys = tt_ipm.IneqMatVecWrapper.keys if ineq else tt_ipm.MatVecWrapper.keys
+    L = {k: dev.from_numpy(rng.standard_normal((r, s, r)) * 0.1) for k in keys}
+    Am = {k: dev.from_numpy(rng.standard_normal((s, n, n, s)) * 0.1) for k in keys}
+    Rr = {k: dev.from_numpy(rng.standard_normal((R, s, R)) * 0.1) for k in keys}
+    for k in [(0, 0), (2, 1)]:
+        L[k][:, 0] += dev.from_numpy(np.eye(r))
+        Am[k][0, :, :, 0] += dev.from_numpy(np.eye(n))
+        Rr[k][:, 0] += dev.from_numpy(np.eye(R))
+    invI = dev.from_numpy(rng.uniform(0.5, 2.0, (r, n, R)))
+    cls = tt_ipm.IneqMatVecWrapper if ineq else tt_ipm.MatVecWrapper
+    op = cls(L, Am, Rr, invI, (r, n, R))
+    old = tt_ipm.SCHUR_OP
+    try:
+        tt_ipm.SCHUR_OP = False
+        ref = cls(L, Am, Rr, invI, (r, n, R))
+    finally:
+        tt_ipm.SCHUR_OP = old
+    assert op.h != 0 and ref.h == 0
+    nb = 3 if ineq else 2
+    x = dev.from_numpy(rng.standard_normal(nb * r * n * R))
+    assert np.array_equal(dev.read(op.matvec(x)), dev.read(ref.matvec(x)))
+    m = r * n * R
+    b = dev.from_numpy(rng.standard_normal(nb * m))
+    i1, i2 = {}, {}
+    x1 = LG.lgmres(op.matvec_into, b, rtol=1e-5, max_it=60, restart=40, augment=4, info=i1, native=op.h)
+    x2 = LG.lgmres(ref.matvec_into, b, rtol=1e-5, max_it=60, restart=40, augment=4, info=i2)
+    assert i1["its"] == i2["its"] and i1["reason"] == i2["reason"]
+    assert np.array_equal(dev.read(x1), dev.read(x2))
+
+
 @pytest.mark.parametrize("ci", range(3))
 def test_lgmres_chunked_syncs_are_exact(dev, ci):
     """speculative Arnoldi chunks (one host read per chunk) give the step-by-step iterates exactly"""

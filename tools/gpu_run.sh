@@ -3,6 +3,7 @@
 #   gpurun --timeout 900 -- 'bash tools/gpu_run.sh TAG STEP [STEP ...]'
 # STEP is one of
 #   tests           pytest -m gpu (one process, per-test timeout)
+#   pytest:PATHS    pytest on the given test files / node ids
 #   smoke           __graft_entry__.smoke()
 #   bench[:ARGS]    python bench.py ARGS (default --steps 5 --warmup 1), JSON line -> gpurun_out/TAG_bench.json
 #   stats[:ARGS]    rocprofv3 --kernel-trace --stats over bench.py ARGS -> gpurun_out/TAG_stats/
@@ -21,6 +22,9 @@ for step in "$@"; do
     tests) timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
              > gpurun_out/${tag}_tests.log 2>&1 || { tail -30 gpurun_out/${tag}_tests.log; exit 1; }
            tail -3 gpurun_out/${tag}_tests.log ;;
+    pytest) timeout -k 10 900 python -u -m pytest ${rest} -x -v --timeout 300 --timeout-method thread \
+             > gpurun_out/${tag}_pytest.log 2>&1 || { tail -30 gpurun_out/${tag}_pytest.log; exit 1; }
+           tail -3 gpurun_out/${tag}_pytest.log ;;
     smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${tag}_smoke.log 2>&1 \
              || { tail -20 gpurun_out/${tag}_smoke.log; exit 1; }
            tail -2 gpurun_out/${tag}_smoke.log ;;
@@ -29,7 +33,7 @@ for step in "$@"; do
              || { tail -20 gpurun_out/${tag}_bench.err; exit 1; }
            cut -c1-600 gpurun_out/${tag}_bench.json ;;
     stats) args=${rest:-"--steps 5 --warmup 1 --no-cpu-baseline"}
-           timeout -k 10 900 rocprofv3 --kernel-trace --stats -d /tmp/${tag}_stats -o run -- \
+           timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/${tag}_stats -o run -- \
              python3 bench.py $args > gpurun_out/${tag}_stats.log 2>&1 || { tail -20 gpurun_out/${tag}_stats.log; exit 1; }
            # keep the summaries only (the full kernel trace exceeds what gpurun copies back)
            for f in $(find /tmp/${tag}_stats -name "*stats.csv"); do cp $f gpurun_out/${tag}_$(basename $f); done
