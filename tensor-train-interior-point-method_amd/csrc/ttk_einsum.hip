@@ -927,7 +927,8 @@ int ttk_schur_build(int ineq, int64_t m, const int64_t *descs, const double *inv
       for (int k = 0; k < L.task[t].nterms; ++k) op.flops += term_flops(L.task[t].t[k]);
     }
     op.shm[s] = multi_lds(L);
-    if (op.shm[s] > (size_t)APPLY_LDS_DOUBLES * sizeof(double)) return TTK_OK;
+    if (op.shm[s] > (size_t)APPLY_LDS_DOUBLES * sizeof(double))  // multi-task stage beyond LDS
+      return schur_build_pairwise(ineq, m, descs, inv_I, handle);
   }
   return schur_store(op, m, handle);
 }
