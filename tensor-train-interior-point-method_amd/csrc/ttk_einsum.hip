@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -798,7 +799,26 @@ double term_flops(const ApplyArgs &g) {
 }  // namespace
 
 static int schur_store(SchurOp &op, int64_t m, int64_t *handle) {
-  return schur_store(op, m, handle);
+  ttk::Ctx &cx = ttk::ctx();
+  if (m > cx.schur_wcap) {
+    if (cx.schur_w) {
+      TTK_HIP(cx.stream ? hipStreamSynchronize(cx.stream) : hipDeviceSynchronize());
+      (void)hipFree(cx.schur_w);
+    }
+    cx.schur_w = nullptr;
+    cx.schur_wcap = 0;
+    const int64_t want = m < 65536 ? 65536 : m;
+    TTK_HIP(hipMalloc(reinterpret_cast<void **>(&cx.schur_w), want * sizeof(double)));
+    cx.schur_wcap = want;
+  }
+  op.used = true;
+  std::vector<SchurOp> &ops = schur_ops();
+  size_t slot = 0;
+  while (slot < ops.size() && ops[slot].used) ++slot;
+  if (slot == ops.size()) ops.push_back(op);
+  else ops[slot] = op;
+  *handle = (int64_t)slot + 1;
+  return TTK_OK;
 }
 
 // descriptor words: [0] nops|flags, P record 1..8, A record 9..18, Q record 19..26, x record 27..34
