@@ -94,6 +94,11 @@ int ttk_einsum(void *stream, const char *eq, const int64_t *desc, double *out, d
  * block local products and the rank loop's candidate products (`src/tt_als.py:334-346`).
  * ttk_copy_nd / ttk_mul_nd flush pending steps first.  Nesting counts; only the outermost end
  * launches.  stats: [flushes, recorded steps, launches]. */
+/* Local applies beyond the VALU fused kernel's FLOP range (graphm-sized blocks) run the same three
+ * stages on fp64 MFMA in one launch (one workgroup per output row) when they fit LDS; off: the
+ * pairwise plan.  Returns the previous setting (default on; env TTK_FUSED_MFMA=0 turns it off). */
+int ttk_fused_set_mfma(int on);
+
 int ttk_einsum_batch_begin(void *stream);
 int ttk_einsum_batch_flush(void *stream);
 int ttk_einsum_batch_end(void *stream);

@@ -510,6 +510,7 @@ struct ApplyArgs {
   int64_t ps[3], as[4], qs[3], xs[3], os[3];
   int na, ns, nb, ni, nj, nS, nc, nd;
   double alpha, beta;
+  int mfma;  // 1: the row runs on the MFMA stages (apply_row_mfma), 0: VALU (apply_row)
 };
 
 // Association follows the greedy pairwise plan the reference's opt_einsum picks for these shapes
@@ -578,6 +579,116 @@ __device__ void apply_row(const ApplyArgs &g, int a, double *sm, double *orow) {
   }
 }
 
+// ---- MFMA variant of one output row, for operator blocks beyond the VALU kernel's FLOP range
+// (graphm-sized ranks: r, R ~ 44, operator ranks ~ 10): the same three stages (t1 = P x over b,
+// t2 = A t1 over (s, j), out = Q t2 over (S, d) -- the association of apply_row and of the greedy
+// pairwise plan) as small GEMMs on v_mfma_f64_16x16x4f64, 4 waves sharing the 16x16 output tiles.
+// LDS: X (x staged), Pa (row a of P), As (A as [(i,S)][(s,j)]), T1 [(s,j)][d], T2 [(i,S)][d] and a
+// chunk of Q ([c][S'][d] for a range of S) per stage-3 K block.
+typedef double dbl4 __attribute__((ext_vector_type(4)));
+
+// C(m, n) += sum_k A(m, k) B(k, n) over 16x16 tiles, waves round-robin over tiles; A/B/C functors
+// (LDS reads / writes).  Two independent accumulators per tile (even / odd K steps) shorten the MFMA
+// dependency chain; they are added at the end.
+template <class FA, class FB, class FC>
+__device__ __forceinline__ void wg_mfma(int M, int N, int K, FA fa, FB fb, FC fc) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int tm = (M + 15) >> 4, tn = (N + 15) >> 4;
+  for (int t = wid; t < tm * tn; t += nw) {
+    const int m0 = (t / tn) << 4, n0 = (t % tn) << 4;
+    const int am = m0 + (lane & 15), bn = n0 + (lane & 15), kl = lane >> 4;
+    const bool mok = am < M, nok = bn < N;
+    dbl4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+    int k0 = 0;
+    for (; k0 + 8 <= K; k0 += 8) {
+      const double a0 = mok ? fa(am, k0 + kl) : 0.0, b0 = nok ? fb(k0 + kl, bn) : 0.0;
+      const double a1 = mok ? fa(am, k0 + 4 + kl) : 0.0, b1 = nok ? fb(k0 + 4 + kl, bn) : 0.0;
+      acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc1, 0, 0, 0);
+    }
+    for (; k0 < K; k0 += 4) {
+      const int k = k0 + kl;
+      const double a0 = (mok && k < K) ? fa(am, k) : 0.0, b0 = (nok && k < K) ? fb(k, bn) : 0.0;
+      acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = m0 + (lane >> 4) + 4 * r;
+      if (row < M && nok) fc(row, bn, acc0[r] + acc1[r]);
+    }
+  }
+}
+
+constexpr int QCHUNK_MAX = 4096;  // doubles of Q staged per stage-3 K block
+
+int64_t apply_mfma_lds(const ApplyArgs &g) {
+  return (int64_t)g.nb * g.nj * g.nd + (int64_t)g.ns * g.nb + (int64_t)g.ni * g.nS * g.ns * g.nj +
+         (int64_t)g.ns * g.nj * g.nd + (int64_t)g.ni * g.nS * g.nd + QCHUNK_MAX + (int64_t)g.ni * g.nc;
+}
+
+template <bool DIRECT>
+__device__ void apply_row_mfma(const ApplyArgs &g, int a, double *sm, double *orow) {
+  const int tid = threadIdx.x, nt = blockDim.x;
+  const int nb = g.nb, nj = g.nj, nd = g.nd, nS = g.nS, ns = g.ns, ni = g.ni, nc = g.nc;
+  const int jd = nj * nd, sj = ns * nj;
+  double *X = sm;                       // [b][j][d]
+  double *Pa = X + nb * jd;             // [s][b]
+  double *As = Pa + ns * nb;            // [(i,S)][(s,j)]
+  double *T1 = As + ni * nS * sj;       // [(s,j)][d]
+  double *T2 = T1 + sj * nd;            // [(i,S)][d]
+  double *Qc = T2 + ni * nS * nd;       // [c][S'][d], QCHUNK_MAX
+  for (int e = tid; e < nb * jd; e += nt) {
+    const int b = e / jd, r = e - b * jd, j = r / nd, d = r - j * nd;
+    X[e] = g.x[b * g.xs[0] + j * g.xs[1] + d * g.xs[2]];
+  }
+  for (int e = tid; e < ns * nb; e += nt) {
+    const int s_ = e / nb, b = e - s_ * nb;
+    Pa[e] = g.P[a * g.ps[0] + s_ * g.ps[1] + b * g.ps[2]];
+  }
+  for (int e = tid; e < ni * nS * sj; e += nt) {
+    const int m = e / sj, k = e - m * sj, i = m / nS, S = m - i * nS, s_ = k / nj, j = k - s_ * nj;
+    As[e] = g.A[s_ * g.as[0] + i * g.as[1] + j * g.as[2] + S * g.as[3]];
+  }
+  __syncthreads();
+  // stage 1: T1[s][(j,d)] = sum_b Pa[s][b] X[b][(j,d)]
+  wg_mfma(ns, jd, nb, [&](int m, int k) { return Pa[m * nb + k]; }, [&](int k, int n) { return X[k * jd + n]; },
+          [&](int m, int n, double v) { T1[m * jd + n] = v; });
+  __syncthreads();
+  // stage 2: T2[(i,S)][d] = sum_{(s,j)} As[(i,S)][(s,j)] T1[(s,j)][d]
+  wg_mfma(ni * nS, nd, sj, [&](int m, int k) { return As[m * sj + k]; }, [&](int k, int n) { return T1[k * nd + n]; },
+          [&](int m, int n, double v) { T2[m * nd + n] = v; });
+  __syncthreads();
+  // stage 3: out[i][c] = sum_{(S,d)} T2[(i,S)][d] Q[c,S,d], K blocked over S (Q chunk staged in LDS)
+  int sc = QCHUNK_MAX / (nc * nd);
+  sc = sc < 1 ? 1 : (sc > nS ? nS : sc);
+  double *acc = DIRECT ? Qc + sc * nc * nd : orow;  // DIRECT: partial sums after the Q chunk
+  for (int S0 = 0; S0 < nS; S0 += sc) {
+    const int se = S0 + sc < nS ? S0 + sc : nS, w = se - S0;
+    for (int e = tid; e < nc * w * nd; e += nt) {
+      const int c = e / (w * nd), r = e - c * (w * nd), S = r / nd, d = r - S * nd;
+      Qc[e] = g.Q[c * g.qs[0] + (S0 + S) * g.qs[1] + d * g.qs[2]];
+    }
+    __syncthreads();
+    const bool first = S0 == 0;
+    wg_mfma(ni, nc, w * nd, [&](int m, int k) { const int S = k / nd, d = k - S * nd; return T2[(m * nS + S0 + S) * nd + d]; },
+            [&](int k, int n) { return Qc[n * (w * nd) + k]; },
+            [&](int m, int n, double v) { acc[m * nc + n] = first ? v : acc[m * nc + n] + v; });
+    __syncthreads();
+  }
+  if (DIRECT) {
+    for (int e = tid; e < ni * nc; e += nt) {
+      const int i = e / nc, c = e - i * nc;
+      double *o = g.out + a * g.os[0] + i * g.os[1] + c * g.os[2];
+      *o = g.beta != 0.0 ? g.alpha * acc[e] + g.beta * *o : g.alpha * acc[e];
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void fused_apply_mfma_kernel(ApplyArgs g) {
+  extern __shared__ double sm[];
+  apply_row_mfma<true>(g, blockIdx.x, sm, nullptr);
+}
+
 __global__ __launch_bounds__(256) void fused_apply_kernel(ApplyArgs g) {
   extern __shared__ double sm[];
   apply_row<true>(g, blockIdx.x, sm, nullptr);
@@ -608,7 +719,8 @@ __global__ __launch_bounds__(256) void fused_apply_multi_kernel(ApplyLaunch L) {
   const int ni = g0.ni, nc = g0.nc, tid = threadIdx.x, nt = blockDim.x;
   double *orow = sm, *acc = sm + ni * nc, *work = acc + ni * nc;
   for (int k = 0; k < T.nterms; ++k) {
-    apply_row<false>(T.t[k], a, work, k == 0 ? orow : acc);
+    if (T.t[k].mfma) apply_row_mfma<false>(T.t[k], a, work, k == 0 ? orow : acc);
+    else apply_row<false>(T.t[k], a, work, k == 0 ? orow : acc);
     __syncthreads();
     if (k > 0) {
       const double al = T.t[k].alpha;
@@ -647,6 +759,16 @@ static double fused_max_flops() {
 
 // ApplyArgs of a local-apply equation from an einsum descriptor (see ttk_einsum); 1 if the fused
 // kernel can run it (LDS and grid limits), 0 otherwise
+// MFMA stages for the blocks beyond the VALU kernel's FLOP range (TTK_FUSED_MFMA=0: pairwise plan)
+static int g_fused_mfma = !getenv("TTK_FUSED_MFMA") || atoi(getenv("TTK_FUSED_MFMA")) != 0;
+static bool mfma_enabled() { return g_fused_mfma != 0; }
+
+extern "C" int ttk_fused_set_mfma(int on) {
+  const int old = g_fused_mfma;
+  g_fused_mfma = on;
+  return old;
+}
+
 static int apply_args(const char *eq, const int64_t *desc, double *out, double alpha, double beta, ApplyArgs &g) {
   const bool fwd = std::strcmp(eq, "lsr,smnS,LSR,rnR->lmL") == 0;
   const bool bwd = !fwd && std::strcmp(eq, "lsr,smnS,LSR,lmL->rnR") == 0;
@@ -706,9 +828,14 @@ static int apply_args(const char *eq, const int64_t *desc, double *out, double a
     g.os[1] = g.nc;
     g.os[0] = (int64_t)g.ni * g.nc;
   }
-  const int64_t need = apply_lds(g.nb, g.nj, g.nd, g.nS, g.ns, g.ni);
-  if (need > APPLY_LDS_DOUBLES || g.na < 1 || g.na > 65535) return 0;
-  return 1;
+  g.mfma = 0;
+  if (g.na < 1 || g.na > 65535) return 0;
+  if (apply_lds(g.nb, g.nj, g.nd, g.nS, g.ns, g.ni) <= APPLY_LDS_DOUBLES) return 1;
+  if (mfma_enabled() && apply_mfma_lds(g) <= APPLY_LDS_DOUBLES) {  // only the MFMA stages fit LDS
+    g.mfma = 1;
+    return 1;
+  }
+  return 0;
 }
 
 static int batch_add_fused(const ApplyArgs &g, int64_t lds_doubles);
@@ -717,7 +844,6 @@ int fused_apply_try(void *stream, const char *eq, const int64_t *desc, double *o
   if (!(desc[0] & 256)) return 0;  // caller did not opt in
   ApplyArgs g;
   if (!apply_args(eq, desc, out, alpha, beta, g)) return 0;
-  const int64_t need = apply_lds(g.nb, g.nj, g.nd, g.nS, g.ns, g.ni);
   // one workgroup per output row runs the three stages on the VALU: past a few MFLOP per launch
   // the pairwise MFMA plan (with split-K) is faster (graphm_3 r=2 sizes)
   const double flops = 2.0 * g.na *
@@ -728,17 +854,25 @@ int fused_apply_try(void *stream, const char *eq, const int64_t *desc, double *o
   // a larger share of the chain: fused only while small
   static const double env_max_flops =
       getenv("TTK_FUSED_ENV_MAX_FLOPS") ? atof(getenv("TTK_FUSED_ENV_MAX_FLOPS")) : 1e6;
-  if (flops > ((desc[0] & 512) ? env_max_flops : max_flops)) return 0;
+  if (flops > ((desc[0] & 512) ? env_max_flops : max_flops)) {
+    // beyond the VALU kernel's range: the MFMA stages when they fit LDS, else the pairwise plan
+    if (!mfma_enabled() || apply_mfma_lds(g) > APPLY_LDS_DOUBLES) return 0;
+    g.mfma = 1;
+  }
+  const int64_t need = g.mfma ? apply_mfma_lds(g) : apply_lds(g.nb, g.nj, g.nd, g.nS, g.ns, g.ni);
   if (batch_on()) return batch_add_fused(g, need) == TTK_OK ? 1 : -1;
   const size_t shm = need * sizeof(double);
-  if (shm > 65536)
-    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(fused_apply_kernel),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+  const void *kern = g.mfma ? reinterpret_cast<const void *>(fused_apply_mfma_kernel)
+                            : reinterpret_cast<const void *>(fused_apply_kernel);
+  if (shm > 65536) (void)hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
   static const int dbg_sync = getenv("TTK_FUSED_SYNC") != nullptr;
   if (dbg_sync) (void)hipStreamSynchronize(TTK_STREAM(stream));
   hipEvent_t e0, e1;
   if (ttk::contract_events_ext(&e0, &e1) != TTK_OK) return -1;
-  hipExtLaunchKernelGGL(fused_apply_kernel, dim3(g.na), dim3(256), shm, TTK_STREAM(stream), e0, e1, 0, g);
+  if (g.mfma)
+    hipExtLaunchKernelGGL(fused_apply_mfma_kernel, dim3(g.na), dim3(256), shm, TTK_STREAM(stream), e0, e1, 0, g);
+  else
+    hipExtLaunchKernelGGL(fused_apply_kernel, dim3(g.na), dim3(256), shm, TTK_STREAM(stream), e0, e1, 0, g);
   TTK_LAUNCH_CHECK();
   ttk::contract_count_ext(flops);
   return 1;
@@ -781,7 +915,7 @@ size_t multi_lds(const ApplyLaunch &L) {
     int64_t w = 0;
     for (int k = 0; k < T.nterms; ++k) {
       const ApplyArgs &g = T.t[k];
-      const int64_t l = apply_lds(g.nb, g.nj, g.nd, g.nS, g.ns, g.ni);
+      const int64_t l = g.mfma ? apply_mfma_lds(g) : apply_lds(g.nb, g.nj, g.nd, g.nS, g.ns, g.ni);
       w = l > w ? l : w;
     }
     need += w;
@@ -899,7 +1033,10 @@ int ttk_schur_build(int ineq, int64_t m, const int64_t *descs, const double *inv
   for (int b = 0; b < nblk && fused_ok; ++b) {
     if (!apply_args(b == 4 ? T : F, descs + (int64_t)b * W, nullptr, 1.0, 0.0, g[b])) fused_ok = false;
     else if ((int64_t)g[b].na * g[b].ni * g[b].nc != m) return TTK_OK;
-    else if (term_flops(g[b]) > fused_max_flops()) fused_ok = false;  // the pairwise MFMA plan is faster there
+    else if (term_flops(g[b]) > fused_max_flops()) {  // beyond the VALU range: MFMA stages if they fit
+      if (mfma_enabled() && apply_mfma_lds(g[b]) <= APPLY_LDS_DOUBLES) g[b].mfma = 1;
+      else fused_ok = false;
+    }
   }
   if (!fused_ok) return schur_build_pairwise(ineq, m, descs, inv_I, handle);
   SchurOp op{};
@@ -1046,7 +1183,8 @@ __global__ __launch_bounds__(256) void fused_apply_group_kernel(FusedGroup G) {
   extern __shared__ double sm[];
   int t = 0;
   while (t + 1 < G.n && (int)blockIdx.x >= G.off[t + 1]) ++t;
-  apply_row<true>(G.t[t], (int)blockIdx.x - G.off[t], sm, nullptr);
+  if (G.t[t].mfma) apply_row_mfma<true>(G.t[t], (int)blockIdx.x - G.off[t], sm, nullptr);
+  else apply_row<true>(G.t[t], (int)blockIdx.x - G.off[t], sm, nullptr);
 }
 
 inline bool overlap(const Span &a, const Span &b) { return a.lo < b.hi && b.lo < a.hi; }

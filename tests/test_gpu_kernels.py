@@ -507,3 +507,29 @@ def test_rank_scan_matches_sequential_updates(dev):
     ss = dev.rank_scan(r2, dev.from_numpy(negs))
     assert list(ss) == ss_ref
     assert np.array_equal(dev.read(r1), dev.read(r2))
+
+
+@pytest.mark.parametrize("eq", ["lsr,smnS,LSR,rnR->lmL", "lsr,smnS,LSR,lmL->rnR"])
+@pytest.mark.parametrize("shapes", [[(44, 10, 44), (10, 4, 4, 10), (44, 10, 44), (44, 4, 44)],
+                                    [(30, 18, 25), (18, 4, 4, 9), (28, 9, 33), (25, 4, 33)]])
+def test_fused_apply_mfma_matches_numpy(dev, eq, shapes):
+    """graphm-sized local applies (beyond the VALU kernel's FLOP range) on the MFMA stages, with and
+    without accumulation, against NumPy (fp64; MFMA accumulation order -> 1e-13 relative)"""
+    from ttipm_amd._lib import lib
+    rng = _rng(13)
+    P, A, Q = (rng.standard_normal(s) for s in shapes[:3])
+    if eq.endswith("->lmL"):
+        x = rng.standard_normal(shapes[3])
+    else:
+        x = rng.standard_normal((P.shape[0], A.shape[1], Q.shape[0]))
+    ref = np.einsum(eq, P, A, Q, x)
+    old = lib.ttk_fused_set_mfma(1)
+    try:
+        got = dev.read(dev.einsum(eq, *[dev.from_numpy(o) for o in (P, A, Q, x)], fused=True))
+        out = dev.from_numpy(np.ones(ref.shape))
+        dev.einsum(eq, *[dev.from_numpy(o) for o in (P, A, Q, x)], out=out, alpha=0.5, beta=2.0, fused=True)
+    finally:
+        lib.ttk_fused_set_mfma(old)
+    scale = np.max(np.abs(ref))
+    assert np.max(np.abs(got - ref)) <= 1e-13 * scale
+    assert np.max(np.abs(dev.read(out) - (0.5 * ref + 2.0))) <= 1e-13 * scale
