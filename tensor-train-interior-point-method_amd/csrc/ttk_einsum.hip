@@ -584,7 +584,7 @@ __device__ void apply_row(const ApplyArgs &g, int a, double *sm, double *orow) {
 // t2 = A t1 over (s, j), out = Q t2 over (S, d) -- the association of apply_row and of the greedy
 // pairwise plan) as small GEMMs on v_mfma_f64_16x16x4f64, 4 waves sharing the 16x16 output tiles.
 // LDS: X (x staged), Pa (row a of P), As (A as [(i,S)][(s,j)]), T1 [(s,j)][d], T2 [(i,S)][d] and a
-// chunk of Q ([c][S'][d] for a range of S) per stage-3 K block.
+// chunk of Q ([c][k] for a range of k = (S,d)) per stage-3 K block.
 typedef double dbl4 __attribute__((ext_vector_type(4)));
 
 // C(m, n) += sum_k A(m, k) B(k, n) over 16x16 tiles, waves round-robin over tiles; A/B/C functors
@@ -619,9 +619,10 @@ __device__ __forceinline__ void wg_mfma(int M, int N, int K, FA fa, FB fb, FC fc
   }
 }
 
-constexpr int QCHUNK_MAX = 4096;  // doubles of Q staged per stage-3 K block
+constexpr int QCHUNK_MAX = 4096;  // doubles of Q staged per stage-3 K block ([c][k], k = (S,d) range)
 
 int64_t apply_mfma_lds(const ApplyArgs &g) {
+  if (g.nc > QCHUNK_MAX / 4) return INT64_MAX;  // stage 3 needs K blocks of >= 4
   return (int64_t)g.nb * g.nj * g.nd + (int64_t)g.ns * g.nb + (int64_t)g.ni * g.nS * g.ns * g.nj +
          (int64_t)g.ns * g.nj * g.nd + (int64_t)g.ni * g.nS * g.nd + QCHUNK_MAX + (int64_t)g.ni * g.nc;
 }
@@ -636,7 +637,7 @@ __device__ void apply_row_mfma(const ApplyArgs &g, int a, double *sm, double *or
   double *As = Pa + ns * nb;            // [(i,S)][(s,j)]
   double *T1 = As + ni * nS * sj;       // [(s,j)][d]
   double *T2 = T1 + sj * nd;            // [(i,S)][d]
-  double *Qc = T2 + ni * nS * nd;       // [c][S'][d], QCHUNK_MAX
+  double *Qc = T2 + ni * nS * nd;       // [c][k], QCHUNK_MAX
   for (int e = tid; e < nb * jd; e += nt) {
     const int b = e / jd, r = e - b * jd, j = r / nd, d = r - j * nd;
     X[e] = g.x[b * g.xs[0] + j * g.xs[1] + d * g.xs[2]];
@@ -658,20 +659,23 @@ __device__ void apply_row_mfma(const ApplyArgs &g, int a, double *sm, double *or
   wg_mfma(ni * nS, nd, sj, [&](int m, int k) { return As[m * sj + k]; }, [&](int k, int n) { return T1[k * nd + n]; },
           [&](int m, int n, double v) { T2[m * nd + n] = v; });
   __syncthreads();
-  // stage 3: out[i][c] = sum_{(S,d)} T2[(i,S)][d] Q[c,S,d], K blocked over S (Q chunk staged in LDS)
-  int sc = QCHUNK_MAX / (nc * nd);
-  sc = sc < 1 ? 1 : (sc > nS ? nS : sc);
-  double *acc = DIRECT ? Qc + sc * nc * nd : orow;  // DIRECT: partial sums after the Q chunk
-  for (int S0 = 0; S0 < nS; S0 += sc) {
-    const int se = S0 + sc < nS ? S0 + sc : nS, w = se - S0;
-    for (int e = tid; e < nc * w * nd; e += nt) {
-      const int c = e / (w * nd), r = e - c * (w * nd), S = r / nd, d = r - S * nd;
-      Qc[e] = g.Q[c * g.qs[0] + (S0 + S) * g.qs[1] + d * g.qs[2]];
+  // stage 3: out[i][c] = sum_{(S,d)} T2[(i,S)][d] Q[c,S,d] -- K = (S,d) flattened (row i of T2 is
+  // contiguous over it), blocked so a [c][k] chunk of Q fits QCHUNK_MAX doubles of LDS
+  const int K3 = nS * nd;
+  int kc = QCHUNK_MAX / nc;
+  kc = kc >= 8 ? (kc & ~7) : kc;
+  kc = kc > K3 ? K3 : kc;
+  double *acc = DIRECT ? Qc + QCHUNK_MAX : orow;  // DIRECT: partial sums after the Q chunk
+  for (int k0 = 0; k0 < K3; k0 += kc) {
+    const int w = k0 + kc < K3 ? kc : K3 - k0;
+    for (int e = tid; e < nc * w; e += nt) {
+      const int c = e / w, k = k0 + e - c * w, S = k / nd, d = k - S * nd;
+      Qc[e] = g.Q[c * g.qs[0] + S * g.qs[1] + d * g.qs[2]];
     }
     __syncthreads();
-    const bool first = S0 == 0;
-    wg_mfma(ni, nc, w * nd, [&](int m, int k) { const int S = k / nd, d = k - S * nd; return T2[(m * nS + S0 + S) * nd + d]; },
-            [&](int k, int n) { return Qc[n * (w * nd) + k]; },
+    const bool first = k0 == 0;
+    const double *T2k = T2 + k0;
+    wg_mfma(ni, nc, w, [&](int m, int k) { return T2k[m * K3 + k]; }, [&](int k, int n) { return Qc[n * w + k]; },
             [&](int m, int n, double v) { acc[m * nc + n] = first ? v : acc[m * nc + n] + v; });
     __syncthreads();
   }

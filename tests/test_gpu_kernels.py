@@ -533,3 +533,29 @@ def test_fused_apply_mfma_matches_numpy(dev, eq, shapes):
     scale = np.max(np.abs(ref))
     assert np.max(np.abs(got - ref)) <= 1e-13 * scale
     assert np.max(np.abs(dev.read(out) - (0.5 * ref + 2.0))) <= 1e-13 * scale
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("backward,shapes", [
+    (True, [(64, 3, 64), (78, 4, 64), (4, 4, 4, 3), (78, 4, 64)]),   # nc * nd = 78 * 64 > one Q chunk
+    (False, [(47, 5, 47), (47, 4, 97), (5, 4, 4, 4), (47, 4, 97)]),
+    (False, [(2, 12, 97), (2, 4, 2), (12, 4, 4, 13), (97, 4, 50)]),
+    (True, [(44, 10, 44), (44, 4, 44), (10, 4, 4, 10), (44, 4, 44)]),
+])
+def test_env_update_mfma_matches_numpy(dev, backward, shapes):
+    """Environment updates of one core step (ttk_env_update: relabelled strided local applies) on the
+    MFMA stages and on the default plan, against NumPy `compute_phi_*_A` (src/tt_als.py:252-257)"""
+    from ttipm_amd import tt_als
+    from ttipm_amd._lib import lib
+    rng = _rng(17)
+    P, x, A, y = (rng.standard_normal(s) for s in shapes)
+    eq = "LSR,lML,sMNS,rNR->lsr" if backward else "lsr,lML,sMNS,rNR->LSR"
+    ref = np.einsum(eq, P, x, A, y)
+    items = [tuple(dev.from_numpy(o) for o in (P, x, A, y))]
+    for mode in (1, 0):
+        old = lib.ttk_fused_set_mfma(mode)
+        try:
+            got = dev.read(tt_als.env_update_many(backward, items)[0])
+        finally:
+            lib.ttk_fused_set_mfma(old)
+        assert np.max(np.abs(got - ref)) <= 1e-12 * np.max(np.abs(ref)), mode
