@@ -13,6 +13,12 @@
   and at N=1 the steps cycle through the config's seeds.  `replica`: every rank solves step i's
   N=1 seed.  Problems are created once per distinct seed on rank 0 and delivered by ONE broadcast
   (RCCL over xGMI with the nccl backend) before the timed region; no collective inside the IPM loop.
+* Solves in flight per GPU (`--inflight P`, default 2, at most 16 processes per node): a solve is a
+  chain of small dependent launches that leaves most of the chip idle, so each GPU runs P seeds at
+  once -- this process plus P-1 worker processes on the same device (each its own HIP stream and
+  library context), spawned before the GPU is touched and released together at the start of the
+  timed region.  A step is then P solves per GPU: step i, rank p, slot j solves
+  seeds[(i*N*P + p*P + j) mod S].
 * Timed region: barrier + device sync on both sides of the K steps, max over ranks.
   `value` = (max-over-ranks wall) / (IPM iterations of all ranks): whole-job s per IPM-iteration.
   `median_seed_s_per_iter` is SURVEY.md §8(d)'s statistic: the median over the distinct seeds of
@@ -116,6 +122,53 @@ def _cpu_worker(problem, cfg_path, seed, rank_tt, cap):
     print(json.dumps(out), flush=True)
 
 
+def _gpu_worker(args, seeds):
+    """Child process (one more solve in flight on this rank's GPU): create its seeds' problems,
+    warm up, print 'ready', wait for 'go' on stdin, run the solves back to back, print one JSON
+    line with the elapsed wall time (device-synchronised) and the per-seed results."""
+    import torch
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local % torch.cuda.device_count())
+    from ttipm_amd import shard
+    from ttipm_amd.utils import create
+    from ttipm_amd.utils import solve as _solve
+    config = yaml.safe_load(open(args.config))
+    with contextlib.redirect_stdout(sys.stderr):
+        packed = {s: shard.pack(create(args.problem, config, s, args.rank, verbose=False))
+                  for s in dict.fromkeys(seeds)}
+
+        def solve(seed, trace=None):
+            return _solve(shard.unpack(*packed[seed]), config, quiet=True, verbose=False, trace=trace)
+
+        for _ in range(args.warmup):
+            solve(seeds[0])
+        torch.cuda.synchronize()
+    print("ready", flush=True)
+    sys.stdin.readline()
+    traces = [[] for _ in seeds]
+    t0 = time.perf_counter()
+    with contextlib.redirect_stdout(sys.stderr):
+        results = [solve(sd, trace=tr) for sd, tr in zip(seeds, traces)]
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    for r, tr in zip(results, traces):
+        r["assembly_t"] = [e["t"] - tr[0]["t"] for e in tr] if tr else []
+    keep = ("seed", "num_iters", "runtime", "sec_per_iter", "gap", "feas", "dual_feas", "assembly_t")
+    print(json.dumps({"elapsed": elapsed, "results": [{k: r.get(k) for k in keep} for r in results]}), flush=True)
+
+
+def _spawn_gpu_workers(args, slot_seeds):
+    """Started BEFORE this process initialises the GPU; each prints 'ready' once warmed up."""
+    procs = []
+    for seeds in slot_seeds:
+        cmd = [sys.executable, os.path.abspath(__file__), "--gpu-worker", ",".join(map(str, seeds)),
+               "--problem", args.problem, "--config", args.config, "--rank", str(args.rank),
+               "--warmup", str(args.warmup)]
+        procs.append(subprocess.Popen(cmd, stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=sys.stderr,
+                                      text=True))
+    return procs
+
+
 def _spawn_cpu_workers(args, seeds, threads):
     """Started BEFORE the GPU is initialised (no exec from a GPU process); each blocks on stdin."""
     procs = []
@@ -179,13 +232,18 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--schedule", choices=("shard", "replica"), default="shard")
+    ap.add_argument("--inflight", type=int, default=None,
+                    help="solves in flight per GPU (default: 2, capped at 16 processes per node)")
     ap.add_argument("--cpu-worker", type=int, default=None, help=argparse.SUPPRESS)
+    ap.add_argument("--gpu-worker", default=None, help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.problem is None:
         base = os.path.basename(args.config)
         args.problem = next(p for p in ("maxcut", "corr_clust", "graphm", "max_stable_set") if base.startswith(p))
     if args.cpu_worker is not None:
         return _cpu_worker(args.problem, args.config, args.cpu_worker, args.rank, args.cpu_cap)
+    if args.gpu_worker is not None:
+        return _gpu_worker(args, [int(x) for x in args.gpu_worker.split(",")])
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -198,14 +256,18 @@ def main():
         seeds = list(config["seeds"])
         if args.schedule == "shard" and world > len(seeds):
             seeds += [s for s in EXTRA_SEEDS.get(os.path.basename(args.config), []) if s not in seeds]
+    P = args.inflight if args.inflight else max(1, min(2, 16 // world))
+    per_step = world * P  # solves per step, rank-major then slot
     if args.schedule == "shard":
-        step_seeds = [seeds[(i * world + p) % len(seeds)] for i in range(args.steps) for p in range(world)]
+        step_seeds = [seeds[(i * per_step + q) % len(seeds)] for i in range(args.steps) for q in range(per_step)]
     else:
-        step_seeds = [seeds[i % len(seeds)] for i in range(args.steps) for p in range(world)]
-    sched = [step_seeds[i * world:(i + 1) * world] for i in range(args.steps)]
-    mine_seeds = [step_seeds[i * world + rank] for i in range(args.steps)]
+        step_seeds = [seeds[i % len(seeds)] for i in range(args.steps) for q in range(per_step)]
+    sched = [step_seeds[i * per_step:(i + 1) * per_step] for i in range(args.steps)]
+    slot_seeds = [[step_seeds[i * per_step + rank * P + j] for i in range(args.steps)] for j in range(P)]
+    mine_seeds = slot_seeds[0]
+    gpu_procs = _spawn_gpu_workers(args, slot_seeds[1:])  # before any GPU call
 
-    cpu_seeds = list(dict.fromkeys(mine_seeds))  # the distinct seeds this (only) rank times
+    cpu_seeds = list(dict.fromkeys(s for sl in slot_seeds for s in sl))  # the distinct seeds this (only) rank times
     cpu_procs, allcore_proc = [], []
     do_cpu = rank == 0 and world == 1 and not args.no_cpu_baseline
     if do_cpu:  # before any GPU call
@@ -247,16 +309,35 @@ def main():
         solve(shard.unpack(*packed[mine_seeds[0]]))
     preps = [shard.unpack(*packed[s]) for s in mine_seeds]
     traces = [[] for _ in mine_seeds]
+    for p in gpu_procs:  # every worker warmed up and waiting
+        line = p.stdout.readline()
+        while line and line.strip() != "ready":
+            line = p.stdout.readline()
+        if not line:
+            raise RuntimeError("bench: a GPU worker failed before the timed region")
     barrier()
     sync()
     t0 = time.perf_counter()
+    for p in gpu_procs:
+        p.stdin.write("go\n")
+        p.stdin.flush()
     results = [solve(p, trace=tr) for p, tr in zip(preps, traces)]
+    for r, tr in zip(results, traces):  # per-iteration stamps (Newton-system assemblies)
+        r["assembly_t"] = [e["t"] - tr[0]["t"] for e in tr] if tr else []
+    worker_out = []
+    for p in gpu_procs:
+        line = p.stdout.readline()
+        while line and not line.startswith("{"):
+            line = p.stdout.readline()
+        if p.wait() != 0 or not line:
+            raise RuntimeError("bench: a GPU worker failed in the timed region")
+        worker_out.append(json.loads(line))
     sync()
     barrier()
     elapsed = time.perf_counter() - t0
+    slot_elapsed = [elapsed] + [w["elapsed"] for w in worker_out]
+    results = results + [r for w in worker_out for r in w["results"]]
     iters = sum(r["num_iters"] for r in results)
-    for r, tr in zip(results, traces):  # per-iteration stamps (Newton-system assemblies)
-        r["assembly_t"] = [e["t"] - tr[0]["t"] for e in tr] if tr else []
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if torch.cuda.is_available() else "cpu")
         n = torch.tensor([float(iters)], dtype=torch.float64, device=t.device)
@@ -342,9 +423,12 @@ def main():
                "data": "synthetic: the reference's generators (seeded MT19937 graph TT), problems broadcast "
                        "from rank 0",
                "config": {"workload": f"{args.problem} dim={config['dim']} rank={args.rank} "
-                                      f"({os.path.basename(args.config)}), one tt_ipm solve per GPU per step",
+                                      f"({os.path.basename(args.config)}), {P} concurrent tt_ipm solves per GPU "
+                                      f"per step",
+                          "inflight_per_gpu": P,
                           "seeds": seeds, "seeds_per_step": sched,
-                          "parallelism": f"seed-parallel x{world} ({args.schedule})", "total_ipm_iters": iters},
+                          "parallelism": f"seed-parallel x{world} GPUs x{P} in flight ({args.schedule})",
+                          "total_ipm_iters": iters},
                "median_seed_s_per_iter": med,
                "pathological_seeds": sorted({p["seed"] for p in per_seed if p["pathological"]}),
                "roofline": roofline, "cpu_baseline": cpu,

@@ -44,18 +44,22 @@ struct GroupPtrs {
 
 typedef double double4_t __attribute__((ext_vector_type(4)));
 
-// One 32x32 output tile over the K range [kb, ke).  The next K stage's offsets and operands are
-// loaded into registers while the MFMAs consume the current stage from LDS (one barrier pair per
-// stage), so the two dependent global loads of the offset-table gather (table entry, then
-// operand) overlap with compute instead of serialising every stage.
+// One 32x32 output tile over the K range [kb, ke), staged TS = 64 K values per LDS stage (4x fewer
+// barrier / global-latency rounds than one 16-K stage).  Software pipeline: the offset-table
+// entries of stage s+2 and the operands of stage s+1 are in flight while stage s's MFMAs run, so
+// the gather's two dependent global loads (table entry, then operand) are each hidden behind a
+// stage of compute.  The MFMA sequence per output tile is k = kb, kb+4, ... in order, exactly as
+// with 16-K stages (trailing all-zero K groups are skipped), so results are unchanged bit for bit.
 // out != nullptr: raw partial sums (no alpha/beta) to a dense [M][N] slab (split-K);
 // out == nullptr: alpha/beta epilogue into C through the output offset tables.
+template <int TS>  // K per LDS stage (16 / 32 / 64: picked per launch from K; LDS 8.4 / 17 / 34 KB)
 __device__ __forceinline__ void gemm_tile(const double *__restrict__ A, const double *__restrict__ B,
                                           double *__restrict__ C, const int64_t *__restrict__ offs,
                                           int nb, int M, int N, int K, double alpha, double beta,
                                           int b, int m0, int n0, int kb, int ke, double *__restrict__ out) {
-  __shared__ double As[TK][TM + 1];
-  __shared__ double Bs[TK][TN + 1];
+  constexpr int TQ = TS / 8, RP = 256 / TS;  // staged elements per thread per operand; rows per pass
+  __shared__ double As[TS][TM + 1];
+  __shared__ double Bs[TS][TN + 1];
   const int64_t *a_b = offs;
   const int64_t *a_m = a_b + nb;
   const int64_t *a_k = a_m + M;
@@ -69,37 +73,71 @@ __device__ __forceinline__ void gemm_tile(const double *__restrict__ A, const do
   const int lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 1, wc = wid & 1;
   const int64_t abase = a_b[b], bbase = b_b[b];
-  // each thread stages 2 A and 2 B elements per K stage: (m, k), (m, k+8) and (k, n), (k+8, n)
-  const int l_mn = tid & 31, l_k = tid >> 5;
-  const bool am_ok = (m0 + l_mn) < M;
-  const bool bn_ok = (n0 + l_mn) < N;
-  const double *Ap = A + abase + (am_ok ? a_m[m0 + l_mn] : 0);
-  const double *Bp = B + bbase + (bn_ok ? b_n[n0 + l_mn] : 0);
-  double ra0, ra1, rb0, rb1;
-  auto fetch = [&](int k0) {
-    const int k_0 = k0 + l_k, k_1 = k0 + l_k + 8;
-    const bool ok0 = k_0 < ke, ok1 = k_1 < ke;
-    const int64_t o_a0 = ok0 ? a_k[k_0] : 0, o_a1 = ok1 ? a_k[k_1] : 0;
-    const int64_t o_b0 = ok0 ? b_k[k_0] : 0, o_b1 = ok1 ? b_k[k_1] : 0;
-    ra0 = (am_ok && ok0) ? Ap[o_a0] : 0.0;
-    ra1 = (am_ok && ok1) ? Ap[o_a1] : 0.0;
-    rb0 = (bn_ok && ok0) ? Bp[o_b0] : 0.0;
-    rb1 = (bn_ok && ok1) ? Bp[o_b1] : 0.0;
+  // Staging map per operand, picked from its offset tables (uniform per workgroup): element q of a
+  // thread is (row r0 + q*dr, k k0 + kq + q*dk).  Row-major staging (lanes along m|n, the K runs
+  // of 8 spread over the waves) unless the operand is contiguous along K but not along m|n; then
+  // lanes run along K (TS consecutive k, 256/TS rows per pass), so a wave load covers contiguous
+  // runs of K instead of 32 rows' worth of scattered lines.
+  const bool a_kmaj = K > 1 && a_k[1] - a_k[0] == 1 && !(M > 1 && a_m[1] - a_m[0] == 1);
+  const bool b_kmaj = K > 1 && b_k[1] - b_k[0] == 1 && !(N > 1 && b_n[1] - b_n[0] == 1);
+  const int ar0 = a_kmaj ? tid / TS : tid & 31, adr = a_kmaj ? RP : 0;
+  const int akq = a_kmaj ? tid % TS : tid >> 5, adk = a_kmaj ? 0 : 8;
+  const int br0 = b_kmaj ? tid / TS : tid & 31, bdr = b_kmaj ? RP : 0;
+  const int bkq = b_kmaj ? tid % TS : tid >> 5, bdk = b_kmaj ? 0 : 8;
+  int64_t arow[TQ], brow[TQ];
+  unsigned aok = 0, bok = 0;  // row-valid bits
+#pragma unroll
+  for (int q = 0; q < TQ; ++q) {
+    const int m = m0 + ar0 + q * adr, n = n0 + br0 + q * bdr;
+    arow[q] = abase + (m < M ? a_m[m] : 0);
+    brow[q] = bbase + (n < N ? b_n[n] : 0);
+    aok |= (m < M ? 1u : 0u) << q;
+    bok |= (n < N ? 1u : 0u) << q;
+  }
+  int64_t oa[TQ], ob[TQ];
+  double ra[TQ], rb[TQ];
+  auto fetch_offs = [&](int k0) {
+#pragma unroll
+    for (int q = 0; q < TQ; ++q) {
+      const int ka = k0 + akq + q * adk, kb_ = k0 + bkq + q * bdk;
+      oa[q] = ka < ke ? a_k[ka] : 0;
+      ob[q] = kb_ < ke ? b_k[kb_] : 0;
+    }
+  };
+  auto fetch_vals = [&](int k0) {
+#pragma unroll
+    for (int q = 0; q < TQ; ++q) {
+      const bool oka = ((aok >> q) & 1u) && k0 + akq + q * adk < ke;
+      const bool okb = ((bok >> q) & 1u) && k0 + bkq + q * bdk < ke;
+      ra[q] = oka ? A[arow[q] + oa[q]] : 0.0;
+      rb[q] = okb ? B[brow[q] + ob[q]] : 0.0;
+    }
   };
   double4_t acc = {0.0, 0.0, 0.0, 0.0};
-  if (kb < ke) fetch(kb);
-  for (int k0 = kb; k0 < ke; k0 += TK) {
-    As[l_k][l_mn] = ra0;
-    As[l_k + 8][l_mn] = ra1;
-    Bs[l_k][l_mn] = rb0;
-    Bs[l_k + 8][l_mn] = rb1;
-    __syncthreads();
-    if (k0 + TK < ke) fetch(k0 + TK);
+  if (kb < ke) {
+    fetch_offs(kb);
+    fetch_vals(kb);
+    if (kb + TS < ke) fetch_offs(kb + TS);
+  }
+  for (int k0 = kb; k0 < ke; k0 += TS) {
 #pragma unroll
-    for (int s = 0; s < TK / 4; ++s) {
-      const double a = As[s * 4 + (lane >> 4)][wr * 16 + (lane & 15)];
-      const double bv = Bs[s * 4 + (lane >> 4)][wc * 16 + (lane & 15)];
-      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bv, acc, 0, 0, 0);
+    for (int q = 0; q < TQ; ++q) {
+      As[akq + q * adk][ar0 + q * adr] = ra[q];
+      Bs[bkq + q * bdk][br0 + q * bdr] = rb[q];
+    }
+    __syncthreads();
+    if (k0 + TS < ke) {
+      fetch_vals(k0 + TS);
+      if (k0 + 2 * TS < ke) fetch_offs(k0 + 2 * TS);
+    }
+    const int ns = (ke - k0 + 3) >> 2;  // K groups of 4 with data in this stage
+#pragma unroll
+    for (int s = 0; s < TS / 4; ++s) {
+      if (s < ns) {
+        const double a = As[s * 4 + (lane >> 4)][wr * 16 + (lane & 15)];
+        const double bv = Bs[s * 4 + (lane >> 4)][wc * 16 + (lane & 15)];
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bv, acc, 0, 0, 0);
+      }
     }
     __syncthreads();
   }
@@ -148,19 +186,44 @@ __global__ __launch_bounds__(256) void gemm_offs64_kernel(GemmArgs g) {
   const int64_t *c_n = c_m + M;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 1, wc = wid & 1;
-  const int l_mn = tid & 63, l_k = tid >> 6;  // stages (m|n = l_mn, k = l_k + 4q), q = 0..3
-  const bool am_ok = (m0 + l_mn) < M, bn_ok = (n0 + l_mn) < N;
-  const double *Ap = g.A + a_b[b] + (am_ok ? a_m[m0 + l_mn] : 0);
-  const double *Bp = g.B + b_b[b] + (bn_ok ? b_n[n0 + l_mn] : 0);
+  // staging map per operand as in gemm_tile: element q = (row r0 + q*dr, k kq + q*dk); row-major
+  // (lanes along m|n, k = tid/64 + 4q) unless the operand is contiguous along K only, then lanes
+  // run along K (KS consecutive k, 256/KS rows per pass)
+  constexpr int RP = 256 / KS;
+  const bool a_kmaj = K > 1 && a_k[1] - a_k[0] == 1 && !(M > 1 && a_m[1] - a_m[0] == 1);
+  const bool b_kmaj = K > 1 && b_k[1] - b_k[0] == 1 && !(N > 1 && b_n[1] - b_n[0] == 1);
+  const int ar0 = a_kmaj ? tid / KS : tid & 63, adr = a_kmaj ? RP : 0;
+  const int akq = a_kmaj ? tid % KS : tid >> 6, adk = a_kmaj ? 0 : 4;
+  const int br0 = b_kmaj ? tid / KS : tid & 63, bdr = b_kmaj ? RP : 0;
+  const int bkq = b_kmaj ? tid % KS : tid >> 6, bdk = b_kmaj ? 0 : 4;
+  const int64_t abase = a_b[b], bbase = b_b[b];
+  int64_t arow[NQ], brow[NQ];
+  unsigned aok = 0, bok = 0;
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    const int m = m0 + ar0 + q * adr, n = n0 + br0 + q * bdr;
+    arow[q] = abase + (m < M ? a_m[m] : 0);
+    brow[q] = bbase + (n < N ? b_n[n] : 0);
+    aok |= (m < M ? 1u : 0u) << q;
+    bok |= (n < N ? 1u : 0u) << q;
+  }
+  int64_t oa[NQ], ob[NQ];
   double ra[NQ], rb[NQ];
+  auto fetch_offs = [&](int k0) {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const int ka = k0 + akq + q * adk, kb_ = k0 + bkq + q * bdk;
+      oa[q] = ka < K ? a_k[ka] : 0;
+      ob[q] = kb_ < K ? b_k[kb_] : 0;
+    }
+  };
   auto fetch = [&](int k0) {
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
-      const int k = k0 + l_k + 4 * q;
-      const bool ok = k < K;
-      const int64_t oa = ok ? a_k[k] : 0, ob = ok ? b_k[k] : 0;
-      ra[q] = (am_ok && ok) ? Ap[oa] : 0.0;
-      rb[q] = (bn_ok && ok) ? Bp[ob] : 0.0;
+      const bool oka = ((aok >> q) & 1u) && k0 + akq + q * adk < K;
+      const bool okb = ((bok >> q) & 1u) && k0 + bkq + q * bdk < K;
+      ra[q] = oka ? g.A[arow[q] + oa[q]] : 0.0;
+      rb[q] = okb ? g.B[brow[q] + ob[q]] : 0.0;
     }
   };
   double4_t acc[2][2];
@@ -168,15 +231,20 @@ __global__ __launch_bounds__(256) void gemm_offs64_kernel(GemmArgs g) {
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = double4_t{0.0, 0.0, 0.0, 0.0};
+  fetch_offs(0);
   fetch(0);
+  if (KS < K) fetch_offs(KS);
   for (int k0 = 0; k0 < K; k0 += KS) {
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
-      As[l_k + 4 * q][l_mn] = ra[q];
-      Bs[l_k + 4 * q][l_mn] = rb[q];
+      As[akq + q * adk][ar0 + q * adr] = ra[q];
+      Bs[bkq + q * bdk][br0 + q * bdr] = rb[q];
     }
     __syncthreads();
-    if (k0 + KS < K) fetch(k0 + KS);
+    if (k0 + KS < K) {
+      fetch(k0 + KS);
+      if (k0 + 2 * KS < K) fetch_offs(k0 + 2 * KS);
+    }
 #pragma unroll
     for (int s = 0; s < KS / 4; ++s) {
       const int kr = s * 4 + (lane >> 4);
@@ -208,18 +276,20 @@ __global__ __launch_bounds__(256) void gemm_offs64_kernel(GemmArgs g) {
   }
 }
 
+template <int TS>
 __global__ __launch_bounds__(256) void gemm_offs_kernel(GemmArgs g) {
   const int n0 = blockIdx.x * TN, m0 = blockIdx.y * TM, b = blockIdx.z;
-  gemm_tile(g.A, g.B, g.C, g.offs, g.nb, g.M, g.N, g.K, g.alpha, g.beta, b, m0, n0, 0, g.K, nullptr);
+  gemm_tile<TS>(g.A, g.B, g.C, g.offs, g.nb, g.M, g.N, g.K, g.alpha, g.beta, b, m0, n0, 0, g.K, nullptr);
 }
 
 // split-K: blockIdx.z = b * nsplit + split; partial tile sums to part[split][b][M][N]
+template <int TS>
 __global__ __launch_bounds__(256) void gemm_offs_splitk_kernel(GemmArgs g, int nsplit, int kc, double *part) {
   const int n0 = blockIdx.x * TN, m0 = blockIdx.y * TM;
   const int b = blockIdx.z / nsplit, sp = blockIdx.z % nsplit;
   const int kb = sp * kc, ke = kb + kc < g.K ? kb + kc : g.K;
   double *out = part + ((int64_t)sp * g.nb + b) * g.M * g.N;
-  gemm_tile(g.A, g.B, g.C, g.offs, g.nb, g.M, g.N, g.K, g.alpha, g.beta, b, m0, n0, kb, ke, out);
+  gemm_tile<TS>(g.A, g.B, g.C, g.offs, g.nb, g.M, g.N, g.K, g.alpha, g.beta, b, m0, n0, kb, ke, out);
 }
 
 // C = alpha * sum_split part + beta * C (fixed summation order: deterministic)
@@ -241,12 +311,17 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce_kernel(GemmArgs g, int
   *p = (g.beta == 0.0) ? v : v + g.beta * (*p);
 }
 
+template <int TS>
 __global__ __launch_bounds__(256) void gemm_offs_grouped_kernel(GemmArgs g, GroupPtrs p) {
   const int n0 = blockIdx.x * TN, m0 = blockIdx.y * TM;
   const int grp = blockIdx.z / g.nb, b = blockIdx.z % g.nb;
-  gemm_tile(p.A[grp], p.B[grp], p.C[grp], g.offs, g.nb, g.M, g.N, g.K, g.alpha, g.beta, b, m0, n0, 0, g.K,
+  gemm_tile<TS>(p.A[grp], p.B[grp], p.C[grp], g.offs, g.nb, g.M, g.N, g.K, g.alpha, g.beta, b, m0, n0, 0, g.K,
             nullptr);
 }
+
+// K per LDS stage for a launch: short contractions keep the small LDS footprint (occupancy hides
+// the gather latency), long ones take fewer, deeper stages.  Any choice gives the same results.
+static inline int stage_k(int K) { return K < 32 ? 16 : (K < 128 ? 32 : 64); }
 
 // Independent problems of one einsum batch level in ONE launch: workgroup -> (problem, tile) through
 // the tile prefix; each tile runs gemm_tile exactly as gemm_offs_kernel would (same n/m/b tile
@@ -258,6 +333,7 @@ struct GemmGroup {
   int n;
 };
 
+template <int TS>
 __global__ __launch_bounds__(256) void gemm_offs_group_kernel(GemmGroup G) {
   const int bid = blockIdx.x;
   int p = 0;
@@ -269,7 +345,7 @@ __global__ __launch_bounds__(256) void gemm_offs_group_kernel(GemmGroup G) {
   t /= ntn;
   const int m0 = (t % ntm) * TM;
   const int b = t / ntm;
-  gemm_tile(g.A, g.B, g.C, g.offs, g.nb, g.M, g.N, g.K, g.alpha, g.beta, b, m0, n0, 0, g.K, nullptr);
+  gemm_tile<TS>(g.A, g.B, g.C, g.offs, g.nb, g.M, g.N, g.K, g.alpha, g.beta, b, m0, n0, 0, g.K, nullptr);
 }
 
 // ------------------------------------------------------------------ element-wise (N-D strided)
@@ -642,7 +718,7 @@ int ttk_gemm_hist(int on, const char *dump_path) {
 
 static int g_splitk_mink = getenv("TTK_SPLITK_MINK") ? atoi(getenv("TTK_SPLITK_MINK")) : 256;  // K per split (128 is 15 % faster on graphm_3 but moves maxcut_12 s80 off the reference path)
 static int g_gemm64_min = getenv("TTK_GEMM64_MIN") ? atoi(getenv("TTK_GEMM64_MIN")) : 64;
-static int g_gemm64_ks = getenv("TTK_GEMM64_KS") ? atoi(getenv("TTK_GEMM64_KS")) : 16;
+static int g_gemm64_ks = getenv("TTK_GEMM64_KS") ? atoi(getenv("TTK_GEMM64_KS")) : 32;
 
 int ttk_gemm_offs(void *stream, const double *A, const double *B, double *C, const int64_t *offs,
                   int nb, int M, int N, int K, double alpha, double beta) {
@@ -679,7 +755,7 @@ int ttk_gemm_offs(void *stream, const double *A, const double *B, double *C, con
       return TTK_ERR_HIP;
     }
     dim3 gs(grid.x, grid.y, nb * nsplit);
-    hipExtLaunchKernelGGL(gemm_offs_splitk_kernel, gs, dim3(256), 0, TTK_STREAM(stream), e0, nullptr, 0, g, nsplit,
+    hipExtLaunchKernelGGL(gemm_offs_splitk_kernel<64>, gs, dim3(256), 0, TTK_STREAM(stream), e0, nullptr, 0, g, nsplit,
                           kc, part);
     const int64_t tot = (int64_t)nb * M * N;
     hipExtLaunchKernelGGL(gemm_splitk_reduce_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0,
@@ -692,7 +768,11 @@ int ttk_gemm_offs(void *stream, const double *A, const double *B, double *C, con
     else
       hipExtLaunchKernelGGL(gemm_offs64_kernel<16>, g64, dim3(256), 0, TTK_STREAM(stream), e0, e1, 0, g);
   } else {
-    hipExtLaunchKernelGGL(gemm_offs_kernel, grid, dim3(256), 0, TTK_STREAM(stream), e0, e1, 0, g);
+    switch (stage_k(K)) {
+      case 16: hipExtLaunchKernelGGL(gemm_offs_kernel<16>, grid, dim3(256), 0, TTK_STREAM(stream), e0, e1, 0, g); break;
+      case 32: hipExtLaunchKernelGGL(gemm_offs_kernel<32>, grid, dim3(256), 0, TTK_STREAM(stream), e0, e1, 0, g); break;
+      default: hipExtLaunchKernelGGL(gemm_offs_kernel<64>, grid, dim3(256), 0, TTK_STREAM(stream), e0, e1, 0, g);
+    }
   }
   TTK_LAUNCH_CHECK();
   contract_count(2.0 * M * N * (double)K * nb);
@@ -719,8 +799,10 @@ int gemm_group(hipStream_t st, const GemmProblem *p, int n) {
     G.n = n - base < GROUP_MAX ? n - base : GROUP_MAX;
     G.tile0[0] = 0;
     double flops = 0.0;
+    int kmax = 0;
     for (int i = 0; i < G.n; ++i) {
       const GemmProblem &q = p[base + i];
+      kmax = q.K > kmax ? q.K : kmax;
       G.p[i] = GemmArgs{q.A, q.B, q.C, q.offs, q.nb, q.M, q.N, q.K, q.alpha, q.beta};
       G.tile0[i + 1] = G.tile0[i] + ((q.N + TN - 1) / TN) * ((q.M + TM - 1) / TM) * q.nb;
       flops += 2.0 * q.M * q.N * (double)q.K * q.nb;
@@ -728,7 +810,11 @@ int gemm_group(hipStream_t st, const GemmProblem *p, int n) {
     hipEvent_t e0, e1;
     int rc = contract_events(&e0, &e1);
     if (rc != TTK_OK) return rc;
-    hipExtLaunchKernelGGL(gemm_offs_group_kernel, dim3(G.tile0[G.n]), dim3(256), 0, st, e0, e1, 0, G);
+    switch (stage_k(kmax)) {
+      case 16: hipExtLaunchKernelGGL(gemm_offs_group_kernel<16>, dim3(G.tile0[G.n]), dim3(256), 0, st, e0, e1, 0, G); break;
+      case 32: hipExtLaunchKernelGGL(gemm_offs_group_kernel<32>, dim3(G.tile0[G.n]), dim3(256), 0, st, e0, e1, 0, G); break;
+      default: hipExtLaunchKernelGGL(gemm_offs_group_kernel<64>, dim3(G.tile0[G.n]), dim3(256), 0, st, e0, e1, 0, G);
+    }
     TTK_LAUNCH_CHECK();
     contract_count(flops);
   }
@@ -753,7 +839,11 @@ int ttk_gemm_offs_grouped(void *stream, const double *const *Aptr, const double 
   hipEvent_t e0, e1;
   int rc = contract_events(&e0, &e1);
   if (rc != TTK_OK) return rc;
-  hipExtLaunchKernelGGL(gemm_offs_grouped_kernel, grid, dim3(256), 0, TTK_STREAM(stream), e0, e1, 0, g, p);
+  switch (stage_k(K)) {
+    case 16: hipExtLaunchKernelGGL(gemm_offs_grouped_kernel<16>, grid, dim3(256), 0, TTK_STREAM(stream), e0, e1, 0, g, p); break;
+    case 32: hipExtLaunchKernelGGL(gemm_offs_grouped_kernel<32>, grid, dim3(256), 0, TTK_STREAM(stream), e0, e1, 0, g, p); break;
+    default: hipExtLaunchKernelGGL(gemm_offs_grouped_kernel<64>, grid, dim3(256), 0, TTK_STREAM(stream), e0, e1, 0, g, p);
+  }
   TTK_LAUNCH_CHECK();
   contract_count(2.0 * M * N * (double)K * nb * ngroups);
   return TTK_OK;

@@ -1222,10 +1222,9 @@ __device__ void tridiag_extreme_finish(double *A, int n, int which, double *dv, 
   if (tid == 0) {
     double d = dv[0] - lam;
     double u = (1 < n) ? ov[0] : 0.0;
-    for (int i = 0; i + 1 < n; ++i) {  // dgttrf
-      const double l = ov[i];
-      double dn = dv[i + 1] - lam;
-      double un = (i + 2 < n) ? ov[i + 1] : 0.0;
+    // dgttrf step i from l = ov[i], dn = dv[i+1] - lam, un = ov[i+1] (0 past the end).  The loops
+    // below load the operands of 4 steps ahead of the recurrence (one LDS round trip per 4 steps).
+    auto trf = [&](int i, double l, double dn, double un) {
       double u2 = 0.0, pvt = 0.0, lf = l, dfin = d;
       if (fabs(d) >= fabs(l)) {
         if (d != 0.0) {
@@ -1252,7 +1251,17 @@ __device__ void tridiag_extreme_finish(double *A, int n, int which, double *dv, 
       fpiv[i] = pvt;
       d = dn;
       u = un;
+    };
+    int i = 0;
+    for (; i + 4 < n; i += 4) {
+      const double o0 = ov[i], o1 = ov[i + 1], o2 = ov[i + 2], o3 = ov[i + 3], o4 = ov[i + 4];
+      const double d1 = dv[i + 1], d2 = dv[i + 2], d3 = dv[i + 3], d4 = dv[i + 4];
+      trf(i, o0, d1 - lam, o1);
+      trf(i + 1, o1, d2 - lam, o2);
+      trf(i + 2, o2, d3 - lam, o3);
+      trf(i + 3, o3, d4 - lam, (i + 5 < n) ? o4 : 0.0);
     }
+    for (; i + 1 < n; ++i) trf(i, ov[i], dv[i + 1] - lam, (i + 2 < n) ? ov[i + 1] : 0.0);
     fd[n - 1] = d;
     fdu[n - 1] = 0.0;
     fdl[n - 1] = 0.0;
@@ -1274,10 +1283,8 @@ __device__ void tridiag_extreme_finish(double *A, int n, int which, double *dv, 
     double sc = 1.0;  // scale of the previous iterate, applied as it is loaded
     for (int it = 0; it < 3; ++it) {
       double zc = z[0] * sc;
-      for (int i = 0; i + 1 < n; ++i) {  // dgtts2 forward
-        double zn = z[i + 1] * sc;
-        const double l = fdl[i];
-        if (fpiv[i] == 0.0) {
+      auto fwd = [&](int i, double zn, double l, double pv_) {  // dgtts2 forward step
+        if (pv_ == 0.0) {
           zn -= l * zc;
           z[i] = zc;
           zc = zn;
@@ -1285,7 +1292,18 @@ __device__ void tridiag_extreme_finish(double *A, int n, int which, double *dv, 
           z[i] = zn;
           zc = zc - l * zn;
         }
+      };
+      int i = 0;
+      for (; i + 4 < n; i += 4) {  // z[i+1..i+4] are loaded before this block writes z[i..i+3]
+        const double z1_ = z[i + 1], z2_ = z[i + 2], z3_ = z[i + 3], z4_ = z[i + 4];
+        const double l0 = fdl[i], l1 = fdl[i + 1], l2 = fdl[i + 2], l3 = fdl[i + 3];
+        const double q0 = fpiv[i], q1 = fpiv[i + 1], q2 = fpiv[i + 2], q3 = fpiv[i + 3];
+        fwd(i, z1_ * sc, l0, q0);
+        fwd(i + 1, z2_ * sc, l1, q1);
+        fwd(i + 2, z3_ * sc, l2, q2);
+        fwd(i + 3, z4_ * sc, l3, q3);
       }
+      for (; i + 1 < n; ++i) fwd(i, z[i + 1] * sc, fdl[i], fpiv[i]);
       double z1 = zc * fd[n - 1], z2 = 0.0;
       z[n - 1] = z1;
       double mx = fabs(z1);
@@ -1296,18 +1314,33 @@ __device__ void tridiag_extreme_finish(double *A, int n, int which, double *dv, 
         z1 = zz;
         mx = fmax(mx, fabs(zz));
       }
-      for (int i = n - 3; i >= 0; --i) {
-        const double zz = (z[i] - fdu[i] * z1 - fdu2[i] * z2) * fd[i];
+      auto bwd = [&](int i, double zi, double du, double du2, double di) {
+        const double zz = (zi - du * z1 - du2 * z2) * di;
         z[i] = zz;
         z2 = z1;
         z1 = zz;
         mx = fmax(mx, fabs(zz));
+      };
+      int ib = n - 3;
+      for (; ib >= 3; ib -= 4) {
+        const double a0 = z[ib], a1 = z[ib - 1], a2 = z[ib - 2], a3 = z[ib - 3];
+        const double u0 = fdu[ib], u1 = fdu[ib - 1], u2_ = fdu[ib - 2], u3 = fdu[ib - 3];
+        const double w0 = fdu2[ib], w1 = fdu2[ib - 1], w2 = fdu2[ib - 2], w3 = fdu2[ib - 3];
+        const double e0 = fd[ib], e1 = fd[ib - 1], e2 = fd[ib - 2], e3 = fd[ib - 3];
+        bwd(ib, a0, u0, w0, e0);
+        bwd(ib - 1, a1, u1, w1, e1);
+        bwd(ib - 2, a2, u2_, w2, e2);
+        bwd(ib - 3, a3, u3, w3, e3);
       }
+      for (; ib >= 0; --ib) bwd(ib, z[ib], fdu[ib], fdu2[ib], fd[ib]);
       sc = mx > 0.0 ? fast_rcp(mx) : 1.0;
     }
-    for (int i = 0; i < n; ++i) z[i] *= sc;
     double nn = 0.0;
-    for (int i = 0; i < n; ++i) nn += z[i] * z[i];
+    for (int i = 0; i < n; ++i) {
+      const double t = z[i] * sc;
+      z[i] = t;
+      nn += t * t;
+    }
     const double sc2 = 1.0 / sqrt(nn);
     for (int i = 0; i < n; ++i) z[i] *= sc2;
     ev_out[0] = lam;
@@ -1412,7 +1445,7 @@ __global__ __launch_bounds__(1024) void syev_extreme_kernel(const double *__rest
 }
 
 // Small-n extreme eigenpair (n <= SYEV_SMALL_N), built for latency: 4 waves, A in LDS with an odd
-// leading dimension (row starts on different banks), 3 cheap 4-wave barriers per reflector.
+// leading dimension (row starts on different banks), 2 barriers per reflector.
 //   reflector  wave 0 (dlarfg on row k, which holds the sub-column by symmetry)
 //   p = tau A22 v   two lanes per row (row i -> lanes 2i, 2i+1 of one wave), halves combined by a
 //                   lane-pair shuffle; v read as LDS broadcasts
@@ -1439,65 +1472,76 @@ __global__ __launch_bounds__(NT) void syev_small_kernel(const double *__restrict
     A[i * ld + j] = Ain[e];
   }
   __syncthreads();
-  for (int k = 0; k + 2 < n; ++k) {
+  // two barriers per reflector: wave 0 owns A22's first row in the rank-2 update, so right after
+  // updating it (same wave, LDS order) it builds the next reflector from that row while the other
+  // waves finish their rows; nobody else reads the row in that phase
+  auto reflector = [&](int k) {  // wave 0: dlarfg on row k (the sub-column by symmetry)
     double *v = A + k * ld + k + 1;
     const int m = n - k - 1;
-    if (wid == 0) {
-      const double x1 = (1 + lane < m) ? v[1 + lane] : 0.0;
-      const double x2 = (65 + lane < m) ? v[65 + lane] : 0.0;
-      const double sigma = ttk::wave_sum(fma(x1, x1, x2 * x2));
-      const double alpha = v[0];
-      double tau = 0.0, beta = alpha;
-      if (sigma > 0.0) {
-        beta = -copysign(sqrt(fma(alpha, alpha, sigma)), alpha);
-        tau = (beta - alpha) / beta;
-        const double sc = 1.0 / (alpha - beta);
-        if (1 + lane < m) v[1 + lane] = x1 * sc;
-        if (65 + lane < m) v[65 + lane] = x2 * sc;
-      }
-      if (lane == 0) {
-        v[0] = 1.0;
-        tv[k] = tau;
-        ov[k] = beta;
-        dv[k] = A[k * ld + k];
-      }
+    const double x1 = (1 + lane < m) ? v[1 + lane] : 0.0;
+    const double x2 = (65 + lane < m) ? v[65 + lane] : 0.0;
+    const double sigma = ttk::wave_sum(fma(x1, x1, x2 * x2));
+    const double alpha = v[0];
+    double tau = 0.0, beta = alpha;
+    if (sigma > 0.0) {
+      beta = -copysign(sqrt(fma(alpha, alpha, sigma)), alpha);
+      tau = (beta - alpha) / beta;
+      const double sc = 1.0 / (alpha - beta);
+      if (1 + lane < m) v[1 + lane] = x1 * sc;
+      if (65 + lane < m) v[65 + lane] = x2 * sc;
     }
-    __syncthreads();
+    if (lane == 0) {
+      v[0] = 1.0;
+      tv[k] = tau;
+      ov[k] = beta;
+      dv[k] = A[k * ld + k];
+    }
+  };
+  if (wid == 0 && n > 2) reflector(0);
+  __syncthreads();
+  for (int k = 0; k + 2 < n; ++k) {
+    const double *v = A + k * ld + k + 1;
+    const int m = n - k - 1;
     const double tau = tv[k];
-    if (tau == 0.0) continue;
-    const double *A22 = A + (k + 1) * ld + k + 1;
-    {  // p = tau A22 v: row r = tid / G, lane h = tid % G of the row takes columns h, h+G, ...
-      const int r = tid / G, h = tid % G;
-      double acc = 0.0;
-      if (r < m) {  // four independent chains: the LDS loads of one batch overlap
-        const double *ar = A22 + r * ld;
-        double a1 = 0.0, a2 = 0.0, a3 = 0.0;
-        int j = h;
-        for (; j + 3 * G < m; j += 4 * G) {
-          acc = fma(ar[j], v[j], acc);
-          a1 = fma(ar[j + G], v[j + G], a1);
-          a2 = fma(ar[j + 2 * G], v[j + 2 * G], a2);
-          a3 = fma(ar[j + 3 * G], v[j + 3 * G], a3);
+    if (tau != 0.0) {
+      const double *A22 = A + (k + 1) * ld + k + 1;
+      {  // p = tau A22 v: row r = tid / G, lane h = tid % G of the row takes columns h, h+G, ...
+        const int r = tid / G, h = tid % G;
+        double acc = 0.0;
+        if (r < m) {  // four independent chains: the LDS loads of one batch overlap
+          const double *ar = A22 + r * ld;
+          double a1 = 0.0, a2 = 0.0, a3 = 0.0;
+          int j = h;
+          for (; j + 3 * G < m; j += 4 * G) {
+            acc = fma(ar[j], v[j], acc);
+            a1 = fma(ar[j + G], v[j + G], a1);
+            a2 = fma(ar[j + 2 * G], v[j + 2 * G], a2);
+            a3 = fma(ar[j + 3 * G], v[j + 3 * G], a3);
+          }
+          for (; j < m; j += G) acc = fma(ar[j], v[j], acc);
+          acc = (acc + a1) + (a2 + a3);
         }
-        for (; j < m; j += G) acc = fma(ar[j], v[j], acc);
-        acc = (acc + a1) + (a2 + a3);
-      }
 #pragma unroll
-      for (int o = 1; o < G; o <<= 1) acc += __shfl_xor(acc, o, 64);
-      if (h == 0 && r < m) pv[r] = tau * acc;
-    }
-    __syncthreads();
-    const int j0 = lane, j1 = lane + 64;
-    const double v0 = j0 < m ? v[j0] : 0.0, v1 = j1 < m ? v[j1] : 0.0;
-    const double p0 = j0 < m ? pv[j0] : 0.0, p1 = j1 < m ? pv[j1] : 0.0;
-    const double K = 0.5 * tau * ttk::wave_sum(fma(p0, v0, p1 * v1));
-    const double w0 = fma(-K, v0, p0), w1 = fma(-K, v1, p1);
+        for (int o = 1; o < G; o <<= 1) acc += __shfl_xor(acc, o, 64);
+        if (h == 0 && r < m) pv[r] = tau * acc;
+      }
+      __syncthreads();
+      const int j0 = lane, j1 = lane + 64;
+      const double v0 = j0 < m ? v[j0] : 0.0, v1 = j1 < m ? v[j1] : 0.0;
+      const double p0 = j0 < m ? pv[j0] : 0.0, p1 = j1 < m ? pv[j1] : 0.0;
+      const double K = 0.5 * tau * ttk::wave_sum(fma(p0, v0, p1 * v1));
+      const double w0 = fma(-K, v0, p0), w1 = fma(-K, v1, p1);
 #pragma unroll 4
-    for (int i = wid; i < m; i += NW) {
-      const double vi = v[i], wi = fma(-K, vi, pv[i]);
-      double *ai = A + (k + 1 + i) * ld + k + 1;
-      if (j0 < m) ai[j0] -= fma(vi, w0, wi * v0);
-      if (j1 < m) ai[j1] -= fma(vi, w1, wi * v1);
+      for (int i = wid; i < m; i += NW) {
+        const double vi = v[i], wi = fma(-K, vi, pv[i]);
+        double *ai = A + (k + 1 + i) * ld + k + 1;
+        if (j0 < m) ai[j0] -= fma(vi, w0, wi * v0);
+        if (j1 < m) ai[j1] -= fma(vi, w1, wi * v1);
+      }
+    }
+    if (wid == 0 && k + 3 < n) {
+      __threadfence_block();
+      reflector(k + 1);
     }
     __syncthreads();
   }

@@ -14,7 +14,8 @@ PEAK = 78.6e12
 
 def main():
     shapes = [(1344, 1344, 1344), (2048, 2048, 2048), (4096, 4096, 4096), (172, 600, 64), (60, 40, 2580),
-              (225, 688, 17), (172, 840, 64), (56, 48, 2408), (272, 196, 43), (841, 31, 15624), (336, 336, 336)]
+              (225, 688, 17), (172, 840, 64), (56, 48, 2408), (272, 196, 43), (841, 31, 15624), (336, 336, 336),
+              (212, 64, 2544), (116, 64, 1160), (216, 59, 2160), (60, 44, 2700), (192, 52, 1728)]
     print(f"{'M':>5s} {'N':>5s} {'K':>6s} {'ttk_us':>9s} {'ttk_TF':>7s} {'frac':>6s} {'torch_us':>9s} {'torch_TF':>8s}")
     for M, N, K in shapes:
         a = torch.randn(M, K, dtype=torch.float64, device="cuda")
