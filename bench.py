@@ -116,7 +116,7 @@ def _cpu_worker(problem, cfg_path, seed, rank_tt, cap):
             full, wall = None, None
     n_it = len(trace.t) - 1
     out = {"seed": seed, "iters": n_it, "s_per_iter": (trace.t[n_it] - trace.t[0]) / max(n_it, 1),
-           "threads": os.environ.get("OPENBLAS_NUM_THREADS")}
+           "assembly_t": [t - trace.t[0] for t in trace.t], "threads": os.environ.get("OPENBLAS_NUM_THREADS")}
     if full is not None:
         out.update(full_solve_iters=full, full_solve_s_per_iter=wall / max(full, 1))
     print(json.dumps(out), flush=True)
@@ -194,6 +194,11 @@ def _release(procs):
     return out
 
 
+def _profiled():
+    """True under rocprofv3 (its tool library is preloaded and initialises the GPU before main)."""
+    return any(k.startswith("ROCPROF") for k in os.environ) or "rocprof" in os.environ.get("LD_PRELOAD", "")
+
+
 def _cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -213,10 +218,36 @@ def _pmc_traffic():
             ks = json.load(open(os.path.join(HERE, "profiles", name)))["kernels"]
         except (OSError, KeyError, ValueError):
             continue
-        for k in ("gemm_offs_kernel",):
-            if k in ks:
-                return (ks[k]["FETCH_SIZE_KB"] + ks[k]["WRITE_SIZE_KB"]) * 1024.0
+        # dispatch-weighted over the gemm_offs_kernel<TS> instantiations
+        num = den = 0.0
+        for k, e in ks.items():
+            base = k.replace("void ", "").split("<")[0].strip()
+            if base == "gemm_offs_kernel" and "FETCH_SIZE_KB" in e and "WRITE_SIZE_KB" in e:
+                num += (e["FETCH_SIZE_KB"] + e["WRITE_SIZE_KB"]) * e["dispatches"]
+                den += e["dispatches"]
+        if den:
+            return num / den * 1024.0
     return None
+
+
+def make_schedule(config, cfg_name, seeds_arg, steps, world, rank, P, mode):
+    """(seeds, per-step seed lists, this rank's per-slot seed lists).  Step i, rank p, slot j
+    solves seeds[(i*N*P + p*P + j) mod S] (`shard`) or step i's N=1 seed (`replica`); the config's
+    seeds only, plus the vetted EXTRA_SEEDS when a shard step has more solves than seeds."""
+    if seeds_arg:
+        seeds = [int(s) for s in seeds_arg.split(",")]
+    else:
+        seeds = list(config["seeds"])
+        if mode == "shard" and world * P > len(seeds):
+            seeds += [s for s in EXTRA_SEEDS.get(cfg_name, []) if s not in seeds]
+    per_step = world * P
+    if mode == "shard":
+        step_seeds = [seeds[(i * per_step + q) % len(seeds)] for i in range(steps) for q in range(per_step)]
+    else:
+        step_seeds = [seeds[i % len(seeds)] for i in range(steps) for q in range(per_step)]
+    sched = [step_seeds[i * per_step:(i + 1) * per_step] for i in range(steps)]
+    slot_seeds = [[sched[i][rank * P + j] for i in range(steps)] for j in range(P)]
+    return seeds, sched, slot_seeds
 
 
 def main():
@@ -250,20 +281,15 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     with open(args.config) as f:
         config = yaml.safe_load(f)
-    if args.seeds:
-        seeds = [int(s) for s in args.seeds.split(",")]
-    else:
-        seeds = list(config["seeds"])
-        if args.schedule == "shard" and world > len(seeds):
-            seeds += [s for s in EXTRA_SEEDS.get(os.path.basename(args.config), []) if s not in seeds]
     P = args.inflight if args.inflight else max(1, min(2, 16 // world))
-    per_step = world * P  # solves per step, rank-major then slot
-    if args.schedule == "shard":
-        step_seeds = [seeds[(i * per_step + q) % len(seeds)] for i in range(args.steps) for q in range(per_step)]
-    else:
-        step_seeds = [seeds[i % len(seeds)] for i in range(args.steps) for q in range(per_step)]
-    sched = [step_seeds[i * per_step:(i + 1) * per_step] for i in range(args.steps)]
-    slot_seeds = [[step_seeds[i * per_step + rank * P + j] for i in range(args.steps)] for j in range(P)]
+    if _profiled() and (P > 1 or not args.no_cpu_baseline):
+        # a profiler's preloaded library has initialised the GPU already: no child processes
+        print("bench: under a profiler -> --inflight 1 --no-cpu-baseline", file=sys.stderr)
+        P, args.no_cpu_baseline = 1, True
+    seeds, sched, slot_seeds = make_schedule(config, os.path.basename(args.config), args.seeds, args.steps, world,
+                                             rank, P, args.schedule)
+    step_seeds = [s for st in sched for s in st]
+    per_step = world * P
     mine_seeds = slot_seeds[0]
     gpu_procs = _spawn_gpu_workers(args, slot_seeds[1:])  # before any GPU call
 
@@ -386,11 +412,13 @@ def main():
             if c is None:
                 continue
             g = gpu_by_seed[c["seed"]]
-            k = c["iters"]
-            gt = g["assembly_t"]
-            gk = (gt[k] - gt[0]) / k if len(gt) > k else None
-            rows.append({"seed": c["seed"], "iters": k, "cpu_s_per_iter": c["s_per_iter"], "gpu_s_per_iter": gk,
-                         "gpu_over_cpu": (gk / c["s_per_iter"]) if gk else None})
+            gt, ct = g["assembly_t"], c["assembly_t"]
+            k = min(c["iters"], len(gt) - 1)  # the common prefix of IPM iterations
+            gk = (gt[k] - gt[0]) / k if k > 0 else None
+            ck = (ct[k] - ct[0]) / k if k > 0 else None
+            rows.append({"seed": c["seed"], "iters": k, "cpu_s_per_iter": ck, "gpu_s_per_iter": gk,
+                         "gpu_over_cpu": (gk / ck) if gk and ck else None})
+        rows = [r for r in rows if r["cpu_s_per_iter"]]
         med = float(np.median([r["cpu_s_per_iter"] for r in rows])) if rows else None
         gmed = [r["gpu_s_per_iter"] for r in rows if r["gpu_s_per_iter"]]
         cpu = {"value": med, "unit": "s/IPM-iter", "cores": 1, "kind": "port",

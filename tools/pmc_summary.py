@@ -12,7 +12,7 @@ for path in glob.glob(os.path.join(sys.argv[1], "**", "*counter_collection.csv")
     with open(path) as f:
         for r in csv.DictReader(f):
             name = re.sub(r"\(anonymous namespace\)::", "", r.get("Kernel_Name", ""))
-            name = name.split("(")[0]
+            name = name.split("(")[0].replace("void ", "").strip()
             ctr = r.get("Counter_Name", "")
             val = float(r.get("Counter_Value", 0.0))
             e = rows.setdefault(name, {}).setdefault(ctr, [0, 0.0])
