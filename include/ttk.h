@@ -36,7 +36,8 @@ enum ttk_status {
   TTK_ERR_HIP = 2,          /* HIP runtime error */
   TTK_ERR_NOT_PD = 3,       /* Cholesky: matrix not positive definite (scipy LinAlgError) */
   TTK_ERR_SINGULAR = 4,     /* LU / triangular: exact zero pivot (scipy LinAlgError) */
-  TTK_ERR_NOT_CONVERGED = 5 /* iterative kernel hit its sweep cap */
+  TTK_ERR_NOT_CONVERGED = 5, /* iterative kernel hit its sweep cap */
+  TTK_ILL_CONDITIONED = 6    /* LU: rcond < eps/2 (scipy's LinAlgWarning, raised as an error) */
 };
 
 /* ---------------------------------------------------------------------------------------
@@ -344,6 +345,37 @@ typedef struct {
 } ttk_lgmres_info;
 int ttk_lgmres(ttk_ctx ctx, int64_t schur, const double *b, double *x, int64_t n, int restart, int augment,
                double rtol, int max_it, int chunk, ttk_lgmres_info *info);
+
+/* ---------------------------------------------------------------------------------------
+ * TT rounding in one call (SURVEY §8(b) `ttk_round`): replaces `tt_rank_reduce`
+ * (cy_src/tt_ops_cy.pyx:179-226: right-to-left QR sweep `tt_rl_orthogonalise` :132-159, then the
+ * left-to-right truncated-SVD sweep at eps/sqrt(d-1) with `prune_singular_vals` :161-177) and,
+ * mode 1, the tracked sweep of `tt_psd_rank_reduce` / `tt_mask_rank_reduce` (:261-388: eps/2,
+ * discarded energy accumulated; *tail_out = (sum of discarded sigma^2)^(1/(2d)), the factor the
+ * caller adds as factor*I or factor*mask; NaN when the train was returned unchanged).
+ * cores[k]: device, contiguous (r_k, inner[k], r_{k+1}) fp64, caller-owned, rewritten IN PLACE with
+ * the rounded core (ranks never grow, so it fits); ranks[0..d]: in the input bond ranks
+ * (ranks[0] = ranks[d] = 1), out the new ones.  Same launches as the Python sweep: bit-identical.
+ * Host decisions read the singular values (one sync per bond). */
+int ttk_round(ttk_ctx ctx, int d, double *const *cores, const int64_t *inner, int64_t *ranks, double eps, int mode,
+              double *tail_out);
+
+/* Dense Schur-complement local KKT solve in one call (SURVEY §8(b) `ttk_local_assemble` +
+ * `ttk_dense_schur_solve`; the dense branch of `_ipm_local_solver`, src/tt_ipm.py:183-229):
+ * assembles L_XI = B22 diag(inv_I), L_eq = B01, L_Z = B21 (each 'lsr,smnS,LSR->lmLrnR'), Cholesky of
+ * L_Z, forward/backward substitutions, A = L_eq L_Z^-1 L_XI L_eq^T + B00 + 1e-11 I, LU with
+ * dgecon, then back-substitutes Y, Z, X into sol (r, 3, n, R).  blk: the blocks (0,0), (0,1), (2,1),
+ * (2,2) of the local operator -- XAX_k[key] (r, s, r), A_k[key] (s, n, n, S) with element strides,
+ * XAX_k1[key] (R, S, R), all contiguous but A.  rhs (r, 3, n, R) and inv_I (r, n, R) contiguous.
+ * Status: TTK_OK; TTK_ERR_NOT_PD (Cholesky failed: scipy LinAlgError), TTK_ERR_SINGULAR (exact
+ * zero pivot), TTK_ILL_CONDITIONED (rcond < eps/2: LinAlgWarning) -- the reference then falls back
+ * to its iterative solve (src/tt_ipm.py:224-229).  Same launches as the Python path: bit-identical. */
+typedef struct {
+  const double *L, *A, *R;
+  int64_t s, S, a_strides[4];
+} ttk_local_block;
+int ttk_dense_schur_solve(ttk_ctx ctx, int64_t r, int64_t n, int64_t R, const ttk_local_block *blocks,
+                          const double *rhs, const double *inv_I, double *sol, double *rcond_out);
 
 #ifdef __cplusplus
 }

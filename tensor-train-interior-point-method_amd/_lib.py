@@ -77,6 +77,8 @@ _SIGS = {
     "ttk_ctx_stream": (vp, [vp]),
     "ttk_lgmres": (i32, [vp, i64, vp, vp, i64, i32, i32, f64, i32, i32, vp]),
     "ttk_env_update": (i32, [vp, i32, i32, vp]),
+    "ttk_round": (i32, [vp, i32, vp, vp, vp, f64, i32, vp]),
+    "ttk_dense_schur_solve": (i32, [vp, i64, i64, i64, vp, vp, vp, vp, vp]),
     "ttk_fused_set_mfma": (i32, [i32]),
     "ttk_einsum_set_fused": (i32, [i32]),
     "ttk_qr_set_big_threshold": (i32, [i32]),

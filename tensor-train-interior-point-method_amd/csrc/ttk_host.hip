@@ -1,0 +1,282 @@
+// TT-level entry points composed from the library's own kernels: the host-side
+// orchestration that the Python layer would otherwise run, behind the C ABI so a reference-side
+// caller (Cython / ctypes) reaches the whole operation in one call.  Every step issues the same
+// kernel launches with the same shapes, strides and plans as the Python path, so the results are
+// bit-identical to it (tests/test_gpu_abi.py).
+#include <cmath>
+#include <tuple>
+#include <cstring>
+#include <vector>
+
+#include "ttk_common.h"
+#include "ttk_internal.h"
+
+namespace {
+
+// stream-ordered scratch released when the call returns
+struct Scratch {
+  hipStream_t st;
+  std::vector<void *> ptrs;
+  explicit Scratch(hipStream_t s) : st(s) {}
+  double *get(int64_t n) {
+    void *p = nullptr;
+    if (hipMallocAsync(&p, (size_t)(n > 0 ? n : 1) * sizeof(double), st) != hipSuccess) return nullptr;
+    ptrs.push_back(p);
+    return static_cast<double *>(p);
+  }
+  ~Scratch() {
+    for (void *p : ptrs) (void)hipFreeAsync(p, st);
+  }
+};
+
+struct View {
+  const double *p;
+  int nd;
+  int64_t sh[4], st[4];
+};
+
+View mat(const double *p, int64_t rows, int64_t cols) { return View{p, 2, {rows, cols}, {cols, 1}}; }
+
+// ttk_einsum on views, fresh contiguous output (dev.einsum with out=None, fused=False)
+int einsum(hipStream_t st, const char *eq, std::initializer_list<View> ops, double *out) {
+  int64_t d[1 + 8 * 10 + 1];
+  int k = 0;
+  d[k++] = (int64_t)ops.size();
+  for (const View &o : ops) {
+    d[k++] = reinterpret_cast<int64_t>(o.p);
+    d[k++] = o.nd;
+    for (int i = 0; i < o.nd; ++i) d[k++] = o.sh[i];
+    for (int i = 0; i < o.nd; ++i) d[k++] = o.st[i];
+  }
+  d[k++] = 0;
+  return ttk_einsum(st, eq, d, out, 1.0, 0.0);
+}
+
+// contiguous copy of a 2-D strided view (dev.clone)
+int copy2(hipStream_t st, const double *src, int64_t rows, int64_t cols, int64_t s0, int64_t s1, double *dst) {
+  const int64_t shape[2] = {rows, cols}, ss[2] = {s0, s1}, ds[2] = {cols, 1};
+  return ttk_copy_nd(st, src, dst, 2, shape, ss, ds, 1.0, 0.0);
+}
+
+// `prune_singular_vals` (cy_src/tt_ops_cy.pyx:161-177) / the tracked variant of the PSD and mask
+// roundings (:261-388): sc[i] = sum_{j>=i} s_j^2 accumulated from the end as np.cumsum does.
+int truncation_rank(const std::vector<double> &s, double eps, bool track, double *tail) {
+  const int k = (int)s.size();
+  *tail = 0.0;
+  if (!track) {
+    bool zero = true;
+    for (double v : s) zero = zero && v == 0.0;
+    if (zero) return 1;
+  }
+  std::vector<double> sc(k);
+  double acc = 0.0;
+  for (int i = k - 1; i >= 0; --i) {
+    acc += std::fabs(s[i]) * std::fabs(s[i]);
+    sc[i] = acc;
+  }
+  const double e2 = eps * eps;
+  int r = 0;
+  for (int i = 0; i < k; ++i)
+    if (sc[i] < e2) {
+      r = i;
+      break;
+    }
+  r = r < 1 ? 1 : r;
+  if (sc[k - 1] > e2) r = k;
+  if (track && r < k) *tail = sc[r];
+  return r;
+}
+
+View v3(const double *p, int64_t a, int64_t b, int64_t c) { return View{p, 3, {a, b, c}, {b * c, c, 1}}; }
+
+// einsum with an explicit (strided) output view and alpha / beta (dev.einsum(..., out=view))
+int einsum_out(hipStream_t st, const char *eq, std::initializer_list<View> ops, double *out, int ond,
+               const int64_t *ost, double alpha, double beta) {
+  int64_t d[1 + 8 * 10 + 2 + 8];
+  int k = 0;
+  d[k++] = (int64_t)ops.size();
+  for (const View &o : ops) {
+    d[k++] = reinterpret_cast<int64_t>(o.p);
+    d[k++] = o.nd;
+    for (int i = 0; i < o.nd; ++i) d[k++] = o.sh[i];
+    for (int i = 0; i < o.nd; ++i) d[k++] = o.st[i];
+  }
+  d[k++] = 1;
+  d[k++] = ond;
+  for (int i = 0; i < ond; ++i) d[k++] = ost[i];
+  return ttk_einsum(st, eq, d, out, alpha, beta);
+}
+
+}  // namespace
+
+extern "C" {
+
+int ttk_dense_schur_solve(ttk_ctx ctx, int64_t r, int64_t n, int64_t R, const ttk_local_block *blk,
+                          const double *rhs, const double *inv_I, double *sol, double *rcond_out) {
+  ttk::CtxScope scope(ctx);
+  hipStream_t st = ttk::ctx().stream;
+  if (rcond_out) *rcond_out = NAN;
+  const int64_t m = r * n * R;
+  if (r < 1 || n < 1 || R < 1 || !blk || !rhs || !inv_I || !sol || m > (1 << 20)) {
+    ttk::set_error("ttk_dense_schur_solve: bad arguments");
+    return TTK_ERR_ARG;
+  }
+  static const char *ASSEMBLE = "lsr,smnS,LSR->lmLrnR", *APPLY = "lsr,smnS,LSR,rnR->lmL",
+                    *APPLY_T = "lsr,smnS,LSR,lmL->rnR", *MATMUL = "ik,kj->ij";
+  enum { B00, B01, B21, B22 };
+  auto ops3 = [&](int b) {
+    const ttk_local_block &q = blk[b];
+    return std::make_tuple(v3(q.L, r, q.s, r),
+                           View{q.A, 4, {q.s, n, n, q.S}, {q.a_strides[0], q.a_strides[1], q.a_strides[2], q.a_strides[3]}},
+                           v3(q.R, R, q.S, R));
+  };
+  Scratch sc(st);
+  double *rd = sc.get(m), *rc = sc.get(m), *rp = sc.get(m), *LXI = sc.get(m * m), *Leq = sc.get(m * m),
+         *LZ = sc.get(m * m), *t = sc.get(m), *bvec = sc.get(m), *T1 = sc.get(m * m), *Am = sc.get(m * m),
+         *t2 = sc.get(m), *t3 = sc.get(m), *work = sc.get(2 * m + 16);
+  int *piv = reinterpret_cast<int *>(sc.get(m / 2 + 1));
+  if (!rd || !rc || !rp || !LXI || !Leq || !LZ || !t || !bvec || !T1 || !Am || !t2 || !t3 || !work || !piv) {
+    ttk::set_error("ttk_dense_schur_solve: scratch allocation failed");
+    return TTK_ERR_HIP;
+  }
+  const int64_t sh3[3] = {r, n, R}, st_blk[3] = {3 * n * R, R, 1}, st_c[3] = {n * R, R, 1};
+  const int64_t out6[6] = {n * R * m, R * m, m, n * R, R, 1};
+  const int64_t mm[2] = {m, m}, s_mat[2] = {m, 1}, s_row[2] = {0, 1}, out2[2] = {1, 1};
+  auto col = [&](int j) { return rhs + j * n * R; };  // rhs[:, j] as (r, n, R) view, strides st_blk
+  int rc_ = TTK_OK;
+#define STEP(x)              \
+  do {                       \
+    if (rc_ == TTK_OK) rc_ = (x); \
+  } while (0)
+  STEP(ttk_copy_nd(st, col(1), rd, 3, sh3, st_blk, st_c, 1.0, 0.0));
+  STEP(ttk_copy_nd(st, col(2), rc, 3, sh3, st_blk, st_c, 1.0, 0.0));
+  STEP(ttk_copy_nd(st, col(0), rp, 3, sh3, st_blk, st_c, 1.0, 0.0));
+  {
+    auto [a, b, c] = ops3(B22);
+    STEP(einsum(st, ASSEMBLE, {a, b, c}, LXI));
+  }
+  STEP(ttk_mul_nd(st, LXI, inv_I, LXI, 2, mm, s_mat, s_row, s_mat, 1.0, 0.0));  // LXI * inv_I[col]
+  {
+    auto [a, b, c] = ops3(B01);
+    STEP(einsum(st, ASSEMBLE, {a, b, c}, Leq));
+  }
+  {
+    auto [a, b, c] = ops3(B21);
+    STEP(einsum(st, ASSEMBLE, {a, b, c}, LZ));
+  }
+  if (rc_) return rc_;
+  rc_ = ttk_cholesky_sync(st, LZ, (int)m);
+  if (rc_) return rc_;  // TTK_ERR_NOT_PD: scipy's LinAlgError -> the caller's iterative fallback
+  STEP(hipMemcpyAsync(t, rc, m * sizeof(double), hipMemcpyDeviceToDevice, st) ? TTK_ERR_HIP : 0);
+  STEP(einsum_out(st, MATMUL, {mat(LXI, m, m), mat(rd, m, 1)}, t, 2, out2, -1.0, 1.0));
+  STEP(ttk_trsm_lower(st, LZ, (int)m, t, 1, 1, 0));
+  STEP(ttk_trsm_lower(st, LZ, (int)m, t, 1, 1, 1));
+  STEP(hipMemcpyAsync(bvec, rp, m * sizeof(double), hipMemcpyDeviceToDevice, st) ? TTK_ERR_HIP : 0);
+  STEP(einsum_out(st, MATMUL, {mat(Leq, m, m), mat(t, m, 1)}, bvec, 2, out2, -1.0, 1.0));
+  STEP(ttk_trsm_lower(st, LZ, (int)m, LXI, (int)m, (int)m, 0));
+  STEP(ttk_trsm_lower(st, LZ, (int)m, LXI, (int)m, (int)m, 1));
+  STEP(einsum(st, MATMUL, {mat(LXI, m, m), View{Leq, 2, {m, m}, {1, m}}}, T1));
+  STEP(einsum(st, MATMUL, {mat(Leq, m, m), mat(T1, m, m)}, Am));
+  {
+    auto [a, b, c] = ops3(B00);
+    STEP(einsum_out(st, ASSEMBLE, {a, b, c}, Am, 6, out6, 1.0, 1.0));
+  }
+  STEP(ttk_add_diag(st, Am, (int)m, (int)m, 1e-11));
+  if (rc_) return rc_;
+  double rcond = 0.0;
+  rc_ = ttk_lu_sync(st, Am, (int)m, piv, work, &rcond);
+  if (rcond_out) *rcond_out = rcond;
+  if (rc_) return rc_;  // TTK_ERR_SINGULAR
+  if (rcond < 0.5 * 2.220446049250313e-16) return TTK_ILL_CONDITIONED;  // LinAlgWarning as an error
+  STEP(ttk_lu_solve(st, Am, (int)m, piv, bvec, 1, 1));
+  double *s0 = sol, *s1 = sol + n * R, *s2 = sol + 2 * n * R;  // sol[:, j] views, strides st_blk
+  STEP(ttk_copy_nd(st, bvec, s0, 3, sh3, st_c, st_blk, 1.0, 0.0));
+  STEP(hipMemcpyAsync(t2, rd, m * sizeof(double), hipMemcpyDeviceToDevice, st) ? TTK_ERR_HIP : 0);
+  {
+    auto [a, b, c] = ops3(B01);
+    const View x{s0, 3, {r, n, R}, {st_blk[0], st_blk[1], st_blk[2]}};
+    STEP(einsum_out(st, APPLY_T, {a, b, c, x}, t2, 3, st_c, -1.0, 1.0));
+  }
+  STEP(ttk_mul_nd(st, t2, inv_I, s2, 3, sh3, st_c, st_c, st_blk, 1.0, 0.0));
+  STEP(hipMemcpyAsync(t3, rc, m * sizeof(double), hipMemcpyDeviceToDevice, st) ? TTK_ERR_HIP : 0);
+  {
+    auto [a, b, c] = ops3(B22);
+    const View x{s2, 3, {r, n, R}, {st_blk[0], st_blk[1], st_blk[2]}};
+    STEP(einsum_out(st, APPLY, {a, b, c, x}, t3, 3, st_c, -1.0, 1.0));
+  }
+  STEP(ttk_trsm_lower(st, LZ, (int)m, t3, 1, 1, 0));
+  STEP(ttk_trsm_lower(st, LZ, (int)m, t3, 1, 1, 1));
+  STEP(ttk_copy_nd(st, t3, s1, 3, sh3, st_c, st_blk, 1.0, 0.0));
+#undef STEP
+  return rc_;
+}
+
+int ttk_round(ttk_ctx ctx, int d, double *const *cores, const int64_t *inner, int64_t *ranks, double eps, int mode,
+              double *tail_out) {
+  ttk::CtxScope scope(ctx);
+  hipStream_t st = ttk::ctx().stream;
+  if (tail_out) *tail_out = NAN;
+  if (d < 1 || !cores || !inner || !ranks || (mode != 0 && mode != 1) || ranks[0] != 1 || ranks[d] != 1) {
+    ttk::set_error("ttk_round: bad arguments");
+    return TTK_ERR_ARG;
+  }
+  bool all1 = true;
+  for (int k = 0; k <= d; ++k) all1 = all1 && ranks[k] == 1;
+  if (d == 1 || all1) return TTK_OK;  // tt_rank_reduce returns the train unchanged
+  const bool track = mode == 1;
+  if (track) eps = eps / 2.0;
+  eps = eps / std::sqrt((double)(d - 1));
+  std::vector<int64_t> r(ranks, ranks + d + 1);
+  Scratch sc(st);
+  int rc = TTK_OK;
+  // ---- right-to-left QR sweep (tt_rl_orthogonalise, cy_src/tt_ops_cy.pyx:132-159)
+  for (int i = d - 1; i >= 1 && rc == TTK_OK; --i) {
+    const int64_t m = inner[i] * r[i + 1], n = r[i], k = m < n ? m : n;
+    double *At = sc.get(m * n), *Q = sc.get(m * k), *R = sc.get(k * n), *w = sc.get(ttk_qr_work((int)m, (int)n));
+    const int64_t lead = r[i - 1] * inner[i - 1];
+    double *prev = sc.get(lead * k);
+    if (!At || !Q || !R || !w || !prev) {
+      ttk::set_error("ttk_round: scratch allocation failed");
+      return TTK_ERR_HIP;
+    }
+    rc = copy2(st, cores[i], m, n, 1, m, At);  // unfolding (r_i, n_i R_i) transposed
+    if (!rc) rc = ttk_qr(st, At, (int)m, (int)n, Q, R, w);
+    if (!rc) rc = copy2(st, Q, k, m, 1, k, cores[i]);  // Q^T -> core i (k, n_i, R_i)
+    if (!rc) rc = einsum(st, "ij,kj->ik", {mat(cores[i - 1], lead, n), mat(R, k, n)}, prev);
+    if (!rc) rc = hipMemcpyAsync(cores[i - 1], prev, lead * k * sizeof(double), hipMemcpyDeviceToDevice, st) ? TTK_ERR_HIP : 0;
+    r[i] = k;
+  }
+  // ---- left-to-right truncated-SVD sweep (cy_src/tt_ops_cy.pyx:200-222)
+  double tail = 0.0;
+  int64_t rank = 1;
+  std::vector<double> s;
+  for (int idx = 0; idx + 1 < d && rc == TTK_OK; ++idx) {
+    const int64_t m = rank * inner[idx], n = r[idx + 1], k = m < n ? m : n;
+    double *U = sc.get(m * k), *S = sc.get(k), *Vt = sc.get(k * n), *w = sc.get(ttk_svd_work((int)m, (int)n));
+    const int64_t rest = inner[idx + 1] * r[idx + 2];
+    double *nxt = sc.get(k * rest);
+    if (!U || !S || !Vt || !w || !nxt) {
+      ttk::set_error("ttk_round: scratch allocation failed");
+      return TTK_ERR_HIP;
+    }
+    rc = ttk_svd_tol(st, cores[idx], (int)m, (int)n, U, S, Vt, w, track ? 0.0 : 1e-3 * eps);
+    s.assign(k, 0.0);
+    if (!rc) rc = ttk_read_sync(st, S, s.data(), k);
+    if (rc) break;
+    double t = 0.0;
+    const int64_t nr = truncation_rank(s, eps, track, &t);
+    tail += t;
+    rc = copy2(st, U, m, nr, k, 1, cores[idx]);  // U[:, :nr] -> core idx (rank, n_idx, nr)
+    const View sv{S, 1, {nr}, {1}}, vv{Vt, 2, {nr, n}, {n, 1}};
+    if (!rc) rc = einsum(st, "r,rj,jk->rk", {sv, vv, mat(cores[idx + 1], n, rest)}, nxt);
+    if (!rc) rc = hipMemcpyAsync(cores[idx + 1], nxt, nr * rest * sizeof(double), hipMemcpyDeviceToDevice, st) ? TTK_ERR_HIP : 0;
+    r[idx + 1] = nr;
+    rank = nr;
+  }
+  if (rc) return rc;
+  for (int k = 0; k <= d; ++k) ranks[k] = r[k];
+  if (track && tail_out) *tail_out = std::pow(tail, 1.0 / (2 * d));
+  return TTK_OK;
+}
+
+}  // extern "C"

@@ -42,6 +42,8 @@ INEQ_MATVEC_BUG = False
 FUSED_MATVEC = os.environ.get("TTIPM_FUSED_MATVEC", "1") == "1"
 # ... and the whole Schur matvec as one native operator (2 launches per matvec, same arithmetic)
 SCHUR_OP = os.environ.get("TTIPM_SCHUR_OP", "1") == "1"
+# the dense Schur local solve as one library call (ttk_dense_schur_solve, bit-identical launches)
+NATIVE_DENSE = os.environ.get("TTIPM_NATIVE_DENSE", "1") == "1"
 
 
 class IneqMatvecBug(TypeError):
@@ -187,6 +189,38 @@ def _assemble(XAX_k, A_k, XAX_k1, key, m):
     return einsum(ASSEMBLE, XAX_k[key], A_k[key], XAX_k1[key]).view(m, m)
 
 
+class _LocalBlock(ctypes.Structure):
+    _fields_ = [("L", ctypes.c_void_p), ("A", ctypes.c_void_p), ("R", ctypes.c_void_p), ("s", ctypes.c_int64),
+                ("S", ctypes.c_int64), ("a_strides", ctypes.c_int64 * 4)]
+
+
+_TTK_ILL_CONDITIONED = 6
+
+
+def _dense_native(XAX_k, A_k, XAX_k1, rhs, inv_I, xs):
+    """`ttk_dense_schur_solve`: the dense branch below in one library call; its status maps onto
+    the exceptions the Python steps raise (LinAlgError, LinAlgWarning-as-error)."""
+    r, n, R = xs[0], xs[2], xs[3]
+    arr = (_LocalBlock * 4)()
+    keep = []
+    for e, key in zip(arr, ((0, 0), (0, 1), (2, 1), (2, 2))):
+        L, A, Rr = D.contig(XAX_k[key]), A_k[key], D.contig(XAX_k1[key])
+        keep += [L, A, Rr]
+        e.L, e.A, e.R = L.data_ptr(), A.data_ptr(), Rr.data_ptr()
+        e.s, e.S = A.shape[0], A.shape[3]
+        e.a_strides[:] = tuple(A.stride())
+    rhs, inv_I = D.contig(rhs), D.contig(inv_I)
+    sol = D.empty(*xs)
+    rc = ctypes.c_double(0.0)
+    D._stream()
+    st = lib.ttk_dense_schur_solve(D.CTX[0], r, n, R, arr, rhs.data_ptr(), inv_I.data_ptr(), sol.data_ptr(),
+                                   ctypes.byref(rc))
+    if st == _TTK_ILL_CONDITIONED:
+        raise D.LinAlgWarning(f"Ill-conditioned matrix (rcond={rc.value:.5g}): result may not be accurate.")
+    D.check(st, "dense_schur_solve")
+    return sol
+
+
 def _fbsub_(LZ, B):
     """forward_backward_sub (`src/tt_ipm.py:178-181`) in place on B (n, k)."""
     D.trsm_(LZ, B, trans=False)
@@ -208,6 +242,42 @@ def _run_lgmres(op, rhs_flat, m, rtol):
     return x
 
 
+def _dense_python(XAX_k, A_k, XAX_k1, rhs, inv_I, xs):
+    """The dense branch of `_ipm_local_solver` (`src/tt_ipm.py:200-222`) step by step."""
+    r, n, R = xs[0], xs[2], xs[3]
+    m = r * n * R
+    rd = D.clone(rhs[:, 1]).view(m, 1)
+    rc = D.clone(rhs[:, 2]).view(m, 1)
+    rp = D.clone(rhs[:, 0]).view(m, 1)
+    LXI = _assemble(XAX_k, A_k, XAX_k1, (2, 2), m)
+    D.mul_(LXI, LXI, inv_I.view(1, m).expand(m, m))
+    Leq = _assemble(XAX_k, A_k, XAX_k1, (0, 1), m)
+    LZ = _assemble(XAX_k, A_k, XAX_k1, (2, 1), m)
+    D.cholesky_(LZ)
+    t = D.clone(rc)
+    D.matmul(LXI, rd, out=t, alpha=-1.0, beta=1.0)
+    _fbsub_(LZ, t)
+    bvec = D.clone(rp)
+    D.matmul(Leq, t, out=bvec, alpha=-1.0, beta=1.0)
+    _fbsub_(LZ, LXI)
+    T1 = D.matmul(LXI, Leq.t())
+    Am = D.matmul(Leq, T1)
+    einsum(ASSEMBLE, XAX_k[0, 0], A_k[0, 0], XAX_k1[0, 0], out=Am.view(r, n, R, r, n, R), beta=1.0)
+    D.add_diag_(Am, 1e-11)
+    piv = D.lu_(Am)
+    D.lu_solve_(Am, piv, bvec)
+    sol = D.empty(*xs)
+    D.copy_(sol[:, 0], bvec.view(r, n, R))
+    t2 = D.clone(rd).view(r, n, R)
+    einsum(APPLY_T, XAX_k[0, 1], A_k[0, 1], XAX_k1[0, 1], sol[:, 0], out=t2, alpha=-1.0, beta=1.0)
+    D.mul_(sol[:, 2], t2, inv_I)
+    t3 = D.clone(rc).view(r, n, R)
+    einsum(APPLY, XAX_k[2, 2], A_k[2, 2], XAX_k1[2, 2], sol[:, 2], out=t3, alpha=-1.0, beta=1.0)
+    _fbsub_(LZ, t3.view(m, 1))
+    D.copy_(sol[:, 1], t3)
+    return sol
+
+
 def _ipm_local_solver(XAX_k, A_k, XAX_k1, Xb_k, b_k, Xb_k1, prev, size_limit, dense_solve=True, rtol=1e-5):
     """`_ipm_local_solver` (`src/tt_ipm.py:183-282`) on the device."""
     xs = tuple(prev.shape)
@@ -221,35 +291,8 @@ def _ipm_local_solver(XAX_k, A_k, XAX_k1, Xb_k, b_k, Xb_k1, prev, size_limit, de
     sol = None
     if dense_solve:
         try:
-            rd = D.clone(rhs[:, 1]).view(m, 1)
-            rc = D.clone(rhs[:, 2]).view(m, 1)
-            rp = D.clone(rhs[:, 0]).view(m, 1)
-            LXI = _assemble(XAX_k, A_k, XAX_k1, (2, 2), m)
-            D.mul_(LXI, LXI, inv_I.view(1, m).expand(m, m))
-            Leq = _assemble(XAX_k, A_k, XAX_k1, (0, 1), m)
-            LZ = _assemble(XAX_k, A_k, XAX_k1, (2, 1), m)
-            D.cholesky_(LZ)
-            t = D.clone(rc)
-            D.matmul(LXI, rd, out=t, alpha=-1.0, beta=1.0)
-            _fbsub_(LZ, t)
-            bvec = D.clone(rp)
-            D.matmul(Leq, t, out=bvec, alpha=-1.0, beta=1.0)
-            _fbsub_(LZ, LXI)
-            T1 = D.matmul(LXI, Leq.t())
-            Am = D.matmul(Leq, T1)
-            einsum(ASSEMBLE, XAX_k[0, 0], A_k[0, 0], XAX_k1[0, 0], out=Am.view(r, n, R, r, n, R), beta=1.0)
-            D.add_diag_(Am, 1e-11)
-            piv = D.lu_(Am)
-            D.lu_solve_(Am, piv, bvec)
-            sol = D.empty(*xs)
-            D.copy_(sol[:, 0], bvec.view(r, n, R))
-            t2 = D.clone(rd).view(r, n, R)
-            einsum(APPLY_T, XAX_k[0, 1], A_k[0, 1], XAX_k1[0, 1], sol[:, 0], out=t2, alpha=-1.0, beta=1.0)
-            D.mul_(sol[:, 2], t2, inv_I)
-            t3 = D.clone(rc).view(r, n, R)
-            einsum(APPLY, XAX_k[2, 2], A_k[2, 2], XAX_k1[2, 2], sol[:, 2], out=t3, alpha=-1.0, beta=1.0)
-            _fbsub_(LZ, t3.view(m, 1))
-            D.copy_(sol[:, 1], t3)
+            dense = _dense_native if NATIVE_DENSE and D.DEV.type == "cuda" else _dense_python
+            sol = dense(XAX_k, A_k, XAX_k1, rhs, inv_I, xs)
         except Exception as e:
             print(e)
             _report(e)

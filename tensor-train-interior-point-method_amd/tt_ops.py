@@ -13,6 +13,7 @@ Semantics kept from the reference:
 """
 from functools import reduce
 
+import ctypes
 import os
 
 import numpy as np
@@ -284,12 +285,36 @@ def _svd_step(tt, idx, rank, eps, track):
     return nr, tail
 
 
+NATIVE_ROUND = os.environ.get("TTIPM_NATIVE_ROUND", "1") == "1"
+
+
+def _native_round(tt, eps, mode):
+    """`ttk_round` (one library call per rounding, bit-identical to the Python sweep below).  The
+    cores are copied first (the reference rebinds list entries and never writes the caller's
+    arrays), the rounded cores are views of those copies.  Returns (tt, tail factor or None)."""
+    d = len(tt)
+    cs = [D.clone(c) for c in tt]
+    mids = [tuple(c.shape[1:-1]) for c in tt]
+    ptrs = (ctypes.c_void_p * d)(*[c.data_ptr() for c in cs])
+    inner = (ctypes.c_int64 * d)(*[int(np.prod(m)) for m in mids])
+    ranks = (ctypes.c_int64 * (d + 1))(*([tt[0].shape[0]] + [c.shape[-1] for c in tt]))
+    tail = ctypes.c_double(0.0)
+    D._stream()
+    D.check(D.lib.ttk_round(D.CTX[0], d, ptrs, inner, ranks, float(eps), mode, ctypes.byref(tail)), "round")
+    out = [c.view(-1)[:ranks[k] * inner[k] * ranks[k + 1]].view(ranks[k], *mids[k], ranks[k + 1])
+           for k, c in enumerate(cs)]
+    tt[:] = out  # in place, like the reference's list mutation
+    return tt, (None if np.isnan(tail.value) else tail.value)
+
+
 def tt_rank_reduce(tt, eps=1e-18):
     """`cy_src/tt_ops_cy.pyx:179-226`: QR sweep + left-to-right truncated-SVD sweep."""
     d = len(tt)
     rk = [1] + tt_ranks(tt) + [1]
     if d == 1 or all(r == 1 for r in rk):
         return tt
+    if NATIVE_ROUND and D.DEV.type == "cuda":
+        return _native_round(tt, eps, 0)[0]
     eps = eps / np.sqrt(d - 1)
     tt = tt_rl_orthogonalise(tt)
     rank = 1
@@ -300,10 +325,12 @@ def tt_rank_reduce(tt, eps=1e-18):
 
 def _tail_rank_reduce(tt, eps):
     d = len(tt)
-    eps = eps / 2.0
     rk = [1] + tt_ranks(tt) + [1]
     if d == 1 or all(r == 1 for r in rk):
         return tt, None
+    if NATIVE_ROUND and D.DEV.type == "cuda":
+        return _native_round(tt, eps, 1)
+    eps = eps / 2.0
     eps = eps / np.sqrt(d - 1)
     tt = tt_rl_orthogonalise(tt)
     rank = 1

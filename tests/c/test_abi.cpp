@@ -102,7 +102,9 @@ void solve(const Fixture &f, Result &out) {
     out.rc = ttk_lgmres(ctx, h, b, x, 2 * f.m, (int)f.restart, (int)f.augment, 1e-5, 300, 8, &out.info);
   if (out.rc) std::snprintf(out.err, sizeof(out.err), "%s", ttk_last_error());
   out.x.resize(2 * f.m);
-  (void)hipMemcpy(out.x.data(), x, 2 * f.m * sizeof(double), hipMemcpyDeviceToHost);
+  // the solve's last kernels are still queued on the context's (non-blocking) stream: copy on it
+  (void)hipMemcpyAsync(out.x.data(), x, 2 * f.m * sizeof(double), hipMemcpyDeviceToHost, st);
+  (void)hipStreamSynchronize(st);
   ttk_schur_free(h);
   for (int k = 0; k < 4; ++k) {
     (void)hipFree(L[k]);
