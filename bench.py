@@ -378,12 +378,14 @@ def main():
         lib.ttk_contract_stats(st, 1)
         lib.ttk_contract_timing(1)
         D.ALGO = {"flops": 0.0, "calls": 0, "by": {}}
+        s0, l0 = lib.ttk_sync_count(), lib.ttk_launch_count()
         try:
-            solve(shard.unpack(*packed[mine_seeds[0]]))
+            rr = solve(shard.unpack(*packed[mine_seeds[0]]))
             sync()
         finally:
             lib.ttk_contract_timing(0)
             algo, D.ALGO = D.ALGO, None
+        syncs, all_launches = lib.ttk_sync_count() - s0, lib.ttk_launch_count() - l0
         lib.ttk_contract_stats(st, 1)
         flops, launches, tflops, tl, tms = list(st)
         if tms > 0:
@@ -395,6 +397,8 @@ def main():
                         "seed": mine_seeds[0], "algorithmic_flops_per_solve": algo["flops"],
                         "algorithmic_calls_per_solve": algo["calls"], "device_flops_per_solve": tflops,
                         "launches_per_solve": int(tl), "kernel_ms_per_solve": tms,
+                        "all_launches_per_ipm_iter": all_launches / max(rr["num_iters"], 1),
+                        "host_syncs_per_ipm_iter": syncs / max(rr["num_iters"], 1),
                         "avg_launch_us": tms * 1e3 / max(tl, 1),
                         "algorithmic_flops_per_launch": algo["flops"] / max(tl, 1),
                         "algorithmic_by_op": dict(sorted(algo["by"].items(), key=lambda kv: -kv[1][1])[:10])}

@@ -60,6 +60,8 @@ const char *ttk_last_error(void);
 int ttk_version(void);
 /* number of kernel launches issued since load (profiling / launch-count tests) */
 long long ttk_launch_count(void);
+/* host waits on a stream so far (every device scalar the host branches on costs one) */
+long long ttk_sync_count(void);
 
 /* ---------------------------------------------------------------------------------------
  * Contractions.  One pairwise step of a planned einsum:
@@ -186,6 +188,9 @@ int ttk_scale_axis_ss(void *stream, const double *src, double *dst, int ndim, co
  * the residual of the step-size local solve (src/tt_als.py:1023-1030). */
 int ttk_rayleigh_tail_sync(void *stream, const double *v, double *Mv, int64_t n, double *ev_out,
                            double *res2_out);
+/* the same with (ev, ||Mv - ev v||^2) written to device memory out2[0..1] (no host wait): the
+ * eigen-ALS sweep reads all local residuals of a half-sweep at once */
+int ttk_rayleigh_tail_dev(void *stream, const double *v, double *Mv, int64_t n, double *out2);
 /* dst = src * scales[i_axis] with the (<= 16) scales passed by value from the host: the per-block
  * column scaling / unscaling of the AMEn sweep (`src/tt_als.py:321-322,444-446`), no H2D copy. */
 int ttk_scale_axis(void *stream, const double *src, double *dst, int ndim, const int64_t *shape,

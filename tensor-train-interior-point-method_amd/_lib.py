@@ -28,6 +28,7 @@ _SIGS = {
     "ttk_last_error": (ctypes.c_char_p, []),
     "ttk_version": (i32, []),
     "ttk_launch_count": (ctypes.c_longlong, []),
+    "ttk_sync_count": (ctypes.c_longlong, []),
     "ttk_gemm_offs": (i32, [vp, vp, vp, vp, vp, i32, i32, i32, i32, f64, f64]),
     "ttk_gemm_offs_grouped": (i32, [vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, f64, f64]),
     "ttk_copy_nd": (i32, [vp, vp, vp, i32, c_i64p, c_i64p, c_i64p, f64, f64]),
@@ -38,6 +39,7 @@ _SIGS = {
     "ttk_scale_axis_ss": (i32, [vp, vp, vp, i32, c_i64p, c_i64p, c_i64p, i32, vp, i32]),
     "ttk_normalize": (i32, [vp, vp, vp, i32, c_i64p, c_i64p]),
     "ttk_rayleigh_tail_sync": (i32, [vp, vp, vp, i64, c_dp, c_dp]),
+    "ttk_rayleigh_tail_dev": (i32, [vp, vp, vp, i64, vp]),
     "ttk_scale_axis": (i32, [vp, vp, vp, i32, c_i64p, c_i64p, c_i64p, i32, c_dp]),
     "ttk_fill": (i32, [vp, vp, i64, f64]),
     "ttk_add_diag": (i32, [vp, vp, i32, i32, f64]),

@@ -9,6 +9,7 @@ namespace ttk {
 
 void set_error(const char *fmt, ...);
 void note_launch();
+void note_sync();  // one host wait on a stream (counted for ttk_sync_count)
 double *pinned_stage(size_t n_doubles);  // per-thread pinned host staging buffer
 double *mapped_stage(size_t n_doubles, double **dev_ptr);  // host-coherent mapped buffer (host ptr)
 int contract_events_ext(hipEvent_t *ev0, hipEvent_t *ev1);  // roofline accounting (ttk_contract.hip)

@@ -975,6 +975,7 @@ int ttk_dot_nd_sync(void *stream, const double *x, const double *y, int ndim, co
   hipLaunchKernelGGL(dot_nd_kernel, dim3(1), dim3(1024), 0, TTK_STREAM(stream), x, y, d, h ? dev : ttk::ctx().dev_scalar);
   TTK_LAUNCH_CHECK();
   if (!h) return ttk_read_sync(stream, ttk::ctx().dev_scalar, result, 1);
+  ttk::note_sync();
   TTK_HIP(hipStreamSynchronize(TTK_STREAM(stream)));
   *result = h[0];
   return TTK_OK;
@@ -1024,9 +1025,17 @@ int ttk_rayleigh_tail_sync(void *stream, const double *v, double *Mv, int64_t n,
   }
   hipLaunchKernelGGL(rayleigh_tail_kernel, dim3(1), dim3(1024), 0, TTK_STREAM(stream), v, Mv, n, dev, 1.0);
   TTK_LAUNCH_CHECK();
+  ttk::note_sync();
   TTK_HIP(hipStreamSynchronize(TTK_STREAM(stream)));
   *ev_out = h[0];
   *res2_out = h[1];
+  return TTK_OK;
+}
+
+// the same tail with (ev, ||Mv - ev v||^2) left in device memory (read later, batched with others)
+int ttk_rayleigh_tail_dev(void *stream, const double *v, double *Mv, int64_t n, double *out2) {
+  hipLaunchKernelGGL(rayleigh_tail_kernel, dim3(1), dim3(1024), 0, TTK_STREAM(stream), v, Mv, n, out2, 1.0);
+  TTK_LAUNCH_CHECK();
   return TTK_OK;
 }
 
@@ -1048,6 +1057,7 @@ int ttk_rank_scan_sync(void *stream, double *res, const double *negs, int64_t n,
   }
   hipLaunchKernelGGL(rank_scan_kernel, dim3(1), dim3(1024), 0, TTK_STREAM(stream), res, negs, n, nq, dev);
   TTK_LAUNCH_CHECK();
+  ttk::note_sync();
   TTK_HIP(hipStreamSynchronize(TTK_STREAM(stream)));
   std::memcpy(host_out, h, (size_t)nq * sizeof(double));
   return TTK_OK;

@@ -437,6 +437,7 @@ int ttk_einsum(void *stream, const char *eq, const int64_t *desc, double *out, d
   } else if (pl.scratch > cx.scratch_n) {
     // growing the context's scratch: earlier calls may still be using the old buffer on the stream
     if (cx.scratch) {
+      ttk::note_sync();
       TTK_HIP(hipStreamSynchronize(TTK_STREAM(stream)));
       TTK_HIP(hipFree(cx.scratch));
     }

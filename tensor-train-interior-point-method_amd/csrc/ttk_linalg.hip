@@ -2345,12 +2345,14 @@ static int svd_big(void *stream, const double *A, int m, int n, double *U, doubl
     if ((c & 63) == 63 && c + 1 < p) {  // early-exit check for deflated solves
       int h = 0;
       TTK_HIP(hipMemcpyAsync(&h, ctl + 1, sizeof(int), hipMemcpyDeviceToHost, st));
+      ttk::note_sync();
       TTK_HIP(hipStreamSynchronize(st));
       if (h) break;
     }
   }
   int hk[2] = {p, 0};
   TTK_HIP(hipMemcpyAsync(hk, ctl, 2 * sizeof(int), hipMemcpyDeviceToHost, st));
+  ttk::note_sync();
   TTK_HIP(hipStreamSynchronize(st));
   const int kk = hk[0] < 1 ? 1 : hk[0];  // keep one direction so the epilogue is well defined
   const int nkp = (kk + QB - 1) / QB;
@@ -2367,6 +2369,7 @@ static int svd_big(void *stream, const double *A, int m, int n, double *U, doubl
     TTK_LAUNCH_CHECK();
     int h = 0;
     TTK_HIP(hipMemcpyAsync(&h, flag, sizeof(int), hipMemcpyDeviceToHost, st));
+    ttk::note_sync();
     TTK_HIP(hipStreamSynchronize(st));
     if (!h) break;
   }
@@ -2522,6 +2525,7 @@ int ttk_cholesky_sync(void *stream, double *A, int n) {
   }
   int st = 0;
   TTK_HIP(hipMemcpyAsync(&st, ttk::ctx().status, sizeof(int), hipMemcpyDeviceToHost, TTK_STREAM(stream)));
+  ttk::note_sync();
   TTK_HIP(hipStreamSynchronize(TTK_STREAM(stream)));
   if (st) {
     ttk::set_error("%d-th leading minor of the array is not positive definite", st);
@@ -2553,6 +2557,7 @@ int ttk_lu_sync(void *stream, double *A, int n, int *piv, double *work, double *
   int st = 0;
   TTK_HIP(hipMemcpyAsync(&st, ttk::ctx().status, sizeof(int), hipMemcpyDeviceToHost, TTK_STREAM(stream)));
   TTK_HIP(hipMemcpyAsync(rcond_out, ttk::ctx().rcond, sizeof(double), hipMemcpyDeviceToHost, TTK_STREAM(stream)));
+  ttk::note_sync();
   TTK_HIP(hipStreamSynchronize(TTK_STREAM(stream)));
   if (st) {
     ttk::set_error("Matrix is singular (zero pivot at %d).", st);

@@ -13,6 +13,7 @@ namespace ttk {
 
 static thread_local char g_err[512] = "";
 static std::atomic<long long> g_launches{0};
+static std::atomic<long long> g_syncs{0};
 
 void set_error(const char *fmt, ...) {
   va_list ap;
@@ -22,6 +23,7 @@ void set_error(const char *fmt, ...) {
 }
 
 void note_launch() { g_launches.fetch_add(1, std::memory_order_relaxed); }
+void note_sync() { g_syncs.fetch_add(1, std::memory_order_relaxed); }
 
 struct Stage {
   double *p = nullptr;
@@ -87,6 +89,7 @@ extern "C" {
 const char *ttk_last_error(void) { return ttk::g_err; }
 int ttk_version(void) { return 1; }
 long long ttk_launch_count(void) { return ttk::g_launches.load(); }
+long long ttk_sync_count(void) { return ttk::g_syncs.load(); }
 
 int ttk_upload(void *stream, const double *host, double *dev, int64_t n) {
   if (n <= 0) return TTK_OK;
@@ -124,6 +127,7 @@ int ttk_read_sync(void *stream, const double *src, double *host_dst, int64_t n) 
       const int grid = (int)((n + 255) / 256 < 64 ? (n + 255) / 256 : 64);
       hipLaunchKernelGGL(to_host_kernel, dim3(grid), dim3(256), 0, TTK_STREAM(stream), src, n, dev);
       TTK_LAUNCH_CHECK();
+      ttk::note_sync();
       TTK_HIP(hipStreamSynchronize(TTK_STREAM(stream)));
       std::memcpy(host_dst, h, n * sizeof(double));
       return TTK_OK;
@@ -135,6 +139,7 @@ int ttk_read_sync(void *stream, const double *src, double *host_dst, int64_t n) 
     return TTK_ERR_HIP;
   }
   TTK_HIP(hipMemcpyAsync(st, src, n * sizeof(double), hipMemcpyDeviceToHost, TTK_STREAM(stream)));
+  ttk::note_sync();
   TTK_HIP(hipStreamSynchronize(TTK_STREAM(stream)));
   std::memcpy(host_dst, st, n * sizeof(double));
   return TTK_OK;

@@ -261,6 +261,12 @@ def rayleigh_tail_(v, Mv):
     return ev.value, float(np.sqrt(max(r2.value, 0.0)))
 
 
+def rayleigh_tail_into(v, Mv, out2):
+    """ev = <v, Mv>; Mv -= ev v; (ev, ||Mv||^2) -> device out2 (2 doubles), no host wait."""
+    assert v.is_contiguous() and Mv.is_contiguous() and v.numel() == Mv.numel() and out2.is_contiguous()
+    check(lib.ttk_rayleigh_tail_dev(_stream(), _p(v), _p(Mv), v.numel(), _p(out2)), "rayleigh_tail_dev")
+
+
 def recip(src):
     src = src.contiguous()
     out = empty(*src.shape)

@@ -254,6 +254,48 @@ def lobpcg(A, x0, B=None, tol=1e-8, maxiter=20, largest=True, restart_control=20
     return lam, best
 
 
+class _Deferred:
+    """Local residuals of one eigen-ALS half-sweep kept on the device: each dense local solve's
+    Rayleigh tail writes (ev, ||r||^2) into a slot; the sweep only needs the residuals in
+    np.max(local_res) after the half-sweep, so they are read there in ONE host wait instead of one
+    per local solve (same values: the kernel is the one ttk_rayleigh_tail_sync runs)."""
+
+    def __init__(self, cap):
+        self.buf = D.empty(2 * max(cap, 1))
+        self.n = 0
+        self.pending = []  # (row, col, slot)
+
+    def rayleigh(self, Am, Dm, step, v):
+        M = _shifted(Am, Dm, step)
+        Mv = D.matmul(M, v.view(-1, 1)).view(-1)
+        if self.n * 2 + 2 > self.buf.numel():
+            return _rayleigh(Am, Dm, step, v)[1]
+        D.rayleigh_tail_into(v, Mv, self.buf[2 * self.n:2 * self.n + 2])
+        self.n += 1
+        return _Slot(self.n - 1)
+
+    def put(self, arr, i, j, res):
+        if isinstance(res, _Slot):
+            self.pending.append((i, j, res.k))
+        else:
+            arr[i, j] = res
+
+    def resolve(self, arr):
+        if self.pending:
+            h = D.read(self.buf[:2 * self.n])
+            for i, j, k in self.pending:
+                arr[i, j] = float(np.sqrt(max(h[2 * k + 1], 0.0)))
+        self.pending, self.n = [], 0
+
+
+class _Slot:
+    def __init__(self, k):
+        self.k = k
+
+
+_DEFER = [None]  # the active _Deferred of tt_max_generalised_eigen's sweep, or "skip" (residual unused)
+
+
 def _dense_step(prev, Am, Dm, step, eps, tag):
     """dense branch of the step-size local solves: M = A/step + D, smallest eigenpair; if negative,
     the largest lambda of -D v = lambda A v bounds the step (`src/tt_als.py:957-996,1060-1101`)."""
@@ -273,6 +315,12 @@ def _dense_step(prev, Am, Dm, step, eps, tag):
             branch = f"fail {type(e).__name__}"
     if _DEBUG:
         print(f"  dev {tag} m={prev.numel()} ev={ev:.6e} step {step_in:.12e} -> {step:.12e} {branch}")
+    df = _DEFER[0] if _FUSED_TAIL and prev.is_contiguous() else None
+    if df == "skip":  # the caller discards the residual: only its 1/step (ZeroDivisionError at 0) matters
+        1.0 / step
+        return sol, step, None
+    if df is not None:
+        return sol, step, df.rayleigh(Am, Dm, step, prev)
     old_res = _rayleigh(Am, Dm, step, prev)[1]  # 1/step raises ZeroDivisionError at step 0, as the reference
     return sol, step, old_res
 
@@ -409,6 +457,7 @@ def tt_max_generalised_eigen(A, Delta, x0=None, nswp=10, tol=1e-8, size_limit=25
 
     def finish_fwd():
         nonlocal step
+        _DEFER[0] = "skip"  # the last local solves' residuals are discarded
         for k in range(d):
             sol, step, _ = _step_size_local_solve_last(x[k], XDX[k], Delta[k], XDX[k + 1], XAX[k], A[k], XAX[k + 1],
                                                        np.sqrt(rx[k] * rx[k + 1]) < size_limit, step, tol)
@@ -428,6 +477,7 @@ def tt_max_generalised_eigen(A, Delta, x0=None, nswp=10, tol=1e-8, size_limit=25
 
     def finish_bck():
         nonlocal step
+        _DEFER[0] = "skip"  # the last local solves' residuals are discarded
         for k in range(d - 1, -1, -1):
             sol, step, _ = _step_size_local_solve_last(x[k], XDX[k], Delta[k], XDX[k + 1], XAX[k], A[k], XAX[k + 1],
                                                        np.sqrt(rx[k] * rx[k + 1]) < size_limit, step, tol)
@@ -445,59 +495,66 @@ def tt_max_generalised_eigen(A, Delta, x0=None, nswp=10, tol=1e-8, size_limit=25
             else:
                 x[k] = D.contig(sol).view(rx[k], N[k], rx[k + 1])
 
-    for swp in range(nswp):
-        zero = False
-        for k in range(d - 1, 0, -1):
-            if swp > 0:
-                x[k - 1], x[k], step, res = _step_size_local_solve(
-                    x[k - 1], x[k], XAX[k - 1], A[k - 1], A[k], XAX[k + 1], XDX[k - 1], Delta[k - 1], Delta[k],
-                    XDX[k + 1], step, size_limit, trunc_tol, tol, max_rank, bwd=True)
-                local_res[0, k - 1] = res
+    dfr = _Deferred(d)
+    _DEFER[0] = dfr
+    try:
+        for swp in range(nswp):
+            zero = False
+            for k in range(d - 1, 0, -1):
+                if swp > 0:
+                    x[k - 1], x[k], step, res = _step_size_local_solve(
+                        x[k - 1], x[k], XAX[k - 1], A[k - 1], A[k], XAX[k + 1], XDX[k - 1], Delta[k - 1], Delta[k],
+                        XDX[k + 1], step, size_limit, trunc_tol, tol, max_rank, bwd=True)
+                    dfr.put(local_res, 0, k - 1, res)
+                    if step <= 0:
+                        zero = True
+                        break
+                else:
+                    x[k], vr, r = _svd_left(x, k, rx, N, trunc_tol, max_rank)
+                    x[k - 1] = einsum("rdc,Rc->rdR", x[k - 1], vr)
+                rx[k] = x[k].shape[0]
+                XAX[k] = compute_phi_bck_A(XAX[k + 1], x[k], A[k], x[k])
+                XDX[k] = compute_phi_bck_A(XDX[k + 1], x[k], Delta[k], x[k])
+            dfr.resolve(local_res)
+            if zero:
+                if verbose:
+                    print("\tStep size reached zero; stopping eigen sweeps.", flush=True)
+                break
+            if np.max(local_res) < tol or swp == nswp - 1:
+                finish_fwd()
+                break
+            if verbose:
+                print('\tStarting Sweep: %d' % swp)
+                print('\tStep size: %f' % step)
+                print(f'\tResidual {np.max(local_res[0])}')
+            for k in range(d - 1):
+                x[k], x[k + 1], step, res = _step_size_local_solve(
+                    x[k], x[k + 1], XAX[k], A[k], A[k + 1], XAX[k + 2], XDX[k], Delta[k], Delta[k + 1], XDX[k + 2],
+                    step, size_limit, trunc_tol, tol, max_rank, bwd=False)
+                dfr.put(local_res, 1, k, res)
                 if step <= 0:
                     zero = True
                     break
-            else:
-                x[k], vr, r = _svd_left(x, k, rx, N, trunc_tol, max_rank)
-                x[k - 1] = einsum("rdc,Rc->rdR", x[k - 1], vr)
-            rx[k] = x[k].shape[0]
-            XAX[k] = compute_phi_bck_A(XAX[k + 1], x[k], A[k], x[k])
-            XDX[k] = compute_phi_bck_A(XDX[k + 1], x[k], Delta[k], x[k])
-        if zero:
-            if verbose:
-                print("\tStep size reached zero; stopping eigen sweeps.", flush=True)
-            break
-        if np.max(local_res) < tol or swp == nswp - 1:
-            finish_fwd()
-            break
-        if verbose:
-            print('\tStarting Sweep: %d' % swp)
-            print('\tStep size: %f' % step)
-            print(f'\tResidual {np.max(local_res[0])}')
-        for k in range(d - 1):
-            x[k], x[k + 1], step, res = _step_size_local_solve(
-                x[k], x[k + 1], XAX[k], A[k], A[k + 1], XAX[k + 2], XDX[k], Delta[k], Delta[k + 1], XDX[k + 2],
-                step, size_limit, trunc_tol, tol, max_rank, bwd=False)
-            local_res[1, k] = res
-            if step <= 0:
-                zero = True
+                rx[k + 1] = x[k + 1].shape[0]
+                XAX[k + 1] = compute_phi_fwd_A(XAX[k], x[k], A[k], x[k])
+                XDX[k + 1] = compute_phi_fwd_A(XDX[k], x[k], Delta[k], x[k])
+            dfr.resolve(local_res)
+            if zero:
+                if verbose:
+                    print("\tStep size reached zero; stopping eigen sweeps.", flush=True)
                 break
-            rx[k + 1] = x[k + 1].shape[0]
-            XAX[k + 1] = compute_phi_fwd_A(XAX[k], x[k], A[k], x[k])
-            XDX[k + 1] = compute_phi_fwd_A(XDX[k], x[k], Delta[k], x[k])
-        if zero:
-            if verbose:
-                print("\tStep size reached zero; stopping eigen sweeps.", flush=True)
-            break
-        if np.max(local_res) < tol:
-            finish_bck()
-            break
-        sres = np.max(local_res)
-        if swp >= 2 and _step_stalled(prev_step, step, prev_res, sres, tol):
-            if verbose:
-                print("\tEigen sweep stalled; stopping early.", flush=True)
-            break
-        prev_step = step
-        prev_res = sres
+            if np.max(local_res) < tol:
+                finish_bck()
+                break
+            sres = np.max(local_res)
+            if swp >= 2 and _step_stalled(prev_step, step, prev_res, sres, tol):
+                if verbose:
+                    print("\tEigen sweep stalled; stopping early.", flush=True)
+                break
+            prev_step = step
+            prev_res = sres
+    finally:
+        _DEFER[0] = None
     max_res = np.max(local_res)
     x = T.tt_normalise(x)
     if verbose:

@@ -221,6 +221,14 @@ class EmuLib:
         r2_out._obj.value = float(np.dot(b, b))
         return 0
 
+    def ttk_rayleigh_tail_dev(self, s, v, Mv, n, out2):
+        self.launches += 1
+        a, b = _dv(v, n), _dv(Mv, n)
+        ev = float(np.dot(a, b))
+        b[:] = -ev * a + b
+        _dv(out2, 2)[:] = (ev, float(np.dot(b, b)))
+        return 0
+
     def ttk_recip(self, s, src, dst, n):
         _dv(dst, n)[:] = 1.0 / _dv(src, n)
         return 0
