@@ -689,12 +689,12 @@ __device__ void apply_row_mfma(const ApplyArgs &g, int a, double *sm, double *or
   }
 }
 
-__global__ __launch_bounds__(256) void fused_apply_mfma_kernel(ApplyArgs g) {
+__global__ __launch_bounds__(1024) void fused_apply_mfma_kernel(ApplyArgs g) {
   extern __shared__ double sm[];
   apply_row_mfma<true>(g, blockIdx.x, sm, nullptr);
 }
 
-__global__ __launch_bounds__(256) void fused_apply_kernel(ApplyArgs g) {
+__global__ __launch_bounds__(1024) void fused_apply_kernel(ApplyArgs g) {
   extern __shared__ double sm[];
   apply_row<true>(g, blockIdx.x, sm, nullptr);
 }
@@ -714,7 +714,7 @@ struct ApplyLaunch {
   int off[4];
 };
 
-__global__ __launch_bounds__(256) void fused_apply_multi_kernel(ApplyLaunch L) {
+__global__ __launch_bounds__(1024) void fused_apply_multi_kernel(ApplyLaunch L) {
   extern __shared__ double sm[];
   int t = 0;
   while (t + 1 < L.ntask && (int)blockIdx.x >= L.off[t + 1]) ++t;
@@ -767,6 +767,10 @@ static double fused_max_flops() {
 // MFMA stages for the blocks beyond the VALU kernel's FLOP range (TTK_FUSED_MFMA=0: pairwise plan)
 static int g_fused_mfma = !getenv("TTK_FUSED_MFMA") || atoi(getenv("TTK_FUSED_MFMA")) != 0;
 static bool mfma_enabled() { return g_fused_mfma != 0; }
+// threads per workgroup of launches that carry MFMA-stage rows: the staging loops gather x, Q and A
+// from L2 with one workgroup per CU (LDS-bound occupancy), so 16 waves keep 4x the loads in flight of
+// 4; every output element / tile is still computed by one thread / wave in the same order
+static const int g_mfma_threads = getenv("TTK_MFMA_THREADS") ? atoi(getenv("TTK_MFMA_THREADS")) : 1024;
 
 extern "C" int ttk_fused_set_mfma(int on) {
   const int old = g_fused_mfma;
@@ -875,7 +879,8 @@ int fused_apply_try(void *stream, const char *eq, const int64_t *desc, double *o
   hipEvent_t e0, e1;
   if (ttk::contract_events_ext(&e0, &e1) != TTK_OK) return -1;
   if (g.mfma)
-    hipExtLaunchKernelGGL(fused_apply_mfma_kernel, dim3(g.na), dim3(256), shm, TTK_STREAM(stream), e0, e1, 0, g);
+    hipExtLaunchKernelGGL(fused_apply_mfma_kernel, dim3(g.na), dim3(g_mfma_threads), shm, TTK_STREAM(stream), e0, e1, 0,
+                          g);
   else
     hipExtLaunchKernelGGL(fused_apply_kernel, dim3(g.na), dim3(256), shm, TTK_STREAM(stream), e0, e1, 0, g);
   TTK_LAUNCH_CHECK();
@@ -1121,8 +1126,11 @@ int ttk_schur_apply(void *stream, int64_t handle, const double *v, double *out) 
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)op.shm[s]);
     hipEvent_t e0, e1;
     if (ttk::contract_events_ext(&e0, &e1) != TTK_OK) return TTK_ERR_HIP;
-    hipExtLaunchKernelGGL(fused_apply_multi_kernel, dim3(L.off[L.ntask]), dim3(256), op.shm[s], TTK_STREAM(stream),
-                          e0, e1, 0, L);
+    bool mf = false;
+    for (int t = 0; t < L.ntask; ++t)
+      for (int k = 0; k < L.task[t].nterms; ++k) mf = mf || L.task[t].t[k].mfma;
+    hipExtLaunchKernelGGL(fused_apply_multi_kernel, dim3(L.off[L.ntask]), dim3(mf ? g_mfma_threads : 256), op.shm[s],
+                          TTK_STREAM(stream), e0, e1, 0, L);
     TTK_LAUNCH_CHECK();
   }
   ttk::contract_count_ext(op.flops);
@@ -1184,7 +1192,7 @@ struct FusedGroup {
   int n;
 };
 
-__global__ __launch_bounds__(256) void fused_apply_group_kernel(FusedGroup G) {
+__global__ __launch_bounds__(1024) void fused_apply_group_kernel(FusedGroup G) {
   extern __shared__ double sm[];
   int t = 0;
   while (t + 1 < G.n && (int)blockIdx.x >= G.off[t + 1]) ++t;
@@ -1225,9 +1233,11 @@ int launch_fused_group(hipStream_t st, const std::vector<const BNode *> &v) {
     G.off[0] = 0;
     int64_t lds = 0;
     double flops = 0.0;
+    bool mf = false;
     for (int i = 0; i < G.n; ++i) {
       const BNode &n = *v[base + i];
       G.t[i] = n.f;
+      mf = mf || n.f.mfma;
       G.off[i + 1] = G.off[i] + n.f.na;
       lds = n.lds > lds ? n.lds : lds;
       flops += term_flops(n.f);
@@ -1238,7 +1248,8 @@ int launch_fused_group(hipStream_t st, const std::vector<const BNode *> &v) {
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
     hipEvent_t e0, e1;
     if (ttk::contract_events_ext(&e0, &e1) != TTK_OK) return TTK_ERR_HIP;
-    hipExtLaunchKernelGGL(fused_apply_group_kernel, dim3(G.off[G.n]), dim3(256), shm, st, e0, e1, 0, G);
+    hipExtLaunchKernelGGL(fused_apply_group_kernel, dim3(G.off[G.n]), dim3(mf ? g_mfma_threads : 256), shm, st, e0, e1,
+                          0, G);
     TTK_LAUNCH_CHECK();
     ttk::contract_count_ext(flops);
     ++cur_batch().launches;
