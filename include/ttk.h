@@ -101,6 +101,9 @@ int ttk_einsum(void *stream, const char *eq, const int64_t *desc, double *out, d
  * stages on fp64 MFMA in one launch (one workgroup per output row) when they fit LDS; off: the
  * pairwise plan.  Returns the previous setting (default on; env TTK_FUSED_MFMA=0 turns it off). */
 int ttk_fused_set_mfma(int on);
+/* diagnostics: per-phase wall-clock sums (100 MHz ticks) of the MFMA rows in a -DTTK_MFMA_PROFILE
+ * build: [staging, stage 1, stage 2, stage 3, epilogue, -, -, rows]; zeros otherwise */
+int ttk_mfma_profile(unsigned long long *out8, int reset);
 
 int ttk_einsum_batch_begin(void *stream);
 int ttk_einsum_batch_flush(void *stream);

@@ -82,6 +82,7 @@ _SIGS = {
     "ttk_round": (i32, [vp, i32, vp, vp, vp, f64, i32, vp]),
     "ttk_dense_schur_solve": (i32, [vp, i64, i64, i64, vp, vp, vp, vp, vp]),
     "ttk_fused_set_mfma": (i32, [i32]),
+    "ttk_mfma_profile": (i32, [vp, i32]),
     "ttk_einsum_set_fused": (i32, [i32]),
     "ttk_qr_set_big_threshold": (i32, [i32]),
     "ttk_contract_timing": (i32, [i32]),

@@ -628,8 +628,25 @@ int64_t apply_mfma_lds(const ApplyArgs &g) {
          (int64_t)g.ns * g.nj * g.nd + (int64_t)g.ni * g.nS * g.nd + QCHUNK_MAX + (int64_t)g.ni * g.nc;
 }
 
+// diagnostics build (-DTTK_MFMA_PROFILE): per-phase wall clock of the MFMA rows, summed by thread 0
+__device__ unsigned long long g_mph[8];
+#ifdef TTK_MFMA_PROFILE
+#define TTK_MPH(K)                                      \
+  if (threadIdx.x == 0) {                               \
+    const unsigned long long t1_ = wall_clock64();      \
+    atomicAdd(&g_mph[K], t1_ - t_ph_);                  \
+    t_ph_ = t1_;                                        \
+  }
+#else
+#define TTK_MPH(K)
+#endif
+
 template <bool DIRECT>
 __device__ void apply_row_mfma(const ApplyArgs &g, int a, double *sm, double *orow) {
+#ifdef TTK_MFMA_PROFILE
+  unsigned long long t_ph_ = wall_clock64();
+  if (threadIdx.x == 0) atomicAdd(&g_mph[7], 1ull);
+#endif
   const int tid = threadIdx.x, nt = blockDim.x;
   const int nb = g.nb, nj = g.nj, nd = g.nd, nS = g.nS, ns = g.ns, ni = g.ni, nc = g.nc;
   const int jd = nj * nd, sj = ns * nj;
@@ -652,14 +669,17 @@ __device__ void apply_row_mfma(const ApplyArgs &g, int a, double *sm, double *or
     As[e] = g.A[s_ * g.as[0] + i * g.as[1] + j * g.as[2] + S * g.as[3]];
   }
   __syncthreads();
+  TTK_MPH(0)
   // stage 1: T1[s][(j,d)] = sum_b Pa[s][b] X[b][(j,d)]
   wg_mfma(ns, jd, nb, [&](int m, int k) { return Pa[m * nb + k]; }, [&](int k, int n) { return X[k * jd + n]; },
           [&](int m, int n, double v) { T1[m * jd + n] = v; });
   __syncthreads();
+  TTK_MPH(1)
   // stage 2: T2[(i,S)][d] = sum_{(s,j)} As[(i,S)][(s,j)] T1[(s,j)][d]
   wg_mfma(ni * nS, nd, sj, [&](int m, int k) { return As[m * sj + k]; }, [&](int k, int n) { return T1[k * nd + n]; },
           [&](int m, int n, double v) { T2[m * nd + n] = v; });
   __syncthreads();
+  TTK_MPH(2)
   // stage 3: out[i][c] = sum_{(S,d)} T2[(i,S)][d] Q[c,S,d] -- K = (S,d) flattened (row i of T2 is
   // contiguous over it), blocked so a [c][k] chunk of Q fits QCHUNK_MAX doubles of LDS
   const int K3 = nS * nd;
@@ -680,6 +700,7 @@ __device__ void apply_row_mfma(const ApplyArgs &g, int a, double *sm, double *or
             [&](int m, int n, double v) { acc[m * nc + n] = first ? v : acc[m * nc + n] + v; });
     __syncthreads();
   }
+  TTK_MPH(3)
   if (DIRECT) {
     for (int e = tid; e < ni * nc; e += nt) {
       const int i = e / nc, c = e - i * nc;
@@ -687,6 +708,7 @@ __device__ void apply_row_mfma(const ApplyArgs &g, int a, double *sm, double *or
       *o = g.beta != 0.0 ? g.alpha * acc[e] + g.beta * *o : g.alpha * acc[e];
     }
   }
+  TTK_MPH(4)
 }
 
 __global__ __launch_bounds__(1024) void fused_apply_mfma_kernel(ApplyArgs g) {
@@ -771,6 +793,15 @@ static bool mfma_enabled() { return g_fused_mfma != 0; }
 // from L2 with one workgroup per CU (LDS-bound occupancy), so 16 waves keep 4x the loads in flight of
 // 4; every output element / tile is still computed by one thread / wave in the same order
 static const int g_mfma_threads = getenv("TTK_MFMA_THREADS") ? atoi(getenv("TTK_MFMA_THREADS")) : 1024;
+
+extern "C" int ttk_mfma_profile(unsigned long long *out8, int reset) {  // g_mph (zeros unless profiled)
+  if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_mph), 8 * sizeof(unsigned long long)) != hipSuccess) return TTK_ERR_HIP;
+  if (reset) {
+    const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_mph), z, sizeof(z)) != hipSuccess) return TTK_ERR_HIP;
+  }
+  return TTK_OK;
+}
 
 extern "C" int ttk_fused_set_mfma(int on) {
   const int old = g_fused_mfma;
