@@ -622,6 +622,87 @@ __device__ __forceinline__ void wg_mfma(int M, int N, int K, FA fa, FB fb, FC fc
 
 constexpr int QCHUNK_MAX = 4096;  // doubles of Q staged per stage-3 K block ([c][k], k = (S,d) range)
 
+// Mixed-radix index (digit 0 most significant) of e = start + q * stride, advanced by one stride per
+// step with single carries (each digit of the stride is below its radix)
+template <int N>
+struct MixedIdx {
+  int v[N], st[N];
+  __device__ MixedIdx(int e, int de, const int *rad) {
+#pragma unroll
+    for (int k = N - 1; k > 0; --k) {
+      v[k] = e % rad[k];
+      e /= rad[k];
+      st[k] = de % rad[k];
+      de /= rad[k];
+    }
+    v[0] = e;
+    st[0] = de;
+  }
+  __device__ __forceinline__ void step(const int *rad) {
+    int c = 0;
+#pragma unroll
+    for (int k = N - 1; k > 0; --k) {
+      v[k] += st[k] + c;
+      c = v[k] >= rad[k];
+      if (c) v[k] -= rad[k];
+    }
+    v[0] += st[0] + c;
+  }
+};
+
+// One 16x16 tile of stage 3 over one K block [kbeg, kbeg + w): the same MFMA sequence as wg_mfma
+// (even / odd 8-steps into two accumulators, a 4-step tail, the sum acc0 + acc1 returned) with the B
+// operand Q[c, S, d] read straight from global memory: every Q element is used by exactly one MFMA of
+// the workgroup (all M = ni rows sit in one tile), so staging it through LDS buys no reuse.  Lane
+// (n = lane & 15, kl = lane >> 4) consumes Q at k = kbeg + kl + 4v for v = 0, 1, ... in order, so the
+// (S, d) digits advance incrementally and 8 values are loaded one batch ahead of the MFMAs.
+template <class FA>
+__device__ __forceinline__ dbl4 stage3_tile(FA fa, const double *qrow, int64_t qs1, int64_t qs2, int nd, int kbeg,
+                                             int w, bool mok, bool nok, int am, int kl) {
+  int kabs = kbeg + kl, S = kabs / nd, d = kabs - S * nd, kv = kl;
+  auto next = [&]() -> double {
+    const double v = (nok && kv < w) ? qrow[S * qs1 + d * qs2] : 0.0;
+    kv += 4;
+    d += 4;
+    while (d >= nd) { d -= nd; ++S; }
+    return v;
+  };
+  dbl4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+  const int nfull = w >> 3;
+  double bb[8], nb[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) bb[u] = next();
+  for (int it = 0; it < nfull; it += 4) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) nb[u] = next();
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (it + u < nfull) {
+        const int k0 = (it + u) << 3;
+        const double a0 = mok ? fa(am, k0 + kl) : 0.0, a1 = mok ? fa(am, k0 + 4 + kl) : 0.0;
+        acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, bb[2 * u], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, bb[2 * u + 1], acc1, 0, 0, 0);
+      }
+    }
+    if (it + 4 <= nfull) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) bb[u] = nb[u];
+    }
+  }
+  // tail: 4-steps at k0 = 8 * nfull (+ 4); their values follow the last batch's used ones in bb
+  // (a partial last batch used 2 * (nfull % 4) <= 6 of them), picked without dynamic indexing
+  const int base = (nfull & 3) << 1;
+  for (int k0 = nfull << 3, t = base; k0 < w; k0 += 4, ++t) {
+    const int k = k0 + kl;
+    const double a0 = (mok && k < w) ? fa(am, k) : 0.0;
+    double b0 = bb[0];
+#pragma unroll
+    for (int u = 1; u < 8; ++u) b0 = t == u ? bb[u] : b0;
+    acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc0, 0, 0, 0);
+  }
+  return acc0 + acc1;
+}
+
 int64_t apply_mfma_lds(const ApplyArgs &g) {
   if (g.nc > QCHUNK_MAX / 4) return INT64_MAX;  // stage 3 needs K blocks of >= 4
   return (int64_t)g.nb * g.nj * g.nd + (int64_t)g.ns * g.nb + (int64_t)g.ni * g.nS * g.ns * g.nj +
@@ -656,17 +737,21 @@ __device__ void apply_row_mfma(const ApplyArgs &g, int a, double *sm, double *or
   double *T1 = As + ni * nS * sj;       // [(s,j)][d]
   double *T2 = T1 + sj * nd;            // [(i,S)][d]
   double *Qc = T2 + ni * nS * nd;       // [c][k], QCHUNK_MAX
-  for (int e = tid; e < nb * jd; e += nt) {
-    const int b = e / jd, r = e - b * jd, j = r / nd, d = r - j * nd;
-    X[e] = g.x[b * g.xs[0] + j * g.xs[1] + d * g.xs[2]];
+  {  // staging: the gathers' multi-digit indices advance by carries instead of divisions
+    const int rx[3] = {nb, nj, nd};
+    MixedIdx<3> ix(tid, nt, rx);
+    for (int e = tid; e < nb * jd; e += nt, ix.step(rx))
+      X[e] = g.x[ix.v[0] * g.xs[0] + ix.v[1] * g.xs[1] + ix.v[2] * g.xs[2]];
   }
   for (int e = tid; e < ns * nb; e += nt) {
     const int s_ = e / nb, b = e - s_ * nb;
     Pa[e] = g.P[a * g.ps[0] + s_ * g.ps[1] + b * g.ps[2]];
   }
-  for (int e = tid; e < ni * nS * sj; e += nt) {
-    const int m = e / sj, k = e - m * sj, i = m / nS, S = m - i * nS, s_ = k / nj, j = k - s_ * nj;
-    As[e] = g.A[s_ * g.as[0] + i * g.as[1] + j * g.as[2] + S * g.as[3]];
+  {
+    const int ra[4] = {ni, nS, ns, nj};  // As[(i,S)][(s,j)]
+    MixedIdx<4> ia(tid, nt, ra);
+    for (int e = tid; e < ni * nS * sj; e += nt, ia.step(ra))
+      As[e] = g.A[ia.v[2] * g.as[0] + ia.v[0] * g.as[1] + ia.v[3] * g.as[2] + ia.v[1] * g.as[3]];
   }
   __syncthreads();
   TTK_MPH(0)
@@ -687,6 +772,42 @@ __device__ void apply_row_mfma(const ApplyArgs &g, int a, double *sm, double *or
   kc = kc >= 8 ? (kc & ~7) : kc;
   kc = kc > K3 ? K3 : kc;
   double *acc = DIRECT ? Qc + QCHUNK_MAX : orow;  // DIRECT: partial sums after the Q chunk
+  const int nio = ni * nc;
+  if (nio <= QCHUNK_MAX) {
+    // (tile, K block) pairs spread over all waves (M = ni ~ 4 gives only nc/16 tiles), Q read from
+    // global memory; each pair's block sum goes to part[block][i][c] (the Q chunk's LDS), then the
+    // blocks are summed in K order -- the same additions as the sequential loop below
+    const int lane = tid & 63, wid = tid >> 6, nw = nt >> 6, kl = lane >> 4;
+    const int tn = (nc + 15) >> 4, ntile = ((ni + 15) >> 4) * tn;
+    const int nch = (K3 + kc - 1) / kc, gch = QCHUNK_MAX / nio;
+    double *part = Qc;
+    for (int c0 = 0; c0 < nch; c0 += gch) {
+      const int ng = nch - c0 < gch ? nch - c0 : gch;
+      for (int t = wid; t < ntile * ng; t += nw) {
+        const int tile = t % ntile, ch = c0 + t / ntile;
+        const int m0 = (tile / tn) << 4, n0 = (tile % tn) << 4;
+        const int am = m0 + (lane & 15), bn = n0 + (lane & 15);
+        const bool mok = am < ni, nok = bn < nc;
+        const int k0 = ch * kc, w = k0 + kc < K3 ? kc : K3 - k0;
+        const double *T2k = T2 + k0;
+        const dbl4 v = stage3_tile([&](int m, int k) { return T2k[m * K3 + k]; }, g.Q + (int64_t)(nok ? bn : 0) * g.qs[0],
+                                   g.qs[1], g.qs[2], nd, k0, w, mok, nok, am, kl);
+        double *pp = part + (ch - c0) * nio;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = m0 + (lane >> 4) + 4 * r;
+          if (row < ni && nok) pp[row * nc + bn] = v[r];
+        }
+      }
+      __syncthreads();
+      for (int e = tid; e < nio; e += nt) {
+        double s = c0 == 0 ? part[e] : acc[e] + part[e];
+        for (int j = 1; j < ng; ++j) s = s + part[j * nio + e];
+        acc[e] = s;
+      }
+      __syncthreads();
+    }
+  } else
   for (int k0 = 0; k0 < K3; k0 += kc) {
     const int w = k0 + kc < K3 ? kc : K3 - k0;
     for (int e = tid; e < nc * w; e += nt) {

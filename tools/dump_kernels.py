@@ -31,6 +31,43 @@ def main(path):
         b = torch.randn(K_, N_, dtype=torch.float64, device="cuda", generator=torch.Generator("cuda").manual_seed(N_))
         out[f"mm_{M_}_{N_}_{K_}"] = D.read(D.matmul(a, b))
         out[f"mmT_{M_}_{N_}_{K_}"] = D.read(D.matmul(b.t(), a.t()))
+    # LU with the dgecon estimate (getrf + lu_rcond_kernel) and getrs
+    import ctypes
+    for n in (40, 300, 1000, 2100, 4000):
+        M = rng.standard_normal((n, n)) + np.diag(np.linspace(0.0, 3.0, n))
+        A = D.from_numpy(M)
+        piv = torch.empty(n, dtype=torch.int32, device="cuda")
+        work = D.empty(2 * n + 16)
+        rc = ctypes.c_double(0.0)
+        D.check(lib.ttk_lu_sync(st, D._p(A), n, D._p(piv), D._p(work), ctypes.byref(rc)), "lu")
+        b = D.from_numpy(rng.standard_normal((n, 3)))
+        D.lu_solve_(A, piv, b)
+        out[f"lu_{n}"] = D.read(A)
+        out[f"lu_rcond_{n}"] = np.array([rc.value])
+        out[f"lu_sol_{n}"] = D.read(b)
+    # MFMA local-apply rows (graphm-sized fused applies and environment updates)
+    from ttipm_amd import tt_als
+    old = lib.ttk_fused_set_mfma(1)
+    try:
+        for eq in ("lsr,smnS,LSR,rnR->lmL", "lsr,smnS,LSR,lmL->rnR"):
+            for shapes in ([(44, 10, 44), (10, 4, 4, 10), (44, 10, 44), (44, 4, 44)],
+                           [(30, 18, 25), (18, 4, 4, 9), (28, 9, 33), (25, 4, 33)],
+                           [(60, 12, 60), (12, 4, 4, 12), (60, 12, 60), (60, 4, 60)]):
+                P, A, Q = (rng.standard_normal(s) for s in shapes[:3])
+                x = rng.standard_normal(shapes[3] if eq.endswith("->lmL") else (P.shape[0], A.shape[1], Q.shape[0]))
+                ops = [D.from_numpy(o) for o in (P, A, Q, x)]
+                out[f"fused_{eq[-3:]}_{shapes[0]}"] = D.read(D.einsum(eq, *ops, fused=True))
+                o2 = D.from_numpy(np.ones(out[f"fused_{eq[-3:]}_{shapes[0]}"].shape))
+                D.einsum(eq, *ops, out=o2, alpha=0.5, beta=2.0, fused=True)
+                out[f"fusedab_{eq[-3:]}_{shapes[0]}"] = D.read(o2)
+        for backward, shapes in [(True, [(64, 3, 64), (78, 4, 64), (4, 4, 4, 3), (78, 4, 64)]),
+                                 (False, [(47, 5, 47), (47, 4, 97), (5, 4, 4, 4), (47, 4, 97)]),
+                                 (False, [(2, 12, 97), (2, 4, 2), (12, 4, 4, 13), (97, 4, 50)]),
+                                 (True, [(44, 10, 44), (44, 4, 44), (10, 4, 4, 10), (44, 4, 44)])]:
+            items = [tuple(D.from_numpy(rng.standard_normal(s)) for s in shapes)]
+            out[f"env_{backward}_{shapes[0]}"] = D.read(tt_als.env_update_many(backward, items)[0])
+    finally:
+        lib.ttk_fused_set_mfma(old)
     torch.cuda.synchronize()
     np.savez(path, **out)
     print("dumped", len(out), "arrays to", path)
