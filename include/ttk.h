@@ -385,6 +385,16 @@ typedef struct {
 int ttk_dense_schur_solve(ttk_ctx ctx, int64_t r, int64_t n, int64_t R, const ttk_local_block *blocks,
                           const double *rhs, const double *inv_I, double *sol, double *rcond_out);
 
+/* The inequality variant (the dense branch of `_ipm_local_solver_ineq`, src/tt_ipm.py:284-352):
+ * L_Z = B21 (Cholesky), L_Z^-1 L_X with L_X = B22, L_eq = B01, T_op = B31, the two Schur levels
+ * A = B00 + L_eq L_Z^-1 L_XI L_eq^T and D = B33 + T_op L_Z^-1 L_X + 1e-11 I, both LU-factored without
+ * a condition check (scipy lu_factor), then Y, T, Z, X back-substituted into sol (r, 4, n, R).
+ * blk: the blocks (0,0), (0,1), (2,1), (2,2), (3,1), (3,3) as for ttk_dense_schur_solve; rhs
+ * (r, 4, n, R) and inv_I (r, n, R) contiguous.  Status: TTK_OK, TTK_ERR_NOT_PD, TTK_ERR_SINGULAR
+ * (the reference's LinAlgError -> iterative fallback).  Same launches as the Python path. */
+int ttk_dense_schur_solve_ineq(ttk_ctx ctx, int64_t r, int64_t n, int64_t R, const ttk_local_block *blocks,
+                               const double *rhs, const double *inv_I, double *sol);
+
 #ifdef __cplusplus
 }
 #endif

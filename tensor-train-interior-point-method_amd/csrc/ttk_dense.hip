@@ -424,42 +424,78 @@ constexpr int TB = 32;  // diagonal block of the one-workgroup triangular solves
 // x[r] -= sum_p LU[r][b0+p] x[b0+p] for r in [r0, r1): half-waves own rows (32 lanes over the
 // block's columns, coalesced); beyond 4096 rows one thread per row
 __device__ __forceinline__ double row_dot(const double *__restrict__ a, const double *x, int bs);
-__device__ void rows_update(const double *__restrict__ LU, int n, double *x, int b0, int bs, int r0, int r1) {
+__device__ __forceinline__ void rows_update(const double *__restrict__ LU, int n, double *x, int b0, int bs, int r0, int r1) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, half = lane >> 5, hl = lane & 31;
   if (r1 - r0 > 4096) {
+#pragma unroll 1
     for (int r = r0 + tid; r < r1; r += 1024) x[r] -= row_dot(LU + (int64_t)r * n + b0, x + b0, bs);
     return;
   }
-  for (int r = r0 + 2 * wid + half; r < r1; r += 32) {  // two rows per wave, 32 lanes each
-    double v = hl < bs ? LU[(int64_t)r * n + b0 + hl] * x[b0 + hl] : 0.0;
+  // two rows per wave, 32 lanes each; a half-wave's next 4 rows are loaded before any is reduced
+  const double xv = hl < bs ? x[b0 + hl] : 0.0;
+  for (int r = r0 + 2 * wid + half; r < r1; r += 128) {
+    double a[4];
 #pragma unroll
-    for (int o = 16; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-    if (hl == 0) x[r] -= v;
+    for (int u = 0; u < 4; ++u) a[u] = (hl < bs && r + 32 * u < r1) ? LU[(int64_t)(r + 32 * u) * n + b0 + hl] : 0.0;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      double v = hl < bs ? a[u] * xv : 0.0;
+#pragma unroll
+      for (int o = 16; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+      if (hl == 0 && r + 32 * u < r1) x[r + 32 * u] -= v;
+    }
   }
 }
 
 // sum_p a[p] x[p] over one row segment (bs <= TB), loads issued ahead of the FMAs
 __device__ __forceinline__ double row_dot(const double *__restrict__ a, const double *x, int bs) {
-  double v[TB];
-#pragma unroll
-  for (int p = 0; p < TB; ++p) v[p] = p < bs ? a[p] : 0.0;
   double s0 = 0.0, s1 = 0.0;
 #pragma unroll
-  for (int p = 0; p < TB; p += 2) {
-    s0 = fma(v[p], p < bs ? x[p] : 0.0, s0);
-    s1 = fma(v[p + 1], p + 1 < bs ? x[p + 1] : 0.0, s1);
+  for (int h = 0; h < TB; h += TB / 2) {  // two halves: 16 loads in flight, no spills at 128 VGPRs
+    double v[TB / 2];
+#pragma unroll
+    for (int p = 0; p < TB / 2; ++p) v[p] = h + p < bs ? a[h + p] : 0.0;
+#pragma unroll
+    for (int p = 0; p < TB / 2; p += 2) {
+      s0 = fma(v[p], h + p < bs ? x[h + p] : 0.0, s0);
+      s1 = fma(v[p + 1], h + p + 1 < bs ? x[h + p + 1] : 0.0, s1);
+    }
   }
   return s0 + s1;
 }
 
+// sum_p a[p * lda] x[p] in p order (bs <= TB): the column segment is loaded before the FMA chain
+__device__ __forceinline__ double col_dot(const double *__restrict__ a, int lda, const double *x, int bs) {
+  double v = 0.0;
+#pragma unroll
+  for (int h = 0; h < TB; h += TB / 2) {
+    double c[TB / 2];
+#pragma unroll
+    for (int p = 0; p < TB / 2; ++p) c[p] = h + p < bs ? a[(int64_t)(h + p) * lda] : 0.0;
+#pragma unroll
+    for (int p = 0; p < TB / 2; ++p)
+      if (h + p < bs) v += c[p] * x[h + p];
+  }
+  return v;
+}
+
 // one workgroup (1024 threads): x (in LDS) <- A^-1 x (trans = 0) or A^-T x (trans = 1), with the
 // dgetrf factors LU (row-major n x n) and pivots (staged in LDS: the swap chain is serial)
-__device__ void lu_solve_blk(const double *__restrict__ LU, int n, const int *__restrict__ piv, double *x,
-                             int trans) {
+// perm / tmp (LDS, optional): the composed row permutation of the pivots (x_P[i] = x[perm[i]]) and an
+// n-double buffer, so the swaps become one parallel gather instead of the serial swap chain
+// (TRANS a template parameter and the body inlined: as a called function with a runtime flag the
+// unrolled blocks of both directions spilled ~600 bytes per lane to scratch)
+template <int TRANS>
+__device__ __forceinline__ void lu_solve_blk(const double *__restrict__ LU, int n, const int *__restrict__ piv,
+                                             double *x, const int *perm = nullptr, double *tmp = nullptr) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int half = lane >> 5, hl = lane & 31;
-  if (!trans) {
-    if (tid == 0)
+  if (!TRANS) {
+    if (perm) {
+      for (int i = tid; i < n; i += blockDim.x) tmp[i] = x[perm[i]];
+      __syncthreads();
+      for (int i = tid; i < n; i += blockDim.x) x[i] = tmp[i];
+    } else if (tid == 0)
       for (int i = 0; i < n; ++i) {
         const int p = piv[i];
         if (p != i) {
@@ -531,11 +567,9 @@ __device__ void lu_solve_blk(const double *__restrict__ LU, int n, const int *__
         if (half == 0 && hl < bs) x[b0 + hl] = xq;
       }
       __syncthreads();
-      for (int r = b0 + bs + tid; r < n; r += 1024) {  // one thread per row, coalesced over r
-        double v = 0.0;
-        for (int p = 0; p < bs; ++p) v += LU[(int64_t)(b0 + p) * n + r] * x[b0 + p];
-        x[r] -= v;
-      }
+#pragma unroll 1
+      for (int r = b0 + bs + tid; r < n; r += 1024)  // one thread per row, coalesced over r
+        x[r] -= col_dot(LU + (int64_t)b0 * n + r, n, x + b0, bs);
       __syncthreads();
     }
     for (int bend = n; bend > 0; bend -= TB) {  // L^T z = y (upper, unit)
@@ -553,14 +587,15 @@ __device__ void lu_solve_blk(const double *__restrict__ LU, int n, const int *__
         if (half == 0 && hl < bs) x[b0 + hl] = xq;
       }
       __syncthreads();
-      for (int r = tid; r < b0; r += 1024) {
-        double v = 0.0;
-        for (int p = 0; p < bs; ++p) v += LU[(int64_t)(b0 + p) * n + r] * x[b0 + p];
-        x[r] -= v;
-      }
+#pragma unroll 1
+      for (int r = tid; r < b0; r += 1024) x[r] -= col_dot(LU + (int64_t)b0 * n + r, n, x + b0, bs);
       __syncthreads();
     }
-    if (tid == 0)
+    if (perm) {  // the swaps in reverse order = the inverse permutation
+      for (int i = tid; i < n; i += blockDim.x) tmp[perm[i]] = x[i];
+      __syncthreads();
+      for (int i = tid; i < n; i += blockDim.x) x[i] = tmp[i];
+    } else if (tid == 0)
       for (int i = n - 1; i >= 0; --i) {
         const int p = piv[i];
         if (p != i) {
@@ -576,11 +611,24 @@ __device__ void lu_solve_blk(const double *__restrict__ LU, int n, const int *__
 // dgecon (1-norm) from the factors: colsum = column sums of |A| before factorisation
 __global__ __launch_bounds__(1024) void lu_rcond_kernel(const double *__restrict__ LU, int n, const int *gpiv,
                                                         const double *__restrict__ colsum, const int *status,
-                                                        double *rcond_out) {
+                                                        double *rcond_out, int use_perm) {
   extern __shared__ double xl[];
-  double *x = xl, *xs = xl + n;
-  int *piv = reinterpret_cast<int *>(xl + 2 * n);
+  double *x = xl, *xs = xl + n, *tmp = use_perm ? xl + 2 * n : nullptr;
+  int *piv = reinterpret_cast<int *>(xl + (use_perm ? 3 : 2) * n), *perm = use_perm ? piv + n : nullptr;
   for (int i = threadIdx.x; i < n; i += blockDim.x) piv[i] = gpiv[i];
+  if (use_perm) {  // compose the pivot swaps once for the up to 11 solves below
+    for (int i = threadIdx.x; i < n; i += blockDim.x) perm[i] = i;
+    __syncthreads();
+    if (threadIdx.x == 0)
+      for (int i = 0; i < n; ++i) {
+        const int p = piv[i];
+        if (p != i) {
+          const int t = perm[i];
+          perm[i] = perm[p];
+          perm[p] = t;
+        }
+      }
+  }
   __shared__ double red[16];
   __shared__ double rv[1024];
   __shared__ int ri[1024];
@@ -604,7 +652,7 @@ __global__ __launch_bounds__(1024) void lu_rcond_kernel(const double *__restrict
   __syncthreads();
   int jlast = -1;
   for (int iter = 0; iter < 5; ++iter) {
-    lu_solve_blk(LU, n, piv, x, 0);
+    lu_solve_blk<0>(LU, n, piv, x, perm, tmp);
     double s1 = 0.0;
     for (int i = tid; i < n; i += nt) s1 += fabs(x[i]);
     s1 = ttk::block_sum(s1, red);
@@ -616,7 +664,7 @@ __global__ __launch_bounds__(1024) void lu_rcond_kernel(const double *__restrict
     if (tid == 0) s_est = s1;
     for (int i = tid; i < n; i += nt) xs[i] = (x[i] >= 0.0) ? 1.0 : -1.0;
     __syncthreads();
-    lu_solve_blk(LU, n, piv, xs, 1);
+    lu_solve_blk<1>(LU, n, piv, xs, perm, tmp);
     double best = -1.0;
     int bi = 0;
     for (int i = tid; i < n; i += nt)
@@ -663,7 +711,7 @@ __global__ __launch_bounds__(1024) void lu_rcond_kernel(const double *__restrict
   }
   for (int i = tid; i < n; i += nt) x[i] = ((i & 1) ? -1.0 : 1.0) * (1.0 + (n > 1 ? (double)i / (n - 1) : 0.0));
   __syncthreads();
-  lu_solve_blk(LU, n, piv, x, 0);
+  lu_solve_blk<0>(LU, n, piv, x, perm, tmp);
   double s1 = 0.0;
   for (int i = tid; i < n; i += nt) s1 += fabs(x[i]);
   s1 = ttk::block_sum(s1, red);
@@ -683,7 +731,7 @@ __global__ __launch_bounds__(1024) void lu_solve_cols_kernel(const double *__res
   for (int i = tid; i < n; i += 1024) piv[i] = gpiv[i];
   for (int i = tid; i < n; i += 1024) xl[i] = B[(int64_t)i * ldb + c];
   __syncthreads();
-  lu_solve_blk(LU, n, piv, xl, 0);
+  lu_solve_blk<0>(LU, n, piv, xl);
   for (int i = tid; i < n; i += 1024) B[(int64_t)i * ldb + c] = xl[i];
 }
 
@@ -722,11 +770,14 @@ int lu_blocked(hipStream_t st, double *A, int n, int *piv, double *work, int *st
     k0 += kb;
   }
   if (want_rcond) {
-    const size_t shm = 2 * (size_t)n * sizeof(double) + (size_t)n * sizeof(int);
+    // x, xs (+ the permutation buffer and perm when they fit next to the kernel's static LDS)
+    const size_t shm_perm = 3 * (size_t)n * sizeof(double) + 2 * (size_t)n * sizeof(int);
+    const int use_perm = shm_perm <= 140000;
+    const size_t shm = use_perm ? shm_perm : 2 * (size_t)n * sizeof(double) + (size_t)n * sizeof(int);
     if (shm > 65536)
       (void)hipFuncSetAttribute(reinterpret_cast<const void *>(lu_rcond_kernel),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
-    hipLaunchKernelGGL(lu_rcond_kernel, dim3(1), dim3(1024), shm, st, A, n, piv, colsum, status, rcond);
+    hipLaunchKernelGGL(lu_rcond_kernel, dim3(1), dim3(1024), shm, st, A, n, piv, colsum, status, rcond, use_perm);
     TTK_LAUNCH_CHECK();
   }
   return TTK_OK;

@@ -211,6 +211,129 @@ int ttk_dense_schur_solve(ttk_ctx ctx, int64_t r, int64_t n, int64_t R, const tt
   return rc_;
 }
 
+int ttk_dense_schur_solve_ineq(ttk_ctx ctx, int64_t r, int64_t n, int64_t R, const ttk_local_block *blk,
+                               const double *rhs, const double *inv_I, double *sol) {
+  ttk::CtxScope scope(ctx);
+  hipStream_t st = ttk::ctx().stream;
+  const int64_t m = r * n * R;
+  if (r < 1 || n < 1 || R < 1 || !blk || !rhs || !inv_I || !sol || m > (1 << 20)) {
+    ttk::set_error("ttk_dense_schur_solve_ineq: bad arguments");
+    return TTK_ERR_ARG;
+  }
+  static const char *ASSEMBLE = "lsr,smnS,LSR->lmLrnR", *APPLY = "lsr,smnS,LSR,rnR->lmL",
+                    *APPLY_T = "lsr,smnS,LSR,lmL->rnR", *MATMUL = "ik,kj->ij";
+  enum { B00, B01, B21, B22, B31, B33 };
+  auto ops3 = [&](int b) {
+    const ttk_local_block &q = blk[b];
+    return std::make_tuple(v3(q.L, r, q.s, r),
+                           View{q.A, 4, {q.s, n, n, q.S}, {q.a_strides[0], q.a_strides[1], q.a_strides[2], q.a_strides[3]}},
+                           v3(q.R, R, q.S, R));
+  };
+  Scratch sc(st);
+  double *rp = sc.get(m), *rd = sc.get(m), *rc = sc.get(m), *rt = sc.get(m), *LZ = sc.get(m * m),
+         *LZ_rc = sc.get(m), *LZ_LX = sc.get(m * m), *Leq = sc.get(m * m), *Top = sc.get(m * m),
+         *LZ_LXI = sc.get(m * m), *w = sc.get(m), *u = sc.get(m), *v = sc.get(m), *Am = sc.get(m * m),
+         *T = sc.get(m * m), *Dm = sc.get(m * m), *TL = sc.get(m * m), *Top2 = sc.get(m * m), *Leq2 = sc.get(m * m),
+         *Dv = sc.get(m), *DT = sc.get(m * m), *y = sc.get(m), *t2 = sc.get(m), *t3 = sc.get(m),
+         *work = sc.get(2 * m + 16);
+  int *dpiv = reinterpret_cast<int *>(sc.get(m / 2 + 1)), *piv = reinterpret_cast<int *>(sc.get(m / 2 + 1));
+  for (double *p : {rp, rd, rc, rt, LZ, LZ_rc, LZ_LX, Leq, Top, LZ_LXI, w, u, v, Am, T, Dm, TL, Top2, Leq2, Dv, DT, y,
+                    t2, t3, work})
+    if (!p || !dpiv || !piv) {
+      ttk::set_error("ttk_dense_schur_solve_ineq: scratch allocation failed");
+      return TTK_ERR_HIP;
+    }
+  const int64_t sh3[3] = {r, n, R}, st_blk[3] = {4 * n * R, R, 1}, st_c[3] = {n * R, R, 1};
+  const int64_t mm[2] = {m, m}, s_mat[2] = {m, 1}, s_row[2] = {0, 1}, out1[2] = {1, 1}, outm[2] = {m, 1};
+  const View LeqT{Leq, 2, {m, m}, {1, m}};
+  auto col = [&](int j) { return rhs + j * n * R; };  // rhs[:, j] as (r, n, R) view, strides st_blk
+  auto dcopy = [&](double *dst, const double *src, int64_t len) {
+    return hipMemcpyAsync(dst, src, len * sizeof(double), hipMemcpyDeviceToDevice, st) ? TTK_ERR_HIP : TTK_OK;
+  };
+  auto assemble = [&](int b, double *out) {
+    auto [a, bb, c] = ops3(b);
+    return einsum(st, ASSEMBLE, {a, bb, c}, out);
+  };
+  auto fbsub = [&](double *B, int nrhs) {  // forward_backward_sub, src/tt_ipm.py:178-181
+    int e = ttk_trsm_lower(st, LZ, (int)m, B, nrhs, nrhs, 0);
+    return e ? e : ttk_trsm_lower(st, LZ, (int)m, B, nrhs, nrhs, 1);
+  };
+  int rc_ = TTK_OK;
+#define STEP(x)                   \
+  do {                            \
+    if (rc_ == TTK_OK) rc_ = (x); \
+  } while (0)
+  // the statement order of _ipm_local_solver_ineq's dense branch (src/tt_ipm.py:303-352)
+  STEP(assemble(B21, LZ));
+  if (rc_) return rc_;
+  rc_ = ttk_cholesky_sync(st, LZ, (int)m);
+  if (rc_) return rc_;  // TTK_ERR_NOT_PD: LinAlgError -> the caller's iterative fallback
+  STEP(ttk_copy_nd(st, col(0), rp, 3, sh3, st_blk, st_c, 1.0, 0.0));
+  STEP(ttk_copy_nd(st, col(1), rd, 3, sh3, st_blk, st_c, 1.0, 0.0));
+  STEP(ttk_copy_nd(st, col(2), rc, 3, sh3, st_blk, st_c, 1.0, 0.0));
+  STEP(ttk_copy_nd(st, col(3), rt, 3, sh3, st_blk, st_c, 1.0, 0.0));
+  STEP(dcopy(LZ_rc, rc, m));
+  STEP(fbsub(LZ_rc, 1));
+  STEP(assemble(B22, LZ_LX));
+  STEP(fbsub(LZ_LX, (int)m));
+  STEP(assemble(B01, Leq));
+  STEP(assemble(B31, Top));
+  STEP(ttk_mul_nd(st, LZ_LX, inv_I, LZ_LXI, 2, mm, s_mat, s_row, s_mat, 1.0, 0.0));  // LZ_LX * inv_I[col]
+  STEP(dcopy(w, LZ_rc, m));
+  STEP(einsum_out(st, MATMUL, {mat(LZ_LXI, m, m), mat(rd, m, 1)}, w, 2, out1, -1.0, 1.0));
+  STEP(dcopy(u, rp, m));
+  STEP(einsum_out(st, MATMUL, {mat(Leq, m, m), mat(w, m, 1)}, u, 2, out1, -1.0, 1.0));
+  STEP(dcopy(v, rt, m));
+  STEP(einsum_out(st, MATMUL, {mat(Top, m, m), mat(w, m, 1)}, v, 2, out1, -1.0, 1.0));
+  STEP(assemble(B00, Am));
+  STEP(einsum(st, MATMUL, {mat(LZ_LXI, m, m), LeqT}, T));
+  STEP(einsum_out(st, MATMUL, {mat(Leq, m, m), mat(T, m, m)}, Am, 2, outm, 1.0, 1.0));
+  STEP(assemble(B33, Dm));
+  STEP(einsum_out(st, MATMUL, {mat(Top, m, m), mat(LZ_LX, m, m)}, Dm, 2, outm, 1.0, 1.0));
+  STEP(ttk_add_diag(st, Dm, (int)m, (int)m, 1e-11));
+  STEP(einsum(st, MATMUL, {mat(Top, m, m), mat(LZ_LXI, m, m)}, TL));
+  STEP(einsum(st, MATMUL, {mat(TL, m, m), LeqT}, Top2));
+  STEP(einsum(st, MATMUL, {mat(Leq, m, m), mat(LZ_LX, m, m)}, Leq2));
+  if (rc_) return rc_;
+  double rcond = 0.0;  // scipy.linalg.lu_factor: no condition check (src/tt_ipm.py:330)
+  rc_ = ttk_lu_sync(st, Dm, (int)m, dpiv, work, &rcond);
+  if (rc_) return rc_;  // TTK_ERR_SINGULAR
+  STEP(dcopy(Dv, v, m));
+  STEP(ttk_lu_solve(st, Dm, (int)m, dpiv, Dv, 1, 1));
+  STEP(einsum_out(st, MATMUL, {mat(Leq2, m, m), mat(Dv, m, 1)}, u, 2, out1, -1.0, 1.0));
+  STEP(dcopy(DT, Top2, m * m));
+  STEP(ttk_lu_solve(st, Dm, (int)m, dpiv, DT, (int)m, (int)m));
+  STEP(einsum_out(st, MATMUL, {mat(Leq2, m, m), mat(DT, m, m)}, Am, 2, outm, -1.0, 1.0));
+  if (rc_) return rc_;
+  rc_ = ttk_lu_sync(st, Am, (int)m, piv, work, &rcond);
+  if (rc_) return rc_;
+  STEP(dcopy(y, u, m));
+  STEP(ttk_lu_solve(st, Am, (int)m, piv, y, 1, 1));
+  double *s0 = sol, *s1 = sol + n * R, *s2 = sol + 2 * n * R, *s3 = sol + 3 * n * R;  // sol[:, j], strides st_blk
+  STEP(ttk_copy_nd(st, y, s0, 3, sh3, st_c, st_blk, 1.0, 0.0));
+  STEP(einsum_out(st, MATMUL, {mat(Top2, m, m), mat(y, m, 1)}, v, 2, out1, -1.0, 1.0));
+  STEP(ttk_lu_solve(st, Dm, (int)m, dpiv, v, 1, 1));
+  STEP(ttk_copy_nd(st, v, s3, 3, sh3, st_c, st_blk, 1.0, 0.0));
+  STEP(dcopy(t2, rd, m));
+  {
+    auto [a, b, c] = ops3(B01);
+    const View x{s0, 3, {r, n, R}, {st_blk[0], st_blk[1], st_blk[2]}};
+    STEP(einsum_out(st, APPLY_T, {a, b, c, x}, t2, 3, st_c, -1.0, 1.0));
+  }
+  STEP(ttk_mul_nd(st, t2, inv_I, s2, 3, sh3, st_c, st_c, st_blk, 1.0, 0.0));
+  STEP(ttk_copy_nd(st, s3, s2, 3, sh3, st_blk, st_blk, -1.0, 1.0));
+  STEP(dcopy(t3, rc, m));
+  {
+    auto [a, b, c] = ops3(B22);
+    const View x{s2, 3, {r, n, R}, {st_blk[0], st_blk[1], st_blk[2]}};
+    STEP(einsum_out(st, APPLY, {a, b, c, x}, t3, 3, st_c, -1.0, 1.0));
+  }
+  STEP(fbsub(t3, 1));
+  STEP(ttk_copy_nd(st, t3, s1, 3, sh3, st_c, st_blk, 1.0, 0.0));
+#undef STEP
+  return rc_;
+}
+
 int ttk_round(ttk_ctx ctx, int d, double *const *cores, const int64_t *inner, int64_t *ranks, double eps, int mode,
               double *tail_out) {
   ttk::CtxScope scope(ctx);

@@ -343,6 +343,79 @@ def _ipm_local_solver(XAX_k, A_k, XAX_k1, Xb_k, b_k, Xb_k1, prev, size_limit, de
     return sol, res_old, min(res_old, res_new), rhs, nrhs, failed
 
 
+def _dense_python_ineq(XAX_k, A_k, XAX_k1, rhs, inv_I, xs):
+    """The dense branch of `_ipm_local_solver_ineq` (`src/tt_ipm.py:303-352`) step by step."""
+    r, n, R = xs[0], xs[2], xs[3]
+    m = r * n * R
+    LZ = _assemble(XAX_k, A_k, XAX_k1, (2, 1), m)
+    D.cholesky_(LZ)
+    rp, rd, rc, rt = (D.clone(rhs[:, i]).view(m, 1) for i in range(4))
+    LZ_rc = _fbsub_(LZ, D.clone(rc))
+    LZ_LX = _fbsub_(LZ, _assemble(XAX_k, A_k, XAX_k1, (2, 2), m))
+    Leq = _assemble(XAX_k, A_k, XAX_k1, (0, 1), m)
+    Top = _assemble(XAX_k, A_k, XAX_k1, (3, 1), m)
+    LZ_LXI = D.empty(m, m)
+    D.mul_(LZ_LXI, LZ_LX, inv_I.view(1, m).expand(m, m))
+    w = D.clone(LZ_rc)
+    D.matmul(LZ_LXI, rd, out=w, alpha=-1.0, beta=1.0)
+    u = D.clone(rp)
+    D.matmul(Leq, w, out=u, alpha=-1.0, beta=1.0)
+    v = D.clone(rt)
+    D.matmul(Top, w, out=v, alpha=-1.0, beta=1.0)
+    Am = _assemble(XAX_k, A_k, XAX_k1, (0, 0), m)
+    D.matmul(Leq, D.matmul(LZ_LXI, Leq.t()), out=Am, beta=1.0)
+    Dm = _assemble(XAX_k, A_k, XAX_k1, (3, 3), m)
+    D.matmul(Top, LZ_LX, out=Dm, beta=1.0)
+    D.add_diag_(Dm, 1e-11)
+    Top2 = D.matmul(D.matmul(Top, LZ_LXI), Leq.t())
+    Leq2 = D.matmul(Leq, LZ_LX)
+    dpiv = D.lu_(Dm, check_rcond=False)
+    Dv = D.clone(v)
+    D.lu_solve_(Dm, dpiv, Dv)
+    D.matmul(Leq2, Dv, out=u, alpha=-1.0, beta=1.0)
+    DT = D.clone(Top2)
+    D.lu_solve_(Dm, dpiv, DT)
+    D.matmul(Leq2, DT, out=Am, alpha=-1.0, beta=1.0)
+    piv = D.lu_(Am, check_rcond=False)
+    y = D.clone(u)
+    D.lu_solve_(Am, piv, y)
+    sol = D.empty(*xs)
+    D.copy_(sol[:, 0], y.view(r, n, R))
+    D.matmul(Top2, y, out=v, alpha=-1.0, beta=1.0)
+    D.lu_solve_(Dm, dpiv, v)
+    D.copy_(sol[:, 3], v.view(r, n, R))
+    t2 = D.clone(rd).view(r, n, R)
+    einsum(APPLY_T, XAX_k[0, 1], A_k[0, 1], XAX_k1[0, 1], sol[:, 0], out=t2, alpha=-1.0, beta=1.0)
+    D.mul_(sol[:, 2], t2, inv_I)
+    D.copy_(sol[:, 2], sol[:, 3], -1.0, 1.0)
+    t3 = D.clone(rc).view(r, n, R)
+    einsum(APPLY, XAX_k[2, 2], A_k[2, 2], XAX_k1[2, 2], sol[:, 2], out=t3, alpha=-1.0, beta=1.0)
+    _fbsub_(LZ, t3.view(m, 1))
+    D.copy_(sol[:, 1], t3)
+    return sol
+
+
+def _dense_native_ineq(XAX_k, A_k, XAX_k1, rhs, inv_I, xs):
+    """`ttk_dense_schur_solve_ineq`: the dense branch of `_ipm_local_solver_ineq` in one library call
+    (NOT_PD / SINGULAR raise LinAlgError like the Python steps' Cholesky / LU)."""
+    r, n, R = xs[0], xs[2], xs[3]
+    keys = ((0, 0), (0, 1), (2, 1), (2, 2), (3, 1), (3, 3))
+    arr = (_LocalBlock * len(keys))()
+    keep = []
+    for e, key in zip(arr, keys):
+        L, A, Rr = D.contig(XAX_k[key]), A_k[key], D.contig(XAX_k1[key])
+        keep += [L, A, Rr]
+        e.L, e.A, e.R = L.data_ptr(), A.data_ptr(), Rr.data_ptr()
+        e.s, e.S = A.shape[0], A.shape[3]
+        e.a_strides[:] = tuple(A.stride())
+    rhs, inv_I = D.contig(rhs), D.contig(inv_I)
+    sol = D.empty(*xs)
+    D._stream()
+    D.check(lib.ttk_dense_schur_solve_ineq(D.CTX[0], r, n, R, arr, rhs.data_ptr(), inv_I.data_ptr(), sol.data_ptr()),
+            "dense_schur_solve_ineq")
+    return sol
+
+
 def _ipm_local_solver_ineq(XAX_k, A_k, XAX_k1, Xb_k, b_k, Xb_k1, prev, size_limit, dense_solve=True, rtol=1e-5):
     """`_ipm_local_solver_ineq` (`src/tt_ipm.py:284-401`) on the device."""
     xs = tuple(prev.shape)
@@ -356,51 +429,8 @@ def _ipm_local_solver_ineq(XAX_k, A_k, XAX_k1, Xb_k, b_k, Xb_k1, prev, size_limi
     sol = None
     if dense_solve:
         try:
-            LZ = _assemble(XAX_k, A_k, XAX_k1, (2, 1), m)
-            D.cholesky_(LZ)
-            rp, rd, rc, rt = (D.clone(rhs[:, i]).view(m, 1) for i in range(4))
-            LZ_rc = _fbsub_(LZ, D.clone(rc))
-            LZ_LX = _fbsub_(LZ, _assemble(XAX_k, A_k, XAX_k1, (2, 2), m))
-            Leq = _assemble(XAX_k, A_k, XAX_k1, (0, 1), m)
-            Top = _assemble(XAX_k, A_k, XAX_k1, (3, 1), m)
-            LZ_LXI = D.empty(m, m)
-            D.mul_(LZ_LXI, LZ_LX, inv_I.view(1, m).expand(m, m))
-            w = D.clone(LZ_rc)
-            D.matmul(LZ_LXI, rd, out=w, alpha=-1.0, beta=1.0)
-            u = D.clone(rp)
-            D.matmul(Leq, w, out=u, alpha=-1.0, beta=1.0)
-            v = D.clone(rt)
-            D.matmul(Top, w, out=v, alpha=-1.0, beta=1.0)
-            Am = _assemble(XAX_k, A_k, XAX_k1, (0, 0), m)
-            D.matmul(Leq, D.matmul(LZ_LXI, Leq.t()), out=Am, beta=1.0)
-            Dm = _assemble(XAX_k, A_k, XAX_k1, (3, 3), m)
-            D.matmul(Top, LZ_LX, out=Dm, beta=1.0)
-            D.add_diag_(Dm, 1e-11)
-            Top2 = D.matmul(D.matmul(Top, LZ_LXI), Leq.t())
-            Leq2 = D.matmul(Leq, LZ_LX)
-            dpiv = D.lu_(Dm, check_rcond=False)
-            Dv = D.clone(v)
-            D.lu_solve_(Dm, dpiv, Dv)
-            D.matmul(Leq2, Dv, out=u, alpha=-1.0, beta=1.0)
-            DT = D.clone(Top2)
-            D.lu_solve_(Dm, dpiv, DT)
-            D.matmul(Leq2, DT, out=Am, alpha=-1.0, beta=1.0)
-            piv = D.lu_(Am, check_rcond=False)
-            y = D.clone(u)
-            D.lu_solve_(Am, piv, y)
-            sol = D.empty(*xs)
-            D.copy_(sol[:, 0], y.view(r, n, R))
-            D.matmul(Top2, y, out=v, alpha=-1.0, beta=1.0)
-            D.lu_solve_(Dm, dpiv, v)
-            D.copy_(sol[:, 3], v.view(r, n, R))
-            t2 = D.clone(rd).view(r, n, R)
-            einsum(APPLY_T, XAX_k[0, 1], A_k[0, 1], XAX_k1[0, 1], sol[:, 0], out=t2, alpha=-1.0, beta=1.0)
-            D.mul_(sol[:, 2], t2, inv_I)
-            D.copy_(sol[:, 2], sol[:, 3], -1.0, 1.0)
-            t3 = D.clone(rc).view(r, n, R)
-            einsum(APPLY, XAX_k[2, 2], A_k[2, 2], XAX_k1[2, 2], sol[:, 2], out=t3, alpha=-1.0, beta=1.0)
-            _fbsub_(LZ, t3.view(m, 1))
-            D.copy_(sol[:, 1], t3)
+            dense = _dense_native_ineq if NATIVE_DENSE and D.DEV.type == "cuda" else _dense_python_ineq
+            sol = dense(XAX_k, A_k, XAX_k1, rhs, inv_I, xs)
         except Exception as e:
             _report(e)
             failed = True

@@ -102,3 +102,46 @@ def test_dense_schur_solve_matches_python_steps(dev):
     assert calls["n"] > 10, calls
     g = json.load(open(os.path.join(ROOT, "tests", "golden", "runs.json")))["maxcut_5_r1_s0"]
     assert r["num_iters"] == g["num_iters"]
+
+
+@pytest.mark.gpu
+def test_dense_schur_solve_ineq_matches_python_steps(dev):
+    """ttk_dense_schur_solve_ineq (one C call) = the step-by-step dense branch of
+    `_ipm_local_solver_ineq` (src/tt_ipm.py:284-352) bit for bit -- solution, or the same exception
+    class -- on the first 30 dense inequality local solves of corr_clust_9 r=1 s764 (fixed
+    `lgmres_cy.pyx:510` mode)."""
+    import json
+    import yaml
+    from ttipm_amd import tt_ipm
+    from ttipm_amd.utils import run_and_record
+    native, calls = tt_ipm._dense_native_ineq, {"n": 0, "exc": 0}
+
+    class Stop(BaseException):  # not an Exception: passes the solver's fallback handlers
+        pass
+
+    def both(*a):
+        try:
+            ref = tt_ipm._dense_python_ineq(*a)
+        except Exception as e:  # noqa: BLE001 - compared with the native status below
+            with pytest.raises(type(e)):
+                native(*a)
+            calls["exc"] += 1
+            raise
+        got = native(*a)
+        calls["n"] += 1
+        assert np.array_equal(dev.read(got), dev.read(ref))
+        if calls["n"] >= 30:
+            raise Stop
+        return got
+
+    g = json.load(open(os.path.join(ROOT, "tests", "golden", "runs.json")))["corr_clust_9_r1_s764"]
+    cfg = yaml.safe_load(open(os.path.join(ROOT, "configs", g["config"] + ".yaml")))
+    old = (tt_ipm.NATIVE_DENSE, tt_ipm.INEQ_MATVEC_BUG)
+    tt_ipm._dense_native_ineq, tt_ipm.NATIVE_DENSE, tt_ipm.INEQ_MATVEC_BUG = both, True, False
+    try:
+        with pytest.raises(Stop):
+            run_and_record(g["problem"], cfg, g["seed"], g["rank"], verbose=False)
+    finally:
+        tt_ipm._dense_native_ineq = native
+        tt_ipm.NATIVE_DENSE, tt_ipm.INEQ_MATVEC_BUG = old
+    assert calls["n"] >= 30, calls

@@ -16,7 +16,7 @@ def main():
     rng = np.random.default_rng(0)
     st = D._stream()
     print(os.environ.get("TTK_LU_BLOCK_MIN", "default"), "n  getrf+gecon_us  getrs(1 rhs)_us")
-    for n in [16, 24, 32, 48, 64, 80, 96, 128, 200, 432]:
+    for n in [int(v) for v in os.environ.get("TTK_LU_SIZES", "16,24,32,48,64,80,96,128,200,432").split(",")]:
         A0 = D.from_numpy(rng.standard_normal((n, n)) + n * np.eye(n))
         A = D.empty(n, n)
         piv = torch.empty(n, dtype=torch.int32, device=D.DEV)
