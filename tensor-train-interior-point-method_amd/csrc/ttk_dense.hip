@@ -450,32 +450,20 @@ __device__ __forceinline__ void rows_update(const double *__restrict__ LU, int n
 // sum_p a[p] x[p] over one row segment (bs <= TB), loads issued ahead of the FMAs
 __device__ __forceinline__ double row_dot(const double *__restrict__ a, const double *x, int bs) {
   double s0 = 0.0, s1 = 0.0;
-#pragma unroll
-  for (int h = 0; h < TB; h += TB / 2) {  // two halves: 16 loads in flight, no spills at 128 VGPRs
-    double v[TB / 2];
-#pragma unroll
-    for (int p = 0; p < TB / 2; ++p) v[p] = h + p < bs ? a[h + p] : 0.0;
-#pragma unroll
-    for (int p = 0; p < TB / 2; p += 2) {
-      s0 = fma(v[p], h + p < bs ? x[h + p] : 0.0, s0);
-      s1 = fma(v[p + 1], h + p + 1 < bs ? x[h + p + 1] : 0.0, s1);
-    }
+#pragma unroll 2
+  for (int p = 0; p < TB; p += 2) {  // rows beyond 4096 only: kept small (the unrolled form spilled)
+    const double v0 = p < bs ? a[p] : 0.0, v1 = p + 1 < bs ? a[p + 1] : 0.0;
+    s0 = fma(v0, p < bs ? x[p] : 0.0, s0);
+    s1 = fma(v1, p + 1 < bs ? x[p + 1] : 0.0, s1);
   }
   return s0 + s1;
 }
 
-// sum_p a[p * lda] x[p] in p order (bs <= TB): the column segment is loaded before the FMA chain
+// sum_p a[p * lda] x[p] in p order (bs <= TB)
 __device__ __forceinline__ double col_dot(const double *__restrict__ a, int lda, const double *x, int bs) {
   double v = 0.0;
-#pragma unroll
-  for (int h = 0; h < TB; h += TB / 2) {
-    double c[TB / 2];
-#pragma unroll
-    for (int p = 0; p < TB / 2; ++p) c[p] = h + p < bs ? a[(int64_t)(h + p) * lda] : 0.0;
-#pragma unroll
-    for (int p = 0; p < TB / 2; ++p)
-      if (h + p < bs) v += c[p] * x[h + p];
-  }
+#pragma unroll 8
+  for (int p = 0; p < bs; ++p) v += a[(int64_t)p * lda] * x[p];
   return v;
 }
 

@@ -512,6 +512,7 @@ struct ApplyArgs {
   int na, ns, nb, ni, nj, nS, nc, nd;
   double alpha, beta;
   int mfma;  // 1: the row runs on the MFMA stages (apply_row_mfma), 0: VALU (apply_row)
+  int qlds = 0;  // VALU rows: 1 stages the whole Q (nc*nS*nd doubles after T2) in LDS for stage 3
 };
 
 // Association follows the greedy pairwise plan the reference's opt_einsum picks for these shapes
@@ -519,6 +520,34 @@ struct ApplyArgs {
 // behave like the plan path's.  One workgroup per output index a.
 // the three stages of one output row a; DIRECT writes out = alpha*acc + beta*out, otherwise the raw
 // row goes to orow[i*nc + c] (LDS)
+// Mixed-radix index (digit 0 most significant) of e = start + q * stride, advanced by one stride per
+// step with single carries (each digit of the stride is below its radix)
+template <int N>
+struct MixedIdx {
+  int v[N], st[N];
+  __device__ MixedIdx(int e, int de, const int *rad) {
+#pragma unroll
+    for (int k = N - 1; k > 0; --k) {
+      v[k] = e % rad[k];
+      e /= rad[k];
+      st[k] = de % rad[k];
+      de /= rad[k];
+    }
+    v[0] = e;
+    st[0] = de;
+  }
+  __device__ __forceinline__ void step(const int *rad) {
+    int c = 0;
+#pragma unroll
+    for (int k = N - 1; k > 0; --k) {
+      v[k] += st[k] + c;
+      c = v[k] >= rad[k];
+      if (c) v[k] -= rad[k];
+    }
+    v[0] += st[0] + c;
+  }
+};
+
 template <bool DIRECT>
 __device__ void apply_row(const ApplyArgs &g, int a, double *sm, double *orow) {
   const int tid = threadIdx.x, nt = blockDim.x;
@@ -528,22 +557,29 @@ __device__ void apply_row(const ApplyArgs &g, int a, double *sm, double *orow) {
   double *As = Pa + ns * nb;            // ns*ni*nj*nS  [i][S][s][j]
   double *T1 = As + ns * ni * nj * nS;  // ns*nj*nd     [s][j][d]
   double *T2 = T1 + ns * nj * nd;       // ni*nS*nd     [i][S][d]
-  for (int e = tid; e < nb * nj * nd; e += nt) {
-    const int b = e / (nj * nd), r = e - b * nj * nd, j = r / nd, d = r - j * nd;
-    X[e] = g.x[b * g.xs[0] + j * g.xs[1] + d * g.xs[2]];
+  double *Qs = T2 + ni * nS * nd;       // nc*nS*nd     [c][S][d]  (g.qlds)
+  if (g.qlds) {  // stage 3 reads every Q element once per row: one coalesced pass instead of a
+                 // dependent FMA chain over global loads
+    const int rq[3] = {nc, nS, nd};
+    MixedIdx<3> iq(tid, nt, rq);
+    for (int e = tid; e < nc * nS * nd; e += nt, iq.step(rq))
+      Qs[e] = g.Q[iq.v[0] * g.qs[0] + iq.v[1] * g.qs[1] + iq.v[2] * g.qs[2]];
+  }
+  {  // staging: multi-digit indices advanced by carries (MixedIdx) instead of divisions
+    const int rx[3] = {nb, nj, nd};
+    MixedIdx<3> ix(tid, nt, rx);
+    for (int e = tid; e < nb * nj * nd; e += nt, ix.step(rx))
+      X[e] = g.x[ix.v[0] * g.xs[0] + ix.v[1] * g.xs[1] + ix.v[2] * g.xs[2]];
   }
   for (int e = tid; e < ns * nb; e += nt) {
     const int s = e / nb, b = e - s * nb;
     Pa[e] = g.P[a * g.ps[0] + s * g.ps[1] + b * g.ps[2]];
   }
-  for (int e = tid; e < ns * ni * nj * nS; e += nt) {  // As[i][S][s][j] = A[s, i, j, S]
-    int r = e;
-    const int j = r % nj;
-    r /= nj;
-    const int s = r % ns;
-    r /= ns;
-    const int S = r % nS, i = r / nS;
-    As[e] = g.A[s * g.as[0] + i * g.as[1] + j * g.as[2] + S * g.as[3]];
+  {  // As[i][S][s][j] = A[s, i, j, S]
+    const int ra[4] = {ni, nS, ns, nj};
+    MixedIdx<4> ia(tid, nt, ra);
+    for (int e = tid; e < ns * ni * nj * nS; e += nt, ia.step(ra))
+      As[e] = g.A[ia.v[2] * g.as[0] + ia.v[0] * g.as[1] + ia.v[3] * g.as[2] + ia.v[1] * g.as[3]];
   }
   __syncthreads();
   for (int e = tid; e < ns * nj * nd; e += nt) {  // t1[s][j][d] = sum_b P[a,s,b] x[b,j,d]
@@ -567,9 +603,14 @@ __device__ void apply_row(const ApplyArgs &g, int a, double *sm, double *orow) {
     const int i = e / nc, c = e - i * nc;
     const double *tr = T2 + i * nS * nd;
     double acc = 0.0;
-    for (int S = 0; S < nS; ++S) {
-      const double *qr = g.Q + c * g.qs[0] + S * g.qs[1];
-      for (int d = 0; d < nd; ++d) acc = fma(qr[d * g.qs[2]], tr[S * nd + d], acc);
+    if (g.qlds) {
+      const double *qr = Qs + c * nS * nd;
+      for (int k = 0; k < nS * nd; ++k) acc = fma(qr[k], tr[k], acc);  // k = (S, d): the same order
+    } else {
+      for (int S = 0; S < nS; ++S) {
+        const double *qr = g.Q + c * g.qs[0] + S * g.qs[1];
+        for (int d = 0; d < nd; ++d) acc = fma(qr[d * g.qs[2]], tr[S * nd + d], acc);
+      }
     }
     if (DIRECT) {
       double *o = g.out + a * g.os[0] + i * g.os[1] + c * g.os[2];
@@ -622,33 +663,6 @@ __device__ __forceinline__ void wg_mfma(int M, int N, int K, FA fa, FB fb, FC fc
 
 constexpr int QCHUNK_MAX = 4096;  // doubles of Q staged per stage-3 K block ([c][k], k = (S,d) range)
 
-// Mixed-radix index (digit 0 most significant) of e = start + q * stride, advanced by one stride per
-// step with single carries (each digit of the stride is below its radix)
-template <int N>
-struct MixedIdx {
-  int v[N], st[N];
-  __device__ MixedIdx(int e, int de, const int *rad) {
-#pragma unroll
-    for (int k = N - 1; k > 0; --k) {
-      v[k] = e % rad[k];
-      e /= rad[k];
-      st[k] = de % rad[k];
-      de /= rad[k];
-    }
-    v[0] = e;
-    st[0] = de;
-  }
-  __device__ __forceinline__ void step(const int *rad) {
-    int c = 0;
-#pragma unroll
-    for (int k = N - 1; k > 0; --k) {
-      v[k] += st[k] + c;
-      c = v[k] >= rad[k];
-      if (c) v[k] -= rad[k];
-    }
-    v[0] += st[0] + c;
-  }
-};
 
 // One 16x16 tile of stage 3 over one K block [kbeg, kbeg + w): the same MFMA sequence as wg_mfma
 // (even / odd 8-steps into two accumulators, a 4-step tail, the sum acc0 + acc1 returned) with the B
@@ -1020,8 +1034,12 @@ int fused_apply_try(void *stream, const char *eq, const int64_t *desc, double *o
     if (!mfma_enabled() || apply_mfma_lds(g) > APPLY_LDS_DOUBLES) return 0;
     g.mfma = 1;
   }
-  const int64_t need = g.mfma ? apply_mfma_lds(g) : apply_lds(g.nb, g.nj, g.nd, g.nS, g.ns, g.ni);
+  int64_t need = g.mfma ? apply_mfma_lds(g) : apply_lds(g.nb, g.nj, g.nd, g.nS, g.ns, g.ni);
   if (batch_on()) return batch_add_fused(g, need) == TTK_OK ? 1 : -1;
+  if (!g.mfma && need + (int64_t)g.nc * g.nS * g.nd <= APPLY_LDS_DOUBLES) {
+    need += (int64_t)g.nc * g.nS * g.nd;
+    g.qlds = 1;
+  }
   const size_t shm = need * sizeof(double);
   const void *kern = g.mfma ? reinterpret_cast<const void *>(fused_apply_mfma_kernel)
                             : reinterpret_cast<const void *>(fused_apply_kernel);
@@ -1248,6 +1266,24 @@ int ttk_schur_build(int ineq, int64_t m, const int64_t *descs, const double *inv
     op.shm[s] = multi_lds(L);
     if (op.shm[s] > (size_t)APPLY_LDS_DOUBLES * sizeof(double))  // multi-task stage beyond LDS
       return schur_build_pairwise(ineq, m, descs, inv_I, handle);
+    // VALU terms stage Q in LDS when every task still fits (the path choice above is unchanged)
+    int64_t mq = 0;
+    for (int t = 0; t < L.ntask; ++t) {
+      const ApplyTask &T = L.task[t];
+      int64_t w = 0;
+      for (int k = 0; k < T.nterms; ++k) {
+        const ApplyArgs &q = T.t[k];
+        const int64_t l = q.mfma ? apply_mfma_lds(q) : apply_lds(q.nb, q.nj, q.nd, q.nS, q.ns, q.ni) + (int64_t)q.nc * q.nS * q.nd;
+        w = l > w ? l : w;
+      }
+      const int64_t need = 2 * (int64_t)T.t[0].ni * T.t[0].nc + w;
+      mq = need > mq ? need : mq;
+    }
+    if (mq <= APPLY_LDS_DOUBLES) {
+      for (int t = 0; t < L.ntask; ++t)
+        for (int k = 0; k < L.task[t].nterms; ++k) L.task[t].t[k].qlds = L.task[t].t[k].mfma ? 0 : 1;
+      op.shm[s] = (size_t)mq * sizeof(double);
+    }
   }
   return schur_store(op, m, handle);
 }

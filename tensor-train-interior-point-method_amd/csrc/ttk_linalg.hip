@@ -1119,7 +1119,7 @@ __global__ __launch_bounds__(1024) void syev_kernel(double *__restrict__ Ain, in
 // Phases 2-4 of the extreme eigenpair, shared by the one-workgroup kernel and the finish kernel of
 // the multi-workgroup tridiagonalisation: T from the reduced A (reflectors kept in A's rows), Sturm
 // multisection, inverse iteration, back-transform.
-__device__ void tridiag_extreme_finish(double *A, int n, int which, double *dv, double *ov, double *ev2, double *tv,
+__device__ __forceinline__ void tridiag_extreme_finish(double *A, int n, int which, double *dv, double *ov, double *ev2, double *tv,
                                        double *z, double *fd, double *fdu, double *fdu2, double *fdl, double *fpiv,
                                        double *__restrict__ ev_out, double *__restrict__ vec_out, int lda,
                                        int timing = 0) {

@@ -108,30 +108,36 @@ def test_dense_schur_solve_matches_python_steps(dev):
 def test_dense_schur_solve_ineq_matches_python_steps(dev):
     """ttk_dense_schur_solve_ineq (one C call) = the step-by-step dense branch of
     `_ipm_local_solver_ineq` (src/tt_ipm.py:284-352) bit for bit -- solution, or the same exception
-    class -- on the first 30 dense inequality local solves of corr_clust_9 r=1 s764 (fixed
-    `lgmres_cy.pyx:510` mode)."""
+    class -- on every dense inequality local solve of a corr_clust_9 r=1 s764 solve (fixed
+    `lgmres_cy.pyx:510` mode).  Mismatches are collected (the solver's fallback handlers would
+    swallow an assertion raised inside the local solve) and asserted after the run."""
     import json
     import yaml
     from ttipm_amd import tt_ipm
     from ttipm_amd.utils import run_and_record
-    native, calls = tt_ipm._dense_native_ineq, {"n": 0, "exc": 0}
-
-    class Stop(BaseException):  # not an Exception: passes the solver's fallback handlers
-        pass
+    native, calls, bad = tt_ipm._dense_native_ineq, {"n": 0, "exc": 0}, []
 
     def both(*a):
         try:
             ref = tt_ipm._dense_python_ineq(*a)
         except Exception as e:  # noqa: BLE001 - compared with the native status below
-            with pytest.raises(type(e)):
+            try:
                 native(*a)
+                bad.append(f"python raised {type(e).__name__}, native returned")
+            except Exception as e2:  # noqa: BLE001
+                if type(e2) is not type(e):
+                    bad.append(f"python raised {type(e).__name__}, native {type(e2).__name__}")
             calls["exc"] += 1
             raise
-        got = native(*a)
+        try:
+            got = native(*a)
+        except Exception as e2:  # noqa: BLE001
+            bad.append(f"native raised {type(e2).__name__}: {e2}")
+            return ref
         calls["n"] += 1
-        assert np.array_equal(dev.read(got), dev.read(ref))
-        if calls["n"] >= 30:
-            raise Stop
+        g, r = dev.read(got), dev.read(ref)
+        if not np.array_equal(g, r):
+            bad.append(f"solve {calls['n']}: max diff {np.max(np.abs(g - r)):.3e}")
         return got
 
     g = json.load(open(os.path.join(ROOT, "tests", "golden", "runs.json")))["corr_clust_9_r1_s764"]
@@ -139,9 +145,11 @@ def test_dense_schur_solve_ineq_matches_python_steps(dev):
     old = (tt_ipm.NATIVE_DENSE, tt_ipm.INEQ_MATVEC_BUG)
     tt_ipm._dense_native_ineq, tt_ipm.NATIVE_DENSE, tt_ipm.INEQ_MATVEC_BUG = both, True, False
     try:
-        with pytest.raises(Stop):
-            run_and_record(g["problem"], cfg, g["seed"], g["rank"], verbose=False)
+        r = run_and_record(g["problem"], cfg, g["seed"], g["rank"], verbose=False)
     finally:
         tt_ipm._dense_native_ineq = native
         tt_ipm.NATIVE_DENSE, tt_ipm.INEQ_MATVEC_BUG = old
-    assert calls["n"] >= 30, calls
+    print("dense inequality solves:", calls)
+    assert not bad, bad[:5]
+    assert calls["n"] >= 1, calls
+    assert r["num_iters"] == g["num_iters"]
