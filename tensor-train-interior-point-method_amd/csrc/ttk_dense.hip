@@ -757,17 +757,21 @@ int lu_blocked(hipStream_t st, double *A, int n, int *piv, double *work, int *st
     TTK_LAUNCH_CHECK();
     k0 += kb;
   }
-  if (want_rcond) {
-    // x, xs (+ the permutation buffer and perm when they fit next to the kernel's static LDS)
-    const size_t shm_perm = 3 * (size_t)n * sizeof(double) + 2 * (size_t)n * sizeof(int);
-    const int use_perm = shm_perm <= 140000;
-    const size_t shm = use_perm ? shm_perm : 2 * (size_t)n * sizeof(double) + (size_t)n * sizeof(int);
-    if (shm > 65536)
-      (void)hipFuncSetAttribute(reinterpret_cast<const void *>(lu_rcond_kernel),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
-    hipLaunchKernelGGL(lu_rcond_kernel, dim3(1), dim3(1024), shm, st, A, n, piv, colsum, status, rcond, use_perm);
-    TTK_LAUNCH_CHECK();
-  }
+  if (want_rcond == 1) return lu_rcond_launch(st, A, n, piv, colsum, status, rcond);
+  return TTK_OK;
+}
+
+int lu_rcond_launch(hipStream_t st, const double *LU, int n, const int *piv, const double *colsum, const int *status,
+                    double *rcond) {
+  // x, xs (+ the permutation buffer and perm when they fit next to the kernel's static LDS)
+  const size_t shm_perm = 3 * (size_t)n * sizeof(double) + 2 * (size_t)n * sizeof(int);
+  const int use_perm = shm_perm <= 140000;
+  const size_t shm = use_perm ? shm_perm : 2 * (size_t)n * sizeof(double) + (size_t)n * sizeof(int);
+  if (shm > 65536)
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(lu_rcond_kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+  hipLaunchKernelGGL(lu_rcond_kernel, dim3(1), dim3(1024), shm, st, LU, n, piv, colsum, status, rcond, use_perm);
+  TTK_LAUNCH_CHECK();
   return TTK_OK;
 }
 

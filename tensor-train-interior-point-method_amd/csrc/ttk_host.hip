@@ -183,11 +183,12 @@ int ttk_dense_schur_solve(ttk_ctx ctx, int64_t r, int64_t n, int64_t R, const tt
   }
   STEP(ttk_add_diag(st, Am, (int)m, (int)m, 1e-11));
   if (rc_) return rc_;
-  double rcond = 0.0;
-  rc_ = ttk_lu_sync(st, Am, (int)m, piv, work, &rcond);
-  if (rcond_out) *rcond_out = rcond;
-  if (rc_) return rc_;  // TTK_ERR_SINGULAR
-  if (rcond < 0.5 * 2.220446049250313e-16) return TTK_ILL_CONDITIONED;  // LinAlgWarning as an error
+  // getrf here; its dgecon estimate runs on the context's side stream while the back-substitutions
+  // below proceed speculatively (their result is discarded when the status or rcond rejects the
+  // factors, as the early returns of the step-by-step path would have) -- one host read at the end
+  int forked = 0;
+  rc_ = ttk::lu_factor_fork_rcond(st, Am, (int)m, piv, work, &forked);
+  if (rc_) return rc_;
   STEP(ttk_lu_solve(st, Am, (int)m, piv, bvec, 1, 1));
   double *s0 = sol, *s1 = sol + n * R, *s2 = sol + 2 * n * R;  // sol[:, j] views, strides st_blk
   STEP(ttk_copy_nd(st, bvec, s0, 3, sh3, st_c, st_blk, 1.0, 0.0));
@@ -208,6 +209,20 @@ int ttk_dense_schur_solve(ttk_ctx ctx, int64_t r, int64_t n, int64_t R, const tt
   STEP(ttk_trsm_lower(st, LZ, (int)m, t3, 1, 1, 1));
   STEP(ttk_copy_nd(st, t3, s1, 3, sh3, st_c, st_blk, 1.0, 0.0));
 #undef STEP
+  if (forked && ttk::lu_rcond_join(st)) return TTK_ERR_HIP;
+  int lu_info = 0;
+  double rcond = 0.0;
+  if (hipMemcpyAsync(&lu_info, ttk::ctx().status, sizeof(int), hipMemcpyDeviceToHost, st) ||
+      hipMemcpyAsync(&rcond, ttk::ctx().rcond, sizeof(double), hipMemcpyDeviceToHost, st))
+    return TTK_ERR_HIP;
+  ttk::note_sync();
+  if (hipStreamSynchronize(st)) return TTK_ERR_HIP;
+  if (rcond_out) *rcond_out = rcond;
+  if (lu_info) {
+    ttk::set_error("Matrix is singular (zero pivot at %d).", lu_info);
+    return TTK_ERR_SINGULAR;
+  }
+  if (rcond < 0.5 * 2.220446049250313e-16) return TTK_ILL_CONDITIONED;  // LinAlgWarning as an error
   return rc_;
 }
 

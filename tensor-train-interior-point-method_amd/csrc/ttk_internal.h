@@ -39,6 +39,8 @@ struct Ctx {
   size_t mapped_n = 0;
   UpSlot up[UP_SLOTS];        // pinned upload ring
   int up_next = 0;
+  hipStream_t side = nullptr;  // second stream (dgecon overlapped with the rest of a dense solve)
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
 };
 Ctx &ctx();
 Ctx *ctx_swap(Ctx *c);  // bind c to the calling thread, return the previous binding
@@ -69,6 +71,13 @@ int trsm_blocked(hipStream_t st, const double *L, int n, double *B, int nrhs, in
 // blocked getrf (device pivots and LAPACK info in `status`) and, if want_rcond, the dgecon
 // 1-norm estimate into device `rcond`; work >= n doubles.  Enqueued without synchronising.
 int lu_blocked(hipStream_t st, double *A, int n, int *piv, double *work, int *status, double *rcond, int want_rcond);
+// want_rcond = 2: the column sums only; the dgecon kernel is then launched by lu_rcond_launch
+int lu_rcond_launch(hipStream_t st, const double *LU, int n, const int *piv, const double *colsum, const int *status,
+                    double *rcond);
+// getrf with the dgecon estimate running on the context's side stream (forked after the factors,
+// joined by lu_rcond_join); returns TTK_OK with *forked = 1, or the one-kernel path (*forked = 0)
+int lu_factor_fork_rcond(hipStream_t st, double *A, int n, int *piv, double *work, int *forked);
+int lu_rcond_join(hipStream_t st);
 // getrs for nrhs columns of B (one workgroup per column, n <= 12000)
 int lu_solve_cols(hipStream_t st, const double *LU, int n, const int *piv, double *B, int nrhs, int ldb);
 

@@ -2566,6 +2566,45 @@ int ttk_lu_sync(void *stream, double *A, int n, int *piv, double *work, double *
   return TTK_OK;
 }
 
+}  // extern "C"
+
+namespace ttk {
+int lu_factor_fork_rcond(hipStream_t st, double *A, int n, int *piv, double *work, int *forked) {
+  *forked = 0;
+  if (ensure_status()) {
+    set_error("lu_factor_fork_rcond: status alloc failed");
+    return TTK_ERR_HIP;
+  }
+  Ctx &c = ctx();
+  if (!(n >= g_lu_block_min && n <= 7000)) {  // one-kernel getrf + dgecon (ttk_lu_sync's small path)
+    hipLaunchKernelGGL(lu_kernel, dim3(1), dim3(1024), 0, st, A, n, piv, work, c.status, c.rcond);
+    TTK_LAUNCH_CHECK();
+    return TTK_OK;
+  }
+  if (!c.side) {
+    TTK_HIP(hipStreamCreateWithFlags(&c.side, hipStreamNonBlocking));
+    TTK_HIP(hipEventCreateWithFlags(&c.ev_fork, hipEventDisableTiming));
+    TTK_HIP(hipEventCreateWithFlags(&c.ev_join, hipEventDisableTiming));
+  }
+  const int rc = lu_blocked(st, A, n, piv, work, c.status, c.rcond, 2);
+  if (rc) return rc;
+  TTK_HIP(hipEventRecord(c.ev_fork, st));
+  TTK_HIP(hipStreamWaitEvent(c.side, c.ev_fork, 0));
+  const int rr = lu_rcond_launch(c.side, A, n, piv, work, c.status, c.rcond);
+  if (rr) return rr;
+  TTK_HIP(hipEventRecord(c.ev_join, c.side));
+  *forked = 1;
+  return TTK_OK;
+}
+
+int lu_rcond_join(hipStream_t st) {
+  TTK_HIP(hipStreamWaitEvent(st, ctx().ev_join, 0));
+  return TTK_OK;
+}
+}  // namespace ttk
+
+extern "C" {
+
 int ttk_lu_solve(void *stream, const double *LU, int n, const int *piv, double *B, int nrhs, int ldb) {
   if (n >= g_lu_block_min && n <= 12000 && nrhs <= 8 && nrhs > 0) return ttk::lu_solve_cols(TTK_STREAM(stream), LU, n, piv, B, nrhs, ldb);
   if (n <= 0 || nrhs <= 0) return TTK_OK;

@@ -54,6 +54,12 @@ double *mapped_stage(size_t n, double **dev) {
   Ctx &c = ctx();
   if (c.mapped_n < n) {
     if (c.mapped_h) (void)hipHostFree(c.mapped_h);
+  if (c.side) {
+    (void)hipStreamSynchronize(c.side);
+    (void)hipStreamDestroy(c.side);
+    (void)hipEventDestroy(c.ev_fork);
+    (void)hipEventDestroy(c.ev_join);
+  }
     c.mapped_h = c.mapped_d = nullptr;
     c.mapped_n = 0;
     const size_t want = n < 8192 ? 8192 : n;
@@ -189,6 +195,12 @@ int ttk_ctx_destroy(ttk_ctx h) {
   for (double *p : {c.scratch, c.splitk, c.dev_scalar, c.schur_w, c.lgmres, c.rcond}) if (p) (void)hipFree(p);
   if (c.status) (void)hipFree(c.status);
   if (c.mapped_h) (void)hipHostFree(c.mapped_h);
+  if (c.side) {
+    (void)hipStreamSynchronize(c.side);
+    (void)hipStreamDestroy(c.side);
+    (void)hipEventDestroy(c.ev_fork);
+    (void)hipEventDestroy(c.ev_join);
+  }
   for (ttk::UpSlot &u : c.up) {
     if (u.p) (void)hipHostFree(u.p);
     if (u.ev) (void)hipEventDestroy(u.ev);

@@ -692,10 +692,26 @@ def _tt_approx_product(A, Dm, x0, kick_rank, nswp, tol, verbose):
     def local(k):
         return einsum(e_loc, P[k], A[k], Dm[k], P[k + 1], alpha=nrmsc)
 
+    # relative changes: the two dots of each go to device slots and are read once per half-sweep
+    # (only the running max decides anything, at the end of the half-sweep); the host formula of
+    # D.norm is applied to the read values in call order, so mres is bit-identical
+    rel_buf, rel_n = D.empty(2 * d), [0]
+
     def rel_change(sol, prev):
         diff = D.clone(sol)
         D.copy_(diff, prev, -1.0, 1.0)
-        return D.norm(diff) / max(D.norm(sol), 1e-8)
+        i = rel_n[0]
+        D.dot_into(diff, diff, rel_buf[2 * i:2 * i + 1])
+        D.dot_into(sol, sol, rel_buf[2 * i + 1:2 * i + 2])
+        rel_n[0] += 1
+
+    def rel_max(m):
+        if rel_n[0]:
+            v = D.read(rel_buf[:2 * rel_n[0]])
+            for i in range(rel_n[0]):
+                m = max(m, float(np.sqrt(max(v[2 * i], 0.0))) / max(float(np.sqrt(max(v[2 * i + 1], 0.0))), 1e-8))
+            rel_n[0] = 0
+        return m
 
     def unit(t):
         nn = D.norm(t)
@@ -709,7 +725,7 @@ def _tt_approx_product(A, Dm, x0, kick_rank, nswp, tol, verbose):
         for k in range(d - 1, -1, -1):
             if swp > 0:
                 sol = local(k)
-                mres = max(mres, rel_change(sol, x[k]))
+                rel_change(sol, x[k])
             else:
                 sol = D.contig(x[k])
             if k > 0:
@@ -735,6 +751,7 @@ def _tt_approx_product(A, Dm, x0, kick_rank, nswp, tol, verbose):
                 nrmsc *= nAD[k - 1] / nx[k - 1]
             else:
                 x[k] = D.contig(sol).view(rx[k], *modes[k], rx[k + 1])
+        mres = rel_max(mres)
         if last:
             break
         if mres < tol or swp == nswp - 1:
@@ -742,7 +759,7 @@ def _tt_approx_product(A, Dm, x0, kick_rank, nswp, tol, verbose):
         mres = 0
         for k in range(d):
             sol = local(k)
-            mres = max(mres, rel_change(sol, x[k]))
+            rel_change(sol, x[k])
             if k < d - 1:
                 nrmsc *= nx[k] / nAD[k]
                 U, S, Vt, s = D.svd(D.contig(sol).view(rx[k] * nmod[k], rx[k + 1]))
@@ -765,6 +782,7 @@ def _tt_approx_product(A, Dm, x0, kick_rank, nswp, tol, verbose):
                 nrmsc *= nAD[k] / nx[k]
             else:
                 x[k] = D.contig(sol).view(rx[k], *modes[k], rx[k + 1])
+        mres = rel_max(mres)
         if last:
             break
         if mres < tol:
