@@ -463,6 +463,9 @@ def main():
                           "total_ipm_iters": iters},
                "median_seed_s_per_iter": med,
                "pathological_seeds": sorted({p["seed"] for p in per_seed if p["pathological"]}),
+               # library / path knobs set for this run (several change summation order, hence results at
+               # rounding level)
+               "env_knobs": {k: v for k, v in sorted(os.environ.items()) if k.startswith(("TTK_", "TTIPM_"))},
                "roofline": roofline, "cpu_baseline": cpu,
                "mfma_util_pct": None if roofline is None else 100.0 * roofline["frac"],
                "per_seed": per_seed}
