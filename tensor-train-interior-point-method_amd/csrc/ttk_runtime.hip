@@ -54,12 +54,6 @@ double *mapped_stage(size_t n, double **dev) {
   Ctx &c = ctx();
   if (c.mapped_n < n) {
     if (c.mapped_h) (void)hipHostFree(c.mapped_h);
-  if (c.side) {
-    (void)hipStreamSynchronize(c.side);
-    (void)hipStreamDestroy(c.side);
-    (void)hipEventDestroy(c.ev_fork);
-    (void)hipEventDestroy(c.ev_join);
-  }
     c.mapped_h = c.mapped_d = nullptr;
     c.mapped_n = 0;
     const size_t want = n < 8192 ? 8192 : n;
