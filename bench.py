@@ -13,7 +13,7 @@
   and at N=1 the steps cycle through the config's seeds.  `replica`: every rank solves step i's
   N=1 seed.  Problems are created once per distinct seed on rank 0 and delivered by ONE broadcast
   (RCCL over xGMI with the nccl backend) before the timed region; no collective inside the IPM loop.
-* Solves in flight per GPU (`--inflight P`, default 2, at most 16 processes per node): a solve is a
+* Solves in flight per GPU (`--inflight P`, default 4, at most 16 processes per node): a solve is a
   chain of small dependent launches that leaves most of the chip idle, so each GPU runs P seeds at
   once -- this process plus P-1 worker processes on the same device (each its own HIP stream and
   library context), spawned before the GPU is touched and released together at the start of the
@@ -230,6 +230,12 @@ def _pmc_traffic():
     return None
 
 
+def default_inflight(world):
+    """Solves in flight per GPU: 4 (measured on one MI355X, maxcut_10 whole job: 1 -> 0.39, 2 -> 0.20,
+    3 -> 0.137, 4 -> 0.106, 6 -> 0.112 s/IPM-iter), capped so a node runs at most 16 solve processes"""
+    return max(1, min(4, 16 // world))
+
+
 def make_schedule(config, cfg_name, seeds_arg, steps, world, rank, P, mode):
     """(seeds, per-step seed lists, this rank's per-slot seed lists).  Step i, rank p, slot j
     solves seeds[(i*N*P + p*P + j) mod S] (`shard`) or step i's N=1 seed (`replica`); the config's
@@ -281,7 +287,7 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     with open(args.config) as f:
         config = yaml.safe_load(f)
-    P = args.inflight if args.inflight else max(1, min(2, 16 // world))
+    P = args.inflight if args.inflight else default_inflight(world)
     if _profiled() and (P > 1 or not args.no_cpu_baseline):
         # a profiler's preloaded library has initialised the GPU already: no child processes
         print("bench: under a profiler -> --inflight 1 --no-cpu-baseline", file=sys.stderr)

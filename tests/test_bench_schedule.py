@@ -54,3 +54,11 @@ def test_replica_schedule():
     cfg = _cfg("maxcut_10.yaml")
     _, sched, _ = bench.make_schedule(cfg, "maxcut_10.yaml", None, 3, 2, 1, 1, "replica")
     assert sched == [[41, 41], [23, 23], [235, 235]]
+
+
+def test_default_inflight_caps_processes_per_node():
+    assert bench.default_inflight(1) == 4
+    assert bench.default_inflight(2) == 4
+    assert bench.default_inflight(4) == 4
+    assert bench.default_inflight(8) == 2
+    assert all(w * bench.default_inflight(w) <= 16 for w in (1, 2, 4, 8, 16))
