@@ -13,12 +13,12 @@
   and at N=1 the steps cycle through the config's seeds.  `replica`: every rank solves step i's
   N=1 seed.  Problems are created once per distinct seed on rank 0 and delivered by ONE broadcast
   (RCCL over xGMI with the nccl backend) before the timed region; no collective inside the IPM loop.
-* Solves in flight per GPU (`--inflight P`, default 4, at most 16 processes per node): a solve is a
-  chain of small dependent launches that leaves most of the chip idle, so each GPU runs P seeds at
-  once -- this process plus P-1 worker processes on the same device (each its own HIP stream and
-  library context), spawned before the GPU is touched and released together at the start of the
-  timed region.  A step is then P solves per GPU: step i, rank p, slot j solves
-  seeds[(i*N*P + p*P + j) mod S].
+* Solves in flight per GPU (`--inflight P`, default 2 at every N, so the 1/2/4/8-GPU series is
+  like-for-like and a node runs at most 16 solve processes): a solve is a chain of small dependent
+  launches that leaves most of the chip idle, so each GPU runs P seeds at once -- this process plus
+  P-1 worker processes on the same device (each its own HIP stream and library context), spawned
+  before the GPU is touched and released together at the start of the timed region.  A step is then
+  P solves per GPU: step i, rank p, slot j solves seeds[(i*N*P + p*P + j) mod S].
 * Timed region: barrier + device sync on both sides of the K steps, max over ranks.
   `value` = (max-over-ranks wall) / (IPM iterations of all ranks): whole-job s per IPM-iteration.
   `median_seed_s_per_iter` is SURVEY.md §8(d)'s statistic: the median over the distinct seeds of
@@ -31,11 +31,14 @@
   KKT operator application; `dev.ALGO`) / summed contraction kernel time; peak =
   78.6 TFLOP/s fp64 matrix.  `device_flops` is what the launched kernels executed.
 * `cpu_baseline` (rank 0, N=1 only): the oracle CPU restatement of the reference path (`oracle/`,
-  a port) on this host, each of the timed seeds in its own process with ONE BLAS thread, all seeds
-  concurrently, each bounded to the IPM iterations finished within `--cpu-cap` seconds; the GPU
-  figure over the SAME seeds and iterations (from the timed solves' per-iteration timestamps) sits
-  beside it.  Then one seed again with all the host share's cores as BLAS threads.  The workers
-  are started before this process touches the GPU and wait on a pipe until the GPU work is done.
+  a port) on this host: one single-thread process per core of the host share (16), the timed seeds
+  cycled over them, all concurrently, each bounded to the IPM iterations finished within
+  `--cpu-cap` seconds.  `value` = median over seeds of the per-seed s/IPM-iter (the statistic of
+  SURVEY.md §8(d)); the GPU's per-seed figure over the SAME seeds and iterations (from the timed
+  solves' per-iteration timestamps) sits beside it (`gpu_over_cpu`); `throughput` is the concurrent
+  run's whole-job s/IPM-iter, the counterpart of this line's `value`.  Then one seed again with all
+  the host share's cores as BLAS threads.  The workers are started before this process touches the
+  GPU and wait on a pipe until the GPU work is done.
 """
 import argparse
 import contextlib
@@ -65,6 +68,21 @@ class _Stop(Exception):
     pass
 
 
+_CHILDREN = []  # every worker Popen; terminated on any early exit of main()
+
+
+def _reap_children():
+    for p in _CHILDREN:
+        if p.poll() is None:
+            p.terminate()
+    for p in _CHILDREN:
+        try:
+            p.wait(timeout=10)
+        except subprocess.TimeoutExpired:
+            p.kill()
+            p.wait()
+
+
 class _BoundedTrace(list):
     """Trace sink that time-stamps each Newton-system assembly and stops the solve once `cap`
     seconds have passed since the first assembly (after at least one full iteration)."""
@@ -91,7 +109,8 @@ def _cpu_worker(problem, cfg_path, seed, rank_tt, cap):
         warnings.simplefilter("error")
         np.random.seed(seed)
         prob = OP.PROBLEMS[problem](config["dim"], rank_tt, verbose=False)
-    sys.stdin.readline()  # released by the parent once the GPU work is done
+    if sys.stdin.readline().strip() != "go":  # EOF: the parent is gone -- do not run as an orphan
+        sys.exit(3)
     with warnings.catch_warnings(), contextlib.redirect_stdout(sys.stderr):
         warnings.simplefilter("error")
         if len(prob) == 5:
@@ -116,6 +135,7 @@ def _cpu_worker(problem, cfg_path, seed, rank_tt, cap):
             full, wall = None, None
     n_it = len(trace.t) - 1
     out = {"seed": seed, "iters": n_it, "s_per_iter": (trace.t[n_it] - trace.t[0]) / max(n_it, 1),
+           "work_s": trace.t[n_it] - t_start,
            "assembly_t": [t - trace.t[0] for t in trace.t], "threads": os.environ.get("OPENBLAS_NUM_THREADS")}
     if full is not None:
         out.update(full_solve_iters=full, full_solve_s_per_iter=wall / max(full, 1))
@@ -144,7 +164,8 @@ def _gpu_worker(args, seeds):
             solve(seeds[0])
         torch.cuda.synchronize()
     print("ready", flush=True)
-    sys.stdin.readline()
+    if sys.stdin.readline().strip() != "go":  # EOF: the parent is gone -- do not run as an orphan
+        sys.exit(3)
     traces = [[] for _ in seeds]
     t0 = time.perf_counter()
     with contextlib.redirect_stdout(sys.stderr):
@@ -166,6 +187,7 @@ def _spawn_gpu_workers(args, slot_seeds):
                "--warmup", str(args.warmup)]
         procs.append(subprocess.Popen(cmd, stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=sys.stderr,
                                       text=True))
+    _CHILDREN.extend(procs)
     return procs
 
 
@@ -179,6 +201,7 @@ def _spawn_cpu_workers(args, seeds, threads):
                "--config", args.config, "--rank", str(args.rank), "--cpu-cap", str(args.cpu_cap)]
         procs.append(subprocess.Popen(cmd, stdin=subprocess.PIPE, stdout=subprocess.PIPE,
                                       stderr=subprocess.DEVNULL, env=env, text=True))
+    _CHILDREN.extend(procs)
     return procs
 
 
@@ -231,9 +254,11 @@ def _pmc_traffic():
 
 
 def default_inflight(world):
-    """Solves in flight per GPU: 4 (measured on one MI355X, maxcut_10 whole job: 1 -> 0.39, 2 -> 0.20,
-    3 -> 0.137, 4 -> 0.106, 6 -> 0.112 s/IPM-iter), capped so a node runs at most 16 solve processes"""
-    return max(1, min(4, 16 // world))
+    """Solves in flight per GPU: 2 at every N of the 1/2/4/8-GPU series, so that the series is
+    like-for-like (a node runs at most 16 solve processes: 8 GPUs x 2).  One MI355X is not saturated
+    by 2 (maxcut_10 whole job, round-2 sweep: 1 -> 0.39, 2 -> 0.20, 4 -> 0.106, 6 -> 0.112 s/IPM-iter;
+    `--inflight 4` measures the single-GPU optimum)."""
+    return max(1, min(2, 16 // world))
 
 
 def make_schedule(config, cfg_name, seeds_arg, steps, world, rank, P, mode):
@@ -270,7 +295,7 @@ def main():
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--schedule", choices=("shard", "replica"), default="shard")
     ap.add_argument("--inflight", type=int, default=None,
-                    help="solves in flight per GPU (default: 2, capped at 16 processes per node)")
+                    help="solves in flight per GPU (default: default_inflight())")
     ap.add_argument("--cpu-worker", type=int, default=None, help=argparse.SUPPRESS)
     ap.add_argument("--gpu-worker", default=None, help=argparse.SUPPRESS)
     args = ap.parse_args()
@@ -302,9 +327,12 @@ def main():
     cpu_seeds = list(dict.fromkeys(s for sl in slot_seeds for s in sl))  # the distinct seeds this (only) rank times
     cpu_procs, allcore_proc = [], []
     do_cpu = rank == 0 and world == 1 and not args.no_cpu_baseline
+    cores = min(len(os.sched_getaffinity(0)), HOST_SHARE)
     if do_cpu:  # before any GPU call
-        cores = min(len(os.sched_getaffinity(0)), HOST_SHARE)
-        cpu_procs = _spawn_cpu_workers(args, cpu_seeds, [1] * len(cpu_seeds))
+        # the host share's cores, one single-thread oracle process each, the timed seeds cycled: the
+        # per-seed latency AND the CPU's whole-job throughput come from the same concurrent run
+        cyc = [cpu_seeds[i % len(cpu_seeds)] for i in range(max(cores, len(cpu_seeds)))]
+        cpu_procs = _spawn_cpu_workers(args, cyc, [1] * len(cyc))
         allcore_proc = _spawn_cpu_workers(args, cpu_seeds[:1], [cores])
 
     import torch
@@ -414,32 +442,43 @@ def main():
         with contextlib.redirect_stdout(sys.stderr):
             per = _release(cpu_procs)
             allc = _release(allcore_proc)[0]
-        gpu_by_seed = {}
+        gpu_runs, cpu_runs = {}, {}
         for r in results:
-            gpu_by_seed.setdefault(r["seed"], r)
-        rows = []
+            gpu_runs.setdefault(r["seed"], []).append(r["assembly_t"])
         for c in per:
-            if c is None:
+            if c is not None and c["iters"] > 0:
+                cpu_runs.setdefault(c["seed"], []).append(c["assembly_t"])
+        rows = []
+        for sd in cpu_runs:  # per seed: the common prefix of IPM iterations of all its runs
+            if sd not in gpu_runs:
                 continue
-            g = gpu_by_seed[c["seed"]]
-            gt, ct = g["assembly_t"], c["assembly_t"]
-            k = min(c["iters"], len(gt) - 1)  # the common prefix of IPM iterations
-            gk = (gt[k] - gt[0]) / k if k > 0 else None
-            ck = (ct[k] - ct[0]) / k if k > 0 else None
-            rows.append({"seed": c["seed"], "iters": k, "cpu_s_per_iter": ck, "gpu_s_per_iter": gk,
-                         "gpu_over_cpu": (gk / ck) if gk and ck else None})
-        rows = [r for r in rows if r["cpu_s_per_iter"]]
+            k = min(len(t) - 1 for t in cpu_runs[sd] + gpu_runs[sd])
+            if k <= 0:
+                continue
+            ck = float(np.median([(t[k] - t[0]) / k for t in cpu_runs[sd]]))
+            gk = float(np.median([(t[k] - t[0]) / k for t in gpu_runs[sd]]))
+            rows.append({"seed": sd, "iters": k, "cpu_runs": len(cpu_runs[sd]), "gpu_runs": len(gpu_runs[sd]),
+                         "cpu_s_per_iter": ck, "gpu_s_per_iter": gk, "gpu_over_cpu": gk / ck})
         med = float(np.median([r["cpu_s_per_iter"] for r in rows])) if rows else None
-        gmed = [r["gpu_s_per_iter"] for r in rows if r["gpu_s_per_iter"]]
+        gmed = float(np.median([r["gpu_s_per_iter"] for r in rows])) if rows else None
+        done = [c for c in per if c is not None]
+        cpu_iters = sum(c["iters"] for c in done)
+        cpu_wall = max((c["work_s"] for c in done), default=0.0)
         cpu = {"value": med, "unit": "s/IPM-iter", "cores": 1, "kind": "port",
                "sample": f"oracle/ CPU restatement of the reference path on {args.problem} dim={config['dim']} "
-                         f"rank={args.rank}, seeds {[r['seed'] for r in rows]} (the timed seeds), one process and "
-                         f"ONE BLAS thread per seed, all concurrently; each seed's first IPM iterations up to "
-                         f"{args.cpu_cap:g} s of work; value = median over seeds of s/IPM-iter",
+                         f"rank={args.rank}: {len(done)} single-thread processes at once (the host share's cores), "
+                         f"the timed seeds {sorted(cpu_runs)} cycled over them; each process runs its seed's first "
+                         f"IPM iterations up to {args.cpu_cap:g} s of work; value = median over seeds of each "
+                         f"seed's s/IPM-iter (median over its processes), over the iterations the CPU and GPU "
+                         f"runs of that seed have in common",
                "per_seed": rows,
-               "gpu_same_sample_median": float(np.median(gmed)) if gmed else None,
-               "gpu_over_cpu_median": float(np.median([r["gpu_over_cpu"] for r in rows if r["gpu_over_cpu"]]))
-               if gmed else None,
+               "gpu_same_sample_median": gmed,
+               "gpu_over_cpu": (gmed / med) if med and gmed else None,
+               "gpu_over_cpu_median": float(np.median([r["gpu_over_cpu"] for r in rows])) if rows else None,
+               "throughput": {"s_per_iter": cpu_wall / cpu_iters if cpu_iters else None, "processes": len(done),
+                              "threads_each": 1, "ipm_iters": cpu_iters, "wall_s": cpu_wall,
+                              "note": "whole-job s/IPM-iter of the concurrent CPU run: longest process's work time "
+                                      "/ IPM iterations of all processes (the GPU's `value` formula)"},
                "all_cores": None if allc is None else {
                    "seed": allc["seed"], "threads": int(allc["threads"]), "iters": allc["iters"],
                    "cpu_s_per_iter": allc["s_per_iter"]},
@@ -474,6 +513,11 @@ def main():
                "env_knobs": {k: v for k, v in sorted(os.environ.items()) if k.startswith(("TTK_", "TTIPM_"))},
                "roofline": roofline, "cpu_baseline": cpu,
                "mfma_util_pct": None if roofline is None else 100.0 * roofline["frac"],
+               # like-for-like ratios: per-seed latency (the same statistic on both sides) and whole-job
+               # throughput (this line's value against the concurrent CPU run's)
+               "gpu_over_cpu_per_seed_median": None if cpu is None else cpu["gpu_over_cpu"],
+               "gpu_over_cpu_throughput": None if cpu is None or not cpu["throughput"]["s_per_iter"] else
+               (elapsed / max(iters, 1)) / cpu["throughput"]["s_per_iter"],
                "per_seed": per_seed}
         print(json.dumps(out), flush=True)
     if world > 1:
@@ -482,4 +526,7 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    try:
+        main()
+    finally:
+        _reap_children()

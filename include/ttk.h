@@ -56,6 +56,28 @@ int ttk_ctx_destroy(ttk_ctx ctx);      /* synchronises the context's stream, fre
 int ttk_ctx_bind(ttk_ctx ctx);         /* make ctx current for the calling thread (NULL: default) */
 void *ttk_ctx_stream(ttk_ctx ctx);
 
+/* Numerics knobs, per context.  Each changes which kernel variant (and so which summation order)
+ * a call uses; they live in the context so that flipping one for one context never changes the
+ * results of another.  ctx NULL: the calling thread's current context (bound or default).
+ *   FUSED_APPLY     1: local applies opted in by the caller run on the one-launch fused kernel
+ *   FUSED_MFMA      1: fused applies beyond the VALU kernel's FLOP range run the MFMA stages
+ *                      (default from env TTK_FUSED_MFMA, else 1); 0: the pairwise plan
+ *   SPLITK          1: deterministic split-K for GEMM steps whose tile grid cannot fill the chip
+ *   SPLITK_MINK     K per split (default from env TTK_SPLITK_MINK, else 256)
+ *   LGMRES_MW_MIN   (it+1)*n at or above which the LGMRES Arnoldi / build / augmentation steps
+ *                   run as multi-workgroup kernels (default 16384; 0 everywhere, INT_MAX never)
+ * ttk_ctx_set_knob stores value and returns the previous one in *old (may be NULL). */
+enum ttk_knob {
+  TTK_KNOB_FUSED_APPLY = 0,
+  TTK_KNOB_FUSED_MFMA = 1,
+  TTK_KNOB_SPLITK = 2,
+  TTK_KNOB_SPLITK_MINK = 3,
+  TTK_KNOB_LGMRES_MW_MIN = 4,
+  TTK_KNOB_COUNT = 5
+};
+int ttk_ctx_set_knob(ttk_ctx ctx, int knob, int value, int *old);
+int ttk_ctx_get_knob(ttk_ctx ctx, int knob, int *value);
+
 const char *ttk_last_error(void);
 int ttk_version(void);
 /* number of kernel launches issued since load (profiling / launch-count tests) */
@@ -95,11 +117,14 @@ int ttk_einsum(void *stream, const char *eq, const int64_t *desc, double *out, d
  * launch plus one grouped fused-apply launch per level.  Bit-identical to the unbatched calls.
  * Used for one AMEn core step's environment updates (`src/tt_als.py:372-387,499-514`), the
  * block local products and the rank loop's candidate products (`src/tt_als.py:334-346`).
- * ttk_copy_nd / ttk_mul_nd flush pending steps first.  Nesting counts; only the outermost end
- * launches.  stats: [flushes, recorded steps, launches]. */
+ * Every other entry point that takes a stream (element-wise, reductions, reads, factorisations,
+ * LGMRES steps) flushes the pending steps first, so stream order holds for C callers that read
+ * an einsum output while a batch is open.  Nesting is counted; every end (nested ones included)
+ * launches what is pending.  stats: [flushes, recorded steps, launches]. */
 /* Local applies beyond the VALU fused kernel's FLOP range (graphm-sized blocks) run the same three
  * stages on fp64 MFMA in one launch (one workgroup per output row) when they fit LDS; off: the
- * pairwise plan.  Returns the previous setting (default on; env TTK_FUSED_MFMA=0 turns it off). */
+ * pairwise plan.  Returns the previous setting (default on; env TTK_FUSED_MFMA=0 turns it off).
+ * Shorthand for ttk_ctx_set_knob(NULL, TTK_KNOB_FUSED_MFMA, ...): the current context only. */
 int ttk_fused_set_mfma(int on);
 /* diagnostics: per-phase wall-clock sums (100 MHz ticks) of the MFMA rows in a -DTTK_MFMA_PROFILE
  * build: [staging, stage 1, stage 2, stage 3, epilogue, -, -, rows]; zeros otherwise */
@@ -136,7 +161,8 @@ int ttk_env_update(ttk_ctx ctx, int backward, int nblocks, const ttk_env_block *
 int ttk_rank_scan_sync(void *stream, double *res, const double *negs, int64_t n, int nq, double *host_out);
 /* calls that opt in (desc flag) route 'lsr,smnS,LSR,rnR->lmL' / 'lsr,smnS,LSR,lmL->rnR' (the local
  * operator, src/tt_als.py:190-200, cy_src/lgmres_cy.pyx:126-153) to a one-launch fused kernel when
- * its intermediates fit LDS; this switch disables it globally.  Returns the previous setting. */
+ * its intermediates fit LDS; this switch disables it for the current context (TTK_KNOB_FUSED_APPLY).
+ * Returns the previous setting. */
 int ttk_einsum_set_fused(int on);
 /* out[3] = {plan hits, plan misses, cached plans} */
 int ttk_einsum_stats(long long *out);
@@ -149,7 +175,7 @@ int ttk_contract_stats(double *out, int reset);
 
 /* split-K for GEMM steps whose tile grid cannot fill the chip (< 256 tiles) and K >= 512: the K
  * range is split over workgroups into partial slabs summed in a fixed order by a second kernel.
- * on = 0 disables it (tests).  Returns the previous setting. */
+ * on = 0 disables it for the current context (TTK_KNOB_SPLITK).  Returns the previous setting. */
 int ttk_gemm_set_splitk(int on);
 /* diagnostics: on > 0 records a (nb,M,N,K) histogram of ttk_gemm_offs launches, on < 0 clears it;
  * dump_path != NULL writes "nb M N K launches flops" lines */
@@ -294,12 +320,14 @@ int ttk_syev_extreme(void *stream, const double *A, int n, int which, double *ev
  * or 7 block descriptors of 36 int64 words each, in ttk_einsum's format for the local apply
  * 'lsr,smnS,LSR,rnR->lmL' (4 operands: XAX_k, A_k, XAX_k1, x with any pointer; has_out = 0):
  * B00, B01, B21, B22, B01 (read as its transpose 'lsr,smnS,LSR,lmL->rnR') [, B31, B33].
- * inv_I: m device doubles.  *handle = 0 when a block exceeds the fused kernel's limits (the
- * caller keeps the per-block path).  ttk_schur_apply: out = A v for v = [y; x (; t)] in 2
+ * inv_I: m device doubles.  Handles belong to ctx (NULL: the calling thread's current context).
+ * *handle = 0 when a block's descriptor does not describe the local apply (the caller keeps the
+ * per-block path); blocks beyond the fused kernel's limits give a handle on the pairwise plans.  ttk_schur_apply: out = A v for v = [y; x (; t)] in 2
  * launches, the same operations (and rounding) as the per-block fused applies. */
-int ttk_schur_build(int ineq, int64_t m, const int64_t *descs, const double *inv_I, int64_t *handle);
-int ttk_schur_apply(void *stream, int64_t handle, const double *v, double *out);
-int ttk_schur_free(int64_t handle);
+int ttk_schur_build(ttk_ctx ctx, int ineq, int64_t m, const int64_t *descs, const double *inv_I,
+                    int64_t *handle);
+int ttk_schur_apply(ttk_ctx ctx, int64_t handle, const double *v, double *out);  /* on ctx's stream */
+int ttk_schur_free(ttk_ctx ctx, int64_t handle);
 
 /* ---------------------------------------------------------------------------------------
  * LGMRES building blocks (PETSc KSPLGMRES semantics, see oracle/petsc_lgmres.py):
@@ -335,7 +363,7 @@ int ttk_lgmres_aug(void *stream, const double *hh, int max_k, int it_total, cons
 
 /* (it+1)*n at or above which the Arnoldi / build / augmentation steps run as multi-workgroup
  * kernels (default 16384 elements); 0 forces them everywhere, INT_MAX disables them (tests).
- * Returns the previous threshold. */
+ * Current context only (TTK_KNOB_LGMRES_MW_MIN).  Returns the previous threshold. */
 int ttk_lgmres_set_mw_threshold(int elems);
 
 /* Whole local KKT solve by LGMRES (PETSc KSPLGMRES semantics, `src/tt_ipm.py:101-162,249-266`):
@@ -367,6 +395,22 @@ int ttk_lgmres(ttk_ctx ctx, int64_t schur, const double *b, double *x, int64_t n
  * Host decisions read the singular values (one sync per bond). */
 int ttk_round(ttk_ctx ctx, int d, double *const *cores, const int64_t *inner, int64_t *ranks, double eps, int mode,
               double *tail_out);
+
+/* Zip-up products in one call (SURVEY §8(b) `ttk_zipup`; `tt_fast_matrix_vec_mul`,
+ * `tt_fast_mat_mat_mul`, `tt_fast_hadamard`, cy_src/tt_ops_cy.pyx:391-502).  The device computes the
+ * exact core-wise product (Kronecker bonds) and rounds it once at eps with ttk_round -- the same
+ * represented tensor as the reference's SVD-swap zip-up to within the eps both truncate at
+ * (DESIGN.md §3.1).  kind: 0 matvec  a (ra, m, n, Ra) x b (rb, n, Rb)        -> (ra rb, m, Ra Rb)
+ *                         1 matmat  a (ra, m, k, Ra) x b (rb, k, n, Rb)     -> (ra rb, m, n, Ra Rb)
+ *                         2 hadamard of vector trains (ra, i, Ra) o (rb, i, Rb)
+ *                         3 hadamard of matrix trains (ra, i, j, Ra) o (rb, i, j, Rb)
+ * modes[3k..3k+2] = the physical extents of core k: (m, n, -), (m, k, n), (i, -, -), (i, j, -).
+ * a_ranks / b_ranks: d+1 bond ranks each.  out[k]: caller-owned contiguous buffers of the unrounded
+ * product core's size, rewritten in place by the rounding (ranks never grow); out_ranks: d+1, the
+ * rounded ranks.  eps <= 0 or d == 1: the exact product, unrounded. */
+int ttk_zipup(ttk_ctx ctx, int kind, int d, const double *const *a, const int64_t *a_ranks,
+              const double *const *b, const int64_t *b_ranks, const int64_t *modes, double eps,
+              double *const *out, int64_t *out_ranks);
 
 /* Dense Schur-complement local KKT solve in one call (SURVEY §8(b) `ttk_local_assemble` +
  * `ttk_dense_schur_solve`; the dense branch of `_ipm_local_solver`, src/tt_ipm.py:183-229):

@@ -80,6 +80,7 @@ _SIGS = {
     "ttk_lgmres": (i32, [vp, i64, vp, vp, i64, i32, i32, f64, i32, i32, vp]),
     "ttk_env_update": (i32, [vp, i32, i32, vp]),
     "ttk_round": (i32, [vp, i32, vp, vp, vp, f64, i32, vp]),
+    "ttk_zipup": (i32, [vp, i32, i32, vp, vp, vp, vp, vp, f64, vp, vp]),
     "ttk_dense_schur_solve": (i32, [vp, i64, i64, i64, vp, vp, vp, vp, vp]),
     "ttk_dense_schur_solve_ineq": (i32, [vp, i64, i64, i64, vp, vp, vp, vp]),
     "ttk_fused_set_mfma": (i32, [i32]),
@@ -92,9 +93,11 @@ _SIGS = {
     "ttk_contract_stats": (i32, [vp, i32]),
     "ttk_syev_extreme": (i32, [vp, vp, i32, i32, vp, vp, vp]),
     "ttk_lgmres_arnoldi_sync": (i32, [vp, vp, i32, i32, vp, i32, f64, c_dp, c_ip]),
-    "ttk_schur_build": (i32, [i32, i64, c_i64p, vp, c_i64p]),
+    "ttk_schur_build": (i32, [vp, i32, i64, c_i64p, vp, c_i64p]),
     "ttk_schur_apply": (i32, [vp, i64, vp, vp]),
-    "ttk_schur_free": (i32, [i64]),
+    "ttk_schur_free": (i32, [vp, i64]),
+    "ttk_ctx_set_knob": (i32, [vp, i32, i32, c_ip]),
+    "ttk_ctx_get_knob": (i32, [vp, i32, c_ip]),
     "ttk_lgmres_arnoldi_async": (i32, [vp, vp, i32, i32, vp, i32, f64, f64, f64, vp, i32, f64]),
     "ttk_lgmres_chunk": (i32, [vp, i64, vp, i32, i32, i32, vp, i32, f64, f64, f64, vp, f64]),
     "ttk_lgmres_build": (i32, [vp, vp, i32, i32, ctypes.POINTER(vp), i32, i32, vp, vp]),
@@ -112,6 +115,8 @@ for _name, (_res, _args) in _SIGS.items():
 EXPORTED = tuple(_SIGS)
 
 TTK_OK, TTK_ERR_ARG, TTK_ERR_HIP, TTK_ERR_NOT_PD, TTK_ERR_SINGULAR, TTK_ERR_NOT_CONVERGED = range(6)
+# per-context numerics knobs (include/ttk.h enum ttk_knob)
+KNOB_FUSED_APPLY, KNOB_FUSED_MFMA, KNOB_SPLITK, KNOB_SPLITK_MINK, KNOB_LGMRES_MW_MIN = range(5)
 
 
 class TTKError(RuntimeError):

@@ -667,7 +667,12 @@ extern "C" {
 }  // extern "C"
 
 namespace {
-bool g_splitk_on = true;
+// split-K on/off and K per split: per-context knobs (TTK_KNOB_SPLITK / _SPLITK_MINK)
+static inline bool splitk_on() { return ttk::ctx().knob[TTK_KNOB_SPLITK] != 0; }
+static inline int splitk_mink() {
+  const int k = ttk::ctx().knob[TTK_KNOB_SPLITK_MINK];
+  return k > 0 ? k : 256;
+}
 
 double *splitk_scratch(int64_t n) {  // partial-sum slabs of the current context (grown, never shrunk)
   ttk::Ctx &c = ttk::ctx();
@@ -696,8 +701,9 @@ std::map<std::array<int, 4>, std::pair<long long, double>> g_hist;
 extern "C" {
 
 int ttk_gemm_set_splitk(int on) {
-  const int old = g_splitk_on ? 1 : 0;
-  g_splitk_on = on != 0;
+  int &k = ttk::ctx().knob[TTK_KNOB_SPLITK];
+  const int old = k != 0 ? 1 : 0;
+  k = on != 0;
   return old;
 }
 
@@ -716,7 +722,7 @@ int ttk_gemm_hist(int on, const char *dump_path) {
   return TTK_OK;
 }
 
-static int g_splitk_mink = getenv("TTK_SPLITK_MINK") ? atoi(getenv("TTK_SPLITK_MINK")) : 256;  // K per split (128 is 15 % faster on graphm_3 but moves maxcut_12 s80 off the reference path)
+// K per split: splitk_mink() (128 is 15 % faster on graphm_3 but moves maxcut_12 s80 off the reference path)
 static int g_gemm64_min = getenv("TTK_GEMM64_MIN") ? atoi(getenv("TTK_GEMM64_MIN")) : 64;
 static int g_gemm64_ks = getenv("TTK_GEMM64_KS") ? atoi(getenv("TTK_GEMM64_KS")) : 32;
 
@@ -740,8 +746,8 @@ int ttk_gemm_offs(void *stream, const double *A, const double *B, double *C, con
   // split-K when the tile grid cannot fill the chip and K is long: each split runs >= 256 of K
   const int64_t tiles = (int64_t)grid.x * grid.y * nb;
   int nsplit = 1;
-  if (g_splitk_on && tiles < 256 && K >= 2 * g_splitk_mink) {
-    nsplit = (int)(K / g_splitk_mink);
+  if (splitk_on() && tiles < 256 && K >= 2 * splitk_mink()) {
+    nsplit = (int)(K / splitk_mink());
     const int64_t cap = (512 + tiles - 1) / tiles;
     if (nsplit > cap) nsplit = (int)cap;
     if ((int64_t)nsplit * nb > 65535) nsplit = (int)(65535 / nb);
@@ -786,7 +792,7 @@ namespace ttk {
 bool gemm_groupable(int nb, int M, int N, int K) {
   if (nb <= 0 || M <= 0 || N <= 0 || K <= 0 || nb > 65535) return false;
   const int64_t tiles = (int64_t)((N + TN - 1) / TN) * ((M + TM - 1) / TM) * nb;
-  if (g_splitk_on && tiles < 256 && K >= 2 * g_splitk_mink) return false;  // split-K path
+  if (splitk_on() && tiles < 256 && K >= 2 * splitk_mink()) return false;  // split-K path
   if (M >= g_gemm64_min && N >= g_gemm64_min && K >= 64 &&
       (int64_t)((M + BM - 1) / BM) * ((N + BN - 1) / BN) * nb >= 512)
     return false;  // throughput variant: the problem fills the chip on its own
@@ -879,6 +885,7 @@ int ttk_mul_nd(void *stream, const double *src, const double *src2, double *dst,
 int ttk_axpby_nd(void *stream, const double *src, const double *src2, double *dst, int ndim, const int64_t *shape,
                  const int64_t *sstride, const int64_t *s2stride, const int64_t *dstride, double alpha, double beta,
                  double gamma) {
+  if (int brc = ttk::batch_barrier(stream)) return brc;  // an open einsum batch may feed this call
   ttk::NdDesc d;
   int st = make_nd(d, ndim, shape, sstride, s2stride, dstride);
   if (st) return st;
@@ -891,6 +898,7 @@ int ttk_axpby_nd(void *stream, const double *src, const double *src2, double *ds
 
 int ttk_tt_join(void *stream, const double *a, const double *b, double *out, int ra, int Ra, int rb, int Rb,
                 int64_t mid, int mode) {
+  if (int brc = ttk::batch_barrier(stream)) return brc;  // an open einsum batch may feed this call
   if (mode < 0 || mode > 2 || (mode == 1 && ra != rb) || (mode == 2 && Ra != Rb)) {
     ttk::set_error("ttk_tt_join: bad mode %d / shapes", mode);
     return TTK_ERR_ARG;
@@ -905,6 +913,7 @@ int ttk_tt_join(void *stream, const double *a, const double *b, double *out, int
 
 int ttk_scale_axis(void *stream, const double *src, double *dst, int ndim, const int64_t *shape,
                    const int64_t *sstride, const int64_t *dstride, int axis, const double *scales) {
+  if (int brc = ttk::batch_barrier(stream)) return brc;  // an open einsum batch may feed this call
   ttk::NdDesc d;
   int st = make_nd(d, ndim, shape, sstride, dstride, nullptr);
   if (st) return st;
@@ -924,6 +933,7 @@ int ttk_scale_axis(void *stream, const double *src, double *dst, int ndim, const
 
 int ttk_scale_axis_ss(void *stream, const double *src, double *dst, int ndim, const int64_t *shape,
                       const int64_t *sstride, const int64_t *dstride, int axis, const double *ss, int invert) {
+  if (int brc = ttk::batch_barrier(stream)) return brc;  // an open einsum batch may feed this call
   ttk::NdDesc d;
   int st = make_nd(d, ndim, shape, sstride, dstride, nullptr);
   if (st) return st;
@@ -939,6 +949,7 @@ int ttk_scale_axis_ss(void *stream, const double *src, double *dst, int ndim, co
 }
 
 int ttk_recip(void *stream, const double *src, double *dst, int64_t n) {
+  if (int brc = ttk::batch_barrier(stream)) return brc;  // an open einsum batch may feed this call
   if (n <= 0) return TTK_OK;
   hipLaunchKernelGGL(recip_kernel, dim3(grid_for(n, 256)), dim3(256), 0, TTK_STREAM(stream), src, dst, n);
   TTK_LAUNCH_CHECK();
@@ -946,6 +957,7 @@ int ttk_recip(void *stream, const double *src, double *dst, int64_t n) {
 }
 
 int ttk_fill(void *stream, double *dst, int64_t n, double value) {
+  if (int brc = ttk::batch_barrier(stream)) return brc;  // an open einsum batch may feed this call
   if (n <= 0) return TTK_OK;
   hipLaunchKernelGGL(fill_kernel, dim3(grid_for(n, 256)), dim3(256), 0, TTK_STREAM(stream), dst, n, value);
   TTK_LAUNCH_CHECK();
@@ -953,6 +965,7 @@ int ttk_fill(void *stream, double *dst, int64_t n, double value) {
 }
 
 int ttk_add_diag(void *stream, double *A, int n, int lda, double value) {
+  if (int brc = ttk::batch_barrier(stream)) return brc;  // an open einsum batch may feed this call
   if (n <= 0) return TTK_OK;
   hipLaunchKernelGGL(add_diag_kernel, dim3(grid_for(n, 256)), dim3(256), 0, TTK_STREAM(stream), A, n, lda, value);
   TTK_LAUNCH_CHECK();
@@ -961,6 +974,7 @@ int ttk_add_diag(void *stream, double *A, int n, int lda, double value) {
 
 int ttk_dot_nd_sync(void *stream, const double *x, const double *y, int ndim, const int64_t *shape,
                     const int64_t *xstride, const int64_t *ystride, double *result) {
+  if (int brc = ttk::batch_barrier(stream)) return brc;  // an open einsum batch may feed this call
   ttk::NdDesc d;
   int st = make_nd(d, ndim, shape, xstride, ystride, nullptr);
   if (st) return st;
@@ -983,6 +997,7 @@ int ttk_dot_nd_sync(void *stream, const double *x, const double *y, int ndim, co
 
 int ttk_dot_nd_dev(void *stream, const double *x, const double *y, int ndim, const int64_t *shape,
                    const int64_t *xstride, const int64_t *ystride, double *out) {
+  if (int brc = ttk::batch_barrier(stream)) return brc;  // an open einsum batch may feed this call
   ttk::NdDesc d;
   int st = make_nd(d, ndim, shape, xstride, ystride, nullptr);
   if (st) return st;
@@ -997,6 +1012,7 @@ int ttk_dot_nd_dev(void *stream, const double *x, const double *y, int ndim, con
 
 int ttk_normalize(void *stream, const double *x, double *out, int ndim, const int64_t *shape,
                   const int64_t *xstride) {
+  if (int brc = ttk::batch_barrier(stream)) return brc;  // an open einsum batch may feed this call
   ttk::NdDesc d;
   int64_t ost[ttk::MAXD];
   if (ndim > ttk::MAXD || ndim < 0) {
@@ -1017,6 +1033,7 @@ int ttk_normalize(void *stream, const double *x, double *out, int ndim, const in
 }
 
 int ttk_rayleigh_tail_sync(void *stream, const double *v, double *Mv, int64_t n, double *ev_out, double *res2_out) {
+  if (int brc = ttk::batch_barrier(stream)) return brc;  // an open einsum batch may feed this call
   double *dev = nullptr;
   double *h = ttk::mapped_stage(2, &dev);
   if (!h) {
@@ -1034,12 +1051,14 @@ int ttk_rayleigh_tail_sync(void *stream, const double *v, double *Mv, int64_t n,
 
 // the same tail with (ev, ||Mv - ev v||^2) left in device memory (read later, batched with others)
 int ttk_rayleigh_tail_dev(void *stream, const double *v, double *Mv, int64_t n, double *out2) {
+  if (int brc = ttk::batch_barrier(stream)) return brc;  // an open einsum batch may feed this call
   hipLaunchKernelGGL(rayleigh_tail_kernel, dim3(1), dim3(1024), 0, TTK_STREAM(stream), v, Mv, n, out2, 1.0);
   TTK_LAUNCH_CHECK();
   return TTK_OK;
 }
 
 int ttk_sumsq_batched(void *stream, const double *x, int64_t n, int nb, int64_t bstride, double *out) {
+  if (int brc = ttk::batch_barrier(stream)) return brc;  // an open einsum batch may feed this call
   if (nb <= 0) return TTK_OK;
   hipLaunchKernelGGL(sumsq_batched_kernel, dim3(nb), dim3(256), 0, TTK_STREAM(stream), x, n, bstride, out);
   TTK_LAUNCH_CHECK();

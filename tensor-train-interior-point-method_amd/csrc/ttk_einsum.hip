@@ -342,7 +342,7 @@ bool build_plan(const std::string &eq, int nops, const int *ndims, const int64_t
 }  // namespace
 
 int fused_apply_try(void *stream, const char *eq, const int64_t *desc, double *out, double alpha, double beta);
-static int g_fused_apply = 1;
+static inline int &fused_apply_knob() { return ttk::ctx().knob[TTK_KNOB_FUSED_APPLY]; }
 
 // einsum batches (defined at the end of this file)
 struct Span {
@@ -357,15 +357,15 @@ int batch_flush(hipStream_t st);
 extern "C" {
 
 int ttk_einsum_set_fused(int on) {
-  const int old = g_fused_apply;
-  g_fused_apply = on;
+  const int old = fused_apply_knob();
+  fused_apply_knob() = on;
   return old;
 }
 
 // desc: [nops, then per operand: ptr, ndim, shape..., stride..., then has_out_strides, (out ndim,
 // out strides...)]
 int ttk_einsum(void *stream, const char *eq, const int64_t *desc, double *out, double alpha, double beta) {
-  if (g_fused_apply) {
+  if (fused_apply_knob()) {
     const int rc = fused_apply_try(stream, eq, desc, out, alpha, beta);
     if (rc != 0) return rc < 0 ? TTK_ERR_HIP : TTK_OK;
   }
@@ -922,8 +922,7 @@ static double fused_max_flops() {
 // ApplyArgs of a local-apply equation from an einsum descriptor (see ttk_einsum); 1 if the fused
 // kernel can run it (LDS and grid limits), 0 otherwise
 // MFMA stages for the blocks beyond the VALU kernel's FLOP range (TTK_FUSED_MFMA=0: pairwise plan)
-static int g_fused_mfma = !getenv("TTK_FUSED_MFMA") || atoi(getenv("TTK_FUSED_MFMA")) != 0;
-static bool mfma_enabled() { return g_fused_mfma != 0; }
+static bool mfma_enabled() { return ttk::ctx().knob[TTK_KNOB_FUSED_MFMA] != 0; }
 // threads per workgroup of launches that carry MFMA-stage rows: the staging loops gather x, Q and A
 // from L2 with one workgroup per CU (LDS-bound occupancy), so 16 waves keep 4x the loads in flight of
 // 4; every output element / tile is still computed by one thread / wave in the same order
@@ -939,8 +938,9 @@ extern "C" int ttk_mfma_profile(unsigned long long *out8, int reset) {  // g_mph
 }
 
 extern "C" int ttk_fused_set_mfma(int on) {
-  const int old = g_fused_mfma;
-  g_fused_mfma = on;
+  int &k = ttk::ctx().knob[TTK_KNOB_FUSED_MFMA];
+  const int old = k;
+  k = on;
   return old;
 }
 
@@ -1203,7 +1203,8 @@ static int schur_apply_pairwise(void *stream, const SchurOp &op, const double *v
 
 extern "C" {
 
-int ttk_schur_build(int ineq, int64_t m, const int64_t *descs, const double *inv_I, int64_t *handle) {
+int ttk_schur_build(ttk_ctx ctx, int ineq, int64_t m, const int64_t *descs, const double *inv_I, int64_t *handle) {
+  ttk::CtxScope scope(ctx);
   *handle = 0;
   constexpr int W = 36;  // words per block descriptor: nops + 4 operand records (3/4/3/3-D) + has_out = 0
   const int nblk = ineq ? 7 : 5;
@@ -1288,7 +1289,9 @@ int ttk_schur_build(int ineq, int64_t m, const int64_t *descs, const double *inv
   return schur_store(op, m, handle);
 }
 
-int ttk_schur_apply(void *stream, int64_t handle, const double *v, double *out) {
+}  // extern "C"
+
+int ttk::schur_apply(void *stream, int64_t handle, const double *v, double *out) {
   std::vector<SchurOp> &ops = schur_ops();
   if (handle < 1 || handle > (int64_t)ops.size() || !ops[handle - 1].used) {
     ttk::set_error("ttk_schur_apply: bad handle %lld", (long long)handle);
@@ -1325,7 +1328,15 @@ int ttk_schur_apply(void *stream, int64_t handle, const double *v, double *out) 
   return TTK_OK;
 }
 
-int ttk_schur_free(int64_t handle) {
+extern "C" {
+
+int ttk_schur_apply(ttk_ctx ctx, int64_t handle, const double *v, double *out) {
+  ttk::CtxScope scope(ctx);
+  return ttk::schur_apply(ttk::ctx().stream, handle, v, out);
+}
+
+int ttk_schur_free(ttk_ctx ctx, int64_t handle) {
+  ttk::CtxScope scope(ctx);
   std::vector<SchurOp> &ops = schur_ops();
   if (handle >= 1 && handle <= (int64_t)ops.size()) ops[handle - 1].used = false;
   return TTK_OK;
@@ -1343,8 +1354,9 @@ int ttk_schur_free(int64_t handle) {
 // split-K or 64x64 path alone are launched alone) plus one grouped fused-apply launch, so a core
 // step's environment updates or a rank loop's candidate products cost a handful of launches
 // instead of one per pairwise step.  Results are bit-identical to the unbatched calls (same
-// kernels' per-element operations, same order per output element).  Any other libttk launch made
-// while a batch is open flushes the pending nodes first (ttk::batch_barrier), so stream order holds.
+// kernels' per-element operations, same order per output element).  Every other stream entry point
+// of the library flushes the pending nodes first (ttk::batch_barrier), so stream order holds; each
+// ttk_einsum_batch_end, nested or not, launches what is pending.
 namespace {
 
 struct BNode {

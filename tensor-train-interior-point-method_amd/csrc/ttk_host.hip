@@ -418,3 +418,45 @@ int ttk_round(ttk_ctx ctx, int d, double *const *cores, const int64_t *inner, in
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------- zip-up products (one call)
+// `tt_fast_matrix_vec_mul` / `tt_fast_mat_mat_mul` / `tt_fast_hadamard` (cy_src/tt_ops_cy.pyx:
+// 391-502) as the device path computes them: the exact core-wise product with
+// Kronecker bonds, one einsum per core into the caller's buffer, then ONE rounding at eps
+// (ttk_round mode 0, in place).  Same einsum plans and the same rounding launches as
+// tt_ops.tt_fast_* in Python, so bit-identical to it.
+extern "C" int ttk_zipup(ttk_ctx ctx, int kind, int d, const double *const *a, const int64_t *a_ranks,
+                         const double *const *b, const int64_t *b_ranks, const int64_t *modes, double eps,
+                         double *const *out, int64_t *out_ranks) {
+  ttk::CtxScope scope(ctx);
+  hipStream_t st = ttk::ctx().stream;
+  if (d < 1 || kind < 0 || kind > 3 || !a || !b || !a_ranks || !b_ranks || !modes || !out || !out_ranks) {
+    ttk::set_error("ttk_zipup: bad arguments");
+    return TTK_ERR_ARG;
+  }
+  std::vector<int64_t> inner(d);
+  int rc = TTK_OK;
+  for (int k = 0; k < d && rc == TTK_OK; ++k) {
+    const int64_t ra = a_ranks[k], Ra = a_ranks[k + 1], rb = b_ranks[k], Rb = b_ranks[k + 1];
+    const int64_t m0 = modes[3 * k], m1 = modes[3 * k + 1], m2 = modes[3 * k + 2];
+    const View A4{a[k], 4, {ra, m0, m1, Ra}, {m0 * m1 * Ra, m1 * Ra, Ra, 1}};
+    if (kind == 0) {  // mat (ra, m, n, Ra) x vec (rb, n, Rb) -> (ra rb, m, Ra Rb)
+      rc = einsum(st, "amnA,rnR->armAR", {A4, v3(b[k], rb, m1, Rb)}, out[k]);
+      inner[k] = m0;
+    } else if (kind == 1) {  // (ra, m, k, Ra) x (rb, k, n, Rb) -> (ra rb, m, n, Ra Rb)
+      const View B4{b[k], 4, {rb, m1, m2, Rb}, {m1 * m2 * Rb, m2 * Rb, Rb, 1}};
+      rc = einsum(st, "amkA,bknB->abmnAB", {A4, B4}, out[k]);
+      inner[k] = m0 * m2;
+    } else if (kind == 2) {  // vectors (ra, i, Ra) o (rb, i, Rb)
+      rc = einsum(st, "aiA,biB->abiAB", {v3(a[k], ra, m0, Ra), v3(b[k], rb, m0, Rb)}, out[k]);
+      inner[k] = m0;
+    } else {  // matrices (ra, i, j, Ra) o (rb, i, j, Rb)
+      const View B4{b[k], 4, {rb, m0, m1, Rb}, {m0 * m1 * Rb, m1 * Rb, Rb, 1}};
+      rc = einsum(st, "aijA,bijB->abijAB", {A4, B4}, out[k]);
+      inner[k] = m0 * m1;
+    }
+  }
+  for (int k = 0; k <= d; ++k) out_ranks[k] = a_ranks[k] * b_ranks[k];
+  if (rc != TTK_OK || d == 1 || !(eps > 0.0)) return rc;  // _kron_round: no rounding
+  return ttk_round(ctx, d, out, inner.data(), out_ranks, eps, 0, nullptr);
+}

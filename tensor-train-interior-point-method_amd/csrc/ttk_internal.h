@@ -4,9 +4,15 @@
 
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "../../include/ttk.h"
 
 namespace ttk {
+inline int env_int(const char *name, int dflt) {
+  const char *v = std::getenv(name);
+  return v ? std::atoi(v) : dflt;
+}
 // Per-context state (`ttk_ctx`): every scratch buffer, staging ring and handle table the library
 // keeps between calls lives in a context, so two contexts (each with its own stream, driven by its
 // own host thread) never share mutable state.  The plan cache (immutable plans + their offset
@@ -41,6 +47,11 @@ struct Ctx {
   int up_next = 0;
   hipStream_t side = nullptr;  // second stream (dgecon overlapped with the rest of a dense solve)
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  // numerics knobs (ttk_ctx_set_knob; several change summation order, so they are per context:
+  // flipping one on a context never changes another context's results).  Defaults from the
+  // environment at context creation.
+  int knob[TTK_KNOB_COUNT] = {1, env_int("TTK_FUSED_MFMA", 1) != 0 ? 1 : 0, 1, env_int("TTK_SPLITK_MINK", 256),
+                              16384};
 };
 Ctx &ctx();
 Ctx *ctx_swap(Ctx *c);  // bind c to the calling thread, return the previous binding
@@ -96,6 +107,8 @@ bool gemm_groupable(int nb, int M, int N, int K);
 int gemm_group(hipStream_t st, const GemmProblem *p, int n);
 // ttk_einsum.hip: launch the pending nodes of an open einsum batch (stream order for other launches)
 int batch_barrier(void *stream);
+// ttk_einsum.hip: one application of the current context's Schur operator handle on `stream`
+int schur_apply(void *stream, int64_t handle, const double *v, double *out);
 }  // namespace ttk
 
 #endif

@@ -376,7 +376,8 @@ double *lgmres_scratch(int64_t n) {  // partials / norm parts of the current con
   return c.lgmres;
 }
 
-int g_lgmres_mw_min = 16384;  // (it+1)*n at or above which the multi-workgroup kernels run
+// (it+1)*n at or above which the multi-workgroup kernels run: per-context knob
+static inline int64_t mw_min() { return ttk::ctx().knob[TTK_KNOB_LGMRES_MW_MIN]; }
 
 }  // namespace
 
@@ -390,7 +391,7 @@ static int arnoldi_launch(hipStream_t st_, double *V, int n, int it, double *hh,
     ttk::set_error("%s: restart %d too large (max %d)", who, max_k, MAXV);
     return TTK_ERR_ARG;
   }
-  if ((int64_t)(it + 1) * n >= g_lgmres_mw_min) {
+  if ((int64_t)(it + 1) * n >= mw_min()) {
     const int nchunk = (n + ARN_CHUNK - 1) / ARN_CHUNK, nblk = (n + ARN_UPD - 1) / ARN_UPD;
     double *partials = lgmres_scratch((int64_t)(it + 1) * nchunk + nblk + 64);
     if (!partials) {
@@ -415,6 +416,7 @@ extern "C" {
 
 int ttk_lgmres_arnoldi_sync(void *stream, double *V, int n, int it, double *hh, int max_k, double haptol,
                             double *res_out, int *hapend_out) {
+  if (int brc = ttk::batch_barrier(stream)) return brc;  // an open einsum batch may feed this call
   const Ctl none{nullptr, 0, 0.0, 0.0, 0.0};
   int rc = arnoldi_launch(TTK_STREAM(stream), V, n, it, hh, max_k, haptol, none, "ttk_lgmres_arnoldi_sync");
   if (rc) return rc;
@@ -432,15 +434,17 @@ int ttk_lgmres_arnoldi_sync(void *stream, double *V, int n, int it, double *hh, 
 
 int ttk_lgmres_arnoldi_async(void *stream, double *V, int n, int it, double *hh, int max_k, double haptol,
                              double ttol, double divtol, double *ctl, int slot, double marker) {
+  if (int brc = ttk::batch_barrier(stream)) return brc;  // an open einsum batch may feed this call
   const Ctl cl{ctl, slot, marker, ttol, divtol};
   return arnoldi_launch(TTK_STREAM(stream), V, n, it, hh, max_k, haptol, cl, "ttk_lgmres_arnoldi_async");
 }
 
 int ttk_lgmres_chunk(void *stream, int64_t schur, double *V, int n, int it0, int k, double *hh, int max_k,
                      double haptol, double ttol, double divtol, double *ctl, double marker0) {
+  if (int brc = ttk::batch_barrier(stream)) return brc;  // an open einsum batch may feed this call
   for (int q = 0; q < k; ++q) {
     const int it = it0 + q;
-    int rc = ttk_schur_apply(stream, schur, V + (int64_t)it * n, V + (int64_t)(it + 1) * n);
+    int rc = ttk::schur_apply(stream, schur, V + (int64_t)it * n, V + (int64_t)(it + 1) * n);
     if (rc) return rc;
     rc = ttk_lgmres_arnoldi_async(stream, V, n, it, hh, max_k, haptol, ttol, divtol, ctl, q, marker0 + q);
     if (rc) return rc;
@@ -450,13 +454,14 @@ int ttk_lgmres_chunk(void *stream, int64_t schur, double *V, int n, int it0, int
 
 int ttk_lgmres_build(void *stream, double *hh, int max_k, int it, const double *const *basis, int nvec, int n,
                      double *x, double *aug_temp) {
+  if (int brc = ttk::batch_barrier(stream)) return brc;  // an open einsum batch may feed this call
   if (nvec > MAXV || it + 1 > MAXV) {
     ttk::set_error("ttk_lgmres_build: too many basis vectors %d", nvec);
     return TTK_ERR_ARG;
   }
   PtrList pl;
   for (int j = 0; j < nvec; ++j) pl.p[j] = basis[j];
-  if ((int64_t)nvec * n >= g_lgmres_mw_min) {
+  if ((int64_t)nvec * n >= mw_min()) {
     hipLaunchKernelGGL(build_solve_kernel, dim3(1), dim3(1), 0, TTK_STREAM(stream), hh, max_k, it);
     hipLaunchKernelGGL(build_axpy_kernel, dim3((n + 255) / 256), dim3(256), 0, TTK_STREAM(stream), hh, max_k, pl,
                        nvec, n, x, aug_temp);
@@ -470,12 +475,13 @@ int ttk_lgmres_build(void *stream, double *hh, int max_k, int it, const double *
 
 int ttk_lgmres_aug(void *stream, const double *hh, int max_k, int it_total, const double *V, int n,
                    double inv_nrm_unused, const double *aug_temp, double *augvec, double *a_augvec) {
+  if (int brc = ttk::batch_barrier(stream)) return brc;  // an open einsum batch may feed this call
   (void)inv_nrm_unused;
   if (it_total + 1 > MAXV) {
     ttk::set_error("ttk_lgmres_aug: it_total %d too large", it_total);
     return TTK_ERR_ARG;
   }
-  if ((int64_t)(it_total + 1) * n >= g_lgmres_mw_min) {
+  if ((int64_t)(it_total + 1) * n >= mw_min()) {
     const int nblk = (n + ARN_UPD - 1) / ARN_UPD;
     double *part = lgmres_scratch(nblk + 64);
     if (!part) {
@@ -536,12 +542,17 @@ int ttk_lgmres(ttk_ctx ctx, int64_t schur, const double *b, double *x, int64_t n
   // workspace: V | hh | augvecs | a_augvecs | aug_temp | ctl
   const int64_t nV = (int64_t)(max_k + 1) * n, nH = hh_size(max_k), nA = (int64_t)nd * n, nC = 1 + 5 * (int64_t)chunk;
   const int64_t need = nV + nH + 2 * nA + n + nC + 64;
-  double *ws = lgmres_scratch(need + 1 + 65536);  // the first 65536 doubles stay the partials slab
+  // the scratch base holds the multi-workgroup Arnoldi / augmentation partials (arnoldi_launch,
+  // ttk_lgmres_aug: (it+1)*ceil(n/ARN_CHUNK) + ceil(n/ARN_UPD) + 64 doubles at most); the solve's
+  // workspace starts after that slab so the partials can never overwrite V
+  const int64_t slab0 = (int64_t)(max_k + 2) * ((n + ARN_CHUNK - 1) / ARN_CHUNK) + (n + ARN_UPD - 1) / ARN_UPD + 64;
+  const int64_t slab = slab0 > 65536 ? slab0 : 65536;
+  double *ws = lgmres_scratch(need + 1 + slab);
   if (!ws) {
     ttk::set_error("ttk_lgmres: workspace allocation failed");
     return TTK_ERR_HIP;
   }
-  ws += 65536;
+  ws += slab;
   double *V = ws, *hh = V + nV, *augvecs = hh + nH, *a_augvecs = augvecs + nA, *aug_temp = a_augvecs + nA,
          *ctl = aug_temp + n;
   const int64_t grs_off = 2 * (int64_t)(max_k + 2) * (max_k + 1);
@@ -564,7 +575,7 @@ int ttk_lgmres(ttk_ctx ctx, int64_t schur, const double *b, double *x, int64_t n
   };
   int it_arnoldi = max_k - aug_dim;
   auto matvec_or_aug = [&](int li) {
-    if (li < it_arnoldi) return ttk_schur_apply(stream, schur, V + (int64_t)li * n, V + (int64_t)(li + 1) * n);
+    if (li < it_arnoldi) return ttk::schur_apply(stream, schur, V + (int64_t)li * n, V + (int64_t)(li + 1) * n);
     const int64_t order = li - it_arnoldi + 1;
     int spot = 0;
     for (int ii = 0; ii < aug_dim; ++ii)
@@ -578,7 +589,7 @@ int ttk_lgmres(ttk_ctx ctx, int64_t schur, const double *b, double *x, int64_t n
     if (guess_zero) {
       if ((rc = copy(V, b, 1.0, 0.0))) return rc;
     } else {
-      if ((rc = ttk_schur_apply(stream, schur, x, V))) return rc;
+      if ((rc = ttk::schur_apply(stream, schur, x, V))) return rc;
       ++nmv;
       if ((rc = copy(V, b, 1.0, -1.0))) return rc;  // r = b - A x
     }
@@ -724,8 +735,9 @@ int ttk_lgmres(ttk_ctx ctx, int64_t schur, const double *b, double *x, int64_t n
 }
 
 int ttk_lgmres_set_mw_threshold(int elems) {
-  const int old = g_lgmres_mw_min;
-  g_lgmres_mw_min = elems;
+  int &k = ttk::ctx().knob[TTK_KNOB_LGMRES_MW_MIN];
+  const int old = k;
+  k = elems;
   return old;
 }
 

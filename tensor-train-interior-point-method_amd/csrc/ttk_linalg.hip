@@ -2424,11 +2424,13 @@ int64_t ttk_svd_work(int m, int n) {
 }
 
 int ttk_svd(void *stream, const double *A, int m, int n, double *U, double *S, double *Vt, double *work) {
+  if (int brc = ttk::batch_barrier(stream)) return brc;  // an open einsum batch may feed this call
   return ttk_svd_tol(stream, A, m, n, U, S, Vt, work, 0.0);
 }
 
 int ttk_svd_tol(void *stream, const double *A, int m, int n, double *U, double *S, double *Vt, double *work,
                 double defl) {
+  if (int brc = ttk::batch_barrier(stream)) return brc;  // an open einsum batch may feed this call
   if (m <= 0 || n <= 0) {
     ttk::set_error("ttk_svd: empty matrix %dx%d", m, n);
     return TTK_ERR_ARG;
@@ -2487,6 +2489,7 @@ int64_t ttk_qr_work(int m, int n) {
 }
 
 int ttk_qr(void *stream, const double *A, int m, int n, double *Q, double *R, double *work) {
+  if (int brc = ttk::batch_barrier(stream)) return brc;  // an open einsum batch may feed this call
   if (m <= 0 || n <= 0) {
     ttk::set_error("ttk_qr: empty matrix %dx%d", m, n);
     return TTK_ERR_ARG;
@@ -2512,6 +2515,7 @@ int ttk_dense_set_block_min(int n) {
 }
 
 int ttk_cholesky_sync(void *stream, double *A, int n) {
+  if (int brc = ttk::batch_barrier(stream)) return brc;  // an open einsum batch may feed this call
   if (ensure_status()) {
     ttk::set_error("ttk_cholesky_sync: status alloc failed");
     return TTK_ERR_HIP;
@@ -2535,6 +2539,7 @@ int ttk_cholesky_sync(void *stream, double *A, int n) {
 }
 
 int ttk_trsm_lower(void *stream, const double *L, int n, double *B, int nrhs, int ldb, int trans) {
+  if (int brc = ttk::batch_barrier(stream)) return brc;  // an open einsum batch may feed this call
   if (n <= 0 || nrhs <= 0) return TTK_OK;
   if (n >= g_dense_block_min) return ttk::trsm_blocked(TTK_STREAM(stream), L, n, B, nrhs, ldb, trans);
   hipLaunchKernelGGL(trsm_kernel, dim3((nrhs + 63) / 64), dim3(256), 0, TTK_STREAM(stream), L, n, B, nrhs, ldb, trans);
@@ -2543,6 +2548,7 @@ int ttk_trsm_lower(void *stream, const double *L, int n, double *B, int nrhs, in
 }
 
 int ttk_lu_sync(void *stream, double *A, int n, int *piv, double *work, double *rcond_out) {
+  if (int brc = ttk::batch_barrier(stream)) return brc;  // an open einsum batch may feed this call
   if (ensure_status()) {
     ttk::set_error("ttk_lu_sync: status alloc failed");
     return TTK_ERR_HIP;
@@ -2606,6 +2612,7 @@ int lu_rcond_join(hipStream_t st) {
 extern "C" {
 
 int ttk_lu_solve(void *stream, const double *LU, int n, const int *piv, double *B, int nrhs, int ldb) {
+  if (int brc = ttk::batch_barrier(stream)) return brc;  // an open einsum batch may feed this call
   if (n >= g_lu_block_min && n <= 12000 && nrhs <= 8 && nrhs > 0) return ttk::lu_solve_cols(TTK_STREAM(stream), LU, n, piv, B, nrhs, ldb);
   if (n <= 0 || nrhs <= 0) return TTK_OK;
   hipLaunchKernelGGL(lu_solve_kernel, dim3((nrhs + 63) / 64), dim3(256), 0, TTK_STREAM(stream), LU, n, piv, B, nrhs, ldb);
@@ -2616,6 +2623,7 @@ int ttk_lu_solve(void *stream, const double *LU, int n, const int *piv, double *
 int64_t ttk_syev_work(int n) { return 2 * (int64_t)n * n + 2 * (n / 2 + 1) + 2 * (int64_t)n + 16; }
 
 int ttk_syev(void *stream, double *A, int n, double *ev, double *W, double *work) {
+  if (int brc = ttk::batch_barrier(stream)) return brc;  // an open einsum batch may feed this call
   if (n <= 0) {
     ttk::set_error("ttk_syev: empty matrix");
     return TTK_ERR_ARG;
@@ -2664,6 +2672,7 @@ int ttk_syev_set_fused_max(int n) {
 }
 
 int ttk_syev_extreme(void *stream, const double *A, int n, int which, double *ev, double *vec, double *work) {
+  if (int brc = ttk::batch_barrier(stream)) return brc;  // an open einsum batch may feed this call
   if (n <= 0 || (which != 0 && which != 1)) {
     ttk::set_error("ttk_syev_extreme: bad arguments");
     return TTK_ERR_ARG;

@@ -92,6 +92,7 @@ long long ttk_launch_count(void) { return ttk::g_launches.load(); }
 long long ttk_sync_count(void) { return ttk::g_syncs.load(); }
 
 int ttk_upload(void *stream, const double *host, double *dev, int64_t n) {
+  if (int brc = ttk::batch_barrier(stream)) return brc;  // an open einsum batch may feed this call
   if (n <= 0) return TTK_OK;
   ttk::Ctx &c = ttk::ctx();  // host -> device through the context's ring of pinned slots
   ttk::UpSlot &sl = c.up[c.up_next];
@@ -119,6 +120,7 @@ int ttk_upload(void *stream, const double *host, double *dev, int64_t n) {
 static int g_mapped_reads = getenv("TTK_MAPPED_READS") ? atoi(getenv("TTK_MAPPED_READS")) : 1;
 
 int ttk_read_sync(void *stream, const double *src, double *host_dst, int64_t n) {
+  if (int brc = ttk::batch_barrier(stream)) return brc;  // an open einsum batch may feed this call
   if (n <= 0) return TTK_OK;
   if (n <= 65536 && g_mapped_reads) {  // small reads: one copy kernel into host-coherent memory
     double *dev = nullptr;
@@ -168,6 +170,26 @@ int ttk_ctx_create(void *stream, ttk_ctx *out) {
   }
   h->c.stream = TTK_STREAM(stream);
   *out = h;
+  return TTK_OK;
+}
+
+int ttk_ctx_set_knob(ttk_ctx h, int knob, int value, int *old) {
+  if (knob < 0 || knob >= TTK_KNOB_COUNT) {
+    ttk::set_error("ttk_ctx_set_knob: unknown knob %d", knob);
+    return TTK_ERR_ARG;
+  }
+  ttk::Ctx &c = h ? h->c : ttk::ctx();
+  if (old) *old = c.knob[knob];
+  c.knob[knob] = value;
+  return TTK_OK;
+}
+
+int ttk_ctx_get_knob(ttk_ctx h, int knob, int *value) {
+  if (knob < 0 || knob >= TTK_KNOB_COUNT) {
+    ttk::set_error("ttk_ctx_get_knob: unknown knob %d", knob);
+    return TTK_ERR_ARG;
+  }
+  *value = (h ? h->c : ttk::ctx()).knob[knob];
   return TTK_OK;
 }
 

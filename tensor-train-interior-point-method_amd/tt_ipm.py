@@ -73,15 +73,17 @@ class MatVecWrapper:
                 desc += D.apply_desc(self.L[k], self.A[k], self.R[k], shape)
             h = ctypes.c_int64(0)
             arr = (ctypes.c_int64 * len(desc))(*desc)
-            D.check(lib.ttk_schur_build(int(len(self.keys) > 4), self.m, arr, inv_I.contiguous().data_ptr(),
-                                        ctypes.byref(h)), "schur_build")
+            D._stream()
+            self._ctx = D.CTX[0] if D.CTX else None
+            D.check(lib.ttk_schur_build(self._ctx, int(len(self.keys) > 4), self.m, arr,
+                                        inv_I.contiguous().data_ptr(), ctypes.byref(h)), "schur_build")
             self.h = h.value
             self._inv = inv_I  # keep the operands alive while the handle exists
 
     def __del__(self):
         if getattr(self, "h", 0):
             try:
-                lib.ttk_schur_free(self.h)
+                lib.ttk_schur_free(self._ctx, self.h)
             except Exception:
                 pass
 
@@ -110,7 +112,8 @@ class MatVecWrapper:
     def matvec_into(self, v, out):
         if self.h:
             D.count_algo(self.mv_flops() if D.ALGO is not None else 0.0, what="schur_matvec")
-            D.check(lib.ttk_schur_apply(D._stream(), self.h, v.data_ptr(), out.data_ptr()), "schur_apply")
+            D._stream()
+            D.check(lib.ttk_schur_apply(self._ctx, self.h, v.data_ptr(), out.data_ptr()), "schur_apply")
             return out
         y, x = self._parts(v, 2)
         o0, o1 = self._parts(out, 2)
@@ -135,7 +138,8 @@ class IneqMatVecWrapper(MatVecWrapper):
             raise IneqMatvecBug("reference bug: IneqMatVecWrapper.matvec returns a memoryview")
         if self.h:
             D.count_algo(self.mv_flops() if D.ALGO is not None else 0.0, what="schur_matvec")
-            D.check(lib.ttk_schur_apply(D._stream(), self.h, v.data_ptr(), out.data_ptr()), "schur_apply")
+            D._stream()
+            D.check(lib.ttk_schur_apply(self._ctx, self.h, v.data_ptr(), out.data_ptr()), "schur_apply")
             return out
         y, x, t = self._parts(v, 3)
         o0, o1, o2 = self._parts(out, 3)

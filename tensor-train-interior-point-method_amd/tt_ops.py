@@ -473,11 +473,52 @@ def _kron_round(cores, eps):
     return cores
 
 
+NATIVE_ZIPUP = os.environ.get("TTIPM_NATIVE_ZIPUP", "1") == "1"
+
+
+def _native_zipup(kind, a, b, eps, out_modes):
+    """`ttk_zipup` (one library call: the core-wise products into fresh buffers + one in-place
+    rounding; the same einsum plans and rounding launches as the Python composition below, so
+    bit-identical to it).  out_modes[k]: the product core's physical shape."""
+    d = len(a)
+    ar = [a[0].shape[0]] + [c.shape[-1] for c in a]
+    br = [b[0].shape[0]] + [c.shape[-1] for c in b]
+    mids = []
+    for x, y in zip(a, b):
+        if kind == 0:
+            mids += [x.shape[1], x.shape[2], 1]
+        elif kind == 1:
+            mids += [x.shape[1], x.shape[2], y.shape[2]]
+        elif kind == 2:
+            mids += [x.shape[1], 1, 1]
+        else:
+            mids += [x.shape[1], x.shape[2], 1]
+    inner = [int(np.prod(m)) for m in out_modes]
+    outs = [D.empty(ar[k] * br[k] * inner[k] * ar[k + 1] * br[k + 1]) for k in range(d)]
+    ca = [D.contig(c) for c in a]
+    cb = [D.contig(c) for c in b]
+    P = ctypes.c_void_p
+    I64 = ctypes.c_int64
+    ranks = (I64 * (d + 1))()
+    D._stream()
+    D.check(D.lib.ttk_zipup(D.CTX[0], kind, d, (P * d)(*[c.data_ptr() for c in ca]), (I64 * (d + 1))(*ar),
+                            (P * d)(*[c.data_ptr() for c in cb]), (I64 * (d + 1))(*br), (I64 * (3 * d))(*mids),
+                            float(eps), (P * d)(*[o.data_ptr() for o in outs]), ranks), "zipup")
+    return [o[:ranks[k] * inner[k] * ranks[k + 1]].view(ranks[k], *out_modes[k], ranks[k + 1])
+            for k, o in enumerate(outs)]
+
+
+def _use_native_zipup():
+    return NATIVE_ZIPUP and NATIVE_ROUND and D.DEV.type == "cuda"
+
+
 def tt_fast_matrix_vec_mul(mat, vec, eps=1e-18):
     """`cy_src/tt_ops_cy.pyx:428-447`: mat (r_A,m,n,R_A) x vec (r,n,R) -> (r_A r, m, R_A R), rounded
     at eps (see the note above)."""
     if ZIPUP:
         return _zipup_matrix_vec_mul(mat, vec, eps)
+    if _use_native_zipup():
+        return _native_zipup(0, mat, vec, eps, [(a.shape[1],) for a in mat])
     cores = []
     for a, x in zip(mat, vec):
         ra, m, _, Ra = a.shape
@@ -490,6 +531,8 @@ def tt_fast_mat_mat_mul(m1, m2, eps=1e-18):
     """`cy_src/tt_ops_cy.pyx:449-464`: core-wise matrix product, rounded at eps."""
     if ZIPUP:
         return _zipup_mat_mat_mul(m1, m2, eps)
+    if _use_native_zipup():
+        return _native_zipup(1, m1, m2, eps, [(a.shape[1], b.shape[2]) for a, b in zip(m1, m2)])
     cores = []
     for a, b in zip(m1, m2):
         ra, m, _, Ra = a.shape
@@ -502,8 +545,10 @@ def tt_fast_hadamard(t1, t2, eps=1e-18):
     """`cy_src/tt_ops_cy.pyx:466-502`: core-wise Hadamard product, rounded at eps."""
     if ZIPUP:
         return _zipup_hadamard(t1, t2, eps)
-    cores = []
     four = t1[0].dim() == 4 and t2[0].dim() == 4
+    if _use_native_zipup() and (four or (t1[0].dim() == 3 and t2[0].dim() == 3)):
+        return _native_zipup(3 if four else 2, t1, t2, eps, [tuple(a.shape[1:-1]) for a in t1])
+    cores = []
     for a, b in zip(t1, t2):
         if four:
             cores.append(D.einsum("aijA,bijB->abijAB", a, b).view(a.shape[0] * b.shape[0], a.shape[1], a.shape[2],

@@ -3,11 +3,15 @@
 //
 //   test_abi <fixture>      (tests/golden/abi_lgmres.bin, made by tests/golden/make_abi_fixture.py)
 //
-// Per thread: bind a context, build the Schur-reduced operator (ttk_schur_build, the
+// Per thread: create a context, build the Schur-reduced operator on it (ttk_schur_build, the
 // `MatVecWrapper` of cy_src/lgmres_cy.pyx:203-331) from the fixture's blocks, solve with the
-// whole-solve PETSc LGMRES (ttk_lgmres, src/tt_ipm.py:101-162), copy the solution back.  Checks:
-// both contexts' solutions are bit-identical, the iteration count equals the oracle's, and the
-// solution matches the oracle's PETSc-LGMRES restatement to 1e-8 relative.  Exit 0 = pass.
+// whole-solve PETSc LGMRES (ttk_lgmres, src/tt_ipm.py:101-162), copy the solution back.
+// Round 1 (default knobs on both contexts): both solutions bit-identical, the iteration count equals
+// the oracle's, the solution matches the oracle's PETSc-LGMRES restatement to 1e-8 relative.
+// Round 2 (knob isolation): the second context switches its LGMRES steps to the multi-workgroup
+// kernels (TTK_KNOB_LGMRES_MW_MIN = 0, another summation order) while the first runs concurrently
+// with its defaults: the first context's solution must stay bit-identical to round 1, the second
+// must still match the oracle to 1e-8.  Exit 0 = pass.
 #include <hip/hip_runtime_api.h>
 
 #include <cmath>
@@ -77,12 +81,12 @@ struct Result {
   char err[256] = "";
 };
 
-void solve(const Fixture &f, Result &out) {
+void solve(const Fixture &f, Result &out, int mw_min) {
   hipStream_t st;
   if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return;
   ttk_ctx ctx = nullptr;
   if ((out.rc = ttk_ctx_create(st, &ctx))) return;
-  ttk_ctx_bind(ctx);  // ttk_schur_build takes no context: it uses the thread's bound one
+  if (mw_min >= 0 && (out.rc = ttk_ctx_set_knob(ctx, TTK_KNOB_LGMRES_MW_MIN, mw_min, nullptr))) return;
   double *L[4], *A[4], *Q[4];
   for (int k = 0; k < 4; ++k) {
     L[k] = upload(f.L[k], st);
@@ -96,7 +100,7 @@ void solve(const Fixture &f, Result &out) {
   for (int i = 0; i < 5; ++i) apply_desc(desc.data() + 36 * i, L[order[i]], A[order[i]], Q[order[i]], f);
   (void)hipStreamSynchronize(st);
   int64_t h = 0;
-  out.rc = ttk_schur_build(0, f.m, desc.data(), invI, &h);
+  out.rc = ttk_schur_build(ctx, 0, f.m, desc.data(), invI, &h);
   if (!out.rc && h == 0) out.rc = -2;  // operator not representable as a native handle
   if (!out.rc)
     out.rc = ttk_lgmres(ctx, h, b, x, 2 * f.m, (int)f.restart, (int)f.augment, 1e-5, 300, 8, &out.info);
@@ -105,7 +109,7 @@ void solve(const Fixture &f, Result &out) {
   // the solve's last kernels are still queued on the context's (non-blocking) stream: copy on it
   (void)hipMemcpyAsync(out.x.data(), x, 2 * f.m * sizeof(double), hipMemcpyDeviceToHost, st);
   (void)hipStreamSynchronize(st);
-  ttk_schur_free(h);
+  ttk_schur_free(ctx, h);
   for (int k = 0; k < 4; ++k) {
     (void)hipFree(L[k]);
     (void)hipFree(A[k]);
@@ -114,7 +118,6 @@ void solve(const Fixture &f, Result &out) {
   (void)hipFree(invI);
   (void)hipFree(b);
   (void)hipFree(x);
-  ttk_ctx_bind(nullptr);
   ttk_ctx_destroy(ctx);
   (void)hipStreamDestroy(st);
 }
@@ -131,30 +134,57 @@ int main(int argc, char **argv) {
     std::fprintf(stderr, "cannot read %s\n", argv[1]);
     return 2;
   }
+  auto rel_err = [&](const Result &r) {
+    double num = 0.0, den = 0.0;
+    for (size_t i = 0; i < f.x.size(); ++i) {
+      num = std::fmax(num, std::fabs(r.x[i] - f.x[i]));
+      den = std::fmax(den, std::fabs(f.x[i]));
+    }
+    return num / den;
+  };
+  auto report = [&](const char *tag, const Result *res) {
+    int fail = 0;
+    for (int i = 0; i < 2; ++i) {
+      std::printf("%s ctx %d: rc %d reason %d its %d res %.6e matvecs %d rel.err %.3e %s\n", tag, i, res[i].rc,
+                  res[i].info.reason, res[i].info.its, res[i].info.res, res[i].info.matvecs,
+                  res[i].rc ? 0.0 : rel_err(res[i]), res[i].err);
+      if (res[i].rc) fail = 1;
+    }
+    return fail;
+  };
   Result res[2];
-  std::thread t0(solve, std::cref(f), std::ref(res[0])), t1(solve, std::cref(f), std::ref(res[1]));
-  t0.join();
-  t1.join();
-  int fail = 0;
-  for (int i = 0; i < 2; ++i) {
-    std::printf("ctx %d: rc %d reason %d its %d res %.6e matvecs %d %s\n", i, res[i].rc, res[i].info.reason,
-                res[i].info.its, res[i].info.res, res[i].info.matvecs, res[i].err);
-    if (res[i].rc) fail = 1;
+  {
+    std::thread t0(solve, std::cref(f), std::ref(res[0]), -1), t1(solve, std::cref(f), std::ref(res[1]), -1);
+    t0.join();
+    t1.join();
   }
-  if (fail) return 1;
+  if (report("round 1", res)) return 1;
   if (std::memcmp(res[0].x.data(), res[1].x.data(), res[0].x.size() * sizeof(double)) != 0) {
     std::printf("FAIL: the two contexts' solutions differ\n");
     return 1;
   }
-  double num = 0.0, den = 0.0;
-  for (size_t i = 0; i < f.x.size(); ++i) {
-    num = std::fmax(num, std::fabs(res[0].x[i] - f.x[i]));
-    den = std::fmax(den, std::fabs(f.x[i]));
-  }
   std::printf("its %d (oracle %lld), max |x - x_oracle| / max |x_oracle| = %.3e\n", res[0].info.its,
-              (long long)f.its, num / den);
-  if (res[0].info.its != f.its || !(num <= 1e-8 * den)) {
+              (long long)f.its, rel_err(res[0]));
+  if (res[0].info.its != f.its || !(rel_err(res[0]) <= 1e-8)) {
     std::printf("FAIL\n");
+    return 1;
+  }
+  Result iso[2];
+  {
+    std::thread t0(solve, std::cref(f), std::ref(iso[0]), -1), t1(solve, std::cref(f), std::ref(iso[1]), 0);
+    t0.join();
+    t1.join();
+  }
+  if (report("round 2", iso)) return 1;
+  if (std::memcmp(iso[0].x.data(), res[0].x.data(), res[0].x.size() * sizeof(double)) != 0) {
+    std::printf("FAIL: a knob set on another context changed this context's solution\n");
+    return 1;
+  }
+  const bool moved = std::memcmp(iso[1].x.data(), res[0].x.data(), res[0].x.size() * sizeof(double)) != 0;
+  std::printf("knob context: summation order %s, its %d\n", moved ? "changed (bits differ)" : "bits unchanged",
+              iso[1].info.its);
+  if (!(rel_err(iso[1]) <= 1e-8)) {
+    std::printf("FAIL: the knob context's solution left the oracle's\n");
     return 1;
   }
   std::printf("PASS\n");

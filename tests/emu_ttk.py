@@ -435,11 +435,11 @@ class EmuLib:
         flags[1] = null
         return 0
 
-    def ttk_schur_build(self, ineq, m, descs, inv_I, handle):
+    def ttk_schur_build(self, ctx, ineq, m, descs, inv_I, handle):
         handle._obj.value = 0  # no native operator: the per-block path runs
         return 0
 
-    def ttk_schur_free(self, h):
+    def ttk_schur_free(self, ctx, h):
         return 0
 
     def ttk_lgmres_arnoldi_async(self, s, V, n, it, hh, max_k, haptol, ttol, divtol, ctl, slot, marker):

@@ -195,6 +195,12 @@ RUNS = [
     ("maxcut", "maxcut_12", 0, 2, True, 0),
     ("maxcut", "maxcut_12", 1, 2, True, 0),
     ("maxcut", "maxcut_12", 2, 2, True, 0),
+    # the rest of configs/maxcut_12.yaml's seeds: bounded traces (3 Newton systems each, every AMEn
+    # solve and step pair before them) -- a full 1-thread reference run is ~35 min per seed
+    ("maxcut", "maxcut_12", 45, 2, True, 3),
+    ("maxcut", "maxcut_12", 23, 2, True, 3),
+    ("maxcut", "maxcut_12", 53, 2, True, 3),
+    ("maxcut", "maxcut_12", 12, 2, True, 3),
 ]
 
 
@@ -232,10 +238,14 @@ def make_runs(only=None, jobs=1):
             continue
         res = json.load(open(tmp))
         print(key, {k: res.get(k) for k in ("num_iters", "gap", "feas", "dual_feas", "sec_per_iter")}, flush=True)
-        out = json.load(open(path)) if os.path.exists(path) else {}
-        out[key] = res
-        with open(path, "w") as f:
-            json.dump(out, f, indent=1)
+        import fcntl
+        with open(path + ".lock", "w") as lk:  # several make_runs invocations may merge at once
+            fcntl.flock(lk, fcntl.LOCK_EX)
+            out = json.load(open(path)) if os.path.exists(path) else {}
+            out[key] = res
+            with open(path + ".tmp", "w") as f:
+                json.dump(out, f, indent=1)
+            os.replace(path + ".tmp", path)
 
 
 if __name__ == "__main__":

@@ -56,9 +56,8 @@ def test_replica_schedule():
     assert sched == [[41, 41], [23, 23], [235, 235]]
 
 
-def test_default_inflight_caps_processes_per_node():
-    assert bench.default_inflight(1) == 4
-    assert bench.default_inflight(2) == 4
-    assert bench.default_inflight(4) == 4
-    assert bench.default_inflight(8) == 2
+def test_default_inflight_same_at_every_n_and_caps_processes_per_node():
+    """The 1/2/4/8-GPU series runs the same solves in flight per GPU (like-for-like scaling) and a
+    node never runs more than 16 solve processes."""
+    assert {bench.default_inflight(w) for w in (1, 2, 4, 8)} == {2}
     assert all(w * bench.default_inflight(w) <= 16 for w in (1, 2, 4, 8, 16))

@@ -76,19 +76,31 @@ def test_dense_schur_solve_matches_python_steps(dev):
     import yaml
     from ttipm_amd import tt_ipm
     from ttipm_amd.utils import run_and_record
-    native, calls = tt_ipm._dense_native, {"n": 0, "exc": 0}
+    native, calls, bad = tt_ipm._dense_native, {"n": 0, "exc": 0}, []
 
+    # mismatches are collected, not asserted here: the local solver's fallback handlers
+    # (tt_ipm._ipm_local_solver's try/except) would swallow an AssertionError raised inside
     def both(*a):
         try:
             ref = tt_ipm._dense_python(*a)
         except Exception as e:  # noqa: BLE001 - compared with the native status below
-            with pytest.raises(type(e)):
+            try:
                 native(*a)
+                bad.append(f"python raised {type(e).__name__}, native returned")
+            except Exception as e2:  # noqa: BLE001
+                if type(e2) is not type(e):
+                    bad.append(f"python raised {type(e).__name__}, native {type(e2).__name__}")
             calls["exc"] += 1
             raise
-        got = native(*a)
+        try:
+            got = native(*a)
+        except Exception as e2:  # noqa: BLE001
+            bad.append(f"native raised {type(e2).__name__}: {e2}")
+            return ref
         calls["n"] += 1
-        assert np.array_equal(dev.read(got), dev.read(ref))
+        g, r = dev.read(got), dev.read(ref)
+        if not np.array_equal(g, r):
+            bad.append(f"solve {calls['n']}: max diff {np.max(np.abs(g - r)):.3e}")
         return got
 
     cfg = yaml.safe_load(open(os.path.join(ROOT, "configs", "maxcut_5.yaml")))
@@ -99,6 +111,7 @@ def test_dense_schur_solve_matches_python_steps(dev):
         r = run_and_record("maxcut", cfg, 0, 1, verbose=False)
     finally:
         tt_ipm._dense_native, tt_ipm.NATIVE_DENSE = native, old
+    assert not bad, bad[:5]
     assert calls["n"] > 10, calls
     g = json.load(open(os.path.join(ROOT, "tests", "golden", "runs.json")))["maxcut_5_r1_s0"]
     assert r["num_iters"] == g["num_iters"]
@@ -153,3 +166,36 @@ def test_dense_schur_solve_ineq_matches_python_steps(dev):
     assert not bad, bad[:5]
     assert calls["n"] >= 1, calls
     assert r["num_iters"] == g["num_iters"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["matvec", "matmat", "hadamard3", "hadamard4"])
+@pytest.mark.parametrize("eps", [0.0, 1e-12, 1e-3])
+def test_ttk_zipup_matches_python_composition(dev, kind, eps):
+    """ttk_zipup (one C call: core-wise Kronecker products + one ttk_round) = tt_ops.tt_fast_*'s
+    Python composition (einsum per core, then tt_rank_reduce) bit for bit: ranks and cores
+    (cy_src/tt_ops_cy.pyx:391-502 as redesigned in DESIGN.md §3.1)."""
+    from ttipm_amd import tt_ops as T
+    rng = np.random.default_rng(7)
+    ra, rb = [1, 3, 4, 2, 1], [1, 2, 5, 3, 1]
+    if kind == "matvec":
+        a, b, f = _random_tt(dev, rng, ra, (4, 4)), _random_tt(dev, rng, rb, (4,)), T.tt_fast_matrix_vec_mul
+    elif kind == "matmat":
+        a, b, f = _random_tt(dev, rng, ra, (2, 2)), _random_tt(dev, rng, rb, (2, 2)), T.tt_fast_mat_mat_mul
+    elif kind == "hadamard3":
+        a, b, f = _random_tt(dev, rng, ra, (4,)), _random_tt(dev, rng, rb, (4,)), T.tt_fast_hadamard
+    else:
+        a, b, f = _random_tt(dev, rng, ra, (2, 2)), _random_tt(dev, rng, rb, (2, 2)), T.tt_fast_hadamard
+    keep = [dev.read(c) for c in a + b]
+    old = T.NATIVE_ZIPUP
+    try:
+        T.NATIVE_ZIPUP = True
+        got = f(a, b, eps)
+        T.NATIVE_ZIPUP = False
+        ref = f(a, b, eps)
+    finally:
+        T.NATIVE_ZIPUP = old
+    assert T.tt_ranks(got) == T.tt_ranks(ref)
+    for x, y in zip(got, ref):
+        assert tuple(x.shape) == tuple(y.shape) and np.array_equal(dev.read(x), dev.read(y))
+    assert all(np.array_equal(k, dev.read(c)) for k, c in zip(keep, a + b))  # operands untouched

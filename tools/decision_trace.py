@@ -1,0 +1,153 @@
+"""Decision trace of one solve: every local KKT solve (local shape, dense gate, res_old, res_min,
+failure flag, whether the previous solution was kept, ||sol||), every AMEn call (residual, ranks),
+every step-size pair and every Newton-system assembly, in call order -- the discrete choices the
+reference's control flow takes, so two runs can be aligned event by event.
+
+    python tools/decision_trace.py ref maxcut maxcut_10 14 1 [max_assemblies] > ref.jsonl  (build
+        container: the REFERENCE itself, imported as tests/golden/make_golden.py does)
+    python tools/decision_trace.py dev maxcut maxcut_10 14 1 [max_assemblies] > dev.jsonl  (GPU box)
+    python tools/decision_trace.py diff ref.jsonl dev.jsonl
+
+Hooks wrap the module-level names the reference's tt_ipm looks up at call time
+(`_ipm_local_solver(_ineq)`, `tt_restarted_block_amen`, `_tt_get_step_sizes`,
+`tt_infeasible_newton_system`; src/tt_ipm.py:958-981, 589, 666, 700, 1031) and the same names of
+ttipm_amd.tt_ipm."""
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+
+
+def install(mod, norm, ranks, ev):
+    """wrap mod's hot-path names; norm(t) -> float, ranks(tt) -> list"""
+    for name in ("_ipm_local_solver", "_ipm_local_solver_ineq"):
+        f = getattr(mod, name)
+
+        def ls(*a, _f=f, **k):
+            out = _f(*a, **k)
+            sol, res_old, res_min, rhs, nrhs, dsf = out
+            prev = a[6]
+            ev.append({"e": "local", "shape": [int(s) for s in prev.shape], "dense_arg": bool(a[8] if len(a) > 8
+                                                                                            else k.get("dense_solve", True)),
+                       "res_old": float(res_old), "res_min": float(res_min), "nrhs": float(nrhs), "dsf": bool(dsf),
+                       "kept_prev": sol is prev, "sol": norm(sol)})
+            return out
+        setattr(mod, name, ls)
+    amen = mod.tt_restarted_block_amen
+
+    def am(*a, **k):
+        ev.append({"e": "amen_begin", "restriction": int(k.get("rank_restriction") or 0), "inner_m": int(k.get("inner_m") or 0)})
+        x, res = amen(*a, **k)
+        ev.append({"e": "amen", "res": float(res), "ranks": ranks(x)})
+        return x, res
+    mod.tt_restarted_block_amen = am
+    steps = mod._tt_get_step_sizes
+
+    def stp(*a, **k):
+        xs, zs = steps(*a, **k)
+        ev.append({"e": "steps", "xs": float(xs), "zs": float(zs)})
+        return xs, zs
+    mod._tt_get_step_sizes = stp
+    newton = mod.tt_infeasible_newton_system
+
+    def nw(*a, **k):
+        out = newton(*a, **k)
+        st = out[2]
+        ev.append({"e": "assembly", "mu": float(st.mu), "primal": float(st.primal_error),
+                   "dual": float(st.dual_error), "centrality": float(st.centrality_error), "sigma": float(st.sigma)})
+        return out
+    mod.tt_infeasible_newton_system = nw
+
+
+def run_ref(problem, cfg, seed, rank, nmax):
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    import make_golden as MG
+    rops, rals, ripm = MG._import_reference(True)
+    ev = []
+    install(ripm, lambda t: float(np.linalg.norm(t)), lambda x: [int(c.shape[-1]) for c in x[:-1]], ev)
+    MG.run_reference(problem, cfg, seed, rank, True, nmax)
+    return ev
+
+
+def run_dev(problem, cfg_name, seed, rank, nmax):
+    import torch
+    import yaml
+    torch.cuda.set_device(0)
+    from ttipm_amd import dev as D
+    from ttipm_amd import tt_ipm
+    from ttipm_amd.utils import run_and_record
+    ev = []
+    install(tt_ipm, lambda t: float(D.norm(t)), lambda x: [int(c.shape[-1]) for c in x[:-1]], ev)
+    cfg = yaml.safe_load(open(os.path.join(ROOT, "configs", cfg_name + ".yaml")))
+
+    class Stop(Exception):
+        pass
+    if nmax:
+        inner = tt_ipm.tt_infeasible_newton_system
+
+        def bounded(*a, **k):
+            out = inner(*a, **k)
+            if sum(1 for e in ev if e["e"] == "assembly") >= nmax:
+                raise Stop
+            return out
+        tt_ipm.tt_infeasible_newton_system = bounded
+    try:
+        run_and_record(problem, cfg, seed, rank, verbose=False)
+    except Stop:
+        pass
+    return ev
+
+
+KEYS = {"local": ("res_old", "res_min", "nrhs", "sol"), "amen": ("res",), "steps": ("xs", "zs"),
+        "assembly": ("mu", "primal", "dual", "centrality", "sigma")}
+DISCRETE = {"local": ("shape", "dense_arg", "dsf", "kept_prev"), "amen": ("ranks",), "amen_begin": ("restriction",)}
+
+
+def diff(a_path, b_path, tol=1e-6):
+    A = [json.loads(s) for s in open(a_path) if s.startswith("{")]
+    B = [json.loads(s) for s in open(b_path) if s.startswith("{")]
+    n_asm = 0
+    worst = 0.0
+    for i, (a, b) in enumerate(zip(A, B)):
+        if a["e"] == "assembly":
+            n_asm += 1
+        if a["e"] != b["e"]:
+            print(f"event {i}: kind differs {a['e']} / {b['e']} (after {n_asm} assemblies)")
+            return
+        for k in DISCRETE.get(a["e"], ()):
+            if a.get(k) != b.get(k):
+                print(f"event {i} ({a['e']}, after {n_asm} assemblies): {k} differs: {a.get(k)} / {b.get(k)}")
+                for j in range(max(0, i - 4), min(len(A), i + 3)):
+                    print("  A", j, A[j])
+                    print("  B", j, B[j] if j < len(B) else None)
+                return
+        for k in KEYS.get(a["e"], ()):
+            rel = abs(a[k] - b[k]) / max(abs(a[k]), 1e-300)
+            worst = max(worst, rel)
+            if rel > tol:
+                print(f"event {i} ({a['e']}, after {n_asm} assemblies): {k} rel {rel:.3e}: {a[k]!r} / {b[k]!r}"
+                      f"  (worst before: {worst:.2e})")
+                for j in range(max(0, i - 4), min(len(A), i + 3)):
+                    print("  A", j, A[j])
+                    print("  B", j, B[j] if j < len(B) else None)
+                return
+    print(f"no departure beyond {tol:g} over {min(len(A), len(B))} events (worst {worst:.2e})")
+
+
+if __name__ == "__main__":
+    mode = sys.argv[1]
+    if mode == "diff":
+        diff(sys.argv[2], sys.argv[3], float(sys.argv[4]) if len(sys.argv) > 4 else 1e-6)
+        sys.exit(0)
+    prob, cfg, seed, rank = sys.argv[2], sys.argv[3], int(sys.argv[4]), int(sys.argv[5])
+    nmax = int(sys.argv[6]) if len(sys.argv) > 6 else 0
+    import contextlib
+    with contextlib.redirect_stdout(sys.stderr):
+        ev = (run_ref if mode == "ref" else run_dev)(prob, cfg, seed, rank, nmax)
+    for e in ev:
+        print(json.dumps(e))

@@ -2,9 +2,11 @@
 
     python tools/parity_report.py [key ...]     # default: every full-solve key of runs.json
 
-For each key: iteration counts, the first Newton-system assembly whose (mu, primal, dual,
-centrality) error departs from the reference's by more than 1e-10 / 1e-6 relative, and the relative
-differences of the final gap / feasibility / dual feasibility.  Prints one JSON line per key."""
+For each key: iteration counts, per Newton-system assembly the device's max relative difference
+from the 1-thread reference over (mu, primal, dual, centrality) beside the reference's own
+1-vs-8-thread spread (when the `_t8` twin exists), the first assembly that leaves
+max(FLOOR, 50 x spread), and the relative differences of the final gap / feasibilities.
+Prints one JSON line per key (the per-assembly report committed under profiles/)."""
 import json
 import os
 import sys
@@ -17,6 +19,11 @@ import yaml  # noqa: E402
 
 RUNS = json.load(open(os.path.join(ROOT, "tests", "golden", "runs.json")))
 KEYS = ("mu", "primal_error", "dual_error", "centrality_error")
+FLOOR = 1e-9  # relative: the device's first assemblies differ at ~1e-13 (GEMM association)
+
+
+def rel(a, b):
+    return max(abs(a[k] - b[k]) / abs(b[k]) for k in KEYS)
 
 
 def first_departure(trace, gold, tol):
@@ -27,6 +34,26 @@ def first_departure(trace, gold, tol):
             if abs(a[k] - b[k]) > tol * abs(b[k]) + 1e-300:
                 return i, k
     return None
+
+
+def spread_report(trace, key):
+    g = RUNS[key]["trace"]
+    tw = RUNS.get(key + "_t8")
+    dev = [rel(a, b) for a, b in zip(trace, g)]
+    out = {"per_assembly_dev_vs_t1": dev}
+    if tw:
+        sp = [rel(b, c) for b, c in zip(g, tw["trace"])]
+        out["per_assembly_ref_spread"] = sp
+        first_out = None
+        for i, (dv, s) in enumerate(zip(dev, sp)):
+            if s > 1e-3:
+                break
+            if dv > max(FLOOR, 50 * s):
+                first_out = i
+                break
+        out["first_outside_50x_spread"] = first_out
+        out["checked_assemblies"] = next((i for i, s in enumerate(sp) if s > 1e-3), len(sp))
+    return out
 
 
 def main():
@@ -51,8 +78,10 @@ def main():
                "dep_1e-4": first_departure(trace, g["trace"], 1e-4)}
         for k in ("gap", "feas", "dual_feas"):
             out[k] = [r[k], g[k], abs(r[k] - g[k]) / abs(g[k])]
-        out["per_assembly_max_rel"] = [max(abs(a[k] - b[k]) / abs(b[k]) for k in KEYS)
-                                       for a, b in zip(trace, g["trace"])]
+            if key + "_t8" in RUNS:
+                out[k + "_t8"] = RUNS[key + "_t8"][k]
+        out.update(spread_report(trace, key))
+        out["trace"] = [{k: a[k] for k in KEYS + ("sigma", "ranksX")} for a in trace]
         print(json.dumps(out), flush=True)
 
 
