@@ -141,6 +141,7 @@ def run_reference(problem, cfg_name, seed, rank, fixed_ineq=True, max_assemblies
     return {"problem": problem, "config": cfg_name, "seed": seed, "rank": rank, "fixed_ineq": fixed_ineq,
             "num_iters": int(info["num_iters"]), "runtime": t3 - t2,
             "sec_per_iter": (t3 - t2) / max(1, int(info["num_iters"])), "gap": float(gap), "feas": float(feas),
+            "hash_seed": os.environ.get("PYTHONHASHSEED"),
             "dual_feas": float(dfeas), "ranksX": info["ranksX"], "ranksY": info["ranksY"],
             "ranksZ": info["ranksZ"], "trace": trace, "blas_threads": os.environ.get("OPENBLAS_NUM_THREADS")}
 
@@ -205,11 +206,16 @@ RUNS = [
 
 
 THREADS = int(os.environ.get("GOLDEN_THREADS", "1"))  # >1: the thread-spread runs (key suffix _t<N>)
+# != 0: the summation-order twins (key suffix _h<N>): opt_einsum orders tensordot axes by frozenset
+# iteration, so PYTHONHASHSEED picks among equally valid summation orders of every contraction --
+# the reference's own rounding-level noise, at every problem size (1 vs 8 BLAS threads perturbs
+# nothing below BLAS's threading thresholds)
+HASH = int(os.environ.get("GOLDEN_HASH", "0"))
 
 
 def run_key(cfg, rank, seed, fixed, nmax):
     return f"{cfg}_r{rank}_s{seed}" + ("" if fixed else "_shipped") + (f"_b{nmax}" if nmax else "") + \
-        (f"_t{THREADS}" if THREADS > 1 else "")
+        (f"_t{THREADS}" if THREADS > 1 else "") + (f"_h{HASH}" if HASH else "")
 
 
 def make_runs(only=None, jobs=1):
@@ -225,7 +231,7 @@ def make_runs(only=None, jobs=1):
             continue
         todo.append((key, [sys.executable, __file__, "one", prob, cfg, str(seed), str(rank), str(int(fixed)),
                            os.path.join("/tmp", f"golden_{key}.json"), str(nmax)]))
-    env = dict(os.environ, PYTHONHASHSEED="0", OPENBLAS_NUM_THREADS=str(THREADS), OMP_NUM_THREADS=str(THREADS))
+    env = dict(os.environ, PYTHONHASHSEED=str(HASH), OPENBLAS_NUM_THREADS=str(THREADS), OMP_NUM_THREADS=str(THREADS))
     running = []
     while todo or running:
         while todo and len(running) < jobs:

@@ -386,73 +386,95 @@ def _run(key, trace=None):
         tt_ipm.INEQ_MATVEC_BUG = old
 
 
-# Whole-solve parity policy, anchored on the reference's OWN noise: every full-solve golden was
-# also run with 8 BLAS threads (key suffix _t8, same code, only the BLAS summation order differs).
-# * path-stable configs (the 8-thread reference takes the same iterations and its trajectory stays
-#   within 1e-3 of the 1-thread run to the end): the device takes the same iterations, every
-#   Newton-system assembly agrees to max(1e-5, 50 x the reference's own spread up to that
-#   assembly) and the final gap / feasibility / dual feasibility to max(1e-5, 50 x the reference's
-#   final spread).  50x: the device perturbs the first assemblies at ~1e-13 (different GEMM
-#   association, Jacobi SVD, exact eigensolves) where the thread count perturbs them at 0 to 1e-14,
-#   and both then grow at the same chaotic rate (measured: maxcut_10 s41 device/reference-spread
-#   ratio 5 at the last assembly, s35 25).
-# * path-unstable configs (the reference itself changes its iteration count or leaves 1e-3 between
-#   thread counts -- maxcut_10 s23, s235, s14 -- or no 8-thread run exists): the first two
-#   assemblies agree to 1e-8 (graphm_3 r=2: 5e-10 at the second), the device converges to a non-pathological point (gap and
-#   feasibilities below the runner's 1e-3 rule, src/utils.py:67) in an iteration count within 2 of
-#   the reference runs'.
-TRAJ_RTOL = 1e-4
+# Whole-solve parity policy, anchored on the reference's OWN noise.  Every full-solve golden has
+# twins: the same reference code re-run with 8 BLAS threads (key suffix _t8) and with other
+# PYTHONHASHSEEDs (_h1, _h2, _h3: opt_einsum orders each contraction's tensordot axes by frozenset
+# iteration, so the hash seed selects among equally valid summation orders -- a rounding-level
+# perturbation at every problem size, where 1 vs 8 BLAS threads perturbs nothing below BLAS's
+# threading thresholds).  Per Newton-system assembly i the reference's spread s_i is the largest
+# relative difference of any twin from the golden over (mu, primal, dual, centrality errors).
+# * Every assembly before the first one whose spread exceeds 1e-3 (the reference's own trajectory
+#   has not yet left its noise) must agree with the golden to within max(FLOOR, 50 x max(s_0..s_i)).
+#   FLOOR = 1e-12 covers the first assemblies, where all twins agree exactly and the device differs
+#   by its own summation order (~1e-13).
+# * If the whole envelope is path-stable (every twin takes the golden's iteration count and its
+#   spread stays below 1e-3 to the end): the same iteration count and ranks, and the final gap /
+#   feasibilities within max(1e-5, 50 x the twins' final spread).
+# * Otherwise (the reference itself branches): a non-pathological end point (src/utils.py:67) in an
+#   iteration count within 2 of the twins' range.
 KEYS4 = ("mu", "primal_error", "dual_error", "centrality_error")
 FINAL_KEYS = ("gap", "feas", "dual_feas")
-FACTOR, FLOOR = 50.0, 1e-5
+FACTOR, FLOOR, FINAL_FLOOR, BRANCH = 50.0, 1e-12, 1e-5, 1e-3
+TWIN_SUFFIXES = ("_t8", "_h1", "_h2", "_h3")
+TRAJ_RTOL = 1e-4
 
 
 def _rel(a, b):
     return abs(a - b) / max(abs(b), 1e-300)
 
 
-def _reference_spread(key):
-    """(path_stable, per-assembly cumulative spread, final spreads) of the 1- vs 8-thread references"""
-    g, t8 = RUNS[key], RUNS.get(key + "_t8")
-    if t8 is None or t8["num_iters"] != g["num_iters"] or len(t8["trace"]) != len(g["trace"]):
-        return False, None, None
-    per = [max(_rel(a[k], b[k]) for k in KEYS4) for a, b in zip(t8["trace"], g["trace"])]
-    if max(per) > 1e-3:
-        return False, None, None
-    cum = [max(per[:i + 1]) for i in range(len(per))]
-    return True, cum, {k: _rel(t8[k], g[k]) for k in FINAL_KEYS}
+def _twins(key):
+    return [RUNS[key + sfx] for sfx in TWIN_SUFFIXES if key + sfx in RUNS]
+
+
+def reference_envelope(key):
+    """(per-assembly spread, number of assemblies checked, path_stable, final spreads, iteration range)
+    of the golden's twins (see above)."""
+    g, tw = RUNS[key], _twins(key)
+    n = len(g["trace"])
+    spread = [0.0] * n
+    for t in tw:
+        for i, (a, b) in enumerate(zip(t["trace"], g["trace"])):
+            spread[i] = max(spread[i], max(_rel(a[k], b[k]) for k in KEYS4))
+        for i in range(len(t["trace"]), n):  # a twin that stopped earlier: branched from there on
+            spread[i] = np.inf
+    checked = next((i for i, s in enumerate(spread) if s > BRANCH), n)
+    stable = bool(tw) and checked == n and all(t["num_iters"] == g["num_iters"] for t in tw)
+    fin = {k: max([_rel(t[k], g[k]) for t in tw] or [np.inf]) for k in FINAL_KEYS}
+    its = [g["num_iters"]] + [t["num_iters"] for t in tw]
+    return spread, checked, stable, fin, (min(its), max(its))
+
+
+def check_against_envelope(key, trace, r):
+    """the policy above; returns the per-assembly device differences (for the report)"""
+    from ttipm_amd.utils import is_pathological
+    g = RUNS[key]
+    spread, checked, stable, fin, (lo, hi) = reference_envelope(key)
+    per = [max(_rel(a[k], b[k]) for k in KEYS4) for a, b in zip(trace, g["trace"])]
+    for i in range(min(checked, len(per))):
+        bound = max(FLOOR, FACTOR * max(spread[:i + 1]))
+        assert per[i] <= bound, f"assembly {i}: device {per[i]:.2e} > {bound:.2e} (reference spread {spread[:i + 1]})"
+    if stable:
+        assert r["num_iters"] == g["num_iters"]
+        assert r["ranksX"] == g["ranksX"] and r["ranksZ"] == g["ranksZ"]
+        for k in FINAL_KEYS:
+            assert _rel(r[k], g[k]) <= max(FINAL_FLOOR, FACTOR * fin[k]), (k, r[k], g[k], fin[k])
+    else:
+        assert not is_pathological(r), r
+        assert lo - 2 <= r["num_iters"] <= hi + 2, (r["num_iters"], lo, hi)
+    return per
 
 
 FULL_KEYS = sorted(k for k, v in RUNS.items() if not v.get("bounded") and not k.startswith("maxcut_12")
-                   and "_t" not in k.rsplit("_s", 1)[-1])
+                   and not any(k.endswith(sfx) for sfx in TWIN_SUFFIXES))
 
 
 @pytest.mark.parametrize("key", FULL_KEYS)
 def test_full_solve_matches_reference(dev, key):
     from ttipm_amd._lib import lib
-    from ttipm_amd.utils import is_pathological
     l0 = lib.ttk_launch_count()
     trace = []
     g, r = _run(key, trace)
     assert lib.ttk_launch_count() > l0  # the HIP library did the work
-    stable, cum, fin = _reference_spread(key)
-    per = [max(_rel(a[k], b[k]) for k in KEYS4) for a, b in zip(trace, g["trace"])]
-    print(key, "stable" if stable else "unstable", ["%.0e" % v for v in per])
     if key.endswith("_shipped"):  # the reference's TypeError path: deterministic, two iterations
+        per = [max(_rel(a[k], b[k]) for k in KEYS4) for a, b in zip(trace, g["trace"])]
         assert r["num_iters"] == g["num_iters"] and max(per) <= 1e-12
         return
-    if stable:
-        assert r["num_iters"] == g["num_iters"]
-        assert r["ranksX"] == g["ranksX"] and r["ranksZ"] == g["ranksZ"]
-        for i, v in enumerate(per):
-            assert v <= max(FLOOR, FACTOR * cum[i]), (i, v, cum[i])
-        for k in FINAL_KEYS:
-            assert _rel(r[k], g[k]) <= max(FLOOR, FACTOR * fin[k]), (k, r[k], g[k], fin[k])
-    else:
-        assert max(per[:2]) <= 1e-8, per[:2]
-        assert not is_pathological(r), r
-        iters = [g["num_iters"]] + ([RUNS[key + "_t8"]["num_iters"]] if key + "_t8" in RUNS else [])
-        assert min(iters) - 2 <= r["num_iters"] <= max(iters) + 2, (r["num_iters"], iters)
+    spread, checked, stable, _, _ = reference_envelope(key)
+    print(key, "stable" if stable else f"branches at assembly {checked}", "twins", len(_twins(key)))
+    per = check_against_envelope(key, trace, r)
+    print(" device ", ["%.0e" % v for v in per])
+    print(" spread ", ["%.0e" % v for v in spread])
 
 
 class _Bounded(Exception):

@@ -6,6 +6,7 @@ reference's control flow takes, so two runs can be aligned event by event.
     python tools/decision_trace.py ref maxcut maxcut_10 14 1 [max_assemblies] > ref.jsonl  (build
         container: the REFERENCE itself, imported as tests/golden/make_golden.py does)
     python tools/decision_trace.py dev maxcut maxcut_10 14 1 [max_assemblies] > dev.jsonl  (GPU box)
+    python tools/decision_trace.py oracle maxcut maxcut_10 14 1 [max_assemblies]  (the CPU restatement)
     python tools/decision_trace.py diff ref.jsonl dev.jsonl
 
 Hooks wrap the module-level names the reference's tt_ipm looks up at call time
@@ -23,9 +24,14 @@ sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 
 
-def install(mod, norm, ranks, ev):
+REF_NAMES = ("_ipm_local_solver", "_ipm_local_solver_ineq", "tt_restarted_block_amen", "_tt_get_step_sizes",
+             "tt_infeasible_newton_system")
+ORACLE_NAMES = ("local_solver", "local_solver_ineq", "restarted_block_amen", "step_sizes", "newton_system")
+
+
+def install(mod, norm, ranks, ev, names=REF_NAMES):
     """wrap mod's hot-path names; norm(t) -> float, ranks(tt) -> list"""
-    for name in ("_ipm_local_solver", "_ipm_local_solver_ineq"):
+    for name in names[:2]:
         f = getattr(mod, name)
 
         def ls(*a, _f=f, **k):
@@ -38,22 +44,22 @@ def install(mod, norm, ranks, ev):
                        "kept_prev": sol is prev, "sol": norm(sol)})
             return out
         setattr(mod, name, ls)
-    amen = mod.tt_restarted_block_amen
+    amen = getattr(mod, names[2])
 
     def am(*a, **k):
         ev.append({"e": "amen_begin", "restriction": int(k.get("rank_restriction") or 0), "inner_m": int(k.get("inner_m") or 0)})
         x, res = amen(*a, **k)
         ev.append({"e": "amen", "res": float(res), "ranks": ranks(x)})
         return x, res
-    mod.tt_restarted_block_amen = am
-    steps = mod._tt_get_step_sizes
+    setattr(mod, names[2], am)
+    steps = getattr(mod, names[3])
 
     def stp(*a, **k):
         xs, zs = steps(*a, **k)
         ev.append({"e": "steps", "xs": float(xs), "zs": float(zs)})
         return xs, zs
-    mod._tt_get_step_sizes = stp
-    newton = mod.tt_infeasible_newton_system
+    setattr(mod, names[3], stp)
+    newton = getattr(mod, names[4])
 
     def nw(*a, **k):
         out = newton(*a, **k)
@@ -61,7 +67,7 @@ def install(mod, norm, ranks, ev):
         ev.append({"e": "assembly", "mu": float(st.mu), "primal": float(st.primal_error),
                    "dual": float(st.dual_error), "centrality": float(st.centrality_error), "sigma": float(st.sigma)})
         return out
-    mod.tt_infeasible_newton_system = nw
+    setattr(mod, names[4], nw)
 
 
 def run_ref(problem, cfg, seed, rank, nmax):
@@ -71,6 +77,50 @@ def run_ref(problem, cfg, seed, rank, nmax):
     ev = []
     install(ripm, lambda t: float(np.linalg.norm(t)), lambda x: [int(c.shape[-1]) for c in x[:-1]], ev)
     MG.run_reference(problem, cfg, seed, rank, True, nmax)
+    return ev
+
+
+def run_oracle(problem, cfg_name, seed, rank, nmax):
+    """the CPU restatement (oracle/), same hooks and bound"""
+    import warnings
+    import yaml
+    from oracle import ipm as OI
+    from oracle import problems as OP
+    from oracle import tt as OT
+    ev = []
+    install(OI, lambda t: float(np.linalg.norm(t)), lambda x: [int(c.shape[-1]) for c in x[:-1]], ev, ORACLE_NAMES)
+    config = yaml.safe_load(open(os.path.join(ROOT, "configs", cfg_name + ".yaml")))
+
+    class Stop(Exception):
+        pass
+    inner = OI.newton_system
+
+    def bounded(*a, **k):
+        out = inner(*a, **k)
+        if nmax and sum(1 for e in ev if e["e"] == "assembly") >= nmax:
+            raise Stop
+        return out
+    OI.newton_system = bounded
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")
+        np.random.seed(seed)
+        prob = OP.PROBLEMS[problem](config["dim"], rank, verbose=False)
+        if len(prob) == 5:
+            C, L, b, mask, lag = prob
+        else:
+            C, L, b, lag_y = prob
+            mask, lag = None, {"y": lag_y}
+        lag = {k: OT.reshape(v, (4, 4)) for k, v in lag.items()}
+        C, b = OT.reshape(C, (4,)), OT.reshape(b, (4,))
+        try:
+            OI.tt_ipm(lag, C, L, b, ineq_mask=mask, max_iter=config["max_iter"], verbose=False,
+                      gap_tol=float(config["gap_tol"]), op_tol=float(config["op_tol"]),
+                      warm_up=config["warm_up"], abs_tol=float(config["abs_tol"]), aho_direction=False,
+                      mals_restarts=config["mals_restarts"], max_refinement=config["max_refinement"],
+                      lambdaStar=float(config.get("lambdaStar", 1)),
+                      lambdaStarIneq=float(config.get("lambdaStarIneq", 1)))
+        except Stop:
+            pass
     return ev
 
 
@@ -127,7 +177,9 @@ def diff(a_path, b_path, tol=1e-6):
                     print("  B", j, B[j] if j < len(B) else None)
                 return
         for k in KEYS.get(a["e"], ()):
-            rel = abs(a[k] - b[k]) / max(abs(a[k]), 1e-300)
+            # residuals near round-off (|r| ~ 1e-10 and below) are noise: absolute floor 1e-12
+            floor = 1e-12 if k.startswith("res") else 0.0
+            rel = abs(a[k] - b[k]) / max(abs(a[k]), 1e-300) if abs(a[k] - b[k]) > floor else 0.0
             worst = max(worst, rel)
             if rel > tol:
                 print(f"event {i} ({a['e']}, after {n_asm} assemblies): {k} rel {rel:.3e}: {a[k]!r} / {b[k]!r}"
@@ -148,6 +200,6 @@ if __name__ == "__main__":
     nmax = int(sys.argv[6]) if len(sys.argv) > 6 else 0
     import contextlib
     with contextlib.redirect_stdout(sys.stderr):
-        ev = (run_ref if mode == "ref" else run_dev)(prob, cfg, seed, rank, nmax)
+        ev = {"ref": run_ref, "oracle": run_oracle, "dev": run_dev}[mode](prob, cfg, seed, rank, nmax)
     for e in ev:
         print(json.dumps(e))

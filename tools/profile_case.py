@@ -26,6 +26,8 @@ def cb(it):
         raise Stop
 
 
+if os.environ.get("TTIPM_PROFILE_WARM", "1") == "1":  # plans, allocator and code pages first
+    run_and_record(prob, cfg, seed, rank, verbose=False)
 pr = cProfile.Profile()
 l0 = lib.ttk_launch_count()
 t = time.time()
