@@ -32,9 +32,39 @@ import numpy as np  # noqa: E402
 import yaml  # noqa: E402
 
 
+def patch_svd(kind):
+    """SVD-algorithm twins: the reference's scipy.linalg.svd calls (default gesdd, or the explicit
+    lapack_driver='gesvd' of the rounding / eigen code) on another LAPACK algorithm -- 'jacobi':
+    dgejsv (one-sided Jacobi, high relative accuracy, the algorithm class of the device SVD),
+    'gesvd' / 'swap': the other bidiagonalisation driver.  Rounding-level variation of the
+    reference's own computation, like the thread and hash-seed twins."""
+    import scipy.linalg as sla
+    from scipy.linalg import lapack
+    orig = sla.svd
+
+    def svd(a, *args, **kw):
+        if kind == "jacobi":
+            a = np.asarray(a, dtype=float)
+            if a.shape[0] < a.shape[1]:
+                u, s, vt = svd(a.T)
+                return vt.T, s, u.T
+            sva, u, v, work, _, info = lapack.dgejsv(np.array(a, order="F"), joba=1, jobu=0, jobv=0)
+            if info == 0:
+                return u, sva * (work[0] / work[1]), v.T
+            kw.pop("lapack_driver", None)
+        elif kind == "swap":
+            kw["lapack_driver"] = "gesdd" if kw.get("lapack_driver", "gesdd") == "gesvd" else "gesvd"
+        elif "lapack_driver" not in kw:
+            kw["lapack_driver"] = kind
+        return orig(a, *args, **kw)
+    sla.svd = svd
+
+
 def _import_reference(fixed_ineq=True):
     from oracle.build_ref import build
     build()
+    if os.environ.get("GOLDEN_SVD"):
+        patch_svd(os.environ["GOLDEN_SVD"])
     cy = os.path.join(REPO, "oracle", "_ref", "fixed") if fixed_ineq else os.path.join(REPO, "oracle", "_ref")
     sys.path[:0] = [os.path.join(HERE, "refshim"), cy, REF]
     import src.tt_ops as rops  # noqa
@@ -141,7 +171,7 @@ def run_reference(problem, cfg_name, seed, rank, fixed_ineq=True, max_assemblies
     return {"problem": problem, "config": cfg_name, "seed": seed, "rank": rank, "fixed_ineq": fixed_ineq,
             "num_iters": int(info["num_iters"]), "runtime": t3 - t2,
             "sec_per_iter": (t3 - t2) / max(1, int(info["num_iters"])), "gap": float(gap), "feas": float(feas),
-            "hash_seed": os.environ.get("PYTHONHASHSEED"),
+            "hash_seed": os.environ.get("PYTHONHASHSEED"), "svd": os.environ.get("GOLDEN_SVD") or "scipy default",
             "dual_feas": float(dfeas), "ranksX": info["ranksX"], "ranksY": info["ranksY"],
             "ranksZ": info["ranksZ"], "trace": trace, "blas_threads": os.environ.get("OPENBLAS_NUM_THREADS")}
 
@@ -211,11 +241,13 @@ THREADS = int(os.environ.get("GOLDEN_THREADS", "1"))  # >1: the thread-spread ru
 # the reference's own rounding-level noise, at every problem size (1 vs 8 BLAS threads perturbs
 # nothing below BLAS's threading thresholds)
 HASH = int(os.environ.get("GOLDEN_HASH", "0"))
+SVD = os.environ.get("GOLDEN_SVD", "")  # SVD-algorithm twins (key suffix _j<hash> for 'jacobi', patch_svd)
 
 
 def run_key(cfg, rank, seed, fixed, nmax):
     return f"{cfg}_r{rank}_s{seed}" + ("" if fixed else "_shipped") + (f"_b{nmax}" if nmax else "") + \
-        (f"_t{THREADS}" if THREADS > 1 else "") + (f"_h{HASH}" if HASH else "")
+        (f"_t{THREADS}" if THREADS > 1 else "") + \
+        (f"_j{HASH}" if SVD == "jacobi" else (f"_{SVD}{HASH}" if SVD else (f"_h{HASH}" if HASH else "")))
 
 
 def make_runs(only=None, jobs=1):

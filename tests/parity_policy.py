@@ -1,0 +1,104 @@
+"""Whole-solve parity policy shared by the GPU parity tests, the oracle tests and
+tools/parity_report.py (pure NumPy over tests/golden/runs.json)."""
+import json
+import os
+
+import numpy as np
+
+RUNS = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "runs.json")))
+
+
+def is_pathological(r):
+    """the reference runner's rule (`src/utils.py:67`): feasibility error or slackness > 1e-3"""
+    return r["feas"] > 1e-3 or r["gap"] > 1e-3
+
+
+# Whole-solve parity policy, anchored on the reference's OWN runs.  Every full-solve golden (the
+# reference as shipped: 1 BLAS thread, PYTHONHASHSEED=0) has twins -- the SAME reference code re-run
+# under rounding-level variations of its own computation (tests/golden/make_golden.py):
+#   _t8        8 BLAS threads;
+#   _h1.._h3   other PYTHONHASHSEEDs: opt_einsum orders each contraction's tensordot axes by
+#              frozenset iteration, so the hash seed picks among equally valid summation orders;
+#   _j0.._j3   its scipy.linalg.svd calls on LAPACK's one-sided Jacobi SVD (dgejsv, high relative
+#              accuracy -- the algorithm class of the device SVD) with hash seeds 0..3.
+# The AMEn rank decisions and the step-size eigen-ALS make the reference's trajectory branch under
+# such variations (maxcut_10 s14: the reference with Jacobi SVDs and hash seed 4 reproduces the
+# device's assembly-5 departure to 2e-8; s23: with Jacobi SVDs the reference follows the device to
+# 1e-12 where its shipped run departs by 8e-6; s235: every hash twin leaves the golden at assembly 4).
+# So the device must reproduce ONE of the reference's own runs:
+# * noise n_i at Newton-system assembly i = the largest relative difference over (mu, primal, dual,
+#   centrality) between the golden and its thread / hash twins (the shipped code's own rounding
+#   noise), cumulated over assemblies 0..i;
+# * there must be a reference run R (the golden or any twin) that the device follows at every
+#   assembly i before the shipped code's noise branches (n_i > 1e-3): rel(device_i, R_i) <=
+#   max(1e-12, 50 n_i);
+# * if nothing branches (n_i <= 1e-3 to the end and every twin takes the golden's iteration count):
+#   the same iteration count and ranks as R, final gap / feasibilities within max(1e-5, 50 x the
+#   twins' final spread) of R's; otherwise a non-pathological end point (src/utils.py:67) within 2
+#   iterations of the twins' range.
+KEYS4 = ("mu", "primal_error", "dual_error", "centrality_error")
+FINAL_KEYS = ("gap", "feas", "dual_feas")
+FACTOR, FLOOR, FINAL_FLOOR, BRANCH = 50.0, 1e-12, 1e-5, 1e-3
+NOISE_TWINS = ("_t8", "_h1", "_h2", "_h3")
+ALL_TWINS = NOISE_TWINS + ("_j0", "_j1", "_j2", "_j3")
+TWIN_SUFFIXES = ALL_TWINS
+
+
+def _rel(a, b):
+    return abs(a - b) / max(abs(b), 1e-300)
+
+
+def _twins(key, sfx=ALL_TWINS):
+    return [RUNS[key + x] for x in sfx if key + x in RUNS]
+
+
+def _per(trace, ref):
+    return [max(_rel(a[k], b[k]) for k in KEYS4) for a, b in zip(trace, ref["trace"])]
+
+
+def reference_noise(key):
+    """(cumulative noise per assembly, number of assemblies checked, path_stable) of the golden's
+    thread / hash twins"""
+    g, tw = RUNS[key], _twins(key, NOISE_TWINS)
+    n = len(g["trace"])
+    noise = [0.0] * n
+    for t in tw:
+        per = _per(t["trace"], g)
+        for i in range(n):
+            noise[i] = max(noise[i], per[i] if i < len(per) else np.inf)
+    cum = [max(noise[:i + 1]) for i in range(n)]
+    checked = next((i for i, v in enumerate(cum) if v > BRANCH), n)
+    stable = bool(tw) and checked == n and all(t["num_iters"] == g["num_iters"] for t in tw)
+    return cum, checked, stable
+
+
+def check_against_reference_runs(key, trace, r):
+    """the policy above; returns (name of the reference run the device follows, its per-assembly
+    differences, the noise bound)"""
+    g = RUNS[key]
+    cum, checked, stable = reference_noise(key)
+    runs = [("golden", g)] + [(x, RUNS[key + x]) for x in ALL_TWINS if key + x in RUNS]
+    best, best_per, worst_ratio = None, None, np.inf
+    for name, R in runs:
+        per = _per(trace, R)
+        m = min(checked, len(per), len(R["trace"]))
+        ratio = max([per[i] / max(FLOOR, FACTOR * cum[i]) for i in range(m)] or [0.0])
+        if ratio < worst_ratio:
+            best, best_per, worst_ratio = (name, R), per, ratio
+    assert worst_ratio <= 1.0, (f"no reference run followed within 50x the reference noise: best {best[0]} "
+                                f"{['%.0e' % v for v in best_per]} noise {['%.0e' % v for v in cum]}")
+    name, R = best
+    allruns = [g] + _twins(key)
+    lo, hi = min(x["num_iters"] for x in allruns), max(x["num_iters"] for x in allruns)
+    if stable:
+        fin = {k: max([_rel(t[k], g[k]) for t in _twins(key, NOISE_TWINS)] or [0.0]) for k in FINAL_KEYS}
+        assert r["num_iters"] == R["num_iters"]
+        assert r["ranksX"] == R["ranksX"] and r["ranksZ"] == R["ranksZ"]
+        for k in FINAL_KEYS:
+            assert _rel(r[k], R[k]) <= max(FINAL_FLOOR, FACTOR * fin[k]), (k, r[k], R[k], fin[k])
+    else:
+        assert not is_pathological(r), r
+        assert lo - 2 <= r["num_iters"] <= hi + 2, (r["num_iters"], lo, hi)
+    return name, best_per, cum
+
+

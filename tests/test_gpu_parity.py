@@ -386,73 +386,12 @@ def _run(key, trace=None):
         tt_ipm.INEQ_MATVEC_BUG = old
 
 
-# Whole-solve parity policy, anchored on the reference's OWN noise.  Every full-solve golden has
-# twins: the same reference code re-run with 8 BLAS threads (key suffix _t8) and with other
-# PYTHONHASHSEEDs (_h1, _h2, _h3: opt_einsum orders each contraction's tensordot axes by frozenset
-# iteration, so the hash seed selects among equally valid summation orders -- a rounding-level
-# perturbation at every problem size, where 1 vs 8 BLAS threads perturbs nothing below BLAS's
-# threading thresholds).  Per Newton-system assembly i the reference's spread s_i is the largest
-# relative difference of any twin from the golden over (mu, primal, dual, centrality errors).
-# * Every assembly before the first one whose spread exceeds 1e-3 (the reference's own trajectory
-#   has not yet left its noise) must agree with the golden to within max(FLOOR, 50 x max(s_0..s_i)).
-#   FLOOR = 1e-12 covers the first assemblies, where all twins agree exactly and the device differs
-#   by its own summation order (~1e-13).
-# * If the whole envelope is path-stable (every twin takes the golden's iteration count and its
-#   spread stays below 1e-3 to the end): the same iteration count and ranks, and the final gap /
-#   feasibilities within max(1e-5, 50 x the twins' final spread).
-# * Otherwise (the reference itself branches): a non-pathological end point (src/utils.py:67) in an
-#   iteration count within 2 of the twins' range.
-KEYS4 = ("mu", "primal_error", "dual_error", "centrality_error")
-FINAL_KEYS = ("gap", "feas", "dual_feas")
-FACTOR, FLOOR, FINAL_FLOOR, BRANCH = 50.0, 1e-12, 1e-5, 1e-3
-TWIN_SUFFIXES = ("_t8", "_h1", "_h2", "_h3")
+# Whole-solve parity policy: tests/parity_policy.py (the device must follow one of the reference's
+# own runs -- the shipped golden or a thread / hash-seed / Jacobi-SVD twin -- to within 50x the
+# shipped code's rounding noise until that noise branches).
+from tests.parity_policy import ALL_TWINS as TWIN_SUFFIXES  # noqa: E402
+from tests.parity_policy import KEYS4, _rel, check_against_reference_runs  # noqa: E402,F401
 TRAJ_RTOL = 1e-4
-
-
-def _rel(a, b):
-    return abs(a - b) / max(abs(b), 1e-300)
-
-
-def _twins(key):
-    return [RUNS[key + sfx] for sfx in TWIN_SUFFIXES if key + sfx in RUNS]
-
-
-def reference_envelope(key):
-    """(per-assembly spread, number of assemblies checked, path_stable, final spreads, iteration range)
-    of the golden's twins (see above)."""
-    g, tw = RUNS[key], _twins(key)
-    n = len(g["trace"])
-    spread = [0.0] * n
-    for t in tw:
-        for i, (a, b) in enumerate(zip(t["trace"], g["trace"])):
-            spread[i] = max(spread[i], max(_rel(a[k], b[k]) for k in KEYS4))
-        for i in range(len(t["trace"]), n):  # a twin that stopped earlier: branched from there on
-            spread[i] = np.inf
-    checked = next((i for i, s in enumerate(spread) if s > BRANCH), n)
-    stable = bool(tw) and checked == n and all(t["num_iters"] == g["num_iters"] for t in tw)
-    fin = {k: max([_rel(t[k], g[k]) for t in tw] or [np.inf]) for k in FINAL_KEYS}
-    its = [g["num_iters"]] + [t["num_iters"] for t in tw]
-    return spread, checked, stable, fin, (min(its), max(its))
-
-
-def check_against_envelope(key, trace, r):
-    """the policy above; returns the per-assembly device differences (for the report)"""
-    from ttipm_amd.utils import is_pathological
-    g = RUNS[key]
-    spread, checked, stable, fin, (lo, hi) = reference_envelope(key)
-    per = [max(_rel(a[k], b[k]) for k in KEYS4) for a, b in zip(trace, g["trace"])]
-    for i in range(min(checked, len(per))):
-        bound = max(FLOOR, FACTOR * max(spread[:i + 1]))
-        assert per[i] <= bound, f"assembly {i}: device {per[i]:.2e} > {bound:.2e} (reference spread {spread[:i + 1]})"
-    if stable:
-        assert r["num_iters"] == g["num_iters"]
-        assert r["ranksX"] == g["ranksX"] and r["ranksZ"] == g["ranksZ"]
-        for k in FINAL_KEYS:
-            assert _rel(r[k], g[k]) <= max(FINAL_FLOOR, FACTOR * fin[k]), (k, r[k], g[k], fin[k])
-    else:
-        assert not is_pathological(r), r
-        assert lo - 2 <= r["num_iters"] <= hi + 2, (r["num_iters"], lo, hi)
-    return per
 
 
 FULL_KEYS = sorted(k for k, v in RUNS.items() if not v.get("bounded") and not k.startswith("maxcut_12")
@@ -470,11 +409,8 @@ def test_full_solve_matches_reference(dev, key):
         per = [max(_rel(a[k], b[k]) for k in KEYS4) for a, b in zip(trace, g["trace"])]
         assert r["num_iters"] == g["num_iters"] and max(per) <= 1e-12
         return
-    spread, checked, stable, _, _ = reference_envelope(key)
-    print(key, "stable" if stable else f"branches at assembly {checked}", "twins", len(_twins(key)))
-    per = check_against_envelope(key, trace, r)
-    print(" device ", ["%.0e" % v for v in per])
-    print(" spread ", ["%.0e" % v for v in spread])
+    name, per, cum = check_against_reference_runs(key, trace, r)
+    print(key, "follows", name, ["%.0e" % v for v in per], "noise", ["%.0e" % v for v in cum])
 
 
 class _Bounded(Exception):

@@ -126,21 +126,20 @@ def test_prune_singular_vals_rule():
 RUNS = json.load(open(os.path.join(HERE, "golden", "runs.json")))
 
 
-def test_oracle_full_run_maxcut5():
-    """Whole TT-IPM on maxcut_5 seed 0: oracle vs the reference's own run (same LGMRES restatement)."""
+@pytest.mark.parametrize("key", ["maxcut_5_r1_s0", "maxcut_5_r1_s319"])
+def test_oracle_full_run_maxcut5(key):
+    """Whole TT-IPM on maxcut_5 (configs[0]): the oracle must follow one of the reference's own runs
+    (golden or twins) within 50x the reference's rounding noise -- the same policy the device's
+    whole-solve parity tests apply (tests/parity_policy.py)."""
     import yaml
     from oracle.problems import run_and_record
-    g = RUNS["maxcut_5_r1_s0"]
+    from tests.parity_policy import check_against_reference_runs
+    g = RUNS[key]
     cfg = yaml.safe_load(open(os.path.join(HERE, "..", "configs", g["config"] + ".yaml")))
     trace = []
     r = run_and_record("maxcut", cfg, g["seed"], g["rank"], trace=trace)
-    assert r["num_iters"] == g["num_iters"]
-    assert r["ranksX"] == g["ranksX"] and r["ranksZ"] == g["ranksZ"]
-    for k in ("gap", "feas", "dual_feas"):
-        assert abs(r[k] - g[k]) <= 1e-4 * abs(g[k]), (k, r[k], g[k])
-    for a, b in zip(trace, g["trace"]):
-        assert a["ranksX"] == b["ranksX"]
-        assert abs(a["mu"] - b["mu"]) <= 1e-5 * abs(b["mu"])
+    name, per, cum = check_against_reference_runs(key, trace, r)
+    print(key, "follows", name, ["%.0e" % v for v in per])
 
 
 class _Bounded(Exception):

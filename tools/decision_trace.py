@@ -74,6 +74,28 @@ def run_ref(problem, cfg, seed, rank, nmax):
     sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
     import make_golden as MG
     rops, rals, ripm = MG._import_reference(True)
+    if os.environ.get("REF_SVD_DRIVER"):  # twin: the reference's default-driver (gesdd) SVDs on another driver
+        import scipy.linalg as sla_mod
+        orig_svd, drv = sla_mod.svd, os.environ["REF_SVD_DRIVER"]
+
+        from scipy.linalg import lapack as _lp
+
+        def svd(a, *args, **kw):
+            if drv == "jacobi":  # LAPACK dgejsv (one-sided Jacobi, high relative accuracy)
+                a = np.asarray(a, dtype=float)
+                if a.shape[0] < a.shape[1]:
+                    u, s_, vt = svd(a.T)
+                    return vt.T, s_, u.T
+                sva, u, v, work, _, info = _lp.dgejsv(np.array(a, order="F"), joba=1, jobu=0, jobv=0)
+                if info == 0:
+                    return u, sva * (work[0] / work[1]), v.T
+                kw.pop("lapack_driver", None)
+            if drv == "swap":  # every call on the other LAPACK driver (gesdd <-> gesvd)
+                kw["lapack_driver"] = "gesdd" if kw.get("lapack_driver", "gesdd") == "gesvd" else "gesvd"
+            elif "lapack_driver" not in kw:
+                kw["lapack_driver"] = drv
+            return orig_svd(a, *args, **kw)
+        sla_mod.svd = svd
     ev = []
     install(ripm, lambda t: float(np.linalg.norm(t)), lambda x: [int(c.shape[-1]) for c in x[:-1]], ev)
     MG.run_reference(problem, cfg, seed, rank, True, nmax)
@@ -89,6 +111,83 @@ def run_oracle(problem, cfg_name, seed, rank, nmax):
     from oracle import tt as OT
     ev = []
     install(OI, lambda t: float(np.linalg.norm(t)), lambda x: [int(c.shape[-1]) for c in x[:-1]], ev, ORACLE_NAMES)
+    if os.environ.get("ORACLE_JACOBI_SVD"):  # experiment: LAPACK dgejsv (Jacobi, relative accuracy) SVDs
+        import scipy.linalg as sla_mod
+        from scipy.linalg import lapack
+        from oracle import als as OA
+        orig_svd = sla_mod.svd
+
+        def jsvd(a, full_matrices=False, **kw):
+            a = np.asarray(a, dtype=float)
+            if a.shape[0] < a.shape[1]:
+                u, s_, vt = jsvd(a.T)
+                return vt.T, s_, u.T
+            sva, u, v, work, _, info = lapack.dgejsv(np.array(a, order="F"), joba=1, jobu=0, jobv=0)
+            if info != 0:
+                return orig_svd(a, full_matrices=False)
+            if os.environ.get("ORACLE_JACOBI_SIGNS") == "lapack":  # experiment: LAPACK's singular-vector signs
+                ul, _, _ = orig_svd(a, full_matrices=False, lapack_driver="gesvd")
+                sg = np.sign(np.sum(u * ul, axis=0))
+                sg[sg == 0] = 1.0
+                u, v = u * sg, v * sg
+            return u, sva * (work[0] / work[1]), v.T
+
+        class _S:  # scipy.linalg facade for oracle/als.py only
+            def __getattr__(self, k):
+                return jsvd if k == "svd" else getattr(sla_mod, k)
+        which = os.environ["ORACLE_JACOBI_SVD"]
+        if which == "all":
+            sla_mod.svd = jsvd
+        else:  # comma list of oracle modules whose SVDs go to dgejsv
+            import importlib
+            for mname in which.split(","):
+                importlib.import_module("oracle." + mname).sla = _S()
+    if os.environ.get("ORACLE_KRON_ZIPUP") == "1":  # experiment: the device's zip-up
+        from oracle import tt as OTT
+        from oracle import als as OA2
+
+        def kron_round(cores, eps):
+            return OTT.rank_reduce(cores, eps) if len(cores) > 1 and eps > 0 else cores
+
+        def fmv(mat, vec, eps=1e-18):
+            return kron_round([np.einsum("amnA,rnR->armAR", a, x).reshape(a.shape[0] * x.shape[0], a.shape[1],
+                                                                            a.shape[3] * x.shape[2])
+                               for a, x in zip(mat, vec)], eps)
+
+        def fmm(m1, m2, eps=1e-18):
+            return kron_round([np.einsum("amkA,bknB->abmnAB", a, b).reshape(a.shape[0] * b.shape[0], a.shape[1],
+                                                                             b.shape[2], a.shape[3] * b.shape[3])
+                               for a, b in zip(m1, m2)], eps)
+
+        def fh(t1, t2, eps=1e-18):
+            if t1[0].ndim == 4 and t2[0].ndim == 4:
+                cs = [np.einsum("aijA,bijB->abijAB", a, b).reshape(a.shape[0] * b.shape[0], a.shape[1], a.shape[2],
+                                                                   a.shape[3] * b.shape[3]) for a, b in zip(t1, t2)]
+            else:
+                cs = [np.einsum("aiA,biB->abiAB", a, b).reshape(a.shape[0] * b.shape[0], a.shape[1],
+                                                                a.shape[2] * b.shape[2]) for a, b in zip(t1, t2)]
+            return kron_round(cs, eps)
+        for mod in (OTT, OI, OA2):
+            for name, f in (("fast_matrix_vec_mul", fmv), ("fast_mat_mat_mul", fmm), ("fast_hadamard", fh)):
+                if hasattr(mod, name):
+                    setattr(mod, name, f)
+    if os.environ.get("ORACLE_EXACT_EIG") == "1":  # experiment: exact dense eigenpairs instead of ARPACK
+        import scipy.linalg as sla
+        import scipy.sparse.linalg as spla
+        from oracle import eig as OE
+        orig = spla.eigsh
+
+        def exact_min(M, eps, m, v0):
+            w, V = np.linalg.eigh(M.toarray())
+            return w[:1], V[:, :1].copy()
+
+        def eigsh(A, k=6, M=None, which="LM", **kw):
+            if M is not None and which == "LA":
+                w, V = sla.eigh(-(-A).toarray(), M.toarray())
+                return w[-1:], V[:, -1:].copy()
+            return orig(A, k=k, M=M, which=which, **kw)
+        OE._eigsh_min_with_polish = exact_min
+        OE.spla.eigsh = eigsh
     config = yaml.safe_load(open(os.path.join(ROOT, "configs", cfg_name + ".yaml")))
 
     class Stop(Exception):

@@ -2,10 +2,11 @@
 
     python tools/parity_report.py [key ...]     # default: every full-solve key of runs.json
 
-For each key: iteration counts, per Newton-system assembly the device's max relative difference
-from the 1-thread reference over (mu, primal, dual, centrality) beside the reference's own
-1-vs-8-thread spread (when the `_t8` twin exists), the first assembly that leaves
-max(FLOOR, 50 x spread), and the relative differences of the final gap / feasibilities.
+For each key: iteration counts, the first Newton-system assemblies departing from the shipped
+golden by 1e-10 / 1e-6 / 1e-4, the relative differences of the final gap / feasibility / dual
+feasibility, and the whole-solve parity policy of tests/parity_policy.py (which of the reference's
+own runs -- golden, thread, hash-seed or Jacobi-SVD twin -- the device follows, and the reference's
+own rounding noise per assembly).
 Prints one JSON line per key (the per-assembly report committed under profiles/)."""
 import json
 import os
@@ -19,7 +20,6 @@ import yaml  # noqa: E402
 
 RUNS = json.load(open(os.path.join(ROOT, "tests", "golden", "runs.json")))
 KEYS = ("mu", "primal_error", "dual_error", "centrality_error")
-FLOOR = 1e-9  # relative: the device's first assemblies differ at ~1e-13 (GEMM association)
 
 
 def rel(a, b):
@@ -36,23 +36,20 @@ def first_departure(trace, gold, tol):
     return None
 
 
-def spread_report(trace, key):
-    g = RUNS[key]["trace"]
-    tw = RUNS.get(key + "_t8")
-    dev = [rel(a, b) for a, b in zip(trace, g)]
-    out = {"per_assembly_dev_vs_t1": dev}
-    if tw:
-        sp = [rel(b, c) for b, c in zip(g, tw["trace"])]
-        out["per_assembly_ref_spread"] = sp
-        first_out = None
-        for i, (dv, s) in enumerate(zip(dev, sp)):
-            if s > 1e-3:
-                break
-            if dv > max(FLOOR, 50 * s):
-                first_out = i
-                break
-        out["first_outside_50x_spread"] = first_out
-        out["checked_assemblies"] = next((i for i, s in enumerate(sp) if s > 1e-3), len(sp))
+def policy_report(key, trace, r):
+    """tests/parity_policy.py: which reference run the device follows, per-assembly differences to it,
+    the reference's own noise, and the policy verdict"""
+    from tests import parity_policy as P
+    cum, checked, stable = P.reference_noise(key)
+    out = {"noise": cum, "checked_assemblies": checked, "path_stable": stable,
+           "twins": [x for x in P.ALL_TWINS if key + x in RUNS]}
+    try:
+        name, per, _ = P.check_against_reference_runs(key, trace, r)
+        out.update(follows=name, per_assembly_vs_followed=per, policy="pass")
+    except AssertionError as e:
+        out.update(policy=f"FAIL: {e}")
+    runs = [("golden", RUNS[key])] + [(x, RUNS[key + x]) for x in P.ALL_TWINS if key + x in RUNS]
+    out["final_by_run"] = {n: [R["num_iters"], R["gap"]] for n, R in runs}
     return out
 
 
@@ -61,7 +58,9 @@ def main():
     torch.cuda.set_device(0)
     from ttipm_amd import tt_ipm
     from ttipm_amd.utils import run_and_record
-    keys = sys.argv[1:] or [k for k, v in RUNS.items() if not v.get("bounded") and "_t" not in k.split("_s")[-1]]
+    from tests import parity_policy as P
+    keys = sys.argv[1:] or [k for k, v in RUNS.items() if not v.get("bounded") and not k.startswith("maxcut_12")
+                            and not any(k.endswith(x) for x in P.ALL_TWINS)]
     for key in keys:
         g = RUNS[key]
         cfg = yaml.safe_load(open(os.path.join(ROOT, "configs", g["config"] + ".yaml")))
@@ -80,7 +79,7 @@ def main():
             out[k] = [r[k], g[k], abs(r[k] - g[k]) / abs(g[k])]
             if key + "_t8" in RUNS:
                 out[k + "_t8"] = RUNS[key + "_t8"][k]
-        out.update(spread_report(trace, key))
+        out.update(policy_report(key, trace, r))
         out["trace"] = [{k: a[k] for k in KEYS + ("sigma", "ranksX")} for a in trace]
         print(json.dumps(out), flush=True)
 
