@@ -243,6 +243,9 @@ def _run_lgmres(op, rhs_flat, m, rtol):
                native=getattr(op, "h", 0), info=info)
     if D.ALGO is not None:  # applications made inside native chunks (the others counted themselves)
         D.count_algo(info.get("native_matvecs", 0) * op.mv_flops(), info.get("native_matvecs", 0), "schur_matvec")
+    if _LOCAL_TRACE:
+        print(f"  lgmres n={rhs_flat.numel()} restart={restart} its={info.get('its')} matvecs={info.get('matvecs')} "
+              f"reason={info.get('reason')}")
     return x
 
 
@@ -567,10 +570,12 @@ def tt_infeasible_newton_system(lhs, C, X, Y, Z, Tt, L, Ladj, b, mask, st):
     """`src/tt_ipm.py:429-475`"""
     rhs = TTBlockVector()
     pf = tt_compute_primal_feasibility(L, b, X, st)
-    st.primal_error = np.divide(T.tt_norm(pf), st.primal_error_normalisation)
+    npf = T.tt_norm(pf)
+    st.primal_error = np.divide(npf, st.primal_error_normalisation)
     st.is_primal_feasible = np.less(st.primal_error, st.feasibility_tol)
     df = tt_compute_dual_feasibility(C, Ladj, Z, Y, Tt, st)
-    st.dual_error = np.divide(T.tt_norm(df), st.dual_error_normalisation)
+    ndf = T.tt_norm(df)
+    st.dual_error = np.divide(ndf, st.dual_error_normalisation)
     st.is_dual_feasible = np.less(st.dual_error, (1 + (st.ineq_status is IneqStatus.ACTIVE)) * st.feasibility_tol)
     st.is_last_iter = st.is_last_iter or (st.is_primal_feasible and st.is_dual_feasible and st.is_central)
     if st.aho_direction:
@@ -581,10 +586,15 @@ def tt_infeasible_newton_system(lhs, C, X, Y, Z, Tt, L, Ladj, b, mask, st):
     else:
         lhs[2, 1] = T.tt_psd_rank_reduce(T.tt_MkronI(Z), eps=0.1 * st.eta * st.dual_error_normalisation)
         lhs[2, 2] = T.tt_psd_rank_reduce(T.tt_IkronM(X), eps=0.1 * st.eta * st.primal_error_normalisation)
+    # the row norms the KKT row scaling reads (`_tt_kkt_row_scales`) are these same values: kept with
+    # the row objects instead of being recomputed (one host read each)
+    rhs._norms = {}
     if not st.is_primal_feasible or st.is_last_iter:
         rhs[0] = pf
+        rhs._norms[0] = (pf, npf)
     if not st.is_dual_feasible or st.is_last_iter:
         rhs[1] = df
+        rhs._norms[1] = (df, ndf)
     if not st.is_central or st.is_last_iter:
         rhs[2] = tt_compute_centrality(X, Z, st)
     if st.ineq_status is IneqStatus.ACTIVE:
@@ -625,7 +635,8 @@ def _tt_rhs_row_norm(rhs, i):
     row = rhs.get_row(i)
     if row is None:
         return 0.0
-    n = T.tt_norm(row)
+    cached = getattr(rhs, "_norms", {}).get(i)
+    n = cached[1] if cached is not None and cached[0] is row else T.tt_norm(row)
     return float(n) if np.isfinite(n) else 0.0
 
 

@@ -80,6 +80,7 @@ def main():
             if key + "_t8" in RUNS:
                 out[k + "_t8"] = RUNS[key + "_t8"][k]
         out.update(policy_report(key, trace, r))
+        out["result"] = {k: r[k] for k in ("num_iters", "gap", "feas", "dual_feas", "ranksX", "ranksZ")}
         out["trace"] = [{k: a[k] for k in KEYS + ("sigma", "ranksX")} for a in trace]
         print(json.dumps(out), flush=True)
 

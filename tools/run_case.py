@@ -15,7 +15,7 @@ if os.environ.get("TTIPM_FUSED") == "0":
 
 prob, cfg_name, seed, rank = sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4])
 key = sys.argv[5] if len(sys.argv) > 5 else f"{cfg_name}_r{rank}_s{seed}"
-cfg = yaml.safe_load(open(os.path.join("configs", cfg_name + ".yaml")))
+cfg = yaml.safe_load(open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "configs", cfg_name + ".yaml")))
 trace = []
 t = time.time()
 r = run_and_record(prob, cfg, seed, rank, trace=trace, verbose=bool(os.environ.get("TTIPM_VERBOSE")))

@@ -13,7 +13,7 @@ from ttipm_amd.utils import create, solve  # noqa: E402
 
 prob, cfg_name, seed, rank = sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4])
 reps = int(sys.argv[5]) if len(sys.argv) > 5 else 4
-cfg = yaml.safe_load(open(os.path.join("configs", cfg_name + ".yaml")))
+cfg = yaml.safe_load(open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "configs", cfg_name + ".yaml")))
 out = []
 for i in range(reps + 1):
     prep = create(prob, cfg, seed, rank, verbose=False)
