@@ -194,6 +194,10 @@ int ttk_mul_nd(void *stream, const double *src, const double *src2, double *dst,
                const int64_t *shape, const int64_t *sstride, const int64_t *s2stride,
                const int64_t *dstride, double alpha, double beta);
 int ttk_recip(void *stream, const double *src, double *dst, int64_t n);
+/* n contiguous copies dst[i][0:count[i]] = src[i][0:count[i]] in one launch (the core copies of a
+ * TT before an in-place rounding or scaling: the reference rebinds list entries and never writes
+ * the caller's cores, cy_src/tt_ops_cy.pyx:179-226); src/dst/count are host arrays of n entries. */
+int ttk_copy_many(void *stream, int n, const double *const *src, double *const *dst, const int64_t *count);
 /* tt_add core assembly (`_block_diag_tensor` / concatenation, cy_src/tt_ops_cy.pyx:228-258) in one
  * launch from contiguous cores a (ra, mid, Ra), b (rb, mid, Rb): mode 0 block diagonal, 1 concat
  * along the last axis (ra == rb), 2 along the first axis (Ra == Rb); out contiguous. */

@@ -11,6 +11,9 @@ import scipy.sparse.linalg
 from . import tt as T
 from .tt import einsum
 
+# diagnostics (tools/decision_trace.py): a list receives one record per AMEn truncation rank scan
+RANK_TRACE = None
+
 
 def get_block(i, btt):
     """`src/tt_als.py:12-14`"""
@@ -266,15 +269,20 @@ def _sweep(c, backward, swp, last, dsf):
                 cur = einsum("rbR,Rdk->rbdk", u[:, :, :r0], v[:r0])
                 res = Ak.local_product(c.XAX[k], c.XAX[k + 1], np.transpose(cur, (0, 2, 1, 3))) - rhs
             r = r0
+            rats = []
             for r in range(r0 - 1, 0, -1):
                 if backward:
                     piece = np.reshape((u[:, None, r] @ v[None, r, :]).T, (rx[k], B, N[k], rx[k + 1]))
                 else:
                     piece = einsum("rbR,Rdk->rdbk", u[:, :, None, r], v[None, r])
                 res -= Ak.local_product(c.XAX[k], c.XAX[k + 1], piece)
-                if np.linalg.norm(res) / nrhs > trunc_lim:
+                rats.append(float(np.linalg.norm(res) / nrhs))
+                if rats[-1] > trunc_lim:
                     break
             r += 1
+            if RANK_TRACE is not None:
+                RANK_TRACE.append({"e": "rank", "k": int(k), "bwd": bool(backward), "r0": int(r0), "r": int(r),
+                                   "lim": float(trunc_lim), "rat": rats})
             if backward:
                 u = np.reshape(u[:, :r].T, (r, N[k], rx[k + 1]))
                 v = v[:r].T.reshape(rx[k], B, r)

@@ -92,6 +92,7 @@ _SIGS = {
     "ttk_gemm_set_splitk": (i32, [i32]),
     "ttk_contract_stats": (i32, [vp, i32]),
     "ttk_syev_extreme": (i32, [vp, vp, i32, i32, vp, vp, vp]),
+    "ttk_copy_many": (i32, [vp, i32, vp, vp, vp]),
     "ttk_lgmres_arnoldi_sync": (i32, [vp, vp, i32, i32, vp, i32, f64, c_dp, c_ip]),
     "ttk_schur_build": (i32, [vp, i32, i64, c_i64p, vp, c_i64p]),
     "ttk_schur_apply": (i32, [vp, i64, vp, vp]),

@@ -363,6 +363,25 @@ __device__ __forceinline__ void nd_offsets(const ttk::NdDesc &d, int64_t lin, in
   }
 }
 
+// several contiguous copies in one launch (ttk_copy_many): segment j owns flat indices
+// [off[j], off[j+1]); exact copies
+struct CopyMany {
+  static constexpr int MAXN = 32;
+  const double *src[MAXN];
+  double *dst[MAXN];
+  int64_t off[MAXN + 1];
+  int n;
+};
+
+__global__ void copy_many_kernel(CopyMany m) {
+  const int64_t total = m.off[m.n], stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += stride) {
+    int j = 0;
+    while (e >= m.off[j + 1]) ++j;
+    m.dst[j][e - m.off[j]] = m.src[j][e - m.off[j]];
+  }
+}
+
 __global__ void copy_nd_kernel(const double *__restrict__ src, double *__restrict__ dst,
                                ttk::NdDesc d, double alpha, double beta) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < d.total;
@@ -953,6 +972,24 @@ int ttk_recip(void *stream, const double *src, double *dst, int64_t n) {
   if (n <= 0) return TTK_OK;
   hipLaunchKernelGGL(recip_kernel, dim3(grid_for(n, 256)), dim3(256), 0, TTK_STREAM(stream), src, dst, n);
   TTK_LAUNCH_CHECK();
+  return TTK_OK;
+}
+
+int ttk_copy_many(void *stream, int n, const double *const *src, double *const *dst, const int64_t *count) {
+  if (int brc = ttk::batch_barrier(stream)) return brc;  // an open einsum batch may feed this call
+  for (int i0 = 0; i0 < n; i0 += CopyMany::MAXN) {
+    CopyMany m{};
+    m.n = n - i0 < CopyMany::MAXN ? n - i0 : CopyMany::MAXN;
+    m.off[0] = 0;
+    for (int j = 0; j < m.n; ++j) {
+      m.src[j] = src[i0 + j];
+      m.dst[j] = dst[i0 + j];
+      m.off[j + 1] = m.off[j] + (count[i0 + j] > 0 ? count[i0 + j] : 0);
+    }
+    if (m.off[m.n] == 0) continue;
+    hipLaunchKernelGGL(copy_many_kernel, dim3(grid_for(m.off[m.n], 256)), dim3(256), 0, TTK_STREAM(stream), m);
+    TTK_LAUNCH_CHECK();
+  }
   return TTK_OK;
 }
 

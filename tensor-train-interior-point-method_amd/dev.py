@@ -202,6 +202,24 @@ def clone(src):
     return copy_(out, src)
 
 
+def clone_many(srcs):
+    """[clone(t) for t in srcs] as ONE allocation and ONE launch (ttk_copy_many) when every source
+    is contiguous (exact copies; the clones are views of one buffer)."""
+    n = len(srcs)
+    if n < 2 or DEV.type != "cuda" or not all(t.is_contiguous() for t in srcs):
+        return [clone(t) for t in srcs]
+    counts = [t.numel() for t in srcs]
+    buf = empty(sum(counts))
+    outs, o = [], 0
+    for t, c in zip(srcs, counts):
+        outs.append(buf[o:o + c].view(t.shape))
+        o += c
+    check(lib.ttk_copy_many(_stream(), n, (ctypes.c_void_p * n)(*[t.data_ptr() for t in srcs]),
+                            (ctypes.c_void_p * n)(*[t.data_ptr() for t in outs]), (ctypes.c_int64 * n)(*counts)),
+          "copy_many")
+    return outs
+
+
 def mul_(dst, a, b, alpha=1.0, beta=0.0):
     """dst = alpha * a * b + beta * dst (element-wise, same shapes, any strides)."""
     f = _FAST or _fast()

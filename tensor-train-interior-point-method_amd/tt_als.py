@@ -17,6 +17,8 @@ from . import tt_ops as T
 from .dev import einsum
 
 APPLY = "lsr,smnS,LSR,rnR->lmL"
+# diagnostics (tools/decision_trace.py): a list receives one record per AMEn truncation rank scan
+RANK_TRACE = None
 APPLY_T = "lsr,smnS,LSR,lmL->rnR"
 
 
@@ -414,6 +416,10 @@ def _sweep(c, backward, swp, last, dsf):
                     if D.norm_of(ss[q]) / nrhs > trunc_lim:
                         break
             r += 1
+            if RANK_TRACE is not None:
+                RANK_TRACE.append({"e": "rank", "k": int(k), "bwd": bool(backward), "r0": int(r0), "r": int(r),
+                                   "lim": float(trunc_lim),
+                                   "rat": [float(D.norm_of(ss[q]) / nrhs) for q in range(r0 - r + 1)] if cands else []})
             if backward:
                 u_new = D.clone(U[:, :r].t()).view(r, N[k], rx[k + 1])
                 v_new = D.clone(v[:r].t()).view(rx[k], B, r)

@@ -622,7 +622,7 @@ def _tt_mask_symmetrise(M, mask, e):
 
 
 def _tt_copy(tt):
-    return [D.clone(c) for c in tt]
+    return D.clone_many(tt)
 
 
 def _tt_scale_nondestructive(tt, s):

@@ -293,7 +293,7 @@ def _native_round(tt, eps, mode):
     cores are copied first (the reference rebinds list entries and never writes the caller's
     arrays), the rounded cores are views of those copies.  Returns (tt, tail factor or None)."""
     d = len(tt)
-    cs = [D.clone(c) for c in tt]
+    cs = D.clone_many(tt)
     mids = [tuple(c.shape[1:-1]) for c in tt]
     ptrs = (ctypes.c_void_p * d)(*[c.data_ptr() for c in cs])
     inner = (ctypes.c_int64 * d)(*[int(np.prod(m)) for m in mids])

@@ -259,8 +259,6 @@ def make_runs(only=None, jobs=1):
     """Each run in its own process (1 BLAS thread, PYTHONHASHSEED=0: opt_einsum's tensordot axis order
     follows frozenset iteration, so the hash seed pins the summation order); `jobs` at a time."""
     import subprocess
-    path = os.path.join(HERE, "runs.json")
-    out = json.load(open(path)) if os.path.exists(path) else {}
     todo = []
     for prob, cfg, seed, rank, fixed, nmax in RUNS:
         key = run_key(cfg, rank, seed, fixed, nmax)
@@ -279,16 +277,22 @@ def make_runs(only=None, jobs=1):
         if p.wait() != 0:
             print(key, "FAILED", flush=True)
             continue
-        res = json.load(open(tmp))
-        print(key, {k: res.get(k) for k in ("num_iters", "gap", "feas", "dual_feas", "sec_per_iter")}, flush=True)
-        import fcntl
-        with open(path + ".lock", "w") as lk:  # several make_runs invocations may merge at once
-            fcntl.flock(lk, fcntl.LOCK_EX)
-            out = json.load(open(path)) if os.path.exists(path) else {}
-            out[key] = res
-            with open(path + ".tmp", "w") as f:
-                json.dump(out, f, indent=1)
-            os.replace(path + ".tmp", path)
+        merge(key, tmp)
+
+
+def merge(key, tmp):
+    """add one finished run's JSON (`one` mode output) to runs.json under `key`"""
+    import fcntl
+    path = os.path.join(HERE, "runs.json")
+    res = json.load(open(tmp))
+    print(key, {k: res.get(k) for k in ("num_iters", "gap", "feas", "dual_feas", "sec_per_iter")}, flush=True)
+    with open(path + ".lock", "w") as lk:  # several make_runs invocations may merge at once
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        out = json.load(open(path)) if os.path.exists(path) else {}
+        out[key] = res
+        with open(path + ".tmp", "w") as f:
+            json.dump(out, f, indent=1)
+        os.replace(path + ".tmp", path)
 
 
 if __name__ == "__main__":
@@ -297,6 +301,9 @@ if __name__ == "__main__":
         nmax = int(sys.argv[8]) if len(sys.argv) > 8 else 0
         with open(tmp, "w") as f:
             json.dump(run_reference(prob, cfg, int(seed), int(rank), bool(int(fixed)), nmax), f)
+        sys.exit(0)
+    if len(sys.argv) > 1 and sys.argv[1] == "merge":  # merge KEY TMP: a run finished outside make_runs
+        merge(sys.argv[2], sys.argv[3])
         sys.exit(0)
     what = sys.argv[1] if len(sys.argv) > 1 else "all"
     rest = [a for a in sys.argv[2:] if not a.startswith("-j")]

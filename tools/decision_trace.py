@@ -8,6 +8,7 @@ reference's control flow takes, so two runs can be aligned event by event.
     python tools/decision_trace.py dev maxcut maxcut_10 14 1 [max_assemblies] > dev.jsonl  (GPU box)
     python tools/decision_trace.py oracle maxcut maxcut_10 14 1 [max_assemblies]  (the CPU restatement)
     python tools/decision_trace.py diff ref.jsonl dev.jsonl
+    DT_RANKS=1 (oracle / dev): also every AMEn truncation rank scan (r0, chosen r, limit, ratios)
 
 Hooks wrap the module-level names the reference's tt_ipm looks up at call time
 (`_ipm_local_solver(_ineq)`, `tt_restarted_block_amen`, `_tt_get_step_sizes`,
@@ -111,6 +112,9 @@ def run_oracle(problem, cfg_name, seed, rank, nmax):
     from oracle import tt as OT
     ev = []
     install(OI, lambda t: float(np.linalg.norm(t)), lambda x: [int(c.shape[-1]) for c in x[:-1]], ev, ORACLE_NAMES)
+    if os.environ.get("DT_RANKS"):  # also every AMEn truncation rank scan (oracle/als.py RANK_TRACE)
+        from oracle import als as OA_
+        OA_.RANK_TRACE = ev
     if os.environ.get("ORACLE_JACOBI_SVD"):  # experiment: LAPACK dgejsv (Jacobi, relative accuracy) SVDs
         import scipy.linalg as sla_mod
         from scipy.linalg import lapack
@@ -232,6 +236,9 @@ def run_dev(problem, cfg_name, seed, rank, nmax):
     from ttipm_amd.utils import run_and_record
     ev = []
     install(tt_ipm, lambda t: float(D.norm(t)), lambda x: [int(c.shape[-1]) for c in x[:-1]], ev)
+    if os.environ.get("DT_RANKS"):  # also every AMEn truncation rank scan (tt_als.RANK_TRACE)
+        from ttipm_amd import tt_als
+        tt_als.RANK_TRACE = ev
     cfg = yaml.safe_load(open(os.path.join(ROOT, "configs", cfg_name + ".yaml")))
 
     class Stop(Exception):
