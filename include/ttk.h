@@ -66,6 +66,8 @@ void *ttk_ctx_stream(ttk_ctx ctx);
  *   SPLITK_MINK     K per split (default from env TTK_SPLITK_MINK, else 256)
  *   LGMRES_MW_MIN   (it+1)*n at or above which the LGMRES Arnoldi / build / augmentation steps
  *                   run as multi-workgroup kernels (default 16384; 0 everywhere, INT_MAX never)
+ *   MFMA_CSPLIT     1: wide MFMA-stage apply rows spread their stage-3 output tiles over several
+ *                   workgroups per row (bit-identical; default from env TTK_MFMA_CSPLIT, else 1)
  * ttk_ctx_set_knob stores value and returns the previous one in *old (may be NULL). */
 enum ttk_knob {
   TTK_KNOB_FUSED_APPLY = 0,
@@ -73,7 +75,8 @@ enum ttk_knob {
   TTK_KNOB_SPLITK = 2,
   TTK_KNOB_SPLITK_MINK = 3,
   TTK_KNOB_LGMRES_MW_MIN = 4,
-  TTK_KNOB_COUNT = 5
+  TTK_KNOB_MFMA_CSPLIT = 5,
+  TTK_KNOB_COUNT = 6
 };
 int ttk_ctx_set_knob(ttk_ctx ctx, int knob, int value, int *old);
 int ttk_ctx_get_knob(ttk_ctx ctx, int knob, int *value);

@@ -23,7 +23,55 @@ Parity of this restatement against real PETSc is UNPINNED (no reference fixture 
 the stale `tests/test_tt_preprocessing.py:25-36` only solves a 2x2 system to 1e-10).  The GPU
 LGMRES in the product follows the same algorithm and is pinned against this restatement.
 """
+import os
+
 import numpy as np
+
+# Reduction kernels.  The default restatement uses NumPy/BLAS reductions (np.dot, gemv).  Real
+# PETSc's rounding differs from both the restatement and the device at that level: VecNorm_Seq is
+# BLAS dnrm2 (scaled sum of squares), VecMDot_Seq sums x[i]*y[i] in index order per vector, and
+# VecMAXPY_Seq adds the vectors in groups of 4 (the nv % 4 remainder first).  GOLDEN_PETSC_KERNELS=1
+# (tests/golden/make_golden.py's `_p<H>` twins) restates those kernels, so the reference can be re-run
+# under PETSc-like reduction orders: the spread of those twins is reference rounding noise that the
+# restatement alone cannot show.  Test infrastructure only.
+PETSC_KERNELS = os.environ.get("GOLDEN_PETSC_KERNELS") == "1"
+
+
+def _norm(v):
+    if PETSC_KERNELS:
+        from scipy.linalg import blas
+        return float(blas.dnrm2(v))
+    return float(np.sqrt(np.dot(v, v)))
+
+
+def _mdot(V, w):
+    """h_j = <V_j, w>"""
+    if PETSC_KERNELS:
+        return np.array([np.cumsum(vj * w)[-1] for vj in V]) if len(V) else np.zeros(0)
+    return V @ w
+
+
+def _maxpy_into(x, coef, V):
+    """x += sum_j coef_j V_j in VecMAXPY_Seq's order (the nv % 4 remainder group, then groups of 4,
+    each group's terms summed before it is added to x)"""
+    nv = len(coef)
+    r = nv & 3
+    if r:
+        acc = coef[0] * V[0]
+        for j in range(1, r):
+            acc = acc + coef[j] * V[j]
+        x += acc
+    for j in range(r, nv, 4):
+        x += coef[j] * V[j] + coef[j + 1] * V[j + 1] + coef[j + 2] * V[j + 2] + coef[j + 3] * V[j + 3]
+    return x
+
+
+def _maxpy_sum(coef, V):
+    """sum_j coef_j V_j (VecSet(0) + VecMAXPY when PETSC_KERNELS)"""
+    if not PETSC_KERNELS:
+        return coef @ V
+    return _maxpy_into(np.zeros(V.shape[1]), coef, V)
+
 
 CONVERGED_RTOL = 2
 CONVERGED_ATOL = 3
@@ -86,7 +134,7 @@ def lgmres(matvec, b, rtol=1e-8, max_it=300, restart=30, augment=2,
         it_total = it_arnoldi + aug_ct
         V = np.zeros((it_total + 1, n))
         V[0] = r
-        res = float(np.sqrt(np.dot(r, r)))
+        res = _norm(r)
         GRS[0] = res
         if res == 0.0:
             reason = CONVERGED_ATOL
@@ -109,11 +157,14 @@ def lgmres(matvec, b, rtol=1e-8, max_it=300, restart=30, augment=2,
                         break
                 V[loc_it + 1] = a_augvecs[spot]
             # classical Gram-Schmidt, no refinement
-            h = V[:loc_it + 1] @ V[loc_it + 1]
-            V[loc_it + 1] -= h @ V[:loc_it + 1]
+            h = _mdot(V[:loc_it + 1], V[loc_it + 1])
+            if PETSC_KERNELS:  # VecMAXPY(w, it+1, -h, V)
+                _maxpy_into(V[loc_it + 1], -h, V[:loc_it + 1])
+            else:
+                V[loc_it + 1] -= h @ V[:loc_it + 1]
             HH[:loc_it + 1, loc_it] = h
             HES[:loc_it + 1, loc_it] = h
-            tt = float(np.sqrt(np.dot(V[loc_it + 1], V[loc_it + 1])))
+            tt = _norm(V[loc_it + 1])
             HH[loc_it + 1, loc_it] = tt
             HES[loc_it + 1, loc_it] = tt
             hapbnd = abs(tt / GRS[loc_it])
@@ -168,7 +219,7 @@ def lgmres(matvec, b, rtol=1e-8, max_it=300, restart=30, augment=2,
                 for j in range(k + 1, it + 1):
                     t0 = t0 - HH[k, j] * GRS[j]
                 GRS[k] = t0 / HH[k, k]
-            temp = GRS[:ita] @ V[:ita]
+            temp = _maxpy_sum(GRS[:ita], V[:ita])
             for ii in range(it_aug):
                 spot = 0
                 for jj in range(aug_dim):
@@ -191,7 +242,7 @@ def lgmres(matvec, b, rtol=1e-8, max_it=300, restart=30, augment=2,
                 for ii in range(aug_dim):
                     if aug_order[ii] == aug_dim:
                         spot = ii
-            nrm = float(np.sqrt(np.dot(aug_temp, aug_temp)))
+            nrm = _norm(aug_temp)
             inv = 1.0 / nrm
             augvecs[spot] = aug_temp * inv
             aug_order[:aug_dim] += 1
@@ -200,7 +251,7 @@ def lgmres(matvec, b, rtol=1e-8, max_it=300, restart=30, augment=2,
             for ii in range(it_total + 1):
                 for jj in range(0, min(ii + 2, it_total + 1)):
                     avec[jj] += HES[jj, ii] * GRS[ii]
-            a_augvecs[spot] = (avec @ V[:it_total + 1]) * inv
+            a_augvecs[spot] = _maxpy_sum(avec, V[:it_total + 1]) * inv
         itcount += cycle_its
         if itcount >= max_it:
             if not reason:

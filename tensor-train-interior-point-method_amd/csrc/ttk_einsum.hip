@@ -513,6 +513,11 @@ struct ApplyArgs {
   double alpha, beta;
   int mfma;  // 1: the row runs on the MFMA stages (apply_row_mfma), 0: VALU (apply_row)
   int qlds = 0;  // VALU rows: 1 stages the whole Q (nc*nS*nd doubles after T2) in LDS for stage 3
+  // MFMA rows: workgroups per output row.  Workgroup h of a row computes stage 3 for the 16-column
+  // output tiles j with j % csplit == h only (stages 1-2 are repeated per workgroup), so a wide row's
+  // (tile, K block) pairs spread over csplit CUs; every output element is still computed by the same
+  // MFMA sequence and summed in the same order (bit-identical for any csplit)
+  int csplit = 1;
 };
 
 // Association follows the greedy pairwise plan the reference's opt_einsum picks for these shapes
@@ -736,8 +741,11 @@ __device__ unsigned long long g_mph[8];
 #define TTK_MPH(K)
 #endif
 
+// column c of an output row belongs to workgroup h of the row's csplit workgroups
+__device__ __forceinline__ bool mine(int c, int h, int cs) { return cs == 1 || ((c >> 4) % cs) == h; }
+
 template <bool DIRECT>
-__device__ void apply_row_mfma(const ApplyArgs &g, int a, double *sm, double *orow) {
+__device__ void apply_row_mfma(const ApplyArgs &g, int a, double *sm, double *orow, int h = 0) {
 #ifdef TTK_MFMA_PROFILE
   unsigned long long t_ph_ = wall_clock64();
   if (threadIdx.x == 0) atomicAdd(&g_mph[7], 1ull);
@@ -792,14 +800,14 @@ __device__ void apply_row_mfma(const ApplyArgs &g, int a, double *sm, double *or
     // global memory; each pair's block sum goes to part[block][i][c] (the Q chunk's LDS), then the
     // blocks are summed in K order -- the same additions as the sequential loop below
     const int lane = tid & 63, wid = tid >> 6, nw = nt >> 6, kl = lane >> 4;
-    const int tn = (nc + 15) >> 4, ntile = ((ni + 15) >> 4) * tn;
+    const int cs = g.csplit, tn = (nc + 15) >> 4, tnh = (tn - h + cs - 1) / cs, ntile = ((ni + 15) >> 4) * tnh;
     const int nch = (K3 + kc - 1) / kc, gch = QCHUNK_MAX / nio;
     double *part = Qc;
     for (int c0 = 0; c0 < nch; c0 += gch) {
       const int ng = nch - c0 < gch ? nch - c0 : gch;
       for (int t = wid; t < ntile * ng; t += nw) {
         const int tile = t % ntile, ch = c0 + t / ntile;
-        const int m0 = (tile / tn) << 4, n0 = (tile % tn) << 4;
+        const int m0 = (tile / tnh) << 4, n0 = (h + cs * (tile % tnh)) << 4;
         const int am = m0 + (lane & 15), bn = n0 + (lane & 15);
         const bool mok = am < ni, nok = bn < nc;
         const int k0 = ch * kc, w = k0 + kc < K3 ? kc : K3 - k0;
@@ -815,6 +823,7 @@ __device__ void apply_row_mfma(const ApplyArgs &g, int a, double *sm, double *or
       }
       __syncthreads();
       for (int e = tid; e < nio; e += nt) {
+        if (!mine(e % nc, h, cs)) continue;
         double s = c0 == 0 ? part[e] : acc[e] + part[e];
         for (int j = 1; j < ng; ++j) s = s + part[j * nio + e];
         acc[e] = s;
@@ -839,6 +848,7 @@ __device__ void apply_row_mfma(const ApplyArgs &g, int a, double *sm, double *or
   if (DIRECT) {
     for (int e = tid; e < ni * nc; e += nt) {
       const int i = e / nc, c = e - i * nc;
+      if (!mine(c, h, g.csplit)) continue;
       double *o = g.out + a * g.os[0] + i * g.os[1] + c * g.os[2];
       *o = g.beta != 0.0 ? g.alpha * acc[e] + g.beta * *o : g.alpha * acc[e];
     }
@@ -848,7 +858,7 @@ __device__ void apply_row_mfma(const ApplyArgs &g, int a, double *sm, double *or
 
 __global__ __launch_bounds__(1024) void fused_apply_mfma_kernel(ApplyArgs g) {
   extern __shared__ double sm[];
-  apply_row_mfma<true>(g, blockIdx.x, sm, nullptr);
+  apply_row_mfma<true>(g, (int)blockIdx.x / g.csplit, sm, nullptr, (int)blockIdx.x % g.csplit);
 }
 
 __global__ __launch_bounds__(1024) void fused_apply_kernel(ApplyArgs g) {
@@ -876,25 +886,28 @@ __global__ __launch_bounds__(1024) void fused_apply_multi_kernel(ApplyLaunch L) 
   int t = 0;
   while (t + 1 < L.ntask && (int)blockIdx.x >= L.off[t + 1]) ++t;
   const ApplyTask &T = L.task[t];
-  const int a = (int)blockIdx.x - L.off[t];
   const ApplyArgs &g0 = T.t[0];
+  const int cs = g0.csplit, a = ((int)blockIdx.x - L.off[t]) / cs, h = ((int)blockIdx.x - L.off[t]) % cs;
   const int ni = g0.ni, nc = g0.nc, tid = threadIdx.x, nt = blockDim.x;
   double *orow = sm, *acc = sm + ni * nc, *work = acc + ni * nc;
   for (int k = 0; k < T.nterms; ++k) {
-    if (T.t[k].mfma) apply_row_mfma<false>(T.t[k], a, work, k == 0 ? orow : acc);
+    if (T.t[k].mfma) apply_row_mfma<false>(T.t[k], a, work, k == 0 ? orow : acc, h);
     else apply_row<false>(T.t[k], a, work, k == 0 ? orow : acc);
     __syncthreads();
     if (k > 0) {
       const double al = T.t[k].alpha;
-      for (int e = tid; e < ni * nc; e += nt) orow[e] = al * acc[e] + 1.0 * orow[e];
+      for (int e = tid; e < ni * nc; e += nt)
+        if (mine(e % nc, h, cs)) orow[e] = al * acc[e] + 1.0 * orow[e];
     } else {
       const double al = g0.alpha;
-      for (int e = tid; e < ni * nc; e += nt) orow[e] = al * orow[e];
+      for (int e = tid; e < ni * nc; e += nt)
+        if (mine(e % nc, h, cs)) orow[e] = al * orow[e];
     }
     __syncthreads();
   }
   for (int e = tid; e < ni * nc; e += nt) {
     const int i = e / nc, c = e - i * nc;
+    if (!mine(c, h, cs)) continue;
     const int64_t oi = a * g0.os[0] + i * g0.os[1] + c * g0.os[2];
     double v = orow[e];
     if (T.oscale) v = (1.0 * v) * T.oscale[oi];
@@ -927,6 +940,25 @@ static bool mfma_enabled() { return ttk::ctx().knob[TTK_KNOB_FUSED_MFMA] != 0; }
 // from L2 with one workgroup per CU (LDS-bound occupancy), so 16 waves keep 4x the loads in flight of
 // 4; every output element / tile is still computed by one thread / wave in the same order
 static const int g_mfma_threads = getenv("TTK_MFMA_THREADS") ? atoi(getenv("TTK_MFMA_THREADS")) : 1024;
+
+// workgroups per MFMA output row (ApplyArgs::csplit): enough that each workgroup's share of the
+// stage-3 (tile, K block) pairs is about one round over its waves, but no more workgroups in the
+// launch than CUs (the repeated stages 1-2 would then cost more than the split saves).
+// rows_total: workgroups of the launch at csplit 1.  Knob TTK_KNOB_MFMA_CSPLIT = 0 disables
+// (bit-identical either way).
+static int choose_csplit(const ApplyArgs &g, int64_t rows_total) {
+  if (!ttk::ctx().knob[TTK_KNOB_MFMA_CSPLIT] || !g.mfma || (int64_t)g.ni * g.nc > QCHUNK_MAX || g.nc > QCHUNK_MAX / 4) return 1;
+  const int K3 = g.nS * g.nd, tn = (g.nc + 15) >> 4, tm = (g.ni + 15) >> 4;
+  int kc = QCHUNK_MAX / g.nc;
+  kc = kc >= 8 ? (kc & ~7) : kc;
+  kc = kc > K3 ? K3 : kc;
+  const int64_t pairs = (int64_t)tm * tn * ((K3 + kc - 1) / kc), waves = g_mfma_threads / 64;
+  int cs = (int)((pairs + waves - 1) / waves);
+  cs = cs > tn ? tn : cs;
+  const int64_t cap = rows_total > 0 ? 256 / rows_total : 1;
+  if (cs > cap) cs = (int)cap;
+  return cs < 1 ? 1 : cs;
+}
 
 extern "C" int ttk_mfma_profile(unsigned long long *out8, int reset) {  // g_mph (zeros unless profiled)
   if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_mph), 8 * sizeof(unsigned long long)) != hipSuccess) return TTK_ERR_HIP;
@@ -1048,9 +1080,11 @@ int fused_apply_try(void *stream, const char *eq, const int64_t *desc, double *o
   if (dbg_sync) (void)hipStreamSynchronize(TTK_STREAM(stream));
   hipEvent_t e0, e1;
   if (ttk::contract_events_ext(&e0, &e1) != TTK_OK) return -1;
-  if (g.mfma)
-    hipExtLaunchKernelGGL(fused_apply_mfma_kernel, dim3(g.na), dim3(g_mfma_threads), shm, TTK_STREAM(stream), e0, e1, 0,
-                          g);
+  if (g.mfma) {
+    g.csplit = choose_csplit(g, g.na);
+    hipExtLaunchKernelGGL(fused_apply_mfma_kernel, dim3(g.na * g.csplit), dim3(g_mfma_threads), shm, TTK_STREAM(stream),
+                          e0, e1, 0, g);
+  }
   else
     hipExtLaunchKernelGGL(fused_apply_kernel, dim3(g.na), dim3(256), shm, TTK_STREAM(stream), e0, e1, 0, g);
   TTK_LAUNCH_CHECK();
@@ -1259,10 +1293,20 @@ int ttk_schur_build(ttk_ctx ctx, int ineq, int64_t m, const int64_t *descs, cons
   op.oseg[1][0] = 1;
   for (int s = 0; s < 2; ++s) {
     ApplyLaunch &L = op.st[s];
+    int64_t rows = 0;
+    for (int t = 0; t < L.ntask; ++t) rows += L.task[t].t[0].na;
     L.off[0] = 0;
     for (int t = 0; t < L.ntask; ++t) {
-      L.off[t + 1] = L.off[t] + L.task[t].t[0].na;
-      for (int k = 0; k < L.task[t].nterms; ++k) op.flops += term_flops(L.task[t].t[k]);
+      ApplyTask &T = L.task[t];
+      int cs = 0;  // one split per task (its terms share the output row): the smallest of its MFMA terms'
+      for (int k = 0; k < T.nterms; ++k)
+        if (T.t[k].mfma) {
+          const int c = choose_csplit(T.t[k], rows);
+          cs = cs == 0 || c < cs ? c : cs;
+        }
+      for (int k = 0; k < T.nterms; ++k) T.t[k].csplit = cs > 0 ? cs : 1;
+      L.off[t + 1] = L.off[t] + T.t[0].na * T.t[0].csplit;
+      for (int k = 0; k < T.nterms; ++k) op.flops += term_flops(T.t[k]);
     }
     op.shm[s] = multi_lds(L);
     if (op.shm[s] > (size_t)APPLY_LDS_DOUBLES * sizeof(double))  // multi-task stage beyond LDS
@@ -1396,8 +1440,9 @@ __global__ __launch_bounds__(1024) void fused_apply_group_kernel(FusedGroup G) {
   extern __shared__ double sm[];
   int t = 0;
   while (t + 1 < G.n && (int)blockIdx.x >= G.off[t + 1]) ++t;
-  if (G.t[t].mfma) apply_row_mfma<true>(G.t[t], (int)blockIdx.x - G.off[t], sm, nullptr);
-  else apply_row<true>(G.t[t], (int)blockIdx.x - G.off[t], sm, nullptr);
+  const int local = (int)blockIdx.x - G.off[t];
+  if (G.t[t].mfma) apply_row_mfma<true>(G.t[t], local / G.t[t].csplit, sm, nullptr, local % G.t[t].csplit);
+  else apply_row<true>(G.t[t], local, sm, nullptr);
 }
 
 inline bool overlap(const Span &a, const Span &b) { return a.lo < b.hi && b.lo < a.hi; }
@@ -1431,14 +1476,16 @@ int launch_fused_group(hipStream_t st, const std::vector<const BNode *> &v) {
     FusedGroup G;
     G.n = (int)(v.size() - base < (size_t)FGROUP_MAX ? v.size() - base : FGROUP_MAX);
     G.off[0] = 0;
-    int64_t lds = 0;
+    int64_t lds = 0, rows = 0;
     double flops = 0.0;
     bool mf = false;
+    for (int i = 0; i < G.n; ++i) rows += v[base + i]->f.na;
     for (int i = 0; i < G.n; ++i) {
       const BNode &n = *v[base + i];
       G.t[i] = n.f;
+      G.t[i].csplit = choose_csplit(n.f, rows);
       mf = mf || n.f.mfma;
-      G.off[i + 1] = G.off[i] + n.f.na;
+      G.off[i + 1] = G.off[i] + n.f.na * G.t[i].csplit;
       lds = n.lds > lds ? n.lds : lds;
       flops += term_flops(n.f);
     }

@@ -172,6 +172,7 @@ def run_reference(problem, cfg_name, seed, rank, fixed_ineq=True, max_assemblies
             "num_iters": int(info["num_iters"]), "runtime": t3 - t2,
             "sec_per_iter": (t3 - t2) / max(1, int(info["num_iters"])), "gap": float(gap), "feas": float(feas),
             "hash_seed": os.environ.get("PYTHONHASHSEED"), "svd": os.environ.get("GOLDEN_SVD") or "scipy default",
+            "petsc_kernels": os.environ.get("GOLDEN_PETSC_KERNELS") == "1",
             "dual_feas": float(dfeas), "ranksX": info["ranksX"], "ranksY": info["ranksY"],
             "ranksZ": info["ranksZ"], "trace": trace, "blas_threads": os.environ.get("OPENBLAS_NUM_THREADS")}
 
@@ -227,10 +228,12 @@ RUNS = [
     ("maxcut", "maxcut_12", 1, 2, True, 0),
     ("maxcut", "maxcut_12", 2, 2, True, 0),  # pathological in the reference (29 iterations, gap 4.3e-2)
     ("maxcut", "maxcut_12", 3, 2, True, 0),  # pathological in the reference (14 iterations, gap 1.3e-2)
-    ("maxcut", "maxcut_12", 4, 2, True, 0),
-    ("maxcut", "maxcut_12", 5, 2, True, 0),
+    ("maxcut", "maxcut_12", 4, 2, True, 0),  # pathological in the reference (13 iterations, gap 0.38)
+    ("maxcut", "maxcut_12", 5, 2, True, 0),  # pathological in the reference (10 iterations, gap 4.7)
     ("maxcut", "maxcut_12", 6, 2, True, 0),
     ("maxcut", "maxcut_12", 7, 2, True, 0),
+    ("maxcut", "maxcut_12", 8, 2, True, 0),
+    ("maxcut", "maxcut_12", 9, 2, True, 0),
     # the rest of configs/maxcut_12.yaml's seeds: bounded traces (3 Newton systems each, every AMEn
     # solve and step pair before them) -- a full 1-thread reference run is ~35 min per seed
     ("maxcut", "maxcut_12", 45, 2, True, 3),
@@ -247,12 +250,16 @@ THREADS = int(os.environ.get("GOLDEN_THREADS", "1"))  # >1: the thread-spread ru
 # nothing below BLAS's threading thresholds)
 HASH = int(os.environ.get("GOLDEN_HASH", "0"))
 SVD = os.environ.get("GOLDEN_SVD", "")  # SVD-algorithm twins (key suffix _j<hash> for 'jacobi', patch_svd)
+# PETSc-reduction twins (key suffix _p<hash>): the LGMRES restatement with PETSc's Seq reduction
+# kernels (dnrm2, index-order VecMDot, grouped VecMAXPY; oracle/petsc_lgmres.py PETSC_KERNELS)
+PETSC = os.environ.get("GOLDEN_PETSC_KERNELS") == "1"
 
 
 def run_key(cfg, rank, seed, fixed, nmax):
     return f"{cfg}_r{rank}_s{seed}" + ("" if fixed else "_shipped") + (f"_b{nmax}" if nmax else "") + \
         (f"_t{THREADS}" if THREADS > 1 else "") + \
-        (f"_j{HASH}" if SVD == "jacobi" else (f"_{SVD}{HASH}" if SVD else (f"_h{HASH}" if HASH else "")))
+        (f"_p{HASH}" if PETSC else
+         (f"_j{HASH}" if SVD == "jacobi" else (f"_{SVD}{HASH}" if SVD else (f"_h{HASH}" if HASH else ""))))
 
 
 def make_runs(only=None, jobs=1):

@@ -20,7 +20,10 @@ def is_pathological(r):
 #   _h1.._h3   other PYTHONHASHSEEDs: opt_einsum orders each contraction's tensordot axes by
 #              frozenset iteration, so the hash seed picks among equally valid summation orders;
 #   _j0.._j7   its scipy.linalg.svd calls on LAPACK's one-sided Jacobi SVD (dgejsv, high relative
-#              accuracy -- the algorithm class of the device SVD) with hash seeds 0..7.
+#              accuracy -- the algorithm class of the device SVD) with hash seeds 0..7;
+#   _p0.._p3   its LGMRES (the PETSc restatement, PETSc itself is absent) with PETSc's Seq reduction
+#              kernels (dnrm2 norms, index-order VecMDot, grouped VecMAXPY), hash seeds 0..3 -- the
+#              real PETSc's rounding is unknown here, so these spreads count as the reference's noise.
 # The AMEn rank decisions and the step-size eigen-ALS make the reference's trajectory branch under
 # such variations (maxcut_10 s14: the reference with Jacobi SVDs and hash seed 4 reproduces the
 # device's assembly-5 departure to 2e-8; s23: with Jacobi SVDs the reference follows the device to
@@ -39,7 +42,7 @@ def is_pathological(r):
 KEYS4 = ("mu", "primal_error", "dual_error", "centrality_error")
 FINAL_KEYS = ("gap", "feas", "dual_feas")
 FACTOR, FLOOR, FINAL_FLOOR, BRANCH = 50.0, 1e-12, 1e-5, 1e-3
-NOISE_TWINS = ("_t8", "_h1", "_h2", "_h3")
+NOISE_TWINS = ("_t8", "_h1", "_h2", "_h3", "_p0", "_p1", "_p2", "_p3")
 ALL_TWINS = NOISE_TWINS + tuple(f"_j{h}" for h in range(8))
 TWIN_SUFFIXES = ALL_TWINS
 

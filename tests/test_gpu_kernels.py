@@ -559,3 +559,77 @@ def test_env_update_mfma_matches_numpy(dev, backward, shapes):
         finally:
             lib.ttk_fused_set_mfma(old)
         assert np.max(np.abs(got - ref)) <= 1e-12 * np.max(np.abs(ref)), mode
+
+
+def _set_csplit(on):
+    import ctypes
+    from ttipm_amd import _lib
+    old = ctypes.c_int(0)
+    assert _lib.lib.ttk_ctx_set_knob(None, _lib.KNOB_MFMA_CSPLIT, int(on), ctypes.byref(old)) == 0
+    return old.value
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("eq", ["lsr,smnS,LSR,rnR->lmL", "lsr,smnS,LSR,lmL->rnR"])
+@pytest.mark.parametrize("shapes", [[(14, 10, 14), (10, 4, 4, 9), (96, 9, 96), (14, 4, 96)],
+                                    [(20, 10, 20), (10, 4, 4, 9), (113, 9, 113), (20, 4, 113)],
+                                    [(44, 10, 44), (10, 4, 4, 10), (44, 10, 44), (44, 4, 44)]])
+def test_mfma_rows_split_over_workgroups_bit_identical(dev, eq, shapes):
+    """MFMA-stage apply rows with their stage-3 output tiles spread over several workgroups per row
+    (TTK_KNOB_MFMA_CSPLIT) give the single-workgroup rows' results bit for bit, as one launch and
+    inside an einsum batch (grouped launch), and agree with NumPy"""
+    from ttipm_amd._lib import lib
+    rng = _rng(31)
+    P, A, Q = (rng.standard_normal(s) for s in shapes[:3])
+    x = rng.standard_normal(shapes[3]) if eq.endswith("->lmL") else \
+        rng.standard_normal((P.shape[0], A.shape[1], Q.shape[0]))
+    ops = [dev.from_numpy(o) for o in (P, A, Q, x)]
+    ref = np.einsum(eq, P, A, Q, x)
+    res = {}
+    old_m = lib.ttk_fused_set_mfma(1)
+    try:
+        for on in (0, 1):
+            old = _set_csplit(on)
+            try:
+                one = dev.read(dev.einsum(eq, *ops, fused=True))
+                outs = [dev.from_numpy(np.ones(ref.shape)) for _ in range(2)]
+                with dev.einsum_batch():
+                    dev.einsum(eq, *ops, out=outs[0], alpha=0.5, beta=2.0, fused=True)
+                    dev.einsum(eq, *ops, out=outs[1], fused=True)
+                res[on] = (one, dev.read(outs[0]), dev.read(outs[1]))
+            finally:
+                _set_csplit(old)
+    finally:
+        lib.ttk_fused_set_mfma(old_m)
+    for a, b in zip(res[0], res[1]):
+        assert np.array_equal(a, b)
+    scale = np.max(np.abs(ref))
+    assert np.max(np.abs(res[1][0] - ref)) <= 1e-13 * scale
+    assert np.max(np.abs(res[1][1] - (0.5 * ref + 2.0))) <= 1e-13 * scale
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ineq", [False, True])
+def test_schur_mfma_rows_split_bit_identical(dev, ineq):
+    """the Schur-reduced operator (two multi-task launches) with wide MFMA rows: split rows (knob on)
+    and single-workgroup rows (knob off) give the same matvec bit for bit"""
+    from ttipm_amd import tt_ipm
+    rng = np.random.default_rng(9)
+    r, R, s, S, n = 14, 96, 10, 9, 4
+    cls = tt_ipm.IneqMatVecWrapper if ineq else tt_ipm.MatVecWrapper
+    L = {k: dev.from_numpy(rng.standard_normal((r, s, r)) * 0.1) for k in cls.keys}
+    Am = {k: dev.from_numpy(rng.standard_normal((s, n, n, S)) * 0.1) for k in cls.keys}
+    Rr = {k: dev.from_numpy(rng.standard_normal((R, S, R)) * 0.1) for k in cls.keys}
+    invI = dev.from_numpy(rng.uniform(0.5, 2.0, (r, n, R)))
+    nb = 3 if ineq else 2
+    v = dev.from_numpy(rng.standard_normal(nb * r * n * R))
+    outs = {}
+    for on in (0, 1):
+        old = _set_csplit(on)
+        try:
+            op = cls(L, Am, Rr, invI, (r, n, R))
+            assert op.h != 0
+            outs[on] = dev.read(op.matvec(v))
+        finally:
+            _set_csplit(old)
+    assert np.array_equal(outs[0], outs[1])
