@@ -63,7 +63,7 @@ void *ttk_ctx_stream(ttk_ctx ctx);
  *   FUSED_MFMA      1: fused applies beyond the VALU kernel's FLOP range run the MFMA stages
  *                      (default from env TTK_FUSED_MFMA, else 1); 0: the pairwise plan
  *   SPLITK          1: deterministic split-K for GEMM steps whose tile grid cannot fill the chip
- *   SPLITK_MINK     K per split (default from env TTK_SPLITK_MINK, else 256)
+ *   SPLITK_MINK     K per split (default from env TTK_SPLITK_MINK, else 128)
  *   LGMRES_MW_MIN   (it+1)*n at or above which the LGMRES Arnoldi / build / augmentation steps
  *                   run as multi-workgroup kernels (default 16384; 0 everywhere, INT_MAX never)
  *   MFMA_CSPLIT     1: wide MFMA-stage apply rows spread their stage-3 output tiles over several
@@ -176,7 +176,7 @@ int ttk_contract_timing(int on);
  * timed launches, summed kernel ms of the timed launches}; synchronises pending events */
 int ttk_contract_stats(double *out, int reset);
 
-/* split-K for GEMM steps whose tile grid cannot fill the chip (< 256 tiles) and K >= 512: the K
+/* split-K for GEMM steps whose tile grid cannot fill the chip (< 256 tiles) and K >= 2 x SPLITK_MINK: the K
  * range is split over workgroups into partial slabs summed in a fixed order by a second kernel.
  * on = 0 disables it for the current context (TTK_KNOB_SPLITK).  Returns the previous setting. */
 int ttk_gemm_set_splitk(int on);
@@ -291,7 +291,12 @@ int ttk_dense_set_block_min(int n);
 int ttk_trsm_lower(void *stream, const double *L, int n, double *B, int nrhs, int ldb, int trans);
 /* LU with partial pivoting in place (getrf) + rcond estimate (gecon, 1-norm, Hager/Higham);
  * `piv` device int[n]; returns TTK_ERR_SINGULAR on an exact zero pivot.  `rcond_out` host.
- * (`scipy.linalg.solve(assume_a='gen')` / `lu_factor`, `src/tt_ipm.py:215,320,323`) */
+ * (`scipy.linalg.solve(assume_a='gen')` / `lu_factor`, `src/tt_ipm.py:215,320,323`)
+ * rcond_out is dgecon's estimate, except when one comparison-matrix sweep already certifies that
+ * estimate to be >= 1e-13 (1 / (||A||_1 max(M(L)^-T M(U)^-T e)) <= dgecon's value): then that
+ * certified lower bound is returned and the estimator is skipped.  The LinAlgWarning test of the
+ * callers (rcond < eps) decides identically either way; the same holds for the rcond of
+ * ttk_dense_schur_solve. */
 int ttk_lu_sync(void *stream, double *A, int n, int *piv, double *work, double *rcond_out);
 /* solve with LU factors, B(n,nrhs) in place (getrs) */
 int ttk_lu_solve(void *stream, const double *LU, int n, const int *piv, double *B, int nrhs, int ldb);

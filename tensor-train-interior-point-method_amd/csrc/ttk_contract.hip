@@ -741,7 +741,8 @@ int ttk_gemm_hist(int on, const char *dump_path) {
   return TTK_OK;
 }
 
-// K per split: splitk_mink() (128 is 15 % faster on graphm_3 but moves maxcut_12 s80 off the reference path)
+// K per split: splitk_mink(), 128 by default (round 3: the graphm_3 split-K shapes 6-16 % faster per call
+// than at 256, and every whole-solve golden key follows a reference run under tests/parity_policy.py)
 static int g_gemm64_min = getenv("TTK_GEMM64_MIN") ? atoi(getenv("TTK_GEMM64_MIN")) : 64;
 static int g_gemm64_ks = getenv("TTK_GEMM64_KS") ? atoi(getenv("TTK_GEMM64_KS")) : 32;
 
@@ -762,7 +763,7 @@ int ttk_gemm_offs(void *stream, const double *A, const double *B, double *C, con
   hipEvent_t e0, e1;
   int rc = contract_events(&e0, &e1);
   if (rc != TTK_OK) return rc;
-  // split-K when the tile grid cannot fill the chip and K is long: each split runs >= 256 of K
+  // split-K when the tile grid cannot fill the chip and K is long: each split runs >= splitk_mink() of K
   const int64_t tiles = (int64_t)grid.x * grid.y * nb;
   int nsplit = 1;
   if (splitk_on() && tiles < 256 && K >= 2 * splitk_mink()) {

@@ -459,11 +459,12 @@ __device__ __forceinline__ double row_dot(const double *__restrict__ a, const do
   return s0 + s1;
 }
 
-// sum_p a[p * lda] x[p] in p order (bs <= TB)
+// sum_p a[p * lda] x[p] in p order (bs <= TB); ABS: sum_p |a[p * lda]| x[p]
+template <bool ABS = false>
 __device__ __forceinline__ double col_dot(const double *__restrict__ a, int lda, const double *x, int bs) {
   double v = 0.0;
 #pragma unroll 8
-  for (int p = 0; p < bs; ++p) v += a[(int64_t)p * lda] * x[p];
+  for (int p = 0; p < bs; ++p) v += (ABS ? fabs(a[(int64_t)p * lda]) : a[(int64_t)p * lda]) * x[p];
   return v;
 }
 
@@ -473,7 +474,10 @@ __device__ __forceinline__ double col_dot(const double *__restrict__ a, int lda,
 // n-double buffer, so the swaps become one parallel gather instead of the serial swap chain
 // (TRANS a template parameter and the body inlined: as a called function with a runtime flag the
 // unrolled blocks of both directions spilled ~600 bytes per lane to scratch)
-template <int TRANS>
+// ABS (TRANS = 1 only): the same sweep on the comparison matrices, x <- M(L)^-T M(U)^-T x with M(T) =
+// |diag T| - |offdiag T| (Higham, Accuracy and Stability, Thm 8.12): for x >= 0 every term is
+// non-negative, and |A^-T| <= P M(L)^-T M(U)^-T entrywise, so max(x) for x = e bounds ||A^-1||_1
+template <int TRANS, bool ABS = false>
 __device__ __forceinline__ void lu_solve_blk(const double *__restrict__ LU, int n, const int *__restrict__ piv,
                                              double *x, const int *perm = nullptr, double *tmp = nullptr) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -536,20 +540,25 @@ __device__ __forceinline__ void lu_solve_blk(const double *__restrict__ LU, int 
       __syncthreads();
     }
   } else {
+    const double sg = ABS ? -1.0 : 1.0;  // M(T) negates the off-diagonal magnitudes
     for (int b0 = 0; b0 < n; b0 += TB) {  // U^T y = b (lower, non-unit)
       const int bs = n - b0 < TB ? n - b0 : TB;
       if (wid == 0) {
         double uc[TB];
 #pragma unroll
-        for (int p = 0; p < TB; ++p) uc[p] = (p < hl && hl < bs) ? LU[(int64_t)(b0 + p) * n + b0 + hl] : 0.0;
-        const double d = hl < bs ? LU[(int64_t)(b0 + hl) * n + b0 + hl] : 1.0;
+        for (int p = 0; p < TB; ++p) {
+          const double u = (p < hl && hl < bs) ? LU[(int64_t)(b0 + p) * n + b0 + hl] : 0.0;
+          uc[p] = ABS ? fabs(u) : u;
+        }
+        const double dd = hl < bs ? LU[(int64_t)(b0 + hl) * n + b0 + hl] : 1.0;
+        const double d = ABS ? fabs(dd) : dd;
         double xq = hl < bs ? x[b0 + hl] : 0.0;
 #pragma unroll
         for (int p = 0; p < TB; ++p) {
           if (p < bs) {
             if (hl == p) xq = xq / d;
             const double xp = __shfl(xq, p, 64);
-            xq -= uc[p] * xp;
+            xq -= sg * uc[p] * xp;
           }
         }
         if (half == 0 && hl < bs) x[b0 + hl] = xq;
@@ -557,7 +566,7 @@ __device__ __forceinline__ void lu_solve_blk(const double *__restrict__ LU, int 
       __syncthreads();
 #pragma unroll 1
       for (int r = b0 + bs + tid; r < n; r += 1024)  // one thread per row, coalesced over r
-        x[r] -= col_dot(LU + (int64_t)b0 * n + r, n, x + b0, bs);
+        x[r] -= sg * col_dot<ABS>(LU + (int64_t)b0 * n + r, n, x + b0, bs);
       __syncthreads();
     }
     for (int bend = n; bend > 0; bend -= TB) {  // L^T z = y (upper, unit)
@@ -565,18 +574,21 @@ __device__ __forceinline__ void lu_solve_blk(const double *__restrict__ LU, int 
       if (wid == 0) {
         double lc[TB];
 #pragma unroll
-        for (int p = 0; p < TB; ++p) lc[p] = (p > hl && p < bs && hl < bs) ? LU[(int64_t)(b0 + p) * n + b0 + hl] : 0.0;
+        for (int p = 0; p < TB; ++p) {
+          const double l = (p > hl && p < bs && hl < bs) ? LU[(int64_t)(b0 + p) * n + b0 + hl] : 0.0;
+          lc[p] = ABS ? fabs(l) : l;
+        }
         double xq = hl < bs ? x[b0 + hl] : 0.0;
 #pragma unroll
         for (int p = TB - 1; p >= 0; --p) {
           const double xp = __shfl(xq, p, 64);
-          xq -= lc[p] * xp;
+          xq -= sg * lc[p] * xp;
         }
         if (half == 0 && hl < bs) x[b0 + hl] = xq;
       }
       __syncthreads();
 #pragma unroll 1
-      for (int r = tid; r < b0; r += 1024) x[r] -= col_dot(LU + (int64_t)b0 * n + r, n, x + b0, bs);
+      for (int r = tid; r < b0; r += 1024) x[r] -= sg * col_dot<ABS>(LU + (int64_t)b0 * n + r, n, x + b0, bs);
       __syncthreads();
     }
     if (perm) {  // the swaps in reverse order = the inverse permutation
@@ -595,6 +607,10 @@ __device__ __forceinline__ void lu_solve_blk(const double *__restrict__ LU, int 
     __syncthreads();
   }
 }
+
+// rcond above which the comparison-matrix bound settles dgecon's LinAlgWarning test (eps = 2.2e-16):
+// a margin of ~450x over eps for the bound's own rounding
+constexpr double RCOND_CERT = 1e-13;
 
 // dgecon (1-norm) from the factors: colsum = column sums of |A| before factorisation
 __global__ __launch_bounds__(1024) void lu_rcond_kernel(const double *__restrict__ LU, int n, const int *gpiv,
@@ -636,6 +652,30 @@ __global__ __launch_bounds__(1024) void lu_rcond_kernel(const double *__restrict
     s_anorm = mx;
     s_est = 0.0;
   }
+  // certified shortcut: bound = max(M(L)^-T M(U)^-T e) >= ||A^-1||_1 (lu_solve_blk ABS), and dlacn2's
+  // estimate never exceeds ||A^-1||_1, so 1 / (anorm * bound) is a lower bound of the rcond that
+  // dgecon returns.  When it already exceeds RCOND_CERT (>> eps) the LinAlgWarning decision
+  // (rcond < eps) is settled and the bound is reported instead of running the estimator.
+  for (int i = tid; i < n; i += nt) x[i] = 1.0;
+  __syncthreads();
+  lu_solve_blk<1, true>(LU, n, piv, x, perm, tmp);
+  double bmax = 0.0;
+  for (int i = tid; i < n; i += nt) bmax = fmax(bmax, x[i]);
+  rv[tid] = bmax;
+  __syncthreads();
+  if (tid == 0) {
+    double mx = 0.0;
+    for (int i = 0; i < nt; ++i) mx = fmax(mx, rv[i]);
+    const double lb = (s_anorm > 0.0 && mx > 0.0 && mx < INFINITY) ? (1.0 / s_anorm) / mx : 0.0;
+    s_est = lb >= RCOND_CERT ? lb : 0.0;
+  }
+  __syncthreads();
+  if (s_est > 0.0) {
+    if (tid == 0) *rcond_out = s_est;
+    return;
+  }
+  __syncthreads();
+  if (tid == 0) s_est = 0.0;
   for (int i = tid; i < n; i += nt) x[i] = 1.0 / n;
   __syncthreads();
   int jlast = -1;

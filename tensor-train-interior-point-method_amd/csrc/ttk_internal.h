@@ -50,7 +50,7 @@ struct Ctx {
   // numerics knobs (ttk_ctx_set_knob; several change summation order, so they are per context:
   // flipping one on a context never changes another context's results).  Defaults from the
   // environment at context creation.
-  int knob[TTK_KNOB_COUNT] = {1, env_int("TTK_FUSED_MFMA", 1) != 0 ? 1 : 0, 1, env_int("TTK_SPLITK_MINK", 256),
+  int knob[TTK_KNOB_COUNT] = {1, env_int("TTK_FUSED_MFMA", 1) != 0 ? 1 : 0, 1, env_int("TTK_SPLITK_MINK", 128),
                               16384, env_int("TTK_MFMA_CSPLIT", 1) != 0 ? 1 : 0};
 };
 Ctx &ctx();

@@ -224,16 +224,19 @@ RUNS = [
     ("maxcut", "maxcut_12", 80, 2, True, 0),
     # the bench's extra maxcut_12 seeds (configs[4] needs 8 distinct seeds for 8 ranks): vetted as
     # non-pathological by these reference runs (src/utils.py:67-84)
-    ("maxcut", "maxcut_12", 0, 2, True, 0),
+    ("maxcut", "maxcut_12", 0, 2, True, 0),  # pathological in the reference (29 iterations, gap 2.1e-2)
     ("maxcut", "maxcut_12", 1, 2, True, 0),
     ("maxcut", "maxcut_12", 2, 2, True, 0),  # pathological in the reference (29 iterations, gap 4.3e-2)
     ("maxcut", "maxcut_12", 3, 2, True, 0),  # pathological in the reference (14 iterations, gap 1.3e-2)
     ("maxcut", "maxcut_12", 4, 2, True, 0),  # pathological in the reference (13 iterations, gap 0.38)
     ("maxcut", "maxcut_12", 5, 2, True, 0),  # pathological in the reference (10 iterations, gap 4.7)
-    ("maxcut", "maxcut_12", 6, 2, True, 0),
+    ("maxcut", "maxcut_12", 6, 2, True, 0),  # pathological in the reference (29 iterations, gap 2.1e-2)
     ("maxcut", "maxcut_12", 7, 2, True, 0),
     ("maxcut", "maxcut_12", 8, 2, True, 0),
     ("maxcut", "maxcut_12", 9, 2, True, 0),
+    ("maxcut", "maxcut_12", 10, 2, True, 0),
+    ("maxcut", "maxcut_12", 11, 2, True, 0),
+    ("maxcut", "maxcut_12", 13, 2, True, 0),
     # the rest of configs/maxcut_12.yaml's seeds: bounded traces (3 Newton systems each, every AMEn
     # solve and step pair before them) -- a full 1-thread reference run is ~35 min per seed
     ("maxcut", "maxcut_12", 45, 2, True, 3),

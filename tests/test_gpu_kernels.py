@@ -322,11 +322,38 @@ def test_lu_matches_lapack(dev, n):
     assert np.abs(dev.read(LU) - lu_ref).max() <= 1e-10 * np.abs(lu_ref).max()
     anorm = np.abs(A).sum(axis=0).max()
     rcond_ref, info = sla.lapack.dgecon(lu_ref, anorm, norm="1")
-    assert 0.3 * rcond_ref <= rc.value <= 3.0 * rcond_ref, (rc.value, rcond_ref)
+    # dgecon's estimate, or -- when the comparison-matrix bound already settles the LinAlgWarning test
+    # -- a certified lower bound of it that is >= 1e-13 (include/ttk.h ttk_lu_sync)
+    assert 0.3 * rcond_ref <= rc.value <= 3.0 * rcond_ref or 1e-13 <= rc.value <= rcond_ref * (1 + 1e-8), \
+        (rc.value, rcond_ref)
     B = rng.standard_normal((n, 2))
     X = dev.from_numpy(B)
     dev.lu_solve_(LU, piv, X)
     assert np.allclose(dev.read(X), sla.lu_solve((lu_ref, piv_ref), B), rtol=1e-8, atol=1e-10)
+
+
+@pytest.mark.parametrize("n,scale", [(64, 1e-3), (300, 1e-9), (700, 1e-14), (1200, 1.0)])
+def test_lu_rcond_warning_decision_matches_lapack(dev, n, scale):
+    """the LinAlgWarning decision (rcond < eps) from ttk_lu_sync equals LAPACK dgecon's on matrices
+    from well- to ill-conditioned (a rank-deficient part scaled by `scale`), certified bound or not"""
+    import ctypes
+    import scipy.linalg as sla
+    from ttipm_amd._lib import lib
+    rng = _rng(n)
+    U, _ = np.linalg.qr(rng.standard_normal((n, n)))
+    V, _ = np.linalg.qr(rng.standard_normal((n, n)))
+    sv = np.ones(n)
+    sv[n // 2:] = scale
+    A = (U * sv) @ V.T
+    lu_ref, _ = sla.lu_factor(A)
+    rcond_ref, _ = sla.lapack.dgecon(lu_ref, np.abs(A).sum(axis=0).max(), norm="1")
+    LU = dev.from_numpy(A)
+    piv = dev.torch.empty(n, dtype=dev.torch.int32, device=dev.DEV)
+    work = dev.empty(2 * n + 16)
+    rc = ctypes.c_double(0.0)
+    assert lib.ttk_lu_sync(dev._stream(), LU.data_ptr(), n, piv.data_ptr(), work.data_ptr(), ctypes.byref(rc)) == 0
+    eps = np.finfo(float).eps
+    assert (rc.value < eps) == (rcond_ref < eps), (rc.value, rcond_ref)
 
 
 def test_lu_ill_conditioned_raises_warning(dev):
