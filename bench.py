@@ -236,7 +236,7 @@ def _pmc_traffic():
     """HBM bytes per contraction launch (FETCH_SIZE + WRITE_SIZE, rocprofv3 KB x 1024) from the
     committed PMC passes over the same workload (counters need their own rocprofv3 runs, so they
     cannot be read live here); the newest round's file wins."""
-    for name in ("r02_pmc_maxcut10.json", "r01_pmc_maxcut10.json"):
+    for name in ("r03_pmc_maxcut10.json", "r02_pmc_maxcut10.json", "r01_pmc_maxcut10.json"):
         try:
             ks = json.load(open(os.path.join(HERE, "profiles", name)))["kernels"]
         except (OSError, KeyError, ValueError):

@@ -65,7 +65,8 @@ void *ttk_ctx_stream(ttk_ctx ctx);
  *   SPLITK          1: deterministic split-K for GEMM steps whose tile grid cannot fill the chip
  *   SPLITK_MINK     K per split (default from env TTK_SPLITK_MINK, else 128)
  *   LGMRES_MW_MIN   (it+1)*n at or above which the LGMRES Arnoldi / build / augmentation steps
- *                   run as multi-workgroup kernels (default 16384; 0 everywhere, INT_MAX never)
+ *                   run as multi-workgroup kernels (default from env TTK_LGMRES_MW_MIN, else
+ *                   16384; 0 everywhere, INT_MAX never)
  *   MFMA_CSPLIT     1: wide MFMA-stage apply rows spread their stage-3 output tiles over several
  *                   workgroups per row (bit-identical; default from env TTK_MFMA_CSPLIT, else 1)
  * ttk_ctx_set_knob stores value and returns the previous one in *old (may be NULL). */

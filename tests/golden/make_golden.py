@@ -237,6 +237,9 @@ RUNS = [
     ("maxcut", "maxcut_12", 10, 2, True, 0),
     ("maxcut", "maxcut_12", 11, 2, True, 0),
     ("maxcut", "maxcut_12", 13, 2, True, 0),
+    ("maxcut", "maxcut_12", 18, 2, True, 0),
+    ("maxcut", "maxcut_12", 19, 2, True, 0),
+    ("maxcut", "maxcut_12", 20, 2, True, 0),
     # the rest of configs/maxcut_12.yaml's seeds: bounded traces (3 Newton systems each, every AMEn
     # solve and step pair before them) -- a full 1-thread reference run is ~35 min per seed
     ("maxcut", "maxcut_12", 45, 2, True, 3),
