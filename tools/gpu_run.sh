@@ -15,7 +15,9 @@ cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
 tag=$1; shift
 mkdir -p gpurun_out
+idx=0
 for step in "$@"; do
+  idx=$((idx+1))
   kind=${step%%:*}; rest=${step#*:}; [ "$rest" = "$step" ] && rest=""
   echo "== $tag $step $(date +%T)"
   case $kind in
@@ -33,10 +35,11 @@ for step in "$@"; do
              || { tail -20 gpurun_out/${tag}_bench.err; exit 1; }
            cut -c1-600 gpurun_out/${tag}_bench.json ;;
     stats) args=${rest:-"--steps 5 --warmup 1 --no-cpu-baseline --inflight 1"}
-           timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/${tag}_stats -o run -- \
-             python3 bench.py $args > gpurun_out/${tag}_stats.log 2>&1 || { tail -20 gpurun_out/${tag}_stats.log; exit 1; }
+           st=${tag}_s${idx}
+           timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/${st}_stats -o run -- \
+             python3 bench.py $args > gpurun_out/${st}_stats.log 2>&1 || { tail -20 gpurun_out/${st}_stats.log; exit 1; }
            # keep the summaries only (the full kernel trace exceeds what gpurun copies back)
-           for f in $(find /tmp/${tag}_stats -name "*stats.csv"); do cp $f gpurun_out/${tag}_$(basename $f); done
+           for f in $(find /tmp/${st}_stats -name "*stats.csv"); do cp $f gpurun_out/${st}_$(basename $f); done
            ls gpurun_out/ | grep "^${tag}_" ;;
     pmc)   cn=${rest%%:*}; args=${rest#*:}; [ "$args" = "$rest" ] && args="--steps 1 --warmup 0 --no-cpu-baseline --no-roofline --inflight 1"
            timeout -s KILL 300 rocprofv3 --pmc ${cn//,/ } --kernel-trace --output-format csv -d /tmp/${tag}_pmc_${cn%%,*} -o run -- \
