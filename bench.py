@@ -13,12 +13,17 @@
   and at N=1 the steps cycle through the config's seeds.  `replica`: every rank solves step i's
   N=1 seed.  Problems are created once per distinct seed on rank 0 and delivered by ONE broadcast
   (RCCL over xGMI with the nccl backend) before the timed region; no collective inside the IPM loop.
-* Solves in flight per GPU (`--inflight P`, default 2 at every N, so the 1/2/4/8-GPU series is
-  like-for-like and a node runs at most 16 solve processes): a solve is a chain of small dependent
-  launches that leaves most of the chip idle, so each GPU runs P seeds at once -- this process plus
-  P-1 worker processes on the same device (each its own HIP stream and library context), spawned
-  before the GPU is touched and released together at the start of the timed region.  A step is then
-  P solves per GPU: step i, rank p, slot j solves seeds[(i*N*P + p*P + j) mod S].
+* Solves in flight per GPU (`--inflight P`, default 4 at every N, so the 1/2/4/8-GPU series is
+  like-for-like): a solve is a chain of small dependent launches that leaves most of the chip idle,
+  so each GPU runs P seeds at once.  They run as slot threads (`--threads T`, default 2 per process:
+  each thread its own HIP stream, libttk context and NumPy random stream; the launches release the
+  GIL) in P/T processes per GPU -- this process plus P/T-1 workers spawned before the GPU is touched
+  -- so a node runs at most 16 solve processes (8 GPUs x 2).  All slots warm up, then are released
+  together at the start of the timed region.  A step is P solves per GPU: step i, rank p, slot j
+  solves seeds[(i*N*P + p*P + j) mod S].
+* `solo_median_seed_s_per_iter`: after the timed region (rank 0, N=1) every distinct timed seed is
+  solved once more ALONE on the GPU -- SURVEY.md §8(d)'s per-seed latency as the reference runner
+  measures it (one solve at a time, `src/utils.py:300-302`); the CPU per-seed comparison uses it.
 * Timed region: barrier + device sync on both sides of the K steps, max over ranks.
   `value` = (max-over-ranks wall) / (IPM iterations of all ranks): whole-job s per IPM-iteration.
   `median_seed_s_per_iter` is SURVEY.md §8(d)'s statistic: the median over the distinct seeds of
@@ -61,7 +66,7 @@ HOST_SHARE = 16  # CPU share of one GPU on the box (nproc shows the whole machin
 
 # Seeds beyond a config's own list, vetted non-pathological with the oracle in the build container
 # (maxcut_12 r=2 lists 5 seeds, the 8-GPU run needs 8).  See DESIGN.md §5.
-EXTRA_SEEDS = {"maxcut_12.yaml": [20, 18, 19]}
+EXTRA_SEEDS = {"maxcut_12.yaml": [20, 19, 9]}
 
 
 class _Stop(Exception):
@@ -142,47 +147,113 @@ def _cpu_worker(problem, cfg_path, seed, rank_tt, cap):
     print(json.dumps(out), flush=True)
 
 
-def _gpu_worker(args, seeds):
-    """Child process (one more solve in flight on this rank's GPU): create its seeds' problems,
-    warm up, print 'ready', wait for 'go' on stdin, run the solves back to back, print one JSON
-    line with the elapsed wall time (device-synchronised) and the per-seed results."""
+class _Slots:
+    """The solves in flight of one process: one host thread per slot, each with its own HIP stream,
+    libttk context (`dev`'s per-thread state) and NumPy random stream (`ttipm_amd.rng`).  Every slot
+    thread warms up on its first seed, uploads its problems, then waits for `start()`, solves its
+    seeds back to back and records its wall time (its own stream synchronised).  The launches
+    themselves release the GIL, so the slots' host work overlaps while their kernels run."""
+
+    def __init__(self, slot_seeds, packed, solve, warmup, device):
+        import threading
+        self.n = len(slot_seeds)
+        self.ready = threading.Barrier(self.n + 1)
+        self.go = threading.Event()
+        self.out = [None] * self.n
+        self.err = []
+        self.threads = [threading.Thread(target=self._run, args=(j, sl, packed, solve, warmup, device), daemon=True)
+                        for j, sl in enumerate(slot_seeds)]
+        for t in self.threads:
+            t.start()
+
+    def _run(self, j, seeds, packed, solve, warmup, device):
+        import torch
+        from ttipm_amd import rng, shard
+        preps = None
+        try:
+            if device is not None:
+                torch.cuda.set_device(device)
+                if self.n > 1 or os.environ.get("TTIPM_SLOT_STREAM", "new") != "default":
+                    torch.cuda.set_stream(torch.cuda.Stream())
+            rng.private()
+            for _ in range(warmup):  # untimed: plans, this context's scratch, allocator, code pages
+                solve(shard.unpack(*packed[seeds[0]]))
+            preps = [shard.unpack(*packed[sd]) for sd in seeds]
+            if device is not None:
+                torch.cuda.current_stream().synchronize()
+        except BaseException as e:  # noqa: BLE001 - re-raised by join()
+            self.err.append(e)
+        self.ready.wait()
+        self.go.wait()
+        if preps is None:
+            return
+        try:
+            traces = [[] for _ in seeds]
+            t0 = time.perf_counter()
+            res = [solve(pr, trace=tr) for pr, tr in zip(preps, traces)]
+            if device is not None:
+                torch.cuda.current_stream().synchronize()
+            elapsed = time.perf_counter() - t0
+            for r, tr in zip(res, traces):  # per-iteration stamps (Newton-system assemblies)
+                r["assembly_t"] = [e["t"] - tr[0]["t"] for e in tr] if tr else []
+            self.out[j] = (elapsed, res)
+        except BaseException as e:  # noqa: BLE001
+            self.err.append(e)
+
+    def wait_ready(self):
+        self.ready.wait()
+        if self.err:
+            raise RuntimeError(f"bench: a solve slot failed before the timed region: {self.err[0]!r}")
+
+    def start(self):
+        self.go.set()
+
+    def join(self):
+        for t in self.threads:
+            t.join()
+        if self.err:
+            raise RuntimeError(f"bench: a solve slot failed in the timed region: {self.err[0]!r}")
+        return [o[0] for o in self.out], [r for o in self.out for r in o[1]]
+
+
+def _gpu_worker(args, slot_seeds):
+    """Child process (more solves in flight on this rank's GPU): create its seeds' problems, start
+    one slot thread per seed list (`_Slots`), print 'ready' once all have warmed up, wait for 'go'
+    on stdin, run the solves, print one JSON line with the slots' elapsed wall times and the
+    per-seed results."""
     import torch
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local % torch.cuda.device_count())
+    dev = local % torch.cuda.device_count()
+    torch.cuda.set_device(dev)
     from ttipm_amd import shard
     from ttipm_amd.utils import create
     from ttipm_amd.utils import solve as _solve
     config = yaml.safe_load(open(args.config))
-    with contextlib.redirect_stdout(sys.stderr):
-        packed = {s: shard.pack(create(args.problem, config, s, args.rank, verbose=False))
-                  for s in dict.fromkeys(seeds)}
-
-        def solve(seed, trace=None):
-            return _solve(shard.unpack(*packed[seed]), config, quiet=True, verbose=False, trace=trace)
-
-        for _ in range(args.warmup):
-            solve(seeds[0])
-        torch.cuda.synchronize()
-    print("ready", flush=True)
-    if sys.stdin.readline().strip() != "go":  # EOF: the parent is gone -- do not run as an orphan
-        sys.exit(3)
-    traces = [[] for _ in seeds]
-    t0 = time.perf_counter()
-    with contextlib.redirect_stdout(sys.stderr):
-        results = [solve(sd, trace=tr) for sd, tr in zip(seeds, traces)]
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    for r, tr in zip(results, traces):
-        r["assembly_t"] = [e["t"] - tr[0]["t"] for e in tr] if tr else []
     keep = ("seed", "num_iters", "runtime", "sec_per_iter", "gap", "feas", "dual_feas", "assembly_t")
+    with contextlib.redirect_stdout(sys.stderr):  # once, around all slot threads (not thread-safe)
+        packed = {s: shard.pack(create(args.problem, config, s, args.rank, verbose=False))
+                  for sl in slot_seeds for s in sl}
+
+        def solve(prep, trace=None):
+            return _solve(prep, config, quiet=True, verbose=False, trace=trace)
+
+        slots = _Slots(slot_seeds, packed, solve, args.warmup, dev)
+        slots.wait_ready()
+        print("ready", file=sys.__stdout__, flush=True)
+        if sys.stdin.readline().strip() != "go":  # EOF: the parent is gone -- do not run as an orphan
+            os._exit(3)
+        slots.start()
+        elapsed, results = slots.join()
     print(json.dumps({"elapsed": elapsed, "results": [{k: r.get(k) for k in keep} for r in results]}), flush=True)
 
 
-def _spawn_gpu_workers(args, slot_seeds):
-    """Started BEFORE this process initialises the GPU; each prints 'ready' once warmed up."""
+def _spawn_gpu_workers(args, proc_slots):
+    """Started BEFORE this process initialises the GPU; each prints 'ready' once warmed up.
+    proc_slots: per worker process, its slots' seed lists."""
     procs = []
-    for seeds in slot_seeds:
-        cmd = [sys.executable, os.path.abspath(__file__), "--gpu-worker", ",".join(map(str, seeds)),
+    for slots in proc_slots:
+        cmd = [sys.executable, os.path.abspath(__file__), "--gpu-worker",
+               ";".join(",".join(map(str, sl)) for sl in slots),
                "--problem", args.problem, "--config", args.config, "--rank", str(args.rank),
                "--warmup", str(args.warmup)]
         procs.append(subprocess.Popen(cmd, stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=sys.stderr,
@@ -253,12 +324,15 @@ def _pmc_traffic():
     return None
 
 
+DEFAULT_THREADS = 2  # solves in flight per process (host threads, one HIP stream + libttk context each)
+
+
 def default_inflight(world):
-    """Solves in flight per GPU: 2 at every N of the 1/2/4/8-GPU series, so that the series is
-    like-for-like (a node runs at most 16 solve processes: 8 GPUs x 2).  One MI355X is not saturated
-    by 2 (maxcut_10 whole job, round-2 sweep: 1 -> 0.39, 2 -> 0.20, 4 -> 0.106, 6 -> 0.112 s/IPM-iter;
-    `--inflight 4` measures the single-GPU optimum)."""
-    return max(1, min(2, 16 // world))
+    """Solves in flight per GPU: 4 at every N of the 1/2/4/8-GPU series, so that the series is
+    like-for-like -- 2 processes per GPU x DEFAULT_THREADS slot threads each, so a node runs at most
+    16 solve processes (8 GPUs x 2).  Round-2 process sweep on one MI355X (maxcut_10 whole job):
+    1 -> 0.39, 2 -> 0.20, 4 -> 0.106, 6 -> 0.112 s/IPM-iter: 4 in flight is the knee."""
+    return max(1, min(4, DEFAULT_THREADS * (16 // world)))
 
 
 def make_schedule(config, cfg_name, seeds_arg, steps, world, rank, P, mode):
@@ -293,7 +367,10 @@ def main():
     ap.add_argument("--cpu-cap", type=float, default=20.0, help="seconds of oracle work per seed (0: full solves)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--no-solo", action="store_true", help="skip the one-solve-at-a-time latency pass")
     ap.add_argument("--schedule", choices=("shard", "replica"), default="shard")
+    ap.add_argument("--threads", type=int, default=None,
+                    help=f"solves in flight per process (host threads; default {DEFAULT_THREADS})")
     ap.add_argument("--inflight", type=int, default=None,
                     help="solves in flight per GPU (default: default_inflight())")
     ap.add_argument("--cpu-worker", type=int, default=None, help=argparse.SUPPRESS)
@@ -305,7 +382,7 @@ def main():
     if args.cpu_worker is not None:
         return _cpu_worker(args.problem, args.config, args.cpu_worker, args.rank, args.cpu_cap)
     if args.gpu_worker is not None:
-        return _gpu_worker(args, [int(x) for x in args.gpu_worker.split(",")])
+        return _gpu_worker(args, [[int(x) for x in sl.split(",")] for sl in args.gpu_worker.split(";")])
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -321,8 +398,12 @@ def main():
                                              rank, P, args.schedule)
     step_seeds = [s for st in sched for s in st]
     per_step = world * P
+    T = max(1, min(args.threads or DEFAULT_THREADS, P))
+    if _profiled():
+        T = 1
+    proc_slots = [slot_seeds[i:i + T] for i in range(0, P, T)]  # this process: proc_slots[0]
     mine_seeds = slot_seeds[0]
-    gpu_procs = _spawn_gpu_workers(args, slot_seeds[1:])  # before any GPU call
+    gpu_procs = _spawn_gpu_workers(args, proc_slots[1:])  # before any GPU call
 
     cpu_seeds = list(dict.fromkeys(s for sl in slot_seeds for s in sl))  # the distinct seeds this (only) rank times
     cpu_procs, allcore_proc = [], []
@@ -365,10 +446,15 @@ def main():
         if world > 1:
             dist.barrier()
 
-    for _ in range(args.warmup):  # untimed: step 0's problem (plans, allocator, code pages)
-        solve(shard.unpack(*packed[mine_seeds[0]]))
-    preps = [shard.unpack(*packed[s]) for s in mine_seeds]
-    traces = [[] for _ in mine_seeds]
+    dev_idx = torch.cuda.current_device() if torch.cuda.is_available() else None
+
+    def solve_quiet(prep, trace=None):  # slot threads: stdout is redirected once around them all
+        return _solve(prep, config, quiet=True, verbose=False, trace=trace)
+
+    with contextlib.redirect_stdout(sys.stderr):
+        sync()
+        slots = _Slots(proc_slots[0], packed, solve_quiet, args.warmup, dev_idx)
+        slots.wait_ready()
     for p in gpu_procs:  # every worker warmed up and waiting
         line = p.stdout.readline()
         while line and line.strip() != "ready":
@@ -381,9 +467,9 @@ def main():
     for p in gpu_procs:
         p.stdin.write("go\n")
         p.stdin.flush()
-    results = [solve(p, trace=tr) for p, tr in zip(preps, traces)]
-    for r, tr in zip(results, traces):  # per-iteration stamps (Newton-system assemblies)
-        r["assembly_t"] = [e["t"] - tr[0]["t"] for e in tr] if tr else []
+    with contextlib.redirect_stdout(sys.stderr):
+        slots.start()
+        slot_elapsed, results = slots.join()
     worker_out = []
     for p in gpu_procs:
         line = p.stdout.readline()
@@ -395,7 +481,7 @@ def main():
     sync()
     barrier()
     elapsed = time.perf_counter() - t0
-    slot_elapsed = [elapsed] + [w["elapsed"] for w in worker_out]
+    slot_elapsed = slot_elapsed + [e for w in worker_out for e in w["elapsed"]]
     results = results + [r for w in worker_out for r in w["results"]]
     iters = sum(r["num_iters"] for r in results)
     if world > 1:
@@ -437,13 +523,26 @@ def main():
                         "algorithmic_flops_per_launch": algo["flops"] / max(tl, 1),
                         "algorithmic_by_op": dict(sorted(algo["by"].items(), key=lambda kv: -kv[1][1])[:10])}
 
+    # SURVEY.md §8(d)'s per-seed statistic as the reference runner measures it (src/utils.py:300-302:
+    # one solve at a time): every distinct timed seed solved once more, alone on the GPU (untimed
+    # for `value`; rank 0 at N=1)
+    solo = None
+    if rank == 0 and world == 1 and not args.no_solo:
+        solo = []
+        for sd in dict.fromkeys(step_seeds):
+            tr = []
+            r = solve(shard.unpack(*packed[sd]), trace=tr)
+            r["assembly_t"] = [e["t"] - tr[0]["t"] for e in tr] if tr else []
+            solo.append(r)
+        sync()
+
     cpu = None
     if do_cpu:
         with contextlib.redirect_stdout(sys.stderr):
             per = _release(cpu_procs)
             allc = _release(allcore_proc)[0]
         gpu_runs, cpu_runs = {}, {}
-        for r in results:
+        for r in (solo or results):  # the GPU's one-at-a-time latency when measured
             gpu_runs.setdefault(r["seed"], []).append(r["assembly_t"])
         for c in per:
             if c is not None and c["iters"] > 0:
@@ -470,7 +569,9 @@ def main():
                          f"the timed seeds {sorted(cpu_runs)} cycled over them; each process runs its seed's first "
                          f"IPM iterations up to {args.cpu_cap:g} s of work; value = median over seeds of each "
                          f"seed's s/IPM-iter (median over its processes), over the iterations the CPU and GPU "
-                         f"runs of that seed have in common",
+                         f"runs of that seed have in common; the GPU side is "
+                         + ("the one-solve-at-a-time pass (each seed alone on the GPU)" if solo else
+                            "the timed in-flight solves"),
                "per_seed": rows,
                "gpu_same_sample_median": gmed,
                "gpu_over_cpu": (gmed / med) if med and gmed else None,
@@ -501,12 +602,17 @@ def main():
                        "from rank 0",
                "config": {"workload": f"{args.problem} dim={config['dim']} rank={args.rank} "
                                       f"({os.path.basename(args.config)}), {P} concurrent tt_ipm solves per GPU "
-                                      f"per step",
+                                      f"per step ({len(proc_slots)} processes x {T} slot threads)",
                           "inflight_per_gpu": P,
                           "seeds": seeds, "seeds_per_step": sched,
                           "parallelism": f"seed-parallel x{world} GPUs x{P} in flight ({args.schedule})",
                           "total_ipm_iters": iters},
                "median_seed_s_per_iter": med,
+               "solo_median_seed_s_per_iter": None if not solo else
+               float(np.median([r["runtime"] / max(r["num_iters"], 1) for r in solo])),
+               "solo_per_seed": None if not solo else
+               [{k: r[k] for k in ("seed", "num_iters", "runtime", "sec_per_iter", "gap")} for r in solo],
+               "threads_per_process": T,
                "pathological_seeds": sorted({p["seed"] for p in per_seed if p["pathological"]}),
                # library / path knobs set for this run (several change summation order, hence results at
                # rounding level)

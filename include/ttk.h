@@ -69,6 +69,9 @@ void *ttk_ctx_stream(ttk_ctx ctx);
  *                   16384; 0 everywhere, INT_MAX never)
  *   MFMA_CSPLIT     1: wide MFMA-stage apply rows spread their stage-3 output tiles over several
  *                   workgroups per row (bit-identical; default from env TTK_MFMA_CSPLIT, else 1)
+ *   APPLY_DUAL      1: a Schur-handle task's two VALU terms run side by side, one half of a
+ *                   512-thread workgroup each (bit-identical; read at ttk_schur_build; default from
+ *                   env TTK_APPLY_DUAL, else 1)
  * ttk_ctx_set_knob stores value and returns the previous one in *old (may be NULL). */
 enum ttk_knob {
   TTK_KNOB_FUSED_APPLY = 0,
@@ -77,7 +80,8 @@ enum ttk_knob {
   TTK_KNOB_SPLITK_MINK = 3,
   TTK_KNOB_LGMRES_MW_MIN = 4,
   TTK_KNOB_MFMA_CSPLIT = 5,
-  TTK_KNOB_COUNT = 6
+  TTK_KNOB_APPLY_DUAL = 6,
+  TTK_KNOB_COUNT = 7
 };
 int ttk_ctx_set_knob(ttk_ctx ctx, int knob, int value, int *old);
 int ttk_ctx_get_knob(ttk_ctx ctx, int knob, int *value);

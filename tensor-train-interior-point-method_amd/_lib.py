@@ -117,7 +117,7 @@ EXPORTED = tuple(_SIGS)
 
 TTK_OK, TTK_ERR_ARG, TTK_ERR_HIP, TTK_ERR_NOT_PD, TTK_ERR_SINGULAR, TTK_ERR_NOT_CONVERGED = range(6)
 # per-context numerics knobs (include/ttk.h enum ttk_knob)
-KNOB_FUSED_APPLY, KNOB_FUSED_MFMA, KNOB_SPLITK, KNOB_SPLITK_MINK, KNOB_LGMRES_MW_MIN, KNOB_MFMA_CSPLIT = range(6)
+KNOB_FUSED_APPLY, KNOB_FUSED_MFMA, KNOB_SPLITK, KNOB_SPLITK_MINK, KNOB_LGMRES_MW_MIN, KNOB_MFMA_CSPLIT, KNOB_APPLY_DUAL = range(7)
 
 
 class TTKError(RuntimeError):

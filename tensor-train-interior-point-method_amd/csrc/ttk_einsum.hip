@@ -553,9 +553,11 @@ struct MixedIdx {
   }
 };
 
+// tid / nt: this row's threads (the whole block, or one half of it when a task's two terms run side
+// by side, see fused_apply_multi_kernel); every output element is still one thread's sequential chain,
+// so the thread count never changes a result.  Three block barriers, unconditional.
 template <bool DIRECT>
-__device__ void apply_row(const ApplyArgs &g, int a, double *sm, double *orow) {
-  const int tid = threadIdx.x, nt = blockDim.x;
+__device__ void apply_row(const ApplyArgs &g, int a, double *sm, double *orow, int tid, int nt) {
   const int nb = g.nb, nj = g.nj, nd = g.nd, nS = g.nS, ns = g.ns, ni = g.ni, nc = g.nc;
   double *X = sm;                       // nb*nj*nd     [b][j][d]
   double *Pa = X + nb * nj * nd;        // ns*nb        [s][b]   (P[a, s, b])
@@ -863,7 +865,7 @@ __global__ __launch_bounds__(1024) void fused_apply_mfma_kernel(ApplyArgs g) {
 
 __global__ __launch_bounds__(1024) void fused_apply_kernel(ApplyArgs g) {
   extern __shared__ double sm[];
-  apply_row<true>(g, blockIdx.x, sm, nullptr);
+  apply_row<true>(g, blockIdx.x, sm, nullptr, threadIdx.x, blockDim.x);
 }
 
 // Several local applies in ONE launch (the Schur-reduced KKT matvec of LGMRES): task t owns
@@ -874,11 +876,13 @@ struct ApplyTask {
   ApplyArgs t[2];
   int nterms;
   const double *oscale, *addv;  // same layout as the output, or null
+  int64_t work1;  // side-by-side terms: LDS offset (doubles, after the two rows) of term 1's stages
 };
 struct ApplyLaunch {
   ApplyTask task[3];
   int ntask;
   int off[4];
+  int dual;  // two-term VALU tasks run their terms side by side, one half of the block each
 };
 
 __global__ __launch_bounds__(1024) void fused_apply_multi_kernel(ApplyLaunch L) {
@@ -890,9 +894,28 @@ __global__ __launch_bounds__(1024) void fused_apply_multi_kernel(ApplyLaunch L) 
   const int cs = g0.csplit, a = ((int)blockIdx.x - L.off[t]) / cs, h = ((int)blockIdx.x - L.off[t]) % cs;
   const int ni = g0.ni, nc = g0.nc, tid = threadIdx.x, nt = blockDim.x;
   double *orow = sm, *acc = sm + ni * nc, *work = acc + ni * nc;
+  if (L.dual && T.nterms == 2) {
+    // the two terms side by side (independent until they are summed): half the block each, own LDS
+    // stages; then the same two output updates as the sequential loop below, in the same order
+    const int half = nt >> 1, k = tid >= half ? 1 : 0;
+    apply_row<false>(T.t[k], a, k ? work + T.work1 : work, k ? acc : orow, tid - k * half, half);
+    __syncthreads();
+    {
+      const double al = g0.alpha;
+      for (int e = tid; e < ni * nc; e += nt)
+        if (mine(e % nc, h, cs)) orow[e] = al * orow[e];
+    }
+    __syncthreads();
+    {
+      const double al = T.t[1].alpha;
+      for (int e = tid; e < ni * nc; e += nt)
+        if (mine(e % nc, h, cs)) orow[e] = al * acc[e] + 1.0 * orow[e];
+    }
+    __syncthreads();
+  } else
   for (int k = 0; k < T.nterms; ++k) {
     if (T.t[k].mfma) apply_row_mfma<false>(T.t[k], a, work, k == 0 ? orow : acc, h);
-    else apply_row<false>(T.t[k], a, work, k == 0 ? orow : acc);
+    else apply_row<false>(T.t[k], a, work, k == 0 ? orow : acc, tid, nt);
     __syncthreads();
     if (k > 0) {
       const double al = T.t[k].alpha;
@@ -1329,6 +1352,32 @@ int ttk_schur_build(ttk_ctx ctx, int ineq, int64_t m, const int64_t *descs, cons
         for (int k = 0; k < L.task[t].nterms; ++k) L.task[t].t[k].qlds = L.task[t].t[k].mfma ? 0 : 1;
       op.shm[s] = (size_t)mq * sizeof(double);
     }
+    // side-by-side terms (context knob TTK_KNOB_APPLY_DUAL, on by default): every task VALU and the
+    // two terms' stages fit LDS together; the block doubles (512 threads), the results are unchanged
+    L.dual = 0;
+    if (ttk::ctx().knob[TTK_KNOB_APPLY_DUAL] != 0) {
+      bool ok = true;
+      int64_t md = 0;
+      for (int t = 0; t < L.ntask && ok; ++t) {
+        ApplyTask &T = L.task[t];
+        int64_t wk[2] = {0, 0};
+        for (int k = 0; k < T.nterms; ++k) {
+          const ApplyArgs &q = T.t[k];
+          ok = ok && !q.mfma;
+          wk[k] = apply_lds(q.nb, q.nj, q.nd, q.nS, q.ns, q.ni) + (q.qlds ? (int64_t)q.nc * q.nS * q.nd : 0);
+        }
+        T.work1 = wk[0];
+        const int64_t need = 2 * (int64_t)T.t[0].ni * T.t[0].nc + wk[0] + wk[1];
+        const int64_t single = 2 * (int64_t)T.t[0].ni * T.t[0].nc + (wk[0] > wk[1] ? wk[0] : wk[1]);
+        const int64_t n = T.nterms == 2 ? need : single;
+        md = n > md ? n : md;
+      }
+      if (ok && md <= APPLY_LDS_DOUBLES) {
+        L.dual = 1;
+        const size_t b = (size_t)md * sizeof(double);
+        op.shm[s] = b > op.shm[s] ? b : op.shm[s];
+      }
+    }
   }
   return schur_store(op, m, handle);
 }
@@ -1364,7 +1413,8 @@ int ttk::schur_apply(void *stream, int64_t handle, const double *v, double *out)
     bool mf = false;
     for (int t = 0; t < L.ntask; ++t)
       for (int k = 0; k < L.task[t].nterms; ++k) mf = mf || L.task[t].t[k].mfma;
-    hipExtLaunchKernelGGL(fused_apply_multi_kernel, dim3(L.off[L.ntask]), dim3(mf ? g_mfma_threads : 256), op.shm[s],
+    hipExtLaunchKernelGGL(fused_apply_multi_kernel, dim3(L.off[L.ntask]), dim3(mf ? g_mfma_threads : (L.dual ? 512 : 256)),
+                          op.shm[s],
                           TTK_STREAM(stream), e0, e1, 0, L);
     TTK_LAUNCH_CHECK();
   }
@@ -1442,7 +1492,7 @@ __global__ __launch_bounds__(1024) void fused_apply_group_kernel(FusedGroup G) {
   while (t + 1 < G.n && (int)blockIdx.x >= G.off[t + 1]) ++t;
   const int local = (int)blockIdx.x - G.off[t];
   if (G.t[t].mfma) apply_row_mfma<true>(G.t[t], local / G.t[t].csplit, sm, nullptr, local % G.t[t].csplit);
-  else apply_row<true>(G.t[t], local, sm, nullptr);
+  else apply_row<true>(G.t[t], local, sm, nullptr, threadIdx.x, blockDim.x);
 }
 
 inline bool overlap(const Span &a, const Span &b) { return a.lo < b.hi && b.lo < a.hi; }

@@ -24,7 +24,9 @@ using mul_fn = int (*)(void *, const double *, const double *, double *, int, co
 einsum_fn g_einsum = nullptr;
 copy_fn g_copy = nullptr;
 mul_fn g_mul = nullptr;
-void *g_stream = nullptr;
+// one launch stream per host thread: a process may drive several solves at once, one per thread,
+// each on its own stream and libttk context (bind() is called once on each such thread)
+thread_local void *g_stream = nullptr;
 
 void bind(int64_t einsum_addr, int64_t copy_addr, int64_t mul_addr, int64_t stream) {
   g_einsum = reinterpret_cast<einsum_fn>(einsum_addr);
@@ -112,7 +114,13 @@ at::Tensor einsum(const std::string &eq, const std::vector<at::Tensor> &ops, c10
     beta = 0.0;
     desc[pos++] = 0;
   }
-  check(g_einsum(g_stream, eq.c_str(), desc, res.data_ptr<double>(), alpha, beta), "einsum");
+  double *rp = res.data_ptr<double>();
+  int rc;
+  {  // the launch itself touches no Python object: other solve threads may run meanwhile
+    pybind11::gil_scoped_release nogil;
+    rc = g_einsum(g_stream, eq.c_str(), desc, rp, alpha, beta);
+  }
+  check(rc, "einsum");
   return res;
 }
 

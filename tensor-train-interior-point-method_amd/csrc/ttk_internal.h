@@ -51,7 +51,8 @@ struct Ctx {
   // flipping one on a context never changes another context's results).  Defaults from the
   // environment at context creation.
   int knob[TTK_KNOB_COUNT] = {1, env_int("TTK_FUSED_MFMA", 1) != 0 ? 1 : 0, 1, env_int("TTK_SPLITK_MINK", 128),
-                              env_int("TTK_LGMRES_MW_MIN", 16384), env_int("TTK_MFMA_CSPLIT", 1) != 0 ? 1 : 0};
+                              env_int("TTK_LGMRES_MW_MIN", 16384), env_int("TTK_MFMA_CSPLIT", 1) != 0 ? 1 : 0,
+                              env_int("TTK_APPLY_DUAL", 1) != 0 ? 1 : 0};
 };
 Ctx &ctx();
 Ctx *ctx_swap(Ctx *c);  // bind c to the calling thread, return the previous binding

@@ -13,6 +13,7 @@ random numbers); all arithmetic goes through the C ABI in `include/ttk.h`.
 """
 import ctypes
 import os
+import threading
 from functools import lru_cache
 
 import numpy as np
@@ -25,30 +26,46 @@ F64 = torch.float64
 _vp = ctypes.c_void_p
 
 
-_STREAM = []
+class _PerThread(threading.local):
+    """Per-host-thread state of the path: several solves may run at once in one process, one per
+    thread, each with its own HIP stream and libttk context (bench.py's solves in flight)."""
+
+    def __init__(self):
+        self.stream = []  # the launch stream (the thread's current torch stream when first used)
+        self.ctx = []     # the ttk_ctx bound to this thread (created with the stream)
+        self.batch = [0]  # open einsum batches (dev.einsum_batch)
+        # operands of recorded (not yet launched) einsum steps: held until the flush so that the
+        # caching allocator cannot hand their memory to an allocation whose kernels run before them
+        self.keep = []
+        self.fast = None  # _ttkbind bound to this thread's stream
+        self.ones = {}    # small constant device tensors made on this thread's stream
+        self.anti = {}
 
 
-CTX = []  # the ttk_ctx bound to the host thread that drives the path (created with the stream)
-_BATCH = [0]  # open einsum batches (dev.einsum_batch)
-# operands of recorded (not yet launched) einsum steps: held until the flush so that the caching
-# allocator cannot hand their memory to an allocation whose kernels run before the recorded steps
-_KEEP = []
+_TL = _PerThread()
+
+
+def ctx():
+    """This thread's ttk_ctx handle (None before the first launch)."""
+    c = _TL.ctx
+    return c[0] if c else None
 
 
 def _stream():
-    """The launch stream (the device's current stream when first used; the path never switches
+    """The launch stream (the thread's current stream when first used; the path never switches
     streams, and torch.cuda.current_stream() costs ~10 us per call)."""
-    if not _STREAM:
-        _STREAM.append(torch.cuda.current_stream().cuda_stream if DEV.type == "cuda" else None)
-        if DEV.type == "cuda":  # this process's libttk context: the launch stream + all scratch state
+    tl = _TL
+    if not tl.stream:
+        tl.stream.append(torch.cuda.current_stream().cuda_stream if DEV.type == "cuda" else None)
+        if DEV.type == "cuda":  # this thread's libttk context: the launch stream + all scratch state
             h = ctypes.c_void_p(0)
-            check(lib.ttk_ctx_create(_STREAM[0], ctypes.byref(h)), "ctx_create")
-            CTX.append(h)
+            check(lib.ttk_ctx_create(tl.stream[0], ctypes.byref(h)), "ctx_create")
+            tl.ctx.append(h)
             check(lib.ttk_ctx_bind(h), "ctx_bind")
-    if _BATCH[0]:  # any launch other than an einsum first flushes the recorded steps (stream order)
-        check(lib.ttk_einsum_batch_flush(_STREAM[0]), "einsum_batch_flush")
-        _KEEP.clear()
-    return _STREAM[0]
+    if tl.batch[0]:  # any launch other than an einsum first flushes the recorded steps (stream order)
+        check(lib.ttk_einsum_batch_flush(tl.stream[0]), "einsum_batch_flush")
+        tl.keep.clear()
+    return tl.stream[0]
 
 
 class einsum_batch:
@@ -60,16 +77,18 @@ class einsum_batch:
     def __enter__(self):
         if DEV.type == "cuda":
             _stream()
-            check(lib.ttk_einsum_batch_begin(_STREAM[0]), "einsum_batch_begin")
-            _BATCH[0] += 1
+            tl = _TL
+            check(lib.ttk_einsum_batch_begin(tl.stream[0]), "einsum_batch_begin")
+            tl.batch[0] += 1
         return self
 
     def __exit__(self, *exc):
         if DEV.type == "cuda":
-            _BATCH[0] -= 1
-            check(lib.ttk_einsum_batch_end(_STREAM[0]), "einsum_batch_end")
-            if not _BATCH[0]:
-                _KEEP.clear()
+            tl = _TL
+            tl.batch[0] -= 1
+            check(lib.ttk_einsum_batch_end(tl.stream[0]), "einsum_batch_end")
+            if not tl.batch[0]:
+                tl.keep.clear()
         return False
 
 
@@ -99,17 +118,17 @@ def _load_bind():
 
 
 _BIND = _load_bind()
-_FAST = None
 
 
 def _fast():
-    global _FAST
-    if _FAST is None and _BIND is not None:
+    """_ttkbind bound to this thread's stream (the binder keeps one stream per host thread)."""
+    tl = _TL
+    if tl.fast is None and _BIND is not None:
         def addr(f):
             return ctypes.cast(f, ctypes.c_void_p).value
         _BIND.bind(addr(lib.ttk_einsum), addr(lib.ttk_copy_nd), addr(lib.ttk_mul_nd), _stream() or 0)
-        _FAST = _BIND
-    return _FAST
+        tl.fast = _BIND
+    return tl.fast
 
 
 def empty(*shape):
@@ -177,7 +196,7 @@ def _arr(vals):
 # ------------------------------------------------------------------------ element-wise
 def copy_(dst, src, alpha=1.0, beta=0.0):
     """dst = alpha * src + beta * dst (shapes must match; any strides)."""
-    f = _FAST or _fast()
+    f = _TL.fast or _fast()
     if f is not None:
         return f.copy_(dst, src, float(alpha), float(beta))
     assert tuple(dst.shape) == tuple(src.shape), (dst.shape, src.shape)
@@ -222,7 +241,7 @@ def clone_many(srcs):
 
 def mul_(dst, a, b, alpha=1.0, beta=0.0):
     """dst = alpha * a * b + beta * dst (element-wise, same shapes, any strides)."""
-    f = _FAST or _fast()
+    f = _TL.fast or _fast()
     if f is not None:
         return f.mul_(dst, a, b, float(alpha), float(beta))
     nd = dst.dim()
@@ -356,14 +375,11 @@ def read(t):
 
 
 # ------------------------------------------------------------------------ einsum planner
-_ONES = {}
-
-
 def _ones_buf():
-    t = _ONES.get("o")
+    t = _TL.ones.get("o")
     if t is None:
         t = torch.ones(1, dtype=F64, device=DEV)
-        _ONES["o"] = t
+        _TL.ones["o"] = t
     return t
 
 
@@ -470,11 +486,12 @@ def einsum(eq, *ops, out=None, alpha=1.0, beta=0.0, fused=False, algo=None):
         else:
             count_algo(algo_flops(eq, tuple(tuple(o.shape) for o in ops)), what=eq)
     fused = fused or _FUSED_ALL
-    if _BATCH[0]:
+    tl = _TL
+    if tl.batch[0]:
         if out is None:
             out = _new_out(eq, ops)
             beta = 0.0
-        _KEEP.append((ops, out))
+        tl.keep.append((ops, out))
     if _CHECK_FUSED and fused and eq in _FUSED_EQS:
         return _einsum_checked(eq, ops, out, alpha, beta)
     return _einsum_native(eq, *ops, out=out, alpha=alpha, beta=beta, fused=fused)
@@ -492,7 +509,7 @@ def _einsum_native(eq, *ops, out=None, alpha=1.0, beta=0.0, fused=False):
     if OPSTATS is not None:
         e = OPSTATS.setdefault("einsum_eq", {}).setdefault(eq, [0, 0.0])
         e[0] += 1
-    f = _FAST or _fast()
+    f = _TL.fast or _fast()
     if f is not None:
         return f.einsum(eq, ops, out, float(alpha), float(beta), (256 | 512) if fused == "env" else (256 if fused else 0))
     desc = [len(ops) | ((256 | 512) if fused == "env" else (256 if fused else 0))]
@@ -509,8 +526,8 @@ def _einsum_native(eq, *ops, out=None, alpha=1.0, beta=0.0, fused=False):
         desc.append(1)
         desc.append(out.dim())
         desc.extend(out.stride())
-    _stream() if not _STREAM else None
-    check(lib.ttk_einsum(_STREAM[0], _eq_bytes(eq), (ctypes.c_int64 * len(desc))(*desc), out.data_ptr(),
+    st = _TL.stream[0] if _TL.stream else _stream()  # no batch flush: einsums are recorded
+    check(lib.ttk_einsum(st, _eq_bytes(eq), (ctypes.c_int64 * len(desc))(*desc), out.data_ptr(),
                          float(alpha), float(beta)), "einsum")
     return out
 
@@ -586,14 +603,11 @@ def qr(A):
     return Q, R
 
 
-_ANTI = {}
-
-
 def _anti_identity(n):
-    t = _ANTI.get(n)
+    t = _TL.anti.get(n)
     if t is None:
         t = from_numpy(np.eye(n)[::-1])
-        _ANTI[n] = t
+        _TL.anti[n] = t
     return t
 
 

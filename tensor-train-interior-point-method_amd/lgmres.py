@@ -45,7 +45,7 @@ def _lgmres_native(handle, b, rtol, max_it, max_k, aug_dim, info):
     x = D.empty(n)
     st = _Info()
     s = D._stream()
-    rc = lib.ttk_lgmres(D.CTX[0] if D.CTX else None, int(handle), b.data_ptr(), x.data_ptr(), n, max_k, aug_dim,
+    rc = lib.ttk_lgmres(D.ctx(), int(handle), b.data_ptr(), x.data_ptr(), n, max_k, aug_dim,
                         float(rtol), int(max_it), CHUNK, ctypes.byref(st))
     if rc == TTK_ERR_NOT_CONVERGED:
         raise PetscConvFailed(lib.ttk_last_error().decode())

@@ -13,6 +13,7 @@ import os
 import numpy as np
 
 from . import dev as D
+from . import rng as _rng
 from . import tt_ops as T
 from .dev import einsum
 
@@ -260,7 +261,7 @@ def env_update_many(backward, items):
             eq = "LSR,lML,sMNS,rNR->lsr" if backward else "lsr,lML,sMNS,rNR->LSR"
             D.count_algo(D.algo_flops(eq, _shapes(P, x, A, y)), what=eq)
     D._stream()
-    D.check(D.lib.ttk_env_update(D.CTX[0], int(backward), len(items), arr), "env_update")
+    D.check(D.lib.ttk_env_update(D.ctx(), int(backward), len(items), arr), "env_update")
     return outs
 
 
@@ -545,8 +546,8 @@ def tt_block_amen(block_A, block_b, term_tol, r_max=100, eps=1e-12, nswp=22, x0=
     xshape = tuple(model[0].shape[1:-1])
 
     def fresh():
-        head = T.tt_normalise([D.from_numpy(np.random.randn(1, *c.shape[1:-1], 1)) for c in model[:-1]])
-        return head + [D.from_numpy(np.random.randn(1, B, *xshape, 1))]
+        head = T.tt_normalise([D.from_numpy(_rng.R().randn(1, *c.shape[1:-1], 1)) for c in model[:-1]])
+        return head + [D.from_numpy(_rng.R().randn(1, B, *xshape, 1))]
 
     def block_idx(cores):
         ids = [i for i, cc in enumerate(cores) if cc.dim() == 4 and cc.shape[1] == B]
@@ -590,10 +591,10 @@ def tt_block_amen(block_A, block_b, term_tol, r_max=100, eps=1e-12, nswp=22, x0=
         c.ZAX = [{k: o3 for k in tk}] + [{k: None for k in tk} for _ in range(d - 1)] + [{k: o3 for k in tk}]
         c.Zb = [{k: o2 for k in block_b.keys()}] + [{k: None for k in block_b.keys()} for _ in range(d - 1)] + \
             [{k: o2 for k in block_b.keys()}]
-        z0 = [np.divide(1, np.prod(x[0].shape[1:-1]) * kick_rank ** 2) * np.random.randn(*x[0].shape[:-1], kick_rank)]
-        zm = [np.divide(1, np.prod(cc.shape[1:-1]) * kick_rank ** 2) * np.random.randn(kick_rank, *cc.shape[1:-1], kick_rank)
+        z0 = [np.divide(1, np.prod(x[0].shape[1:-1]) * kick_rank ** 2) * _rng.R().randn(*x[0].shape[:-1], kick_rank)]
+        zm = [np.divide(1, np.prod(cc.shape[1:-1]) * kick_rank ** 2) * _rng.R().randn(kick_rank, *cc.shape[1:-1], kick_rank)
               for cc in x[1:-1]]
-        zl = [np.divide(1, np.prod(x[-1].shape[1:-1]) * kick_rank ** 2) * np.random.randn(kick_rank, *x[-1].shape[1:])]
+        zl = [np.divide(1, np.prod(x[-1].shape[1:-1]) * kick_rank ** 2) * _rng.R().randn(kick_rank, *x[-1].shape[1:])]
         c.z = [D.from_numpy(a) for a in z0 + zm + zl]
         c.rz = np.array([1] + T.tt_ranks(c.z) + [1])
     c.local_solver = local_solver

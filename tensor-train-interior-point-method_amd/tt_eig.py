@@ -8,11 +8,13 @@ generalised problem `-D v = lambda A v` goes through a device Cholesky of A.  Th
 eigenpair is the same to the reference's tolerance (tol = 1e-8); ARPACK's failure branches
 (exceptions) map to the same fallbacks."""
 import os
+import threading
 import time
 
 import numpy as np
 
 from . import dev as D
+from . import rng as _rng
 from . import tt_ops as T
 from .dev import einsum
 from .tt_als import compute_phi_bck_A, compute_phi_fwd_A
@@ -84,7 +86,7 @@ def _normalise(v):
 def _kick(u, v, r_add):
     """`_add_kick_rank` (`src/tt_als.py:1041-1046`)."""
     old = u.shape[-1]
-    uk = D.from_numpy(np.random.randn(u.shape[0], r_add))
+    uk = D.from_numpy(_rng.R().randn(u.shape[0], r_add))
     cat = D.empty(u.shape[0], old + r_add)
     D.copy_(cat[:, :old], u)
     D.copy_(cat[:, old:], uk)
@@ -95,7 +97,7 @@ def _kick(u, v, r_add):
 def _kick_rev(u, v, r_add):
     """`_add_kick_rank_rev` (`src/tt_als.py:1048-1053`)."""
     old = v.shape[0]
-    uk = D.from_numpy(np.random.randn(r_add, v.shape[-1]))
+    uk = D.from_numpy(_rng.R().randn(r_add, v.shape[-1]))
     cat = D.empty(old + r_add, v.shape[-1])
     D.copy_(cat[:old], v)
     D.copy_(cat[old:], uk)
@@ -293,7 +295,13 @@ class _Slot:
         self.k = k
 
 
-_DEFER = [None]  # the active _Deferred of tt_max_generalised_eigen's sweep, or "skip" (residual unused)
+class _EigThread(threading.local):
+    def __init__(self):
+        self.defer = None  # the active _Deferred of tt_max_generalised_eigen's sweep, or "skip" (residual unused)
+        self.min_eig_tol = 1e-8  # tt_min_eig's tolerance for the local LOBPCG solves
+
+
+_ET = _EigThread()  # per host thread: several solves may run at once in one process
 
 
 def _dense_step(prev, Am, Dm, step, eps, tag):
@@ -315,7 +323,7 @@ def _dense_step(prev, Am, Dm, step, eps, tag):
             branch = f"fail {type(e).__name__}"
     if _DEBUG:
         print(f"  dev {tag} m={prev.numel()} ev={ev:.6e} step {step_in:.12e} -> {step:.12e} {branch}")
-    df = _DEFER[0] if _FUSED_TAIL and prev.is_contiguous() else None
+    df = _ET.defer if _FUSED_TAIL and prev.is_contiguous() else None
     if df == "skip":  # the caller discards the residual: only its 1/step (ZeroDivisionError at 0) matters
         1.0 / step
         return sol, step, None
@@ -457,7 +465,7 @@ def tt_max_generalised_eigen(A, Delta, x0=None, nswp=10, tol=1e-8, size_limit=25
 
     def finish_fwd():
         nonlocal step
-        _DEFER[0] = "skip"  # the last local solves' residuals are discarded
+        _ET.defer = "skip"  # the last local solves' residuals are discarded
         for k in range(d):
             sol, step, _ = _step_size_local_solve_last(x[k], XDX[k], Delta[k], XDX[k + 1], XAX[k], A[k], XAX[k + 1],
                                                        np.sqrt(rx[k] * rx[k + 1]) < size_limit, step, tol)
@@ -477,7 +485,7 @@ def tt_max_generalised_eigen(A, Delta, x0=None, nswp=10, tol=1e-8, size_limit=25
 
     def finish_bck():
         nonlocal step
-        _DEFER[0] = "skip"  # the last local solves' residuals are discarded
+        _ET.defer = "skip"  # the last local solves' residuals are discarded
         for k in range(d - 1, -1, -1):
             sol, step, _ = _step_size_local_solve_last(x[k], XDX[k], Delta[k], XDX[k + 1], XAX[k], A[k], XAX[k + 1],
                                                        np.sqrt(rx[k] * rx[k + 1]) < size_limit, step, tol)
@@ -496,7 +504,7 @@ def tt_max_generalised_eigen(A, Delta, x0=None, nswp=10, tol=1e-8, size_limit=25
                 x[k] = D.contig(sol).view(rx[k], N[k], rx[k + 1])
 
     dfr = _Deferred(d)
-    _DEFER[0] = dfr
+    _ET.defer = dfr
     try:
         for swp in range(nswp):
             zero = False
@@ -554,7 +562,7 @@ def tt_max_generalised_eigen(A, Delta, x0=None, nswp=10, tol=1e-8, size_limit=25
             prev_step = step
             prev_res = sres
     finally:
-        _DEFER[0] = None
+        _ET.defer = None
     max_res = np.max(local_res)
     x = T.tt_normalise(x)
     if verbose:
@@ -570,14 +578,13 @@ def _min_lobpcg(apply_A, prev):
     """`lobpcg(A_op, X=prev, tol, largest=False)` with the reference's fallback to prev."""
     m = prev.numel()
     try:
-        return lobpcg(apply_A, prev, tol=_MIN_EIG_TOL[0], largest=False, maxiter=_lobpcg_maxiter(m))
+        return lobpcg(apply_A, prev, tol=_ET.min_eig_tol, largest=False, maxiter=_lobpcg_maxiter(m))
     except Exception as e:
         if not isinstance(e, LobpcgFailure):
             print(f"\tAttention: {e}")
         return D.dot(prev, apply_A(prev)), prev
 
 
-_MIN_EIG_TOL = [1e-8]
 
 
 def _eigen_local_solve(p1, p2, XAX_k, A_k, A_kp1, XAX_k2, size_limit, trunc_tol, max_rank, bwd=True):
@@ -631,7 +638,7 @@ def tt_min_eig(A, x0=None, nswp=10, tol=1e-8, size_limit=64, return_eig_val=Fals
     max_rank = int(np.floor(2 ** (d / 2)))
     trunc_tol = 0.1 * tol / np.sqrt(d)
     prev_res = np.inf
-    _MIN_EIG_TOL[0] = tol
+    _ET.min_eig_tol = tol
 
     def finish_fwd():
         for k in range(d):

@@ -19,6 +19,7 @@ import time
 import numpy as np
 
 from . import dev as D
+from . import rng as _rng
 from ._lib import lib
 from . import tt_ops as T
 from .dev import einsum
@@ -74,7 +75,7 @@ class MatVecWrapper:
             h = ctypes.c_int64(0)
             arr = (ctypes.c_int64 * len(desc))(*desc)
             D._stream()
-            self._ctx = D.CTX[0] if D.CTX else None
+            self._ctx = D.ctx()
             D.check(lib.ttk_schur_build(self._ctx, int(len(self.keys) > 4), self.m, arr,
                                         inv_I.contiguous().data_ptr(), ctypes.byref(h)), "schur_build")
             self.h = h.value
@@ -217,7 +218,7 @@ def _dense_native(XAX_k, A_k, XAX_k1, rhs, inv_I, xs):
     sol = D.empty(*xs)
     rc = ctypes.c_double(0.0)
     D._stream()
-    st = lib.ttk_dense_schur_solve(D.CTX[0], r, n, R, arr, rhs.data_ptr(), inv_I.data_ptr(), sol.data_ptr(),
+    st = lib.ttk_dense_schur_solve(D.ctx(), r, n, R, arr, rhs.data_ptr(), inv_I.data_ptr(), sol.data_ptr(),
                                    ctypes.byref(rc))
     if st == _TTK_ILL_CONDITIONED:
         raise D.LinAlgWarning(f"Ill-conditioned matrix (rcond={rc.value:.5g}): result may not be accurate.")
@@ -418,7 +419,7 @@ def _dense_native_ineq(XAX_k, A_k, XAX_k1, rhs, inv_I, xs):
     rhs, inv_I = D.contig(rhs), D.contig(inv_I)
     sol = D.empty(*xs)
     D._stream()
-    D.check(lib.ttk_dense_schur_solve_ineq(D.CTX[0], r, n, R, arr, rhs.data_ptr(), inv_I.data_ptr(), sol.data_ptr()),
+    D.check(lib.ttk_dense_schur_solve_ineq(D.ctx(), r, n, R, arr, rhs.data_ptr(), inv_I.data_ptr(), sol.data_ptr()),
             "dense_schur_solve_ineq")
     return sol
 
@@ -754,7 +755,7 @@ def _tt_get_step_sizes(X, Z, Tt, DX, DZ, DT, mask, st):
         X = T.tt_add(X, T.tt_scale(st.boundary_val, T.tt_identity(len(X))))
         Z = T.tt_add(Z, T.tt_scale(st.boundary_val, T.tt_identity(len(Z))))
     x0s = (st.eigen_x0, st.eigen_z0)
-    rng = np.random.get_state()
+    rng = _rng.R().get_state()
     xs, st.eigen_x0 = tt_max_generalised_eigen(X, DX, x0=st.eigen_x0, tol=1e-8, verbose=st.verbose)
     zs, st.eigen_z0 = tt_max_generalised_eigen(Z, DZ, x0=st.eigen_z0, tol=1e-8, verbose=st.verbose)
     if _DUMP_DIR:

@@ -18,15 +18,15 @@ import os
 
 import numpy as np
 from . import dev as D
-
-_CONST = {}
-
+from . import rng as _rng
 
 def _const(name, arr):
-    t = _CONST.get(name)
+    """Small constant cores, uploaded once per host thread (on that thread's stream)."""
+    c = D._TL.__dict__.setdefault("consts", {})
+    t = c.get(name)
     if t is None:
         t = D.from_numpy(arr)
-        _CONST[name] = t
+        c[name] = t
     return t
 
 
@@ -84,7 +84,7 @@ def tt_swap_all(tt):
 def tt_scale(alpha, tt):
     """`cy_src/tt_ops_cy.pyx:94-114`: fp32 alpha, one random core."""
     n = len(tt)
-    idx = np.random.randint(0, n)
+    idx = _rng.R().randint(0, n)
     out = list(tt)
     out[idx] = D.scaled(tt[idx], float(np.float32(alpha)))
     return out
@@ -180,7 +180,7 @@ def tt_normalise(tt, radius=1):
 def tt_random_gaussian(target_ranks, shape=(2,)):
     """`cy_src/tt_ops_cy.pyx:528-533` (host MT19937 draws, uploaded)."""
     rk = [1] + list(target_ranks) + [1]
-    cores = [D.from_numpy(np.divide(1, a * int(np.prod(shape)) * b) * np.random.randn(a, *shape, b))
+    cores = [D.from_numpy(np.divide(1, a * int(np.prod(shape)) * b) * _rng.R().randn(a, *shape, b))
              for a, b in zip(rk[:-1], rk[1:])]
     return tt_normalise(cores)
 
@@ -203,7 +203,7 @@ def symmetric_powers_of_two(length):
 def add_kick_rank(u, v, r_add=2):
     """`cy_src/tt_ops_cy.pyx:557-578`"""
     old_r = u.shape[1]
-    uk = D.from_numpy(np.random.randn(u.shape[0], r_add))
+    uk = D.from_numpy(_rng.R().randn(u.shape[0], r_add))
     q, rm = D.qr(_cat(u, uk, -1))
     return q, D.matmul(rm[:, :old_r], v), q.shape[1]
 
@@ -300,7 +300,7 @@ def _native_round(tt, eps, mode):
     ranks = (ctypes.c_int64 * (d + 1))(*([tt[0].shape[0]] + [c.shape[-1] for c in tt]))
     tail = ctypes.c_double(0.0)
     D._stream()
-    D.check(D.lib.ttk_round(D.CTX[0], d, ptrs, inner, ranks, float(eps), mode, ctypes.byref(tail)), "round")
+    D.check(D.lib.ttk_round(D.ctx(), d, ptrs, inner, ranks, float(eps), mode, ctypes.byref(tail)), "round")
     out = [c.view(-1)[:ranks[k] * inner[k] * ranks[k + 1]].view(ranks[k], *mids[k], ranks[k + 1])
            for k, c in enumerate(cs)]
     tt[:] = out  # in place, like the reference's list mutation
@@ -501,7 +501,7 @@ def _native_zipup(kind, a, b, eps, out_modes):
     I64 = ctypes.c_int64
     ranks = (I64 * (d + 1))()
     D._stream()
-    D.check(D.lib.ttk_zipup(D.CTX[0], kind, d, (P * d)(*[c.data_ptr() for c in ca]), (I64 * (d + 1))(*ar),
+    D.check(D.lib.ttk_zipup(D.ctx(), kind, d, (P * d)(*[c.data_ptr() for c in ca]), (I64 * (d + 1))(*ar),
                             (P * d)(*[c.data_ptr() for c in cb]), (I64 * (d + 1))(*br), (I64 * (3 * d))(*mids),
                             float(eps), (P * d)(*[o.data_ptr() for o in outs]), ranks), "zipup")
     return [o[:ranks[k] * inner[k] * ranks[k + 1]].view(ranks[k], *out_modes[k], ranks[k + 1])

@@ -15,14 +15,17 @@ import numpy as np
 import torch
 import yaml
 
+from . import rng as _rng
 from . import tt_ops as T
 from .problems import PROBLEMS
 from .tt_ipm import IneqStatus, tt_ipm
 
 
 def _sync():
+    """Wait for this thread's launch stream (the whole path runs on it; other host threads' solves
+    on other streams are not waited for)."""
     if torch.cuda.is_available():
-        torch.cuda.synchronize()
+        torch.cuda.current_stream().synchronize()
 
 
 def create(problem, config, seed, rank, verbose=None):
@@ -53,7 +56,7 @@ def solve(prepared, config, trace=None, verbose=None, iter_callback=None, quiet=
     the recorded gap / primal / dual feasibility."""
     verbose = config.get("verbose", False) if verbose is None else verbose
     C, L, b, mask, lag = prepared["C"], prepared["L"], prepared["b"], prepared["mask"], prepared["lag"]
-    np.random.set_state(prepared["rng_state"])
+    _rng.R().set_state(prepared["rng_state"])
     _sync()
     t2 = time.time()
     X, Y, Tt, Z, info = tt_ipm(lag, C, L, b, ineq_mask=mask, max_iter=config["max_iter"], verbose=verbose,

@@ -58,6 +58,8 @@ def test_replica_schedule():
 
 def test_default_inflight_same_at_every_n_and_caps_processes_per_node():
     """The 1/2/4/8-GPU series runs the same solves in flight per GPU (like-for-like scaling) and a
-    node never runs more than 16 solve processes."""
-    assert {bench.default_inflight(w) for w in (1, 2, 4, 8)} == {2}
-    assert all(w * bench.default_inflight(w) <= 16 for w in (1, 2, 4, 8, 16))
+    node never runs more than 16 solve processes (slots are host threads, DEFAULT_THREADS per
+    process)."""
+    assert {bench.default_inflight(w) for w in (1, 2, 4, 8)} == {4}
+    T = bench.DEFAULT_THREADS
+    assert all(w * -(-bench.default_inflight(w) // T) <= 16 for w in (1, 2, 4, 8, 16))

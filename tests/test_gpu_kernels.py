@@ -660,3 +660,40 @@ def test_schur_mfma_rows_split_bit_identical(dev, ineq):
         finally:
             _set_csplit(old)
     assert np.array_equal(outs[0], outs[1])
+
+
+def _set_dual(on):
+    import ctypes
+    from ttipm_amd import _lib
+    old = ctypes.c_int(0)
+    assert _lib.lib.ttk_ctx_set_knob(None, _lib.KNOB_APPLY_DUAL, int(on), ctypes.byref(old)) == 0
+    return old.value
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ineq", [False, True])
+@pytest.mark.parametrize("dims", [(12, 16, 10, 9, 4), (3, 4, 5, 5, 4), (16, 20, 12, 12, 4)])
+def test_schur_terms_side_by_side_bit_identical(dev, ineq, dims):
+    """the Schur-reduced operator on VALU rows at maxcut sizes: a task's two terms side by side, one
+    half of the workgroup each (TTK_KNOB_APPLY_DUAL on, the default), and one after the other (off)
+    give the same matvec bit for bit (the sequential form is the one the golden tests pin)"""
+    from ttipm_amd import tt_ipm
+    rng = np.random.default_rng(11)
+    r, R, s, S, n = dims
+    cls = tt_ipm.IneqMatVecWrapper if ineq else tt_ipm.MatVecWrapper
+    L = {k: dev.from_numpy(rng.standard_normal((r, s, r)) * 0.1) for k in cls.keys}
+    Am = {k: dev.from_numpy(rng.standard_normal((s, n, n, S)) * 0.1) for k in cls.keys}
+    Rr = {k: dev.from_numpy(rng.standard_normal((R, S, R)) * 0.1) for k in cls.keys}
+    invI = dev.from_numpy(rng.uniform(0.5, 2.0, (r, n, R)))
+    nb = 3 if ineq else 2
+    v = dev.from_numpy(rng.standard_normal(nb * r * n * R))
+    outs = {}
+    for on in (0, 1):
+        old = _set_dual(on)
+        try:
+            op = cls(L, Am, Rr, invI, (r, n, R))
+            assert op.h != 0
+            outs[on] = dev.read(op.matvec(v))
+        finally:
+            _set_dual(old)
+    assert np.array_equal(outs[0], outs[1])

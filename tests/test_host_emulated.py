@@ -127,3 +127,36 @@ def test_lobpcg_matches_scipy(pkg, gen, largest, n, maxiter):
     assert ok == ref_ok
     if ok:
         assert abs(lam - float(lam_ref[0])) <= 1e-10 * abs(float(lam_ref[0]))
+
+
+def test_concurrent_solves_in_threads_match_one_at_a_time(pkg):
+    """bench.py's solves in flight within one process: slot threads, each with a private NumPy
+    random stream (`ttipm_amd.rng`) and its own per-thread device state (`dev._TL`, the eigen
+    sweep's deferred residuals, the constant cores), give every seed exactly its one-at-a-time
+    result."""
+    import threading
+
+    from ttipm_amd import rng
+    from ttipm_amd.utils import create, solve
+    cfg = yaml.safe_load(open(os.path.join(ROOT, "configs", "maxcut_5.yaml")))
+    seeds = [0, 319]
+    seq = {s: solve(create("maxcut", cfg, s, 1, verbose=False), cfg, quiet=True, verbose=False) for s in seeds}
+    preps = {s: create("maxcut", cfg, s, 1, verbose=False) for s in seeds}  # main thread, global RNG
+    out, errs = {}, []
+
+    def run(s):
+        try:
+            rng.private()
+            out[s] = solve(preps[s], cfg, quiet=True, verbose=False)
+        except Exception as e:  # noqa: BLE001 - reported below
+            errs.append(e)
+
+    th = [threading.Thread(target=run, args=(s,)) for s in seeds]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errs, errs
+    for s in seeds:
+        for k in ("num_iters", "gap", "feas", "dual_feas", "ranksX", "ranksZ"):
+            assert out[s][k] == seq[s][k], (s, k, out[s][k], seq[s][k])

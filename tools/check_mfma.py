@@ -56,7 +56,7 @@ orig_einsum = D.einsum
 
 
 def einsum_checked(eq, *ops, out=None, alpha=1.0, beta=0.0, fused=False, algo=None):
-    if not fused or D._BATCH[0]:
+    if not fused or D._TL.batch[0]:
         return orig_einsum(eq, *ops, out=out, alpha=alpha, beta=beta, fused=fused, algo=algo)
     keep = None if out is None else D.clone(out)
     got = orig_einsum(eq, *ops, out=out, alpha=alpha, beta=beta, fused=fused, algo=algo)
