@@ -173,7 +173,9 @@ class _Slots:
         try:
             if device is not None:
                 torch.cuda.set_device(device)
-                if self.n > 1 or os.environ.get("TTIPM_SLOT_STREAM", "new") != "default":
+                # one slot per process: the default stream (measured: two processes on created streams
+                # slow each other 2.6x, on their default streams not at all, profiles/r03_inflight_layouts.txt)
+                if self.n > 1 or os.environ.get("TTIPM_SLOT_STREAM", "default") != "default":
                     torch.cuda.set_stream(torch.cuda.Stream())
             rng.private()
             for _ in range(warmup):  # untimed: plans, this context's scratch, allocator, code pages
@@ -324,14 +326,15 @@ def _pmc_traffic():
     return None
 
 
-DEFAULT_THREADS = 2  # solves in flight per process (host threads, one HIP stream + libttk context each)
+DEFAULT_THREADS = 1  # solves in flight per process (slot threads; >1: one created HIP stream each)
 
 
 def default_inflight(world):
-    """Solves in flight per GPU: 4 at every N of the 1/2/4/8-GPU series, so that the series is
-    like-for-like -- 2 processes per GPU x DEFAULT_THREADS slot threads each, so a node runs at most
-    16 solve processes (8 GPUs x 2).  Round-2 process sweep on one MI355X (maxcut_10 whole job):
-    1 -> 0.39, 2 -> 0.20, 4 -> 0.106, 6 -> 0.112 s/IPM-iter: 4 in flight is the knee."""
+    """Solves in flight per GPU: 4 (one process each, on its default stream) up to 4 GPUs, 2 on 8 GPUs
+    (a node runs at most 16 solve processes).  Round-2 process sweep on one MI355X (maxcut_10 whole
+    job): 1 -> 0.39, 2 -> 0.20, 4 -> 0.106, 6 -> 0.112 s/IPM-iter: 4 in flight is the knee.  Slot
+    threads sharing a process would keep 4 per GPU at N=8, but they need created streams, and
+    solves on created streams slow each other down (profiles/r03_inflight_layouts.txt)."""
     return max(1, min(4, DEFAULT_THREADS * (16 // world)))
 
 
