@@ -2587,6 +2587,13 @@ int lu_factor_fork_rcond(hipStream_t st, double *A, int n, int *piv, double *wor
     TTK_LAUNCH_CHECK();
     return TTK_OK;
   }
+  // TTK_LU_FORK=0: the estimate on the caller's stream (same results; no second HW queue per process,
+  // which matters when several solve processes share the GPU)
+  static const int fork_on = getenv("TTK_LU_FORK") ? atoi(getenv("TTK_LU_FORK")) : 1;
+  if (!fork_on) {
+    const int rc = lu_blocked(st, A, n, piv, work, c.status, c.rcond, 1);
+    return rc;
+  }
   if (!c.side) {
     TTK_HIP(hipStreamCreateWithFlags(&c.side, hipStreamNonBlocking));
     TTK_HIP(hipEventCreateWithFlags(&c.ev_fork, hipEventDisableTiming));
