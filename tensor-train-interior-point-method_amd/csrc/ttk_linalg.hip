@@ -317,6 +317,7 @@ __global__ __launch_bounds__(1024) void svd_wg_kernel(const double *__restrict__
   const int tid = threadIdx.x, nt = blockDim.x;
   const int lane = tid & 63, wid = tid >> 6, nw = nt >> 6;
   unsigned long long t_ph = timing ? wall_clock64() : 0;
+  const unsigned long long t_w0 = t_ph, t_c0 = timing ? clock64() : 0;  // shader clock vs 100 MHz wall
 #define TTK_PHASE(K)                                    \
   if (timing && tid == 0) {                             \
     const unsigned long long t1 = wall_clock64();       \
@@ -604,7 +605,11 @@ __global__ __launch_bounds__(1024) void svd_wg_kernel(const double *__restrict__
   if (timing) {
     __syncthreads();
     TTK_PHASE(7)
-    if (tid == 0) atomicAdd(&g_dbg[0], 1ull);
+    if (tid == 0) {
+      atomicAdd(&g_dbg[0], 1ull);
+      atomicAdd(&g_dbg[2], clock64() - t_c0);
+      atomicAdd(&g_dbg[3], wall_clock64() - t_w0);
+    }
   }
 #undef TTK_PHASE
 }

@@ -237,7 +237,7 @@ RUNS = [
     ("maxcut", "maxcut_12", 10, 2, True, 0),
     ("maxcut", "maxcut_12", 11, 2, True, 0),
     ("maxcut", "maxcut_12", 13, 2, True, 0),
-    ("maxcut", "maxcut_12", 16, 2, True, 0),
+    ("maxcut", "maxcut_12", 16, 2, True, 0),  # pathological in the reference (12 iterations, gap 0.17)
     ("maxcut", "maxcut_12", 18, 2, True, 0),  # pathological in the reference (17 iterations, gap 1.16e-3)
     ("maxcut", "maxcut_12", 19, 2, True, 0),
     ("maxcut", "maxcut_12", 20, 2, True, 0),

@@ -390,7 +390,7 @@ def _run(key, trace=None):
 # own runs -- the shipped golden or a thread / hash-seed / Jacobi-SVD twin -- to within 50x the
 # shipped code's rounding noise until that noise branches).
 from tests.parity_policy import ALL_TWINS as TWIN_SUFFIXES  # noqa: E402
-from tests.parity_policy import KEYS4, _rel, check_against_reference_runs  # noqa: E402,F401
+from tests.parity_policy import KEYS4, _rel, check_against_reference_runs, is_pathological  # noqa: E402,F401
 TRAJ_RTOL = 1e-4
 
 
@@ -483,6 +483,26 @@ def test_maxcut_12_rank2_matches_reference_trajectory(dev):
     g, r = _run("maxcut_12_r2_s80", trace)
     name, per, cum = check_against_reference_runs("maxcut_12_r2_s80", trace, r)
     print("maxcut_12_r2_s80 follows", name, ["%.0e" % v for v in per], "noise", ["%.0e" % v for v in cum])
+
+
+def _extra_seeds():
+    import sys
+    sys.path.insert(0, ROOT)
+    import bench
+    return bench.EXTRA_SEEDS["maxcut_12.yaml"]
+
+
+@pytest.mark.parametrize("seed", _extra_seeds())
+def test_maxcut_12_extra_seeds_on_device(dev, seed):
+    """The 8-GPU schedule's extra maxcut_12 r=2 seeds (bench.EXTRA_SEEDS; one 1-thread reference run
+    each, no twins): the device's first Newton system equals the reference's (1e-8), and the solve
+    ends non-pathological (src/utils.py:67) within 2 iterations of the reference's count."""
+    key = f"maxcut_12_r2_s{seed}"
+    trace = []
+    g, r = _run(key, trace)
+    assert max(_rel(trace[0][k], g["trace"][0][k]) for k in KEYS4) <= 1e-8
+    assert not is_pathological(r), (key, r["gap"], r["feas"])
+    assert abs(r["num_iters"] - g["num_iters"]) <= 2, (r["num_iters"], g["num_iters"])
 
 
 AP = np.load(os.path.join(HERE, "golden", "approx.npz"))
