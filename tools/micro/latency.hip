@@ -61,7 +61,7 @@ int main() {
   const char *names[] = {"barrier", "lds+2 barriers", "int modulo", "wave_sum (DPP)", "fp64 div", "fp64 sqrt",
                          "group_sum g=2", "8 dep fp64 fma", "8 dep fp32 fma", "2x8 fp64 fma"};
   const int iters = 20000;
-  for (int threads : {64}) {
+  for (int threads : {64, 256, 1024}) {
     for (int mode = 0; mode < 10; ++mode) {
       hipLaunchKernelGGL(k_sync, dim3(1), dim3(threads), 0, 0, iters, d, mode, 7);
       hipMemcpy(h, d, sizeof(h), hipMemcpyDeviceToHost);
