@@ -169,6 +169,18 @@ int ttk_ctx_create(void *stream, ttk_ctx *out) {
     return TTK_ERR_ARG;
   }
   h->c.stream = TTK_STREAM(stream);
+  // TTK_EAGER_SIDE=1: create the context's second stream now instead of at its first forked dgecon
+  // (diagnostics: whether a process's second HW queue changes how concurrent processes share the GPU)
+  static const int eager = getenv("TTK_EAGER_SIDE") ? atoi(getenv("TTK_EAGER_SIDE")) : 0;
+  if (eager && !h->c.side) {
+    if (hipStreamCreateWithFlags(&h->c.side, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&h->c.ev_fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&h->c.ev_join, hipEventDisableTiming) != hipSuccess) {
+      delete h;
+      ttk::set_error("ttk_ctx_create: side stream creation failed");
+      return TTK_ERR_HIP;
+    }
+  }
   *out = h;
   return TTK_OK;
 }
