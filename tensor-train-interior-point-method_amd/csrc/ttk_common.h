@@ -51,6 +51,56 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
                           __builtin_amdgcn_readlane(__double2loint(v), l));
 }
 
+template <int CTRL>
+__device__ __forceinline__ int dpp_mov_i(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xf, 0xf, false);
+}
+
+// (value, index) arg-max over the wave: the largest value, ties to the smallest index (the
+// LAPACK idamax winner whatever the reduction order, for non-NaN values); uniform result.  DPP
+// within each 16-lane row, then the four row winners by readlane -- no LDS round trips.
+__device__ __forceinline__ void wave_argmax(double &v, int &i) {
+  auto take = [&](double ov, int oi) {
+    if (ov > v || (ov == v && oi < i)) {
+      v = ov;
+      i = oi;
+    }
+  };
+  {
+    const double ov = dpp_mov<0xB1>(v);
+    const int oi = dpp_mov_i<0xB1>(i);
+    take(ov, oi);
+  }
+  {
+    const double ov = dpp_mov<0x4E>(v);
+    const int oi = dpp_mov_i<0x4E>(i);
+    take(ov, oi);
+  }
+  {
+    const double ov = dpp_mov<0x141>(v);
+    const int oi = dpp_mov_i<0x141>(i);
+    take(ov, oi);
+  }
+  {
+    const double ov = dpp_mov<0x140>(v);
+    const int oi = dpp_mov_i<0x140>(i);
+    take(ov, oi);
+  }
+  double bv = readlane_d(v, 0);
+  int bi = __builtin_amdgcn_readlane(i, 0);
+#pragma unroll
+  for (int r = 16; r < 64; r += 16) {
+    const double ov = readlane_d(v, r);
+    const int oi = __builtin_amdgcn_readlane(i, r);
+    if (ov > bv || (ov == bv && oi < bi)) {
+      bv = ov;
+      bi = oi;
+    }
+  }
+  v = bv;
+  i = bi;
+}
+
 // wave-wide sum, uniform result; the whole wave must be active
 __device__ __forceinline__ double wave_sum(double v) {
   v = group_sum<16>(v);

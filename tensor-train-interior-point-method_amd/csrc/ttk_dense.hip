@@ -242,15 +242,7 @@ __global__ __launch_bounds__(1024) void getf2_panel_kernel(double *A, int n, int
         bi = i;
       }
     }
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-      const double ov = __shfl_xor(best, o, 64);
-      const int oi = __shfl_xor(bi, o, 64);
-      if (ov > best || (ov == best && oi < bi)) {
-        best = ov;
-        bi = oi;
-      }
-    }
+    ttk::wave_argmax(best, bi);  // DPP + readlane: the same winner as the shuffle butterfly
     if (lane == 0) {
       wv[wid] = best;
       wi[wid] = bi;
@@ -317,15 +309,7 @@ __global__ __launch_bounds__(1024) void getf2_panel_lds_kernel(double *A, int n,
         bi = i;
       }
     }
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-      const double ov = __shfl_xor(best, o, 64);
-      const int oi = __shfl_xor(bi, o, 64);
-      if (ov > best || (ov == best && oi < bi)) {
-        best = ov;
-        bi = oi;
-      }
-    }
+    ttk::wave_argmax(best, bi);  // DPP + readlane: the same winner as the shuffle butterfly
     if (lane == 0) {
       wv[wid] = best;
       wi[wid] = bi;
@@ -334,16 +318,7 @@ __global__ __launch_bounds__(1024) void getf2_panel_lds_kernel(double *A, int n,
     if (tid < 64) {  // wave 0: reduce the 16 wave winners, swap the two panel rows
       double b = tid < 16 ? wv[tid] : -2.0;
       int p = tid < 16 ? wi[tid] : 0x7fffffff;
-#pragma unroll
-      for (int o = 8; o >= 1; o >>= 1) {
-        const double ob = __shfl_xor(b, o, 64);
-        const int op = __shfl_xor(p, o, 64);
-        if (ob > b || (ob == b && op < p)) {
-          b = ob;
-          p = op;
-        }
-      }
-      p = __shfl(p, 0, 64);
+      ttk::wave_argmax(b, p);  // uniform over the wave
       if (p != c && tid < kb) {
         const double t = P[c * ld + tid];
         P[c * ld + tid] = P[p * ld + tid];
@@ -701,15 +676,7 @@ __global__ __launch_bounds__(1024) void lu_rcond_kernel(const double *__restrict
         bi = i;
       }
     // first index of max |z|: wave shuffles, then wave 0 over the 16 wave winners
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-      const double ov = __shfl_xor(best, o, 64);
-      const int oi = __shfl_xor(bi, o, 64);
-      if (ov > best || (ov == best && oi < bi)) {
-        best = ov;
-        bi = oi;
-      }
-    }
+    ttk::wave_argmax(best, bi);  // DPP + readlane: the same winner as the shuffle butterfly
     if ((tid & 63) == 0) {
       rv[tid >> 6] = best;
       ri[tid >> 6] = bi;

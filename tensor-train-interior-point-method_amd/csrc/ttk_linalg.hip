@@ -335,8 +335,11 @@ __global__ __launch_bounds__(1024) void svd_wg_kernel(const double *__restrict__
   double *X = lds, *V = X + ldx * p, *tau = V + ldv * p, *vn1 = tau + p, *vn2 = vn1 + p, *sig = vn2 + p;
   int *perm = reinterpret_cast<int *>(sig + p), *rank = perm + p;
   double *W = use_qr ? (w_in_lds ? reinterpret_cast<double *>(rank + p + (p & 1)) : gwork) : X;
-  const int ldw = use_qr ? q : ldx;
-  double *M = W + (int64_t)q * p;
+  // W / M column stride: odd, so the g2-lane groups of one wave (consecutive columns) start on
+  // different LDS banks (an even q put every group of a wave on the same banks)
+  const int lq = q | 1;
+  const int ldw = use_qr ? lq : ldx;
+  double *M = W + (int64_t)lq * p;
   for (int e = tid; e < q * p; e += nt) {
     const int j = e / q, i = e - j * q;
     W[(int64_t)j * ldw + i] = tall ? A[(int64_t)i * n + j] : A[(int64_t)j * n + i];
@@ -344,7 +347,7 @@ __global__ __launch_bounds__(1024) void svd_wg_kernel(const double *__restrict__
   __syncthreads();
   if (use_qr) {
     for (int j = wid; j < p; j += nw) {
-      const double *w = W + (int64_t)j * q;
+      const double *w = W + (int64_t)j * lq;
       double acc = 0.0;
       #pragma unroll 8
       for (int i = lane; i < q; i += 64) acc += w[i] * w[i];
@@ -368,20 +371,13 @@ __global__ __launch_bounds__(1024) void svd_wg_kernel(const double *__restrict__
             bi = j;
           }
         }
-        for (int off = 32; off > 0; off >>= 1) {
-          const double om = __shfl_xor(bm, off, 64);
-          const int oi = __shfl_xor(bi, off, 64);
-          if (om > bm || (om == bm && oi < bi)) {
-            bm = om;
-            bi = oi;
-          }
-        }
+        ttk::wave_argmax(bm, bi);  // first max of the downdated norms, DPP (same winner as a butterfly)
         if (lane == 0) s_piv = bi < p ? bi : c;
       }
       __syncthreads();
       const int piv = s_piv;
       if (piv != c) {
-        double *a = W + (int64_t)c * q, *b = W + (int64_t)piv * q;
+        double *a = W + (int64_t)c * lq, *b = W + (int64_t)piv * lq;
         for (int i = tid; i < q; i += nt) {
           const double t = a[i];
           a[i] = b[i];
@@ -400,7 +396,7 @@ __global__ __launch_bounds__(1024) void svd_wg_kernel(const double *__restrict__
         }
         __syncthreads();
       }
-      double *x = W + (int64_t)c * q;
+      double *x = W + (int64_t)c * lq;
       if (wid == 0) {  // reflector (dlarfg) by wave 0
         double part = 0.0;
         #pragma unroll 8
@@ -424,7 +420,7 @@ __global__ __launch_bounds__(1024) void svd_wg_kernel(const double *__restrict__
       const double t = tau[c];
       // trailing update + dlaqp2 norm downdate: g2 lanes per column, all columns in flight
       for (int j = c + 1 + gid2; j < p; j += ng2) {
-        double *y = W + (int64_t)j * q;
+        double *y = W + (int64_t)j * lq;
         double yc = y[c];
         if (t != 0.0) {
           double acc = 0.0;
@@ -461,7 +457,7 @@ __global__ __launch_bounds__(1024) void svd_wg_kernel(const double *__restrict__
     // X = R^T (column length p)
     for (int e = tid; e < p * p; e += nt) {
       const int i = e / p, j = e - i * p;
-      X[i * ldx + j] = (j >= i) ? W[(int64_t)j * q + i] : 0.0;
+      X[i * ldx + j] = (j >= i) ? W[(int64_t)j * lq + i] : 0.0;
     }
   }
   for (int e = tid; e < p * p; e += nt) {
@@ -542,7 +538,7 @@ __global__ __launch_bounds__(1024) void svd_wg_kernel(const double *__restrict__
     // left factor of W: M(:, rank[j]) = Q [V(:, j); 0]; g2 lanes per column, each column runs
     // through all reflectors independently (no block barriers)
     for (int j = gid2; j < p; j += ng2) {
-      double *mc = M + (int64_t)rank[j] * q;
+      double *mc = M + (int64_t)rank[j] * lq;
       const double *vj = V + j * ldv;
       #pragma unroll 8
       for (int i = gl2; i < q; i += g2) mc[i] = i < p ? vj[i] : 0.0;
@@ -550,7 +546,7 @@ __global__ __launch_bounds__(1024) void svd_wg_kernel(const double *__restrict__
       for (int c = p - 1; c >= 0; --c) {
         const double t = tau[c];
         if (t == 0.0) continue;
-        const double *v = W + (int64_t)c * q;
+        const double *v = W + (int64_t)c * lq;
         double acc = 0.0;
         #pragma unroll 8
         for (int i = c + 1 + gl2; i < q; i += g2) acc += v[i] * mc[i];
@@ -569,7 +565,7 @@ __global__ __launch_bounds__(1024) void svd_wg_kernel(const double *__restrict__
   if (use_qr) {  // left = M (q x p), right(perm[i], rank[j]) = X(i, j)
     for (int e = tid; e < q * p; e += nt) {
       const int i = e / p, r = e - i * p;
-      const double v = M[(int64_t)r * q + i];
+      const double v = M[(int64_t)r * lq + i];
       if (tall)
         U[(int64_t)i * p + r] = v;
       else
@@ -2043,14 +2039,7 @@ __global__ __launch_bounds__(1024) void qrcp_pivot_kernel(double *W, int m, int 
     }
   }
   // wave reduction of (max, first index) and the sum
-  for (int off = 32; off > 0; off >>= 1) {
-    const double om = __shfl_xor(bm, off, 64);
-    const int oi = __shfl_xor(bi, off, 64);
-    if (om > bm || (om == bm && oi < bi)) {
-      bm = om;
-      bi = oi;
-    }
-  }
+  ttk::wave_argmax(bm, bi);
   sum = ttk::wave_sum(sum);
   if (lane == 0) {
     smax[wid] = bm;
@@ -2424,7 +2413,7 @@ int ttk_svd_set_big_threshold(int p) {
 
 int64_t ttk_svd_work(int m, int n) {
   const int64_t p = m < n ? m : n, q = m < n ? n : m;
-  const int64_t small = 2 * q * p + 16, big = svd_big_work(m, n);
+  const int64_t small = 2 * (q | 1) * p + 16, big = svd_big_work(m, n);
   return small > big ? small : big;
 }
 
@@ -2447,7 +2436,7 @@ int ttk_svd_tol(void *stream, const double *A, int m, int n, double *U, double *
   const int use_qr = !(p <= 16 && q <= 2 * p);
   const int L = use_qr ? p : q;
   const int64_t fixed = (int64_t)(L | 1) * p + (int64_t)(p | 1) * p + 5 * (int64_t)p + 2;  // X, V, vectors
-  const int64_t wm = use_qr ? 2 * (int64_t)q * p : 0;                          // W and M
+  const int64_t wm = use_qr ? 2 * (int64_t)(q | 1) * p : 0;                    // W and M (odd stride)
   const int w_in_lds = fixed + wm <= LDS_DOUBLES;
   const size_t shm = (size_t)(fixed + (w_in_lds ? wm : 0)) * sizeof(double);
 
