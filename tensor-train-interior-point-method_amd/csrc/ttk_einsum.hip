@@ -963,6 +963,9 @@ static bool mfma_enabled() { return ttk::ctx().knob[TTK_KNOB_FUSED_MFMA] != 0; }
 // from L2 with one workgroup per CU (LDS-bound occupancy), so 16 waves keep 4x the loads in flight of
 // 4; every output element / tile is still computed by one thread / wave in the same order
 static const int g_mfma_threads = getenv("TTK_MFMA_THREADS") ? atoi(getenv("TTK_MFMA_THREADS")) : 1024;
+// threads per workgroup of VALU apply rows (per term when a task's two terms run side by side):
+// every output element is one thread's sequential chain whatever the count, so results never change
+static const int g_valu_threads = getenv("TTK_VALU_THREADS") ? atoi(getenv("TTK_VALU_THREADS")) : 256;
 
 // workgroups per MFMA output row (ApplyArgs::csplit): enough that each workgroup's share of the
 // stage-3 (tile, K block) pairs is about one round over its waves, but no more workgroups in the
@@ -1109,7 +1112,7 @@ int fused_apply_try(void *stream, const char *eq, const int64_t *desc, double *o
                           e0, e1, 0, g);
   }
   else
-    hipExtLaunchKernelGGL(fused_apply_kernel, dim3(g.na), dim3(256), shm, TTK_STREAM(stream), e0, e1, 0, g);
+    hipExtLaunchKernelGGL(fused_apply_kernel, dim3(g.na), dim3(g_valu_threads), shm, TTK_STREAM(stream), e0, e1, 0, g);
   TTK_LAUNCH_CHECK();
   ttk::contract_count_ext(flops);
   return 1;
@@ -1413,7 +1416,7 @@ int ttk::schur_apply(void *stream, int64_t handle, const double *v, double *out)
     bool mf = false;
     for (int t = 0; t < L.ntask; ++t)
       for (int k = 0; k < L.task[t].nterms; ++k) mf = mf || L.task[t].t[k].mfma;
-    hipExtLaunchKernelGGL(fused_apply_multi_kernel, dim3(L.off[L.ntask]), dim3(mf ? g_mfma_threads : (L.dual ? 512 : 256)),
+    hipExtLaunchKernelGGL(fused_apply_multi_kernel, dim3(L.off[L.ntask]), dim3(mf ? g_mfma_threads : (L.dual ? 2 * g_valu_threads : g_valu_threads)),
                           op.shm[s],
                           TTK_STREAM(stream), e0, e1, 0, L);
     TTK_LAUNCH_CHECK();
@@ -1545,7 +1548,7 @@ int launch_fused_group(hipStream_t st, const std::vector<const BNode *> &v) {
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
     hipEvent_t e0, e1;
     if (ttk::contract_events_ext(&e0, &e1) != TTK_OK) return TTK_ERR_HIP;
-    hipExtLaunchKernelGGL(fused_apply_group_kernel, dim3(G.off[G.n]), dim3(mf ? g_mfma_threads : 256), shm, st, e0, e1,
+    hipExtLaunchKernelGGL(fused_apply_group_kernel, dim3(G.off[G.n]), dim3(mf ? g_mfma_threads : g_valu_threads), shm, st, e0, e1,
                           0, G);
     TTK_LAUNCH_CHECK();
     ttk::contract_count_ext(flops);
