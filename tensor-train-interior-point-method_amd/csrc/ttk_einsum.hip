@@ -564,13 +564,14 @@ __device__ void apply_row(const ApplyArgs &g, int a, double *sm, double *orow, i
   double *As = Pa + ns * nb;            // ns*ni*nj*nS  [i][S][s][j]
   double *T1 = As + ns * ni * nj * nS;  // ns*nj*nd     [s][j][d]
   double *T2 = T1 + ns * nj * nd;       // ni*nS*nd     [i][S][d]
-  double *Qs = T2 + ni * nS * nd;       // nc*nS*nd     [c][S][d]  (g.qlds)
+  double *Qs = T2 + ni * nS * nd;       // nc rows of (nS*nd | 1)  [c][S][d]  (g.qlds)
+  const int lq3 = (nS * nd) | 1;        // odd row stride: stage 3's lanes (one c each) on distinct banks
   if (g.qlds) {  // stage 3 reads every Q element once per row: one coalesced pass instead of a
                  // dependent FMA chain over global loads
     const int rq[3] = {nc, nS, nd};
     MixedIdx<3> iq(tid, nt, rq);
     for (int e = tid; e < nc * nS * nd; e += nt, iq.step(rq))
-      Qs[e] = g.Q[iq.v[0] * g.qs[0] + iq.v[1] * g.qs[1] + iq.v[2] * g.qs[2]];
+      Qs[iq.v[0] * lq3 + iq.v[1] * nd + iq.v[2]] = g.Q[iq.v[0] * g.qs[0] + iq.v[1] * g.qs[1] + iq.v[2] * g.qs[2]];
   }
   {  // staging: multi-digit indices advanced by carries (MixedIdx) instead of divisions
     const int rx[3] = {nb, nj, nd};
@@ -611,7 +612,7 @@ __device__ void apply_row(const ApplyArgs &g, int a, double *sm, double *orow, i
     const double *tr = T2 + i * nS * nd;
     double acc = 0.0;
     if (g.qlds) {
-      const double *qr = Qs + c * nS * nd;
+      const double *qr = Qs + c * lq3;
       for (int k = 0; k < nS * nd; ++k) acc = fma(qr[k], tr[k], acc);  // k = (S, d): the same order
     } else {
       for (int S = 0; S < nS; ++S) {
@@ -941,6 +942,9 @@ __global__ __launch_bounds__(1024) void fused_apply_multi_kernel(ApplyLaunch L) 
 
 constexpr int64_t APPLY_LDS_DOUBLES = 20000;
 
+// LDS doubles of a VALU row's staged Q (nc rows of odd stride, see apply_row)
+int64_t qlds_doubles(const ApplyArgs &g) { return (int64_t)g.nc * (((int64_t)g.nS * g.nd) | 1); }
+
 int64_t apply_lds(int nb, int nj, int nd, int nS, int ns, int ni) {
   return (int64_t)nb * nj * nd + (int64_t)ns * nb + (int64_t)ns * ni * nj * nS + (int64_t)ns * nj * nd +
          (int64_t)ni * nS * nd;
@@ -1094,8 +1098,8 @@ int fused_apply_try(void *stream, const char *eq, const int64_t *desc, double *o
   }
   int64_t need = g.mfma ? apply_mfma_lds(g) : apply_lds(g.nb, g.nj, g.nd, g.nS, g.ns, g.ni);
   if (batch_on()) return batch_add_fused(g, need) == TTK_OK ? 1 : -1;
-  if (!g.mfma && need + (int64_t)g.nc * g.nS * g.nd <= APPLY_LDS_DOUBLES) {
-    need += (int64_t)g.nc * g.nS * g.nd;
+  if (!g.mfma && need + qlds_doubles(g) <= APPLY_LDS_DOUBLES) {
+    need += qlds_doubles(g);
     g.qlds = 1;
   }
   const size_t shm = need * sizeof(double);
@@ -1344,7 +1348,7 @@ int ttk_schur_build(ttk_ctx ctx, int ineq, int64_t m, const int64_t *descs, cons
       int64_t w = 0;
       for (int k = 0; k < T.nterms; ++k) {
         const ApplyArgs &q = T.t[k];
-        const int64_t l = q.mfma ? apply_mfma_lds(q) : apply_lds(q.nb, q.nj, q.nd, q.nS, q.ns, q.ni) + (int64_t)q.nc * q.nS * q.nd;
+        const int64_t l = q.mfma ? apply_mfma_lds(q) : apply_lds(q.nb, q.nj, q.nd, q.nS, q.ns, q.ni) + qlds_doubles(q);
         w = l > w ? l : w;
       }
       const int64_t need = 2 * (int64_t)T.t[0].ni * T.t[0].nc + w;
@@ -1367,7 +1371,7 @@ int ttk_schur_build(ttk_ctx ctx, int ineq, int64_t m, const int64_t *descs, cons
         for (int k = 0; k < T.nterms; ++k) {
           const ApplyArgs &q = T.t[k];
           ok = ok && !q.mfma;
-          wk[k] = apply_lds(q.nb, q.nj, q.nd, q.nS, q.ns, q.ni) + (q.qlds ? (int64_t)q.nc * q.nS * q.nd : 0);
+          wk[k] = apply_lds(q.nb, q.nj, q.nd, q.nS, q.ns, q.ni) + (q.qlds ? qlds_doubles(q) : 0);
         }
         T.work1 = wk[0];
         const int64_t need = 2 * (int64_t)T.t[0].ni * T.t[0].nc + wk[0] + wk[1];
