@@ -969,7 +969,12 @@ static bool mfma_enabled() { return ttk::ctx().knob[TTK_KNOB_FUSED_MFMA] != 0; }
 static const int g_mfma_threads = getenv("TTK_MFMA_THREADS") ? atoi(getenv("TTK_MFMA_THREADS")) : 1024;
 // threads per workgroup of VALU apply rows (per term when a task's two terms run side by side):
 // every output element is one thread's sequential chain whatever the count, so results never change
-static const int g_valu_threads = getenv("TTK_VALU_THREADS") ? atoi(getenv("TTK_VALU_THREADS")) : 256;
+// (64..512 in steps of 64: a side-by-side launch doubles it and a workgroup holds at most 1024)
+static int valu_threads_env() {
+  const int t = getenv("TTK_VALU_THREADS") ? atoi(getenv("TTK_VALU_THREADS")) : 256;
+  return t < 64 ? 64 : (t > 512 ? 512 : t / 64 * 64);
+}
+static const int g_valu_threads = valu_threads_env();
 
 // workgroups per MFMA output row (ApplyArgs::csplit): enough that each workgroup's share of the
 // stage-3 (tile, K block) pairs is about one round over its waves, but no more workgroups in the
