@@ -367,7 +367,7 @@ def main():
     ap.add_argument("--problem", default=None, help="default: from the config file name")
     ap.add_argument("--rank", type=int, default=1, help="problem rank (create_problem rank)")
     ap.add_argument("--seeds", default=None, help="comma-separated seeds (default: the config's)")
-    ap.add_argument("--cpu-cap", type=float, default=20.0, help="seconds of oracle work per seed (0: full solves)")
+    ap.add_argument("--cpu-cap", type=float, default=60.0, help="seconds of oracle work per seed (0: full solves)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--no-solo", action="store_true", help="skip the one-solve-at-a-time latency pass")
