@@ -553,11 +553,29 @@ struct MixedIdx {
   }
 };
 
+// diagnostics builds: per-phase wall clock of the MFMA rows (-DTTK_MFMA_PROFILE) or of the VALU rows
+// (-DTTK_VALU_PROFILE), summed by each row's first thread (ttk_mfma_profile reads them)
+__device__ unsigned long long g_mph[8];
+#ifdef TTK_VALU_PROFILE
+#define TTK_VPH(K)                                      \
+  if (tid == 0) {                                       \
+    const unsigned long long t1_ = wall_clock64();      \
+    atomicAdd(&g_mph[K], t1_ - t_vh_);                  \
+    t_vh_ = t1_;                                        \
+  }
+#else
+#define TTK_VPH(K)
+#endif
+
 // tid / nt: this row's threads (the whole block, or one half of it when a task's two terms run side
 // by side, see fused_apply_multi_kernel); every output element is still one thread's sequential chain,
 // so the thread count never changes a result.  Three block barriers, unconditional.
 template <bool DIRECT>
 __device__ void apply_row(const ApplyArgs &g, int a, double *sm, double *orow, int tid, int nt) {
+#ifdef TTK_VALU_PROFILE
+  unsigned long long t_vh_ = wall_clock64();
+  if (tid == 0) atomicAdd(&g_mph[7], 1ull);
+#endif
   const int nb = g.nb, nj = g.nj, nd = g.nd, nS = g.nS, ns = g.ns, ni = g.ni, nc = g.nc;
   double *X = sm;                       // nb*nj*nd     [b][j][d]
   double *Pa = X + nb * nj * nd;        // ns*nb        [s][b]   (P[a, s, b])
@@ -590,6 +608,7 @@ __device__ void apply_row(const ApplyArgs &g, int a, double *sm, double *orow, i
       As[e] = g.A[ia.v[2] * g.as[0] + ia.v[0] * g.as[1] + ia.v[3] * g.as[2] + ia.v[1] * g.as[3]];
   }
   __syncthreads();
+  TTK_VPH(0)
   for (int e = tid; e < ns * nj * nd; e += nt) {  // t1[s][j][d] = sum_b P[a,s,b] x[b,j,d]
     const int s = e / (nj * nd), r = e - s * nj * nd;  // r = j*nd + d
     const double *pr = Pa + s * nb;
@@ -598,6 +617,7 @@ __device__ void apply_row(const ApplyArgs &g, int a, double *sm, double *orow, i
     T1[e] = acc;
   }
   __syncthreads();
+  TTK_VPH(1)
   const int sj = ns * nj;
   for (int e = tid; e < ni * nS * nd; e += nt) {  // t2[i][S][d] = sum_{s,j} A[s,i,j,S] t1[s][j][d]
     const int iS = e / nd, d = e - iS * nd;
@@ -607,6 +627,7 @@ __device__ void apply_row(const ApplyArgs &g, int a, double *sm, double *orow, i
     T2[e] = acc;
   }
   __syncthreads();
+  TTK_VPH(2)
   for (int e = tid; e < ni * nc; e += nt) {  // out[a][i][c] = sum_{S,d} Q[c,S,d] t2[i][S][d]
     const int i = e / nc, c = e - i * nc;
     const double *tr = T2 + i * nS * nd;
@@ -627,6 +648,7 @@ __device__ void apply_row(const ApplyArgs &g, int a, double *sm, double *orow, i
       orow[e] = acc;
     }
   }
+  TTK_VPH(3)
 }
 
 // ---- MFMA variant of one output row, for operator blocks beyond the VALU kernel's FLOP range
@@ -732,7 +754,7 @@ int64_t apply_mfma_lds(const ApplyArgs &g) {
 }
 
 // diagnostics build (-DTTK_MFMA_PROFILE): per-phase wall clock of the MFMA rows, summed by thread 0
-__device__ unsigned long long g_mph[8];
+// (g_mph is declared above apply_row, which uses it under -DTTK_VALU_PROFILE)
 #ifdef TTK_MFMA_PROFILE
 #define TTK_MPH(K)                                      \
   if (threadIdx.x == 0) {                               \
