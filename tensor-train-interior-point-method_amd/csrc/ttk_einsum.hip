@@ -553,32 +553,6 @@ struct MixedIdx {
   }
 };
 
-// Mixed-radix gather dst[dix(v)] = src[six(v)] for e = tid, tid + nt, ... < tot (v = the digits of e),
-// four loads in flight per thread: all issued before the first LDS store (pure data movement)
-template <int N, class SI, class DI>
-__device__ __forceinline__ void gather_mixed(const double *__restrict__ src, double *dst, int tot, int tid, int nt,
-                                             const int (&rad)[N], SI six, DI dix) {
-  constexpr int U = 4;
-  MixedIdx<N> ix(tid, nt, rad);
-  for (int e0 = tid; e0 < tot; e0 += U * nt) {
-    double v[U];
-    int d[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      v[u] = 0.0;
-      d[u] = 0;
-      if (e0 + u * nt < tot) {
-        v[u] = src[six(ix.v)];
-        d[u] = dix(ix.v);
-      }
-      ix.step(rad);
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-      if (e0 + u * nt < tot) dst[d[u]] = v[u];
-  }
-}
-
 // diagnostics builds: per-phase wall clock of the MFMA rows (-DTTK_MFMA_PROFILE) or of the VALU rows
 // (-DTTK_VALU_PROFILE), summed by each row's first thread (ttk_mfma_profile reads them)
 __device__ unsigned long long g_mph[8];
@@ -613,27 +587,25 @@ __device__ void apply_row(const ApplyArgs &g, int a, double *sm, double *orow, i
   if (g.qlds) {  // stage 3 reads every Q element once per row: one coalesced pass instead of a
                  // dependent FMA chain over global loads
     const int rq[3] = {nc, nS, nd};
-    gather_mixed(g.Q, Qs, nc * nS * nd, tid, nt, rq,
-                 [&](const int *v) { return v[0] * g.qs[0] + v[1] * g.qs[1] + v[2] * g.qs[2]; },
-                 [&](const int *v) { return v[0] * lq3 + v[1] * nd + v[2]; });
+    MixedIdx<3> iq(tid, nt, rq);
+    for (int e = tid; e < nc * nS * nd; e += nt, iq.step(rq))
+      Qs[iq.v[0] * lq3 + iq.v[1] * nd + iq.v[2]] = g.Q[iq.v[0] * g.qs[0] + iq.v[1] * g.qs[1] + iq.v[2] * g.qs[2]];
   }
   {  // staging: multi-digit indices advanced by carries (MixedIdx) instead of divisions
     const int rx[3] = {nb, nj, nd};
-    gather_mixed(g.x, X, nb * nj * nd, tid, nt, rx,
-                 [&](const int *v) { return v[0] * g.xs[0] + v[1] * g.xs[1] + v[2] * g.xs[2]; },
-                 [&](const int *v) { return (v[0] * nj + v[1]) * nd + v[2]; });
+    MixedIdx<3> ix(tid, nt, rx);
+    for (int e = tid; e < nb * nj * nd; e += nt, ix.step(rx))
+      X[e] = g.x[ix.v[0] * g.xs[0] + ix.v[1] * g.xs[1] + ix.v[2] * g.xs[2]];
   }
-  {
-    const int rp[2] = {ns, nb};
-    const double *Prow = g.P + (int64_t)a * g.ps[0];
-    gather_mixed(Prow, Pa, ns * nb, tid, nt, rp, [&](const int *v) { return v[0] * g.ps[1] + v[1] * g.ps[2]; },
-                 [&](const int *v) { return v[0] * nb + v[1]; });
+  for (int e = tid; e < ns * nb; e += nt) {
+    const int s = e / nb, b = e - s * nb;
+    Pa[e] = g.P[a * g.ps[0] + s * g.ps[1] + b * g.ps[2]];
   }
   {  // As[i][S][s][j] = A[s, i, j, S]
     const int ra[4] = {ni, nS, ns, nj};
-    gather_mixed(g.A, As, ns * ni * nj * nS, tid, nt, ra,
-                 [&](const int *v) { return v[2] * g.as[0] + v[0] * g.as[1] + v[3] * g.as[2] + v[1] * g.as[3]; },
-                 [&](const int *v) { return ((v[0] * nS + v[1]) * ns + v[2]) * nj + v[3]; });
+    MixedIdx<4> ia(tid, nt, ra);
+    for (int e = tid; e < ns * ni * nj * nS; e += nt, ia.step(ra))
+      As[e] = g.A[ia.v[2] * g.as[0] + ia.v[0] * g.as[1] + ia.v[3] * g.as[2] + ia.v[1] * g.as[3]];
   }
   __syncthreads();
   TTK_VPH(0)
