@@ -232,7 +232,7 @@ RUNS = [
     ("maxcut", "maxcut_12", 5, 2, True, 0),  # pathological in the reference (10 iterations, gap 4.7)
     ("maxcut", "maxcut_12", 6, 2, True, 0),  # pathological in the reference (29 iterations, gap 2.1e-2)
     ("maxcut", "maxcut_12", 7, 2, True, 0),
-    ("maxcut", "maxcut_12", 8, 2, True, 0),
+    ("maxcut", "maxcut_12", 8, 2, True, 0),  # pathological in the reference (29 iterations, gap 6.0e-3)
     ("maxcut", "maxcut_12", 9, 2, True, 0),
     ("maxcut", "maxcut_12", 10, 2, True, 0),
     ("maxcut", "maxcut_12", 11, 2, True, 0),
