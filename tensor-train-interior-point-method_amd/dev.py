@@ -40,6 +40,7 @@ class _PerThread(threading.local):
         self.fast = None  # _ttkbind bound to this thread's stream
         self.ones = {}    # small constant device tensors made on this thread's stream
         self.anti = {}
+        self.consts = {}  # tt_ops._const's constant cores
 
 
 _TL = _PerThread()

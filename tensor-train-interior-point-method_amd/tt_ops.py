@@ -22,7 +22,7 @@ from . import rng as _rng
 
 def _const(name, arr):
     """Small constant cores, uploaded once per host thread (on that thread's stream)."""
-    c = D._TL.__dict__.setdefault("consts", {})
+    c = D._TL.consts
     t = c.get(name)
     if t is None:
         t = D.from_numpy(arr)
