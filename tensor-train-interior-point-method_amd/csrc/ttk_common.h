@@ -58,7 +58,8 @@ __device__ __forceinline__ int dpp_mov_i(int v) {
 
 // (value, index) arg-max over the wave: the largest value, ties to the smallest index (the
 // LAPACK idamax winner whatever the reduction order, for non-NaN values); uniform result.  DPP
-// within each 16-lane row, then the four row winners by readlane -- no LDS round trips.
+// within each 16-lane row, then the four row winners by readlane -- no LDS round trips.  The whole
+// wave must be active (DPP and readlane read every lane).
 __device__ __forceinline__ void wave_argmax(double &v, int &i) {
   auto take = [&](double ov, int oi) {
     if (ov > v || (ov == v && oi < i)) {
