@@ -13,37 +13,35 @@
   and at N=1 the steps cycle through the config's seeds.  `replica`: every rank solves step i's
   N=1 seed.  Problems are created once per distinct seed on rank 0 and delivered by ONE broadcast
   (RCCL over xGMI with the nccl backend) before the timed region; no collective inside the IPM loop.
-* Solves in flight per GPU (`--inflight P`, default 4 at every N, so the 1/2/4/8-GPU series is
+* Solves in flight per GPU (`--inflight P`, default 2 at every N, so the 1/2/4/8-GPU series is
   like-for-like): a solve is a chain of small dependent launches that leaves most of the chip idle,
-  so each GPU runs P seeds at once.  They run as slot threads (`--threads T`, default 2 per process:
-  each thread its own HIP stream, libttk context and NumPy random stream; the launches release the
-  GIL) in P/T processes per GPU -- this process plus P/T-1 workers spawned before the GPU is touched
-  -- so a node runs at most 16 solve processes (8 GPUs x 2).  All slots warm up, then are released
-  together at the start of the timed region.  A step is P solves per GPU: step i, rank p, slot j
-  solves seeds[(i*N*P + p*P + j) mod S].
-* `solo_median_seed_s_per_iter`: after the timed region (rank 0, N=1) every distinct timed seed is
-  solved once more ALONE on the GPU -- SURVEY.md §8(d)'s per-seed latency as the reference runner
-  measures it (one solve at a time, `src/utils.py:300-302`); the CPU per-seed comparison uses it.
+  so each GPU runs P seeds at once, one process per solve on its default stream -- this process plus
+  P-1 workers spawned before the GPU is touched (an 8-GPU node runs 16 solve processes).  All slots
+  warm up, then are released together at the start of the timed region.  A step is P solves per GPU:
+  step i, rank p, slot j solves seeds[(i*N*P + p*P + j) mod S].
 * Timed region: barrier + device sync on both sides of the K steps, max over ranks.
   `value` = (max-over-ranks wall) / (IPM iterations of all ranks): whole-job s per IPM-iteration.
-  `median_seed_s_per_iter` is SURVEY.md §8(d)'s statistic: the median over the distinct seeds of
-  each seed's (solve time / iterations).  Seeds the reference runner would call pathological
-  (feas or gap > 1e-3, `src/utils.py:67`) are flagged in `per_seed`.
+* `sec_per_iter_per_seed_median`: SURVEY.md §8(d)'s statistic as the reference runner measures it
+  (`src/utils.py:298-302`: one solve at a time, solve wall / its IPM iterations, median over seeds):
+  after the timed region (rank 0, N=1) every distinct timed seed is solved once more ALONE on the
+  GPU.  `sec_per_iter_per_seed_median_inflight` is the same statistic over the timed (contended)
+  solves.
 * `roofline` (contraction kernels: the MFMA GEMM `gemm_offs*`, the fused local apply and the Schur
   multi-task apply): an untimed re-solve of rank 0's step-0 seed with every contraction launch
   bracketed by HIP events on its stream.  achieved = ALGORITHMIC contraction FLOPs of that solve
   (NumPy `einsum_path` greedy convention per einsum call plus the chained applies of every local
   KKT operator application; `dev.ALGO`) / summed contraction kernel time; peak =
-  78.6 TFLOP/s fp64 matrix.  `device_flops` is what the launched kernels executed.
+  78.6 TFLOP/s fp64 matrix.
 * `cpu_baseline` (rank 0, N=1 only): the oracle CPU restatement of the reference path (`oracle/`,
-  a port) on this host: one single-thread process per core of the host share (16), the timed seeds
-  cycled over them, all concurrently, each bounded to the IPM iterations finished within
-  `--cpu-cap` seconds.  `value` = median over seeds of the per-seed s/IPM-iter (the statistic of
-  SURVEY.md §8(d)); the GPU's per-seed figure over the SAME seeds and iterations (from the timed
-  solves' per-iteration timestamps) sits beside it (`gpu_over_cpu`); `throughput` is the concurrent
-  run's whole-job s/IPM-iter, the counterpart of this line's `value`.  Then one seed again with all
-  the host share's cores as BLAS threads.  The workers are started before this process touches the
-  GPU and wait on a pipe until the GPU work is done.
+  a port) on this host: one single-thread process per distinct timed seed, all at once, each its
+  seed's WHOLE solve (`--cpu-cap` is only a safety bound).  `value` = median over seeds of solve
+  wall / IPM iterations; beside it the GPU's one-at-a-time figure for the same seeds, as a ratio of
+  medians and as the median of per-seed ratios.  Then one seed with all the host share's cores as
+  BLAS threads (bounded to 60 s).  The workers start before this process touches the GPU and wait
+  on a pipe until the GPU work is done.
+* Output: ONE JSON line on stdout (< 4 KB: the contract's keys and the summary statistics); the
+  per-seed results, the per-step schedule, the solo solves, the CPU per-seed rows and the per-op
+  FLOP split go to `--detail` (default gpurun_out/bench_detail.json).
 """
 import argparse
 import contextlib
@@ -264,14 +262,14 @@ def _spawn_gpu_workers(args, proc_slots):
     return procs
 
 
-def _spawn_cpu_workers(args, seeds, threads):
+def _spawn_cpu_workers(args, seeds, threads, cap):
     """Started BEFORE the GPU is initialised (no exec from a GPU process); each blocks on stdin."""
     procs = []
     for s, th in zip(seeds, threads):
         env = dict(os.environ, OPENBLAS_NUM_THREADS=str(th), OMP_NUM_THREADS=str(th), MKL_NUM_THREADS=str(th),
                    CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
         cmd = [sys.executable, os.path.abspath(__file__), "--cpu-worker", str(s), "--problem", args.problem,
-               "--config", args.config, "--rank", str(args.rank), "--cpu-cap", str(args.cpu_cap)]
+               "--config", args.config, "--rank", str(args.rank), "--cpu-cap", str(cap)]
         procs.append(subprocess.Popen(cmd, stdin=subprocess.PIPE, stdout=subprocess.PIPE,
                                       stderr=subprocess.DEVNULL, env=env, text=True))
     _CHILDREN.extend(procs)
@@ -327,15 +325,17 @@ def _pmc_traffic():
 
 
 DEFAULT_THREADS = 1  # solves in flight per process (slot threads; >1: one created HIP stream each)
+DEFAULT_INFLIGHT = 2  # solves in flight per GPU, the same at every N (like-for-like 1->8 series)
 
 
 def default_inflight(world):
-    """Solves in flight per GPU: 4 (one process each, on its default stream) up to 4 GPUs, 2 on 8 GPUs
-    (a node runs at most 16 solve processes).  Round-2 process sweep on one MI355X (maxcut_10 whole
-    job): 1 -> 0.39, 2 -> 0.20, 4 -> 0.106, 6 -> 0.112 s/IPM-iter: 4 in flight is the knee.  Slot
-    threads sharing a process would keep 4 per GPU at N=8, but they need created streams, and
-    solves on created streams slow each other down (profiles/r03_inflight_layouts.txt)."""
-    return max(1, min(4, DEFAULT_THREADS * (16 // world)))
+    """Solves in flight per GPU: DEFAULT_INFLIGHT (one process each, on its default stream) at every
+    N up to 8, so the 1/2/4/8-GPU series carries the same per-GPU load (an 8-GPU node then runs 16
+    solve processes, the process guard's limit).  Round-2/3 sweeps on one MI355X (maxcut_10 whole
+    job, 1 -> 0.39, 2 -> 0.20, 4 -> 0.106 s/IPM-iter) put the knee at 4, which an 8-GPU node cannot
+    hold with one process per solve; slot threads would, but they need created streams, and solves
+    on created streams slow each other down (profiles/r03_inflight_layouts.txt)."""
+    return max(1, min(DEFAULT_INFLIGHT, DEFAULT_THREADS * (16 // max(world, 1))))
 
 
 def make_schedule(config, cfg_name, seeds_arg, steps, world, rank, P, mode):
@@ -358,6 +358,103 @@ def make_schedule(config, cfg_name, seeds_arg, steps, world, rank, P, mode):
     return seeds, sched, slot_seeds
 
 
+def _median(xs):
+    xs = [x for x in xs if x is not None]
+    return float(np.median(xs)) if xs else None
+
+
+def cpu_summary(per, allc, gpu_runs, cap, workload, cores_avail):
+    """cpu_baseline from the oracle workers' lines (`_cpu_worker`) and the GPU's per-seed solves.
+    Per seed, both sides are WHOLE-solve s/IPM-iter (solve wall / its iterations, the reference
+    runner's statistic, src/utils.py:298-302); a CPU process stopped by the safety cap contributes
+    its finished-iteration prefix instead and the seed is flagged."""
+    gpu = {}
+    for r in gpu_runs:
+        gpu.setdefault(r["seed"], []).append(r["runtime"] / max(r["num_iters"], 1))
+    rows = []
+    for c in per:
+        if c is None or c["iters"] <= 0:
+            continue
+        full = "full_solve_s_per_iter" in c
+        cs = c["full_solve_s_per_iter"] if full else c["s_per_iter"]
+        gs = _median(gpu.get(c["seed"], []))
+        rows.append({"seed": c["seed"], "cpu_iters": c.get("full_solve_iters", c["iters"]), "cpu_full_solve": full,
+                     "cpu_s_per_iter": cs, "gpu_s_per_iter": gs,
+                     "gpu_over_cpu": gs / cs if gs is not None and cs else None})
+    cmed = _median([r["cpu_s_per_iter"] for r in rows])
+    gmed = _median([r["gpu_s_per_iter"] for r in rows])
+    done = [c for c in per if c is not None]
+    cpu_iters = sum(c.get("full_solve_iters", c["iters"]) for c in done)
+    cpu_wall = max((c["work_s"] for c in done), default=0.0)
+    return {"value": cmed, "unit": "s/IPM-iter", "cores": 1, "kind": "port",
+            "sample": f"oracle/ CPU restatement of the reference path, {workload}: one single-thread process per "
+                      f"timed seed, all at once, each its seed's whole tt_ipm solve (safety cap {cap:g} s); "
+                      f"value = median over seeds of solve wall / IPM iterations",
+            "seeds_full_solve": sum(r["cpu_full_solve"] for r in rows), "seeds": len(rows),
+            "gpu_same_seeds_median": gmed,
+            "gpu_over_cpu_ratio_of_medians": (gmed / cmed) if cmed and gmed else None,
+            "gpu_over_cpu_median_of_ratios": _median([r["gpu_over_cpu"] for r in rows]),
+            "throughput_s_per_iter": cpu_wall / cpu_iters if cpu_iters else None,
+            "all_cores": None if allc is None else {
+                "seed": allc["seed"], "threads": int(allc["threads"]), "iters": allc["iters"],
+                "cpu_s_per_iter": allc["s_per_iter"]},
+            "host": {"nproc": os.cpu_count(), "used_cores": len(done), "affinity": cores_avail, "model": _cpu_model()},
+            "per_seed": rows}
+
+
+LINE_MAX = 4000  # the driver keeps a ~14.8 KB tail of stdout; the line stays far below it
+
+
+def compose_line(problem, config, cfg_name, rank_tt, world, P, T, n_procs, steps, warmup, schedule, elapsed, iters,
+                 seeds, sched, all_results, solo, roofline, cpu, detail_path):
+    """(the ONE stdout JSON line, the detail dict for the side file).  The line holds the contract's
+    keys plus the summary statistics and stays below LINE_MAX bytes at any N; everything per seed /
+    per step / per op goes to the detail file."""
+    per_seed, by_seed = [], {}
+    for r in all_results:
+        per_seed.append({k: r[k] for k in ("seed", "num_iters", "runtime", "sec_per_iter", "gap", "feas",
+                                           "dual_feas")})
+        per_seed[-1]["pathological"] = bool(r["feas"] > 1e-3 or r["gap"] > 1e-3)  # src/utils.py:67
+        acc = by_seed.setdefault(r["seed"], [0.0, 0])
+        acc[0] += r["runtime"]
+        acc[1] += r["num_iters"]
+    inflight_med = _median([t / max(n, 1) for t, n in by_seed.values()])
+    solo_med = None if not solo else _median([r["runtime"] / max(r["num_iters"], 1) for r in solo])
+    value = elapsed / max(iters, 1)
+    rl = None
+    if roofline is not None:
+        rl = {k: v for k, v in roofline.items() if k != "algorithmic_by_op"}
+    cb = None
+    if cpu is not None:
+        cb = {k: v for k, v in cpu.items() if k != "per_seed"}
+    knobs = {k: v for k, v in sorted(os.environ.items()) if k.startswith(("TTK_", "TTIPM_"))}
+    line = {"metric": METRIC, "value": value, "unit": "s/IPM-iter", "n_gpus": world,
+            "steps": steps, "warmup": warmup, "ms_per_step": elapsed * 1e3 / max(steps, 1),
+            "higher_is_better": False, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic: the reference's generators (seeded MT19937 graph TT), problems broadcast from rank 0",
+            "config": {"workload": f"{problem} dim={config['dim']} rank={rank_tt} ({cfg_name}), {P} concurrent "
+                                   f"tt_ipm solves per GPU per step ({n_procs} processes x {T} slot threads)",
+                       "inflight_per_gpu": P, "seeds": seeds,
+                       "parallelism": f"seed-parallel x{world} GPUs x{P} in flight ({schedule})",
+                       "solves": len(all_results), "total_ipm_iters": iters},
+            # SURVEY.md section 8(d)'s statistic: each seed alone on the GPU, median over seeds
+            "sec_per_iter_per_seed_median": solo_med,
+            "sec_per_iter_per_seed_median_inflight": inflight_med,
+            "roofline": rl, "cpu_baseline": cb,
+            "mfma_util_pct": None if rl is None else 100.0 * rl["frac"],
+            "pathological_seeds": sorted({p["seed"] for p in per_seed if p["pathological"]}),
+            "env_knobs": knobs, "detail": detail_path or None}
+    if len(json.dumps(line)) > LINE_MAX:  # never let the line outgrow the driver's tail
+        line["env_knobs"] = {"n": len(knobs), "see": "detail"}
+    detail = {"line": line, "per_seed": per_seed, "seeds_per_step": sched,
+              "solo_per_seed": None if not solo else
+              [{k: r[k] for k in ("seed", "num_iters", "runtime", "sec_per_iter", "gap", "feas", "dual_feas")}
+               for r in solo],
+              "roofline_algorithmic_by_op": None if roofline is None else roofline.get("algorithmic_by_op"),
+              "cpu_per_seed": None if cpu is None else cpu["per_seed"], "env_knobs": knobs}
+    return line, detail
+
+
 def main():
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
     ap.add_argument("--gpus", type=int, default=1)
@@ -367,7 +464,11 @@ def main():
     ap.add_argument("--problem", default=None, help="default: from the config file name")
     ap.add_argument("--rank", type=int, default=1, help="problem rank (create_problem rank)")
     ap.add_argument("--seeds", default=None, help="comma-separated seeds (default: the config's)")
-    ap.add_argument("--cpu-cap", type=float, default=60.0, help="seconds of oracle work per seed (0: full solves)")
+    ap.add_argument("--cpu-cap", type=float, default=300.0,
+                    help="safety bound on seconds of oracle work per seed (0: none); the default covers every "
+                         "maxcut_10 seed's whole solve on the GPU box's host")
+    ap.add_argument("--detail", default=os.path.join("gpurun_out", "bench_detail.json"),
+                    help="side file for the per-seed / per-step / per-op detail ('' to skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--no-solo", action="store_true", help="skip the one-solve-at-a-time latency pass")
@@ -415,9 +516,11 @@ def main():
     if do_cpu:  # before any GPU call
         # the host share's cores, one single-thread oracle process each, the timed seeds cycled: the
         # per-seed latency AND the CPU's whole-job throughput come from the same concurrent run
-        cyc = [cpu_seeds[i % len(cpu_seeds)] for i in range(max(cores, len(cpu_seeds)))]
-        cpu_procs = _spawn_cpu_workers(args, cyc, [1] * len(cyc))
-        allcore_proc = _spawn_cpu_workers(args, cpu_seeds[:1], [cores])
+        # one single-thread oracle process per distinct timed seed, whole solves (the reference
+        # runner's statistic, src/utils.py:298-302), plus one seed on all the share's cores as BLAS
+        # threads (bounded: a side figure)
+        cpu_procs = _spawn_cpu_workers(args, cpu_seeds, [1] * len(cpu_seeds), args.cpu_cap)
+        allcore_proc = _spawn_cpu_workers(args, cpu_seeds[:1], [cores], min(args.cpu_cap or 60.0, 60.0))
 
     import torch
     import torch.distributed as dist
@@ -430,7 +533,6 @@ def main():
     from ttipm_amd import dev as D
     from ttipm_amd import shard
     from ttipm_amd._lib import lib
-    from ttipm_amd.utils import is_pathological
     from ttipm_amd.utils import solve as _solve
 
     def solve(prep, trace=None):
@@ -544,91 +646,21 @@ def main():
         with contextlib.redirect_stdout(sys.stderr):
             per = _release(cpu_procs)
             allc = _release(allcore_proc)[0]
-        gpu_runs, cpu_runs = {}, {}
-        for r in (solo or results):  # the GPU's one-at-a-time latency when measured
-            gpu_runs.setdefault(r["seed"], []).append(r["assembly_t"])
-        for c in per:
-            if c is not None and c["iters"] > 0:
-                cpu_runs.setdefault(c["seed"], []).append(c["assembly_t"])
-        rows = []
-        for sd in cpu_runs:  # per seed: the common prefix of IPM iterations of all its runs
-            if sd not in gpu_runs:
-                continue
-            k = min(len(t) - 1 for t in cpu_runs[sd] + gpu_runs[sd])
-            if k <= 0:
-                continue
-            ck = float(np.median([(t[k] - t[0]) / k for t in cpu_runs[sd]]))
-            gk = float(np.median([(t[k] - t[0]) / k for t in gpu_runs[sd]]))
-            rows.append({"seed": sd, "iters": k, "cpu_runs": len(cpu_runs[sd]), "gpu_runs": len(gpu_runs[sd]),
-                         "cpu_s_per_iter": ck, "gpu_s_per_iter": gk, "gpu_over_cpu": gk / ck})
-        med = float(np.median([r["cpu_s_per_iter"] for r in rows])) if rows else None
-        gmed = float(np.median([r["gpu_s_per_iter"] for r in rows])) if rows else None
-        done = [c for c in per if c is not None]
-        cpu_iters = sum(c["iters"] for c in done)
-        cpu_wall = max((c["work_s"] for c in done), default=0.0)
-        cpu = {"value": med, "unit": "s/IPM-iter", "cores": 1, "kind": "port",
-               "sample": f"oracle/ CPU restatement of the reference path on {args.problem} dim={config['dim']} "
-                         f"rank={args.rank}: {len(done)} single-thread processes at once (the host share's cores), "
-                         f"the timed seeds {sorted(cpu_runs)} cycled over them; each process runs its seed's first "
-                         f"IPM iterations up to {args.cpu_cap:g} s of work; value = median over seeds of each "
-                         f"seed's s/IPM-iter (median over its processes), over the iterations the CPU and GPU "
-                         f"runs of that seed have in common; the GPU side is "
-                         + ("the one-solve-at-a-time pass (each seed alone on the GPU)" if solo else
-                            "the timed in-flight solves"),
-               "per_seed": rows,
-               "gpu_same_sample_median": gmed,
-               "gpu_over_cpu": (gmed / med) if med and gmed else None,
-               "gpu_over_cpu_median": float(np.median([r["gpu_over_cpu"] for r in rows])) if rows else None,
-               "throughput": {"s_per_iter": cpu_wall / cpu_iters if cpu_iters else None, "processes": len(done),
-                              "threads_each": 1, "ipm_iters": cpu_iters, "wall_s": cpu_wall,
-                              "note": "whole-job s/IPM-iter of the concurrent CPU run: longest process's work time "
-                                      "/ IPM iterations of all processes (the GPU's `value` formula)"},
-               "all_cores": None if allc is None else {
-                   "seed": allc["seed"], "threads": int(allc["threads"]), "iters": allc["iters"],
-                   "cpu_s_per_iter": allc["s_per_iter"]},
-               "host": {"nproc": os.cpu_count(), "affinity": len(os.sched_getaffinity(0)), "model": _cpu_model()}}
+        gpu_side = solo or results  # the GPU's one-at-a-time latency when measured
+        cpu = cpu_summary(per, allc, gpu_side, args.cpu_cap,
+                          f"{args.problem} dim={config['dim']} rank={args.rank}", cores_avail=cores)
 
     if rank == 0:
-        per_seed, by_seed = [], {}
-        for r in all_results:
-            per_seed.append({k: r[k] for k in ("seed", "num_iters", "runtime", "sec_per_iter", "gap", "feas",
-                                               "dual_feas")})
-            per_seed[-1]["pathological"] = bool(is_pathological(r))
-            acc = by_seed.setdefault(r["seed"], [0.0, 0])
-            acc[0] += r["runtime"]
-            acc[1] += r["num_iters"]
-        med = float(np.median([t / max(n, 1) for t, n in by_seed.values()]))
-        out = {"metric": METRIC, "value": elapsed / max(iters, 1), "unit": "s/IPM-iter", "n_gpus": world,
-               "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed * 1e3 / args.steps,
-               "higher_is_better": False, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
-               "data": "synthetic: the reference's generators (seeded MT19937 graph TT), problems broadcast "
-                       "from rank 0",
-               "config": {"workload": f"{args.problem} dim={config['dim']} rank={args.rank} "
-                                      f"({os.path.basename(args.config)}), {P} concurrent tt_ipm solves per GPU "
-                                      f"per step ({len(proc_slots)} processes x {T} slot threads)",
-                          "inflight_per_gpu": P,
-                          "seeds": seeds, "seeds_per_step": sched,
-                          "parallelism": f"seed-parallel x{world} GPUs x{P} in flight ({args.schedule})",
-                          "total_ipm_iters": iters},
-               "median_seed_s_per_iter": med,
-               "solo_median_seed_s_per_iter": None if not solo else
-               float(np.median([r["runtime"] / max(r["num_iters"], 1) for r in solo])),
-               "solo_per_seed": None if not solo else
-               [{k: r[k] for k in ("seed", "num_iters", "runtime", "sec_per_iter", "gap")} for r in solo],
-               "threads_per_process": T,
-               "pathological_seeds": sorted({p["seed"] for p in per_seed if p["pathological"]}),
-               # library / path knobs set for this run (several change summation order, hence results at
-               # rounding level)
-               "env_knobs": {k: v for k, v in sorted(os.environ.items()) if k.startswith(("TTK_", "TTIPM_"))},
-               "roofline": roofline, "cpu_baseline": cpu,
-               "mfma_util_pct": None if roofline is None else 100.0 * roofline["frac"],
-               # like-for-like ratios: per-seed latency (the same statistic on both sides) and whole-job
-               # throughput (this line's value against the concurrent CPU run's)
-               "gpu_over_cpu_per_seed_median": None if cpu is None else cpu["gpu_over_cpu"],
-               "gpu_over_cpu_throughput": None if cpu is None or not cpu["throughput"]["s_per_iter"] else
-               (elapsed / max(iters, 1)) / cpu["throughput"]["s_per_iter"],
-               "per_seed": per_seed}
-        print(json.dumps(out), flush=True)
+        line, detail = compose_line(
+            problem=args.problem, config=config, cfg_name=os.path.basename(args.config), rank_tt=args.rank,
+            world=world, P=P, T=T, n_procs=len(proc_slots), steps=args.steps, warmup=args.warmup,
+            schedule=args.schedule, elapsed=elapsed, iters=iters, seeds=seeds, sched=sched,
+            all_results=all_results, solo=solo, roofline=roofline, cpu=cpu, detail_path=args.detail)
+        if args.detail:
+            os.makedirs(os.path.dirname(os.path.abspath(args.detail)), exist_ok=True)
+            with open(args.detail, "w") as f:
+                json.dump(detail, f, indent=1)
+        print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

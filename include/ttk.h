@@ -60,10 +60,13 @@ void *ttk_ctx_stream(ttk_ctx ctx);
  * a call uses; they live in the context so that flipping one for one context never changes the
  * results of another.  ctx NULL: the calling thread's current context (bound or default).
  *   FUSED_APPLY     1: local applies opted in by the caller run on the one-launch fused kernel
+ *                      (default from env TTK_FUSED_APPLY, else 1)
  *   FUSED_MFMA      1: fused applies beyond the VALU kernel's FLOP range run the MFMA stages
  *                      (default from env TTK_FUSED_MFMA, else 1); 0: the pairwise plan
  *   SPLITK          1: deterministic split-K for GEMM steps whose tile grid cannot fill the chip
- *   SPLITK_MINK     K per split (default from env TTK_SPLITK_MINK, else 128)
+ *                      (default from env TTK_SPLITK, else 1)
+ *   SPLITK_MINK     K per split, > 0 (default from env TTK_SPLITK_MINK, else 128; ttk_ctx_set_knob
+ *                   rejects values <= 0 with TTK_ERR_ARG)
  *   LGMRES_MW_MIN   (it+1)*n at or above which the LGMRES Arnoldi / build / augmentation steps
  *                   run as multi-workgroup kernels (default from env TTK_LGMRES_MW_MIN, else
  *                   16384; 0 everywhere, INT_MAX never)
@@ -72,6 +75,10 @@ void *ttk_ctx_stream(ttk_ctx ctx);
  *   APPLY_DUAL      1: a Schur-handle task's two VALU terms run side by side, one half of a
  *                   512-thread workgroup each (bit-identical; read at ttk_schur_build; default from
  *                   env TTK_APPLY_DUAL, else 1)
+ *   RCOND_EXACT     1: ttk_lu_sync / ttk_dense_schur_solve always run dgecon's estimator, so
+ *                   rcond_out is dgecon's value; 0 (default from env TTK_RCOND_EXACT, else 0): a
+ *                   certified lower bound may be returned instead when it settles the rcond < eps
+ *                   test (the status is identical either way; see ttk_lu_sync)
  * ttk_ctx_set_knob stores value and returns the previous one in *old (may be NULL). */
 enum ttk_knob {
   TTK_KNOB_FUSED_APPLY = 0,
@@ -81,7 +88,8 @@ enum ttk_knob {
   TTK_KNOB_LGMRES_MW_MIN = 4,
   TTK_KNOB_MFMA_CSPLIT = 5,
   TTK_KNOB_APPLY_DUAL = 6,
-  TTK_KNOB_COUNT = 7
+  TTK_KNOB_RCOND_EXACT = 7,
+  TTK_KNOB_COUNT = 8
 };
 int ttk_ctx_set_knob(ttk_ctx ctx, int knob, int value, int *old);
 int ttk_ctx_get_knob(ttk_ctx ctx, int knob, int *value);
@@ -299,9 +307,10 @@ int ttk_trsm_lower(void *stream, const double *L, int n, double *B, int nrhs, in
  * (`scipy.linalg.solve(assume_a='gen')` / `lu_factor`, `src/tt_ipm.py:215,320,323`)
  * rcond_out is dgecon's estimate, except when one comparison-matrix sweep already certifies that
  * estimate to be >= 1e-13 (1 / (||A||_1 max(M(L)^-T M(U)^-T e)) <= dgecon's value): then that
- * certified lower bound is returned and the estimator is skipped.  The LinAlgWarning test of the
- * callers (rcond < eps) decides identically either way; the same holds for the rcond of
- * ttk_dense_schur_solve. */
+ * certified lower bound is returned and the estimator is skipped -- the value is then ONLY valid
+ * for the LinAlgWarning test of the callers (rcond < eps), which decides identically either way.
+ * The same holds for the rcond of ttk_dense_schur_solve.  Callers that log or compare the value
+ * set the context knob TTK_KNOB_RCOND_EXACT = 1 (or env TTK_RCOND_EXACT=1): dgecon's estimate always. */
 int ttk_lu_sync(void *stream, double *A, int n, int *piv, double *work, double *rcond_out);
 /* solve with LU factors, B(n,nrhs) in place (getrs) */
 int ttk_lu_solve(void *stream, const double *LU, int n, const int *piv, double *B, int nrhs, int ldb);
@@ -438,7 +447,8 @@ int ttk_zipup(ttk_ctx ctx, int kind, int d, const double *const *a, const int64_
  * XAX_k1[key] (R, S, R), all contiguous but A.  rhs (r, 3, n, R) and inv_I (r, n, R) contiguous.
  * Status: TTK_OK; TTK_ERR_NOT_PD (Cholesky failed: scipy LinAlgError), TTK_ERR_SINGULAR (exact
  * zero pivot), TTK_ILL_CONDITIONED (rcond < eps/2: LinAlgWarning) -- the reference then falls back
- * to its iterative solve (src/tt_ipm.py:224-229).  Same launches as the Python path: bit-identical. */
+ * to its iterative solve (src/tt_ipm.py:224-229).  Same launches as the Python path: bit-identical.
+ * rcond_out: as for ttk_lu_sync (a certified lower bound unless TTK_KNOB_RCOND_EXACT is set). */
 typedef struct {
   const double *L, *A, *R;
   int64_t s, S, a_strides[4];

@@ -690,7 +690,7 @@ namespace {
 static inline bool splitk_on() { return ttk::ctx().knob[TTK_KNOB_SPLITK] != 0; }
 static inline int splitk_mink() {
   const int k = ttk::ctx().knob[TTK_KNOB_SPLITK_MINK];
-  return k > 0 ? k : 256;
+  return k > 0 ? k : 128;  // the documented default (ttk_ctx_set_knob rejects <= 0)
 }
 
 double *splitk_scratch(int64_t n) {  // partial-sum slabs of the current context (grown, never shrunk)

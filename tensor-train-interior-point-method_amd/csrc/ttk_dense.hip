@@ -590,7 +590,7 @@ constexpr double RCOND_CERT = 1e-13;
 // dgecon (1-norm) from the factors: colsum = column sums of |A| before factorisation
 __global__ __launch_bounds__(1024) void lu_rcond_kernel(const double *__restrict__ LU, int n, const int *gpiv,
                                                         const double *__restrict__ colsum, const int *status,
-                                                        double *rcond_out, int use_perm) {
+                                                        double *rcond_out, int use_perm, int exact) {
   extern __shared__ double xl[];
   double *x = xl, *xs = xl + n, *tmp = use_perm ? xl + 2 * n : nullptr;
   int *piv = reinterpret_cast<int *>(xl + (use_perm ? 3 : 2) * n), *perm = use_perm ? piv + n : nullptr;
@@ -642,7 +642,7 @@ __global__ __launch_bounds__(1024) void lu_rcond_kernel(const double *__restrict
     double mx = 0.0;
     for (int i = 0; i < nt; ++i) mx = fmax(mx, rv[i]);
     const double lb = (s_anorm > 0.0 && mx > 0.0 && mx < INFINITY) ? (1.0 / s_anorm) / mx : 0.0;
-    s_est = lb >= RCOND_CERT ? lb : 0.0;
+    s_est = (!exact && lb >= RCOND_CERT) ? lb : 0.0;
   }
   __syncthreads();
   if (s_est > 0.0) {
@@ -777,7 +777,9 @@ int lu_rcond_launch(hipStream_t st, const double *LU, int n, const int *piv, con
   if (shm > 65536)
     (void)hipFuncSetAttribute(reinterpret_cast<const void *>(lu_rcond_kernel),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
-  hipLaunchKernelGGL(lu_rcond_kernel, dim3(1), dim3(1024), shm, st, LU, n, piv, colsum, status, rcond, use_perm);
+  const int exact = ttk::ctx().knob[TTK_KNOB_RCOND_EXACT] != 0;
+  hipLaunchKernelGGL(lu_rcond_kernel, dim3(1), dim3(1024), shm, st, LU, n, piv, colsum, status, rcond, use_perm,
+                     exact);
   TTK_LAUNCH_CHECK();
   return TTK_OK;
 }

@@ -50,9 +50,11 @@ struct Ctx {
   // numerics knobs (ttk_ctx_set_knob; several change summation order, so they are per context:
   // flipping one on a context never changes another context's results).  Defaults from the
   // environment at context creation.
-  int knob[TTK_KNOB_COUNT] = {1, env_int("TTK_FUSED_MFMA", 1) != 0 ? 1 : 0, 1, env_int("TTK_SPLITK_MINK", 128),
+  int knob[TTK_KNOB_COUNT] = {env_int("TTK_FUSED_APPLY", 1) != 0 ? 1 : 0, env_int("TTK_FUSED_MFMA", 1) != 0 ? 1 : 0,
+                              env_int("TTK_SPLITK", 1) != 0 ? 1 : 0,
+                              env_int("TTK_SPLITK_MINK", 128) > 0 ? env_int("TTK_SPLITK_MINK", 128) : 128,
                               env_int("TTK_LGMRES_MW_MIN", 16384), env_int("TTK_MFMA_CSPLIT", 1) != 0 ? 1 : 0,
-                              env_int("TTK_APPLY_DUAL", 1) != 0 ? 1 : 0};
+                              env_int("TTK_APPLY_DUAL", 1) != 0 ? 1 : 0, env_int("TTK_RCOND_EXACT", 0) != 0 ? 1 : 0};
 };
 Ctx &ctx();
 Ctx *ctx_swap(Ctx *c);  // bind c to the calling thread, return the previous binding

@@ -190,6 +190,10 @@ int ttk_ctx_set_knob(ttk_ctx h, int knob, int value, int *old) {
     ttk::set_error("ttk_ctx_set_knob: unknown knob %d", knob);
     return TTK_ERR_ARG;
   }
+  if (knob == TTK_KNOB_SPLITK_MINK && value <= 0) {
+    ttk::set_error("ttk_ctx_set_knob: SPLITK_MINK must be > 0 (got %d)", value);
+    return TTK_ERR_ARG;
+  }
   ttk::Ctx &c = h ? h->c : ttk::ctx();
   if (old) *old = c.knob[knob];
   c.knob[knob] = value;

@@ -56,9 +56,53 @@ def test_replica_schedule():
     assert sched == [[41, 41], [23, 23], [235, 235]]
 
 
-def test_default_inflight_caps_processes_per_node():
-    """4 solves in flight per GPU up to 4 GPUs, and a node never runs more than 16 solve processes
-    (DEFAULT_THREADS slot threads per process)."""
-    assert [bench.default_inflight(w) for w in (1, 2, 4, 8)] == [4, 4, 4, 2]
+def test_default_inflight_is_constant_across_gpus():
+    """The same solves in flight per GPU at N = 1, 2, 4, 8 (a like-for-like 1->8 series), and a node
+    never runs more than 16 solve processes (DEFAULT_THREADS slot threads per process)."""
+    ps = [bench.default_inflight(w) for w in (1, 2, 4, 8)]
+    assert len(set(ps)) == 1 and ps[0] >= 1
     T = bench.DEFAULT_THREADS
     assert all(w * -(-bench.default_inflight(w) // T) <= 16 for w in (1, 2, 4, 8, 16))
+
+
+def _fake_results(sched, rank_count):
+    import random
+    rnd = random.Random(0)
+    out = []
+    for st in sched:
+        for s in st:
+            n = rnd.randint(10, 30)
+            out.append({"seed": s, "num_iters": n, "runtime": 1.2345678901234 * n, "sec_per_iter": 1.2345678901234,
+                        "gap": 4.123456789e-4, "feas": 2.123456789e-7, "dual_feas": 7.123456789e-10,
+                        "assembly_t": [0.1 * i for i in range(n + 1)]})
+    return out
+
+
+def test_bench_line_fits_the_driver_tail():
+    """The ONE stdout JSON line stays below 4 KB for an 8-GPU maxcut_12 r=2 schedule (configs[4]) with
+    the driver's 20 steps; per-seed / per-step / per-op detail goes to the side file instead."""
+    cfg = _cfg("maxcut_12.yaml")
+    P = bench.default_inflight(8)
+    seeds, sched, _ = bench.make_schedule(cfg, "maxcut_12.yaml", None, 20, 8, 0, P, "shard")
+    results = _fake_results(sched, 8)
+    solo = results[:len(seeds)]
+    roof = {"bound": "mfma", "achieved": 0.00342, "peak": 78.6, "unit": "TFLOP/s", "frac": 4.3e-5,
+            "traffic": 16874.75, "kernel": "contraction kernels", "seed": 80,
+            "algorithmic_flops_per_solve": 1.19e9, "launches_per_solve": 55421,
+            "algorithmic_by_op": {f"op{i}": [i, 1e6 * i] for i in range(10)}}
+    per = [{"seed": s, "iters": 12, "s_per_iter": 3.3, "work_s": 40.0, "full_solve_iters": 12,
+            "full_solve_s_per_iter": 3.4, "assembly_t": [float(i) for i in range(13)], "threads": "1"} for s in seeds]
+    cpu = bench.cpu_summary(per, per[0], solo, 300.0, "maxcut dim=12 rank=2", 16)
+    line, detail = bench.compose_line("maxcut", cfg, "maxcut_12.yaml", 2, 8, P, 1, P, 20, 5, "shard", 123.4,
+                                      sum(r["num_iters"] for r in results), seeds, sched, results, solo, roof, cpu,
+                                      "gpurun_out/bench_detail.json")
+    s = json.dumps(line)
+    assert len(s) < 4096, len(s)
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline", "sec_per_iter_per_seed_median"):
+        assert k in line
+    assert "algorithmic_by_op" not in line["roofline"] and "per_seed" not in line["cpu_baseline"]
+    assert {"bound", "achieved", "peak", "unit", "frac", "traffic"} <= set(line["roofline"])
+    assert {"value", "unit", "cores", "kind", "sample"} <= set(line["cpu_baseline"])
+    assert len(detail["per_seed"]) == len(results) and detail["seeds_per_step"] == sched
+    assert line["cpu_baseline"]["gpu_over_cpu_median_of_ratios"] is not None

@@ -8,10 +8,10 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import yaml  # noqa: E402
 
 from ttipm_amd.utils import run_and_record  # noqa: E402
-from ttipm_amd._lib import lib  # noqa: E402
-
+# TTIPM_FUSED=0 -> TTK_FUSED_APPLY=0: the library reads it when each context is created (a knob set
+# here, before this thread's context exists, would land on the default context only)
 if os.environ.get("TTIPM_FUSED") == "0":
-    lib.ttk_einsum_set_fused(0)
+    os.environ["TTK_FUSED_APPLY"] = "0"
 
 prob, cfg_name, seed, rank = sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4])
 key = sys.argv[5] if len(sys.argv) > 5 else f"{cfg_name}_r{rank}_s{seed}"
