@@ -79,6 +79,10 @@ void *ttk_ctx_stream(ttk_ctx ctx);
  *                   rcond_out is dgecon's value; 0 (default from env TTK_RCOND_EXACT, else 0): a
  *                   certified lower bound may be returned instead when it settles the rcond < eps
  *                   test (the status is identical either way; see ttk_lu_sync)
+ *   SCHUR_ONE       1: a fused Schur matvec (ttk_schur_apply) is ONE launch: the o1 = B21 x - B22 w
+ *                   rows compute B21 x while the w = inv_I o B01^T y rows run, then take w over an
+ *                   in-launch hand-off; 0: two launches (bit-identical either way; default from env
+ *                   TTK_SCHUR_ONE, else 1)
  * ttk_ctx_set_knob stores value and returns the previous one in *old (may be NULL). */
 enum ttk_knob {
   TTK_KNOB_FUSED_APPLY = 0,
@@ -89,7 +93,8 @@ enum ttk_knob {
   TTK_KNOB_MFMA_CSPLIT = 5,
   TTK_KNOB_APPLY_DUAL = 6,
   TTK_KNOB_RCOND_EXACT = 7,
-  TTK_KNOB_COUNT = 8
+  TTK_KNOB_SCHUR_ONE = 8,
+  TTK_KNOB_COUNT = 9
 };
 int ttk_ctx_set_knob(ttk_ctx ctx, int knob, int value, int *old);
 int ttk_ctx_get_knob(ttk_ctx ctx, int knob, int *value);
@@ -145,6 +150,9 @@ int ttk_fused_set_mfma(int on);
 /* diagnostics: per-phase wall-clock sums (100 MHz ticks) of the MFMA rows in a -DTTK_MFMA_PROFILE
  * build: [staging, stage 1, stage 2, stage 3, epilogue, -, -, rows]; zeros otherwise */
 int ttk_mfma_profile(unsigned long long *out8, int reset);
+/* number of in-launch hand-off waits (one-launch Schur matvec, TTK_KNOB_SCHUR_ONE) that gave up
+ * after their spin bound instead of hanging -- 0 unless something is broken; reset: zero it */
+int ttk_dep_timeouts(unsigned *out, int reset);
 
 int ttk_einsum_batch_begin(void *stream);
 int ttk_einsum_batch_flush(void *stream);

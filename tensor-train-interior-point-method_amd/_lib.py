@@ -85,6 +85,7 @@ _SIGS = {
     "ttk_dense_schur_solve_ineq": (i32, [vp, i64, i64, i64, vp, vp, vp, vp]),
     "ttk_fused_set_mfma": (i32, [i32]),
     "ttk_mfma_profile": (i32, [vp, i32]),
+    "ttk_dep_timeouts": (i32, [vp, i32]),
     "ttk_einsum_set_fused": (i32, [i32]),
     "ttk_qr_set_big_threshold": (i32, [i32]),
     "ttk_contract_timing": (i32, [i32]),
@@ -118,7 +119,7 @@ EXPORTED = tuple(_SIGS)
 TTK_OK, TTK_ERR_ARG, TTK_ERR_HIP, TTK_ERR_NOT_PD, TTK_ERR_SINGULAR, TTK_ERR_NOT_CONVERGED = range(6)
 # per-context numerics knobs (include/ttk.h enum ttk_knob)
 (KNOB_FUSED_APPLY, KNOB_FUSED_MFMA, KNOB_SPLITK, KNOB_SPLITK_MINK, KNOB_LGMRES_MW_MIN, KNOB_MFMA_CSPLIT, KNOB_APPLY_DUAL,
- KNOB_RCOND_EXACT) = range(8)
+ KNOB_RCOND_EXACT, KNOB_SCHUR_ONE) = range(9)
 
 
 class TTKError(RuntimeError):

@@ -518,6 +518,10 @@ struct ApplyArgs {
   // (tile, K block) pairs spread over csplit CUs; every output element is still computed by the same
   // MFMA sequence and summed in the same order (bit-identical for any csplit)
   int csplit = 1;
+  // in-launch hand-off (one-launch Schur matvec): x is produced by another task of the SAME launch;
+  // every wave of this row waits until *dep >= dep_target, then loads x with sc1 loads
+  const unsigned *dep = nullptr;
+  unsigned dep_target = 0;
 };
 
 // Association follows the greedy pairwise plan the reference's opt_einsum picks for these shapes
@@ -567,6 +571,43 @@ __device__ unsigned long long g_mph[8];
 #define TTK_VPH(K)
 #endif
 
+// ---- in-launch hand-off of a task's output to another task's input (MI355X_MICROARCH.md, inter-
+// workgroup visibility, first row of the measured hand-off table): the producer stores every
+// handed-off word with an sc1 (write-through) store, every storing wave drains with
+// s_waitcnt vmcnt(0), a workgroup barrier, then ONE lane adds 1 to an agent-scope counter; each
+// consumer WAVE polls that counter with an sc1 load until it reaches the launch's target and only
+// then loads the words, each with an sc1 load.  The counter is monotonic per context (no reset):
+// the host passes target = arrivals of every launch so far.  Producers sit at the lowest block
+// indices and never wait, so the grid drains whatever the residency; a spin past DEP_SPIN_MAX
+// polls gives up (g_dep_timeout is set; ttk_dep_timeouts reads it) instead of hanging.
+__device__ unsigned g_dep_timeout;
+constexpr long DEP_SPIN_MAX = 20000000;
+
+__device__ __forceinline__ double ld_sc1(const double *p) {
+  return __hip_atomic_load((const __attribute__((address_space(1))) double *)(p), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1(double *p, double v) {
+  __hip_atomic_store((__attribute__((address_space(1))) double *)(p), v, __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+// every wave for itself (lane 0 polls; the wave's other lanes are masked off meanwhile)
+__device__ __forceinline__ void dep_wait(const unsigned *dep, unsigned target) {
+  if ((threadIdx.x & 63) == 0) {
+    const __attribute__((address_space(1))) unsigned *d =
+        (const __attribute__((address_space(1))) unsigned *)(dep);
+    long n = 0;
+    while ((int)(__hip_atomic_load(d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) < 0) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++n > DEP_SPIN_MAX) {
+        __hip_atomic_fetch_add(&g_dep_timeout, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+}
+
 // tid / nt: this row's threads (the whole block, or one half of it when a task's two terms run side
 // by side, see fused_apply_multi_kernel); every output element is still one thread's sequential chain,
 // so the thread count never changes a result.  Three block barriers, unconditional.
@@ -577,6 +618,7 @@ __device__ void apply_row(const ApplyArgs &g, int a, double *sm, double *orow, i
   if (tid == 0) atomicAdd(&g_mph[7], 1ull);
 #endif
   const int nb = g.nb, nj = g.nj, nd = g.nd, nS = g.nS, ns = g.ns, ni = g.ni, nc = g.nc;
+  if (g.dep) dep_wait(g.dep, g.dep_target);
   double *X = sm;                       // nb*nj*nd     [b][j][d]
   double *Pa = X + nb * nj * nd;        // ns*nb        [s][b]   (P[a, s, b])
   double *As = Pa + ns * nb;            // ns*ni*nj*nS  [i][S][s][j]
@@ -594,8 +636,12 @@ __device__ void apply_row(const ApplyArgs &g, int a, double *sm, double *orow, i
   {  // staging: multi-digit indices advanced by carries (MixedIdx) instead of divisions
     const int rx[3] = {nb, nj, nd};
     MixedIdx<3> ix(tid, nt, rx);
-    for (int e = tid; e < nb * nj * nd; e += nt, ix.step(rx))
-      X[e] = g.x[ix.v[0] * g.xs[0] + ix.v[1] * g.xs[1] + ix.v[2] * g.xs[2]];
+    if (g.dep)  // handed off inside this launch: sc1 loads (separate loop: no per-element branch)
+      for (int e = tid; e < nb * nj * nd; e += nt, ix.step(rx))
+        X[e] = ld_sc1(g.x + ix.v[0] * g.xs[0] + ix.v[1] * g.xs[1] + ix.v[2] * g.xs[2]);
+    else
+      for (int e = tid; e < nb * nj * nd; e += nt, ix.step(rx))
+        X[e] = g.x[ix.v[0] * g.xs[0] + ix.v[1] * g.xs[1] + ix.v[2] * g.xs[2]];
   }
   for (int e = tid; e < ns * nb; e += nt) {
     const int s = e / nb, b = e - s * nb;
@@ -778,6 +824,7 @@ __device__ void apply_row_mfma(const ApplyArgs &g, int a, double *sm, double *or
   const int tid = threadIdx.x, nt = blockDim.x;
   const int nb = g.nb, nj = g.nj, nd = g.nd, nS = g.nS, ns = g.ns, ni = g.ni, nc = g.nc;
   const int jd = nj * nd, sj = ns * nj;
+  if (g.dep) dep_wait(g.dep, g.dep_target);
   double *X = sm;                       // [b][j][d]
   double *Pa = X + nb * jd;             // [s][b]
   double *As = Pa + ns * nb;            // [(i,S)][(s,j)]
@@ -787,8 +834,12 @@ __device__ void apply_row_mfma(const ApplyArgs &g, int a, double *sm, double *or
   {  // staging: the gathers' multi-digit indices advance by carries instead of divisions
     const int rx[3] = {nb, nj, nd};
     MixedIdx<3> ix(tid, nt, rx);
-    for (int e = tid; e < nb * jd; e += nt, ix.step(rx))
-      X[e] = g.x[ix.v[0] * g.xs[0] + ix.v[1] * g.xs[1] + ix.v[2] * g.xs[2]];
+    if (g.dep)  // handed off inside this launch: sc1 loads
+      for (int e = tid; e < nb * jd; e += nt, ix.step(rx))
+        X[e] = ld_sc1(g.x + ix.v[0] * g.xs[0] + ix.v[1] * g.xs[1] + ix.v[2] * g.xs[2]);
+    else
+      for (int e = tid; e < nb * jd; e += nt, ix.step(rx))
+        X[e] = g.x[ix.v[0] * g.xs[0] + ix.v[1] * g.xs[1] + ix.v[2] * g.xs[2]];
   }
   for (int e = tid; e < ns * nb; e += nt) {
     const int s_ = e / nb, b = e - s_ * nb;
@@ -902,10 +953,14 @@ struct ApplyTask {
   int64_t work1;  // side-by-side terms: LDS offset (doubles, after the two rows) of term 1's stages
 };
 struct ApplyLaunch {
-  ApplyTask task[3];
+  ApplyTask task[4];
   int ntask;
-  int off[4];
+  int off[5];
   int dual;  // two-term VALU tasks run their terms side by side, one half of the block each
+  // in-launch hand-off: task `prod` publishes its output (sc1 stores + one arrival per workgroup on
+  // *dep); -1: none
+  int prod = -1;
+  unsigned *dep = nullptr;
 };
 
 __global__ __launch_bounds__(1024) void fused_apply_multi_kernel(ApplyLaunch L) {
@@ -951,6 +1006,7 @@ __global__ __launch_bounds__(1024) void fused_apply_multi_kernel(ApplyLaunch L) 
     }
     __syncthreads();
   }
+  const bool pub = t == L.prod;
   for (int e = tid; e < ni * nc; e += nt) {
     const int i = e / nc, c = e - i * nc;
     if (!mine(c, h, cs)) continue;
@@ -958,7 +1014,13 @@ __global__ __launch_bounds__(1024) void fused_apply_multi_kernel(ApplyLaunch L) 
     double v = orow[e];
     if (T.oscale) v = (1.0 * v) * T.oscale[oi];
     if (T.addv) v = 1.0 * T.addv[oi] + 1.0 * v;
-    g0.out[oi] = v;
+    if (pub) st_sc1(g0.out + oi, v);
+    else g0.out[oi] = v;
+  }
+  if (pub) {  // every storing wave drained, then one arrival for the workgroup
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) __hip_atomic_fetch_add(L.dep, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -1015,6 +1077,15 @@ static int choose_csplit(const ApplyArgs &g, int64_t rows_total) {
   const int64_t cap = rows_total > 0 ? 256 / rows_total : 1;
   if (cs > cap) cs = (int)cap;
   return cs < 1 ? 1 : cs;
+}
+
+extern "C" int ttk_dep_timeouts(unsigned *out, int reset) {  // in-launch hand-off waits that gave up
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dep_timeout), sizeof(unsigned)) != hipSuccess) return TTK_ERR_HIP;
+  if (reset) {
+    const unsigned z = 0;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_dep_timeout), &z, sizeof(z)) != hipSuccess) return TTK_ERR_HIP;
+  }
+  return TTK_OK;
 }
 
 extern "C" int ttk_mfma_profile(unsigned long long *out8, int reset) {  // g_mph (zeros unless profiled)
@@ -1158,6 +1229,13 @@ namespace {
 
 struct SchurOp {
   ApplyLaunch st[2];
+  // the one-launch form (knob SCHUR_ONE): st[0]'s w task first (the producer), st[0]'s other tasks,
+  // then st[1]'s o1 task whose B22 w term takes w over the in-launch hand-off; built once
+  bool one_ok = false;
+  ApplyLaunch one;
+  int one_src[4][2];  // per task of `one`: (stage, task index) it was copied from
+  size_t one_shm = 0;
+  bool one_mfma = false;
   int xseg[2][3][2];  // input segment of each term: 0 y, 1 x, 2 t, 3 w
   int oseg[2][3];     // output segment of each task: 0, 1, 2, 3 = w
   size_t shm[2];
@@ -1413,6 +1491,34 @@ int ttk_schur_build(ttk_ctx ctx, int ineq, int64_t m, const int64_t *descs, cons
       }
     }
   }
+  {  // one-launch form: producer (w) first, then the rest of stage 1, then the consumer (o1)
+    ApplyLaunch &O = op.one;
+    O = ApplyLaunch{};
+    int order[4][2] = {{0, 1}, {0, 0}, {0, 2}, {1, 0}};
+    int nt_ = 0;
+    for (int q = 0; q < 4; ++q) {
+      const int s_ = order[q][0], t_ = order[q][1];
+      if (t_ >= op.st[s_].ntask) continue;
+      O.task[nt_] = op.st[s_].task[t_];
+      op.one_src[nt_][0] = s_;
+      op.one_src[nt_][1] = t_;
+      ++nt_;
+    }
+    O.ntask = nt_;
+    O.off[0] = 0;
+    for (int t = 0; t < nt_; ++t) {
+      const int s_ = op.one_src[t][0], t_ = op.one_src[t][1];
+      O.off[t + 1] = O.off[t] + (op.st[s_].off[t_ + 1] - op.st[s_].off[t_]);
+    }
+    O.prod = 0;
+    // side by side only when both stages ran that way (the thread count never changes a result)
+    O.dual = op.st[0].dual && op.st[1].dual;
+    op.one_shm = op.shm[0] > op.shm[1] ? op.shm[0] : op.shm[1];
+    op.one_mfma = false;
+    for (int t = 0; t < nt_; ++t)
+      for (int k = 0; k < O.task[t].nterms; ++k) op.one_mfma = op.one_mfma || O.task[t].t[k].mfma;
+    op.one_ok = nt_ >= 2 && O.off[nt_] <= 1024;  // producers are a small share of a small grid
+  }
   return schur_store(op, m, handle);
 }
 
@@ -1427,9 +1533,45 @@ int ttk::schur_apply(void *stream, int64_t handle, const double *v, double *out)
   SchurOp &op = ops[handle - 1];
   if (op.pairwise) return schur_apply_pairwise(stream, op, v, out);
   const int64_t m = op.m;
-  double *w = ttk::ctx().schur_w;
+  ttk::Ctx &cx = ttk::ctx();
+  double *w = cx.schur_w;
   const double *in[4] = {v, v + m, v + 2 * m, w};
   double *o[4] = {out, out + m, out + 2 * m, w};
+  if (op.one_ok && cx.knob[TTK_KNOB_SCHUR_ONE]) {
+    if (!cx.dep) {
+      TTK_HIP(hipMalloc(reinterpret_cast<void **>(&cx.dep), 256));
+      TTK_HIP(hipMemsetAsync(cx.dep, 0, 256, TTK_STREAM(stream)));
+      cx.dep_total = 0;
+    }
+    ApplyLaunch L = op.one;
+    const int nprod = L.off[1] - L.off[0];
+    cx.dep_total += (unsigned)nprod;
+    L.dep = cx.dep;
+    for (int t = 0; t < L.ntask; ++t) {
+      const int s = op.one_src[t][0], tt = op.one_src[t][1];
+      for (int k = 0; k < L.task[t].nterms; ++k) {
+        const int xs = op.xseg[s][tt][k];
+        L.task[t].t[k].x = in[xs];
+        L.task[t].t[k].out = o[op.oseg[s][tt]];
+        if (xs == 3) {  // w: produced by task 0 of this launch
+          L.task[t].t[k].dep = cx.dep;
+          L.task[t].t[k].dep_target = cx.dep_total;
+        }
+      }
+      if (s == 0 && tt == 1 && op.ineq) L.task[t].addv = v + 2 * m;  // w = inv_I o B01^T y + t
+    }
+    if (op.one_shm > 65536)
+      (void)hipFuncSetAttribute(reinterpret_cast<const void *>(fused_apply_multi_kernel),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)op.one_shm);
+    hipEvent_t e0, e1;
+    if (ttk::contract_events_ext(&e0, &e1) != TTK_OK) return TTK_ERR_HIP;
+    hipExtLaunchKernelGGL(fused_apply_multi_kernel, dim3(L.off[L.ntask]),
+                          dim3(op.one_mfma ? g_mfma_threads : (L.dual ? 2 * g_valu_threads : g_valu_threads)),
+                          op.one_shm, TTK_STREAM(stream), e0, e1, 0, L);
+    TTK_LAUNCH_CHECK();
+    ttk::contract_count_ext(op.flops);
+    return TTK_OK;
+  }
   for (int s = 0; s < 2; ++s) {
     ApplyLaunch L = op.st[s];
     for (int t = 0; t < L.ntask; ++t) {

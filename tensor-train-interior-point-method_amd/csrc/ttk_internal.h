@@ -37,6 +37,8 @@ struct Ctx {
   void *schur = nullptr;      // Schur operator handle table (ttk_einsum.hip)
   double *schur_w = nullptr;
   int64_t schur_wcap = 0;
+  unsigned *dep = nullptr;    // in-launch hand-off arrival counter (monotonic; ttk_einsum.hip)
+  unsigned dep_total = 0;     // arrivals of every hand-off launch issued on this context so far
   double *lgmres = nullptr;   // LGMRES partial sums
   int64_t lgmres_n = 0;
   int *status = nullptr;      // dense factorisation status words
@@ -54,7 +56,8 @@ struct Ctx {
                               env_int("TTK_SPLITK", 1) != 0 ? 1 : 0,
                               env_int("TTK_SPLITK_MINK", 128) > 0 ? env_int("TTK_SPLITK_MINK", 128) : 128,
                               env_int("TTK_LGMRES_MW_MIN", 16384), env_int("TTK_MFMA_CSPLIT", 1) != 0 ? 1 : 0,
-                              env_int("TTK_APPLY_DUAL", 1) != 0 ? 1 : 0, env_int("TTK_RCOND_EXACT", 0) != 0 ? 1 : 0};
+                              env_int("TTK_APPLY_DUAL", 1) != 0 ? 1 : 0, env_int("TTK_RCOND_EXACT", 0) != 0 ? 1 : 0,
+                              env_int("TTK_SCHUR_ONE", 1) != 0 ? 1 : 0};
 };
 Ctx &ctx();
 Ctx *ctx_swap(Ctx *c);  // bind c to the calling thread, return the previous binding

@@ -13,37 +13,40 @@ def is_pathological(r):
     return r["feas"] > 1e-3 or r["gap"] > 1e-3
 
 
-# Whole-solve parity policy, anchored on the reference's OWN runs.  Every full-solve golden (the
-# reference as shipped: 1 BLAS thread, PYTHONHASHSEED=0) has twins -- the SAME reference code re-run
-# under rounding-level variations of its own computation (tests/golden/make_golden.py):
+# Whole-solve parity policy, anchored on the reference's OWN, UNMODIFIED runs.  Every full-solve golden
+# (the reference as shipped: 1 BLAS thread, PYTHONHASHSEED=0) has twins -- the SAME shipped code
+# re-run under rounding-level variations of its own computation (tests/golden/make_golden.py):
 #   _t8        8 BLAS threads;
 #   _h1.._h3   other PYTHONHASHSEEDs: opt_einsum orders each contraction's tensordot axes by
-#              frozenset iteration, so the hash seed picks among equally valid summation orders;
-#   _j0.._j7   its scipy.linalg.svd calls on LAPACK's one-sided Jacobi SVD (dgejsv, high relative
-#              accuracy -- the algorithm class of the device SVD) with hash seeds 0..7;
-#   _p0.._p3   its LGMRES (the PETSc restatement, PETSc itself is absent) with PETSc's Seq reduction
-#              kernels (dnrm2 norms, index-order VecMDot, grouped VecMAXPY), hash seeds 0..3 -- the
-#              real PETSc's rounding is unknown here, so these spreads count as the reference's noise.
-# The AMEn rank decisions and the step-size eigen-ALS make the reference's trajectory branch under
-# such variations (maxcut_10 s14: the reference with Jacobi SVDs and hash seed 4 reproduces the
-# device's assembly-5 departure to 2e-8; s23: with Jacobi SVDs the reference follows the device to
-# 1e-12 where its shipped run departs by 8e-6; s235: every hash twin leaves the golden at assembly 4).
-# So the device must reproduce ONE of the reference's own runs:
+#              frozenset iteration, so the hash seed picks among equally valid summation orders.
+# Only these (golden, _t8, _h*) define the reference's noise and are candidates to follow.  Two more
+# families are DIAGNOSTICS only (reported, never used to pass a key), because they change the code:
+#   _j0.._j7   its scipy.linalg.svd calls on LAPACK's one-sided Jacobi SVD (dgejsv -- the algorithm
+#              class of the device SVD) with hash seeds 0..7;
+#   _p0.._p3   its LGMRES restatement (PETSc is absent) with PETSc's Seq reduction kernels.
+# The rule:
 # * noise n_i at Newton-system assembly i = the largest relative difference over (mu, primal, dual,
-#   centrality) between the golden and its thread / hash twins (the shipped code's own rounding
-#   noise), cumulated over assemblies 0..i;
-# * there must be a reference run R (the golden or any twin) that the device follows at every
-#   assembly i before the shipped code's noise branches (n_i > 1e-3): rel(device_i, R_i) <=
-#   max(1e-12, 50 n_i);
-# * if nothing branches (n_i <= 1e-3 to the end and every twin takes the golden's iteration count):
-#   the same iteration count and ranks as R, final gap / feasibilities within max(1e-5, 50 x the
-#   twins' final spread) of R's; otherwise a non-pathological end point (src/utils.py:67) within 2
-#   iterations of the twins' range.
+#   centrality) between the golden and its _t8 / _h* twins, cumulated over assemblies 0..i;
+# * the device must follow one unmodified run R at every assembly i before that noise branches
+#   (n_i > 1e-3): rel(device_i, R_i) <= max(1e-12, 50 n_i);
+# * path-stable keys (n_i <= 1e-3 to the end and every unmodified twin takes the golden's iteration
+#   count): R's iteration count and ranks, final gap / feasibilities within max(1e-5, 50 x the
+#   twins' final spread) of R's;
+# * otherwise (the reference's own runs branch) the end point must lie in the unmodified runs'
+#   ENVELOPE widened 2x: iterations in [lo - w/2, hi + w/2] (w = hi - lo), gap and feas in
+#   [min, max] doubled in log space around its centre ([min sqrt(min/max), max sqrt(max/min)]) and
+#   never narrower than [min / 1.01, max * 1.01] -- the end-point resolution: the final feasibilities
+#   are squared residuals whose leading digits the last rounded update sets (maxcut_10 s35's five
+#   unmodified runs agree in gap to 1e-5 but spread 0.3 % in feas) -- and non-pathological
+#   (src/utils.py:67).
 KEYS4 = ("mu", "primal_error", "dual_error", "centrality_error")
 FINAL_KEYS = ("gap", "feas", "dual_feas")
+ENVELOPE_KEYS = ("gap", "feas")
 FACTOR, FLOOR, FINAL_FLOOR, BRANCH = 50.0, 1e-12, 1e-5, 1e-3
-NOISE_TWINS = ("_t8", "_h1", "_h2", "_h3", "_p0", "_p1", "_p2", "_p3")
-ALL_TWINS = NOISE_TWINS + tuple(f"_j{h}" for h in range(8))
+ENV_FLOOR = 1e-2
+NOISE_TWINS = ("_t8", "_h1", "_h2", "_h3")
+DIAGNOSTIC_TWINS = tuple(f"_p{h}" for h in range(4)) + tuple(f"_j{h}" for h in range(8))
+ALL_TWINS = NOISE_TWINS + DIAGNOSTIC_TWINS
 TWIN_SUFFIXES = ALL_TWINS
 
 
@@ -61,7 +64,7 @@ def _per(trace, ref):
 
 def reference_noise(key):
     """(cumulative noise per assembly, number of assemblies checked, path_stable) of the golden's
-    thread / hash twins"""
+    unmodified (thread / hash) twins"""
     g, tw = RUNS[key], _twins(key, NOISE_TWINS)
     n = len(g["trace"])
     noise = [0.0] * n
@@ -75,12 +78,24 @@ def reference_noise(key):
     return cum, checked, stable
 
 
-def check_against_reference_runs(key, trace, r):
-    """the policy above; returns (name of the reference run the device follows, its per-assembly
-    differences, the noise bound)"""
+def envelope(key):
+    """the unmodified runs' end points widened 2x: {'num_iters': (lo, hi), 'gap': (lo, hi), 'feas': ...}"""
+    runs = [RUNS[key]] + _twins(key, NOISE_TWINS)
+    out = {}
+    its = [x["num_iters"] for x in runs]
+    w = max(its) - min(its)
+    out["num_iters"] = (min(its) - w / 2.0, max(its) + w / 2.0)
+    for k in ENVELOPE_KEYS:
+        v = [abs(x[k]) for x in runs]
+        a, b = min(v), max(v)
+        f = max(np.sqrt(b / a), 1.0 + ENV_FLOOR) if a > 0 else np.inf
+        out[k] = (a / f if a > 0 else 0.0, b * f)
+    return out
+
+
+def _follow(key, trace, names, cum, checked):
     g = RUNS[key]
-    cum, checked, stable = reference_noise(key)
-    runs = [("golden", g)] + [(x, RUNS[key + x]) for x in ALL_TWINS if key + x in RUNS]
+    runs = [("golden", g)] + [(x, RUNS[key + x]) for x in names if key + x in RUNS]
     best, best_per, worst_ratio = None, None, np.inf
     for name, R in runs:
         per = _per(trace, R)
@@ -88,11 +103,32 @@ def check_against_reference_runs(key, trace, r):
         ratio = max([per[i] / max(FLOOR, FACTOR * cum[i]) for i in range(m)] or [0.0])
         if ratio < worst_ratio:
             best, best_per, worst_ratio = (name, R), per, ratio
-    assert worst_ratio <= 1.0, (f"no reference run followed within 50x the reference noise: best {best[0]} "
-                                f"{['%.0e' % v for v in best_per]} noise {['%.0e' % v for v in cum]}")
+    return best, best_per, worst_ratio
+
+
+def diagnose(key, trace, r):
+    """the policy's verdict as data (never raises): which unmodified run the device follows and how
+    closely, the envelope check, and the closest DIAGNOSTIC twin (_j / _p) for the record"""
+    cum, checked, stable = reference_noise(key)
+    (name, R), per, ratio = _follow(key, trace, NOISE_TWINS, cum, checked)
+    (dname, _), _, dratio = _follow(key, trace, DIAGNOSTIC_TWINS, cum, checked)
+    env = envelope(key)
+    inside = {k: bool(env[k][0] <= (r[k] if k == "num_iters" else abs(r[k])) <= env[k][1])
+              for k in ("num_iters",) + ENVELOPE_KEYS}
+    return {"follows": name, "follow_ratio": ratio, "per": per, "noise": cum, "checked": checked,
+            "path_stable": stable, "envelope": env, "inside": inside, "diagnostic_follows": dname,
+            "diagnostic_ratio": dratio}
+
+
+def check_against_reference_runs(key, trace, r):
+    """the policy above; returns (name of the unmodified reference run the device follows, its
+    per-assembly differences, the noise bound)"""
+    cum, checked, stable = reference_noise(key)
+    best, best_per, worst_ratio = _follow(key, trace, NOISE_TWINS, cum, checked)
+    assert worst_ratio <= 1.0, (f"no unmodified reference run followed within 50x the reference noise: best "
+                                f"{best[0]} {['%.0e' % v for v in best_per]} noise {['%.0e' % v for v in cum]}")
     name, R = best
-    allruns = [g] + _twins(key)
-    lo, hi = min(x["num_iters"] for x in allruns), max(x["num_iters"] for x in allruns)
+    g = RUNS[key]
     if stable:
         fin = {k: max([_rel(t[k], g[k]) for t in _twins(key, NOISE_TWINS)] or [0.0]) for k in FINAL_KEYS}
         assert r["num_iters"] == R["num_iters"]
@@ -101,7 +137,8 @@ def check_against_reference_runs(key, trace, r):
             assert _rel(r[k], R[k]) <= max(FINAL_FLOOR, FACTOR * fin[k]), (k, r[k], R[k], fin[k])
     else:
         assert not is_pathological(r), r
-        assert lo - 2 <= r["num_iters"] <= hi + 2, (r["num_iters"], lo, hi)
+        env = envelope(key)
+        assert env["num_iters"][0] <= r["num_iters"] <= env["num_iters"][1], ("num_iters", r["num_iters"], env)
+        for k in ENVELOPE_KEYS:
+            assert env[k][0] <= abs(r[k]) <= env[k][1], (k, r[k], env[k])
     return name, best_per, cum
-
-

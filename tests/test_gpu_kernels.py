@@ -697,3 +697,51 @@ def test_schur_terms_side_by_side_bit_identical(dev, ineq, dims):
         finally:
             _set_dual(old)
     assert np.array_equal(outs[0], outs[1])
+
+
+def _set_knob(knob, on):
+    import ctypes
+    from ttipm_amd import _lib
+    old = ctypes.c_int(0)
+    assert _lib.lib.ttk_ctx_set_knob(None, knob, int(on), ctypes.byref(old)) == 0
+    return old.value
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ineq", [False, True])
+@pytest.mark.parametrize("dims", [(12, 16, 10, 9, 4), (3, 4, 5, 5, 4), (16, 20, 12, 12, 4), (8, 5, 4, 4, 4),
+                                  (14, 96, 10, 9, 4)])
+def test_schur_one_launch_bit_identical(dev, ineq, dims):
+    """the Schur-reduced operator as ONE launch (TTK_KNOB_SCHUR_ONE, the default: the o1 rows take w
+    from the w rows of the same launch over an sc1 hand-off) gives the two-launch matvec bit for bit,
+    over many applies in a row (the arrival counter is monotonic across launches), on VALU rows
+    (side by side or not) and MFMA rows, and no hand-off wait ever gives up"""
+    import ctypes
+    from ttipm_amd import _lib, tt_ipm
+    rng = np.random.default_rng(13)
+    r, R, s, S, n = dims
+    cls = tt_ipm.IneqMatVecWrapper if ineq else tt_ipm.MatVecWrapper
+    L = {k: dev.from_numpy(rng.standard_normal((r, s, r)) * 0.1) for k in cls.keys}
+    Am = {k: dev.from_numpy(rng.standard_normal((s, n, n, S)) * 0.1) for k in cls.keys}
+    Rr = {k: dev.from_numpy(rng.standard_normal((R, S, R)) * 0.1) for k in cls.keys}
+    invI = dev.from_numpy(rng.uniform(0.5, 2.0, (r, n, R)))
+    nb = 3 if ineq else 2
+    vs = [dev.from_numpy(rng.standard_normal(nb * r * n * R)) for _ in range(6)]
+    to = ctypes.c_uint(0)
+    assert _lib.lib.ttk_dep_timeouts(ctypes.byref(to), 1) == 0
+    outs = {}
+    for on in (0, 1):
+        old = _set_knob(_lib.KNOB_SCHUR_ONE, on)
+        try:
+            op = cls(L, Am, Rr, invI, (r, n, R))
+            assert op.h != 0
+            res = []
+            for v in vs:
+                y = op.matvec(v)
+                res.append(dev.read(op.matvec(y)))  # chained: each apply reads the previous output
+            outs[on] = res
+        finally:
+            _set_knob(_lib.KNOB_SCHUR_ONE, old)
+    for a, b in zip(outs[0], outs[1]):
+        assert np.array_equal(a, b)
+    assert _lib.lib.ttk_dep_timeouts(ctypes.byref(to), 0) == 0 and to.value == 0
