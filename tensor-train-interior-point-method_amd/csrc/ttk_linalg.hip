@@ -359,9 +359,15 @@ __global__ __launch_bounds__(1024) void svd_wg_kernel(const double *__restrict__
       }
     }
     __syncthreads();
-    // ---- QRCP (all p steps: zero columns get tau = 0, so every direction keeps a unit vector)
+    // ---- QRCP (all p steps: zero columns get tau = 0, so every direction keeps a unit vector).
+    // Two block barriers per column: every wave picks the pivot itself (the same first max of the
+    // same downdated norms), wave 0 swaps the pivot column into place and builds the reflector,
+    // barrier, trailing update + norm downdate, barrier.  The vn1 / vn2 / perm swap is folded into
+    // the trailing phase (slot piv takes slot c's values; slot c is never read again), so no wave
+    // writes the norms while another still reads them for its pivot search.
     for (int c = 0; c < p; ++c) {
-      if (wid == 0) {  // first max of the downdated norms (idamax) over <= 96 columns, wave 0
+      int piv;
+      {  // first max of the downdated norms (idamax) over <= 96 columns, every wave
         double bm = -1.0;
         int bi = p;
         for (int j = c + lane; j < p; j += 64) {
@@ -372,32 +378,18 @@ __global__ __launch_bounds__(1024) void svd_wg_kernel(const double *__restrict__
           }
         }
         ttk::wave_argmax(bm, bi);  // first max of the downdated norms, DPP (same winner as a butterfly)
-        if (lane == 0) s_piv = bi < p ? bi : c;
-      }
-      __syncthreads();
-      const int piv = s_piv;
-      if (piv != c) {
-        double *a = W + (int64_t)c * lq, *b = W + (int64_t)piv * lq;
-        for (int i = tid; i < q; i += nt) {
-          const double t = a[i];
-          a[i] = b[i];
-          b[i] = t;
-        }
-        if (tid == 0) {
-          double t = vn1[c];
-          vn1[c] = vn1[piv];
-          vn1[piv] = t;
-          t = vn2[c];
-          vn2[c] = vn2[piv];
-          vn2[piv] = t;
-          const int pi = perm[c];
-          perm[c] = perm[piv];
-          perm[piv] = pi;
-        }
-        __syncthreads();
+        piv = bi < p ? bi : c;
       }
       double *x = W + (int64_t)c * lq;
-      if (wid == 0) {  // reflector (dlarfg) by wave 0
+      if (wid == 0) {  // pivot swap + reflector (dlarfg) by wave 0 (LDS ops of one wave stay in order)
+        if (piv != c) {
+          double *b = W + (int64_t)piv * lq;
+          for (int i = lane; i < q; i += 64) {
+            const double t = x[i];
+            x[i] = b[i];
+            b[i] = t;
+          }
+        }
         double part = 0.0;
         #pragma unroll 8
         for (int i = c + 1 + lane; i < q; i += 64) part += x[i] * x[i];
@@ -414,11 +406,17 @@ __global__ __launch_bounds__(1024) void svd_wg_kernel(const double *__restrict__
         if (lane == 0) {
           x[c] = beta;
           tau[c] = t;
+          if (piv != c) {
+            const int pi = perm[c];
+            perm[c] = perm[piv];
+            perm[piv] = pi;
+          }
         }
       }
       __syncthreads();
       const double t = tau[c];
-      // trailing update + dlaqp2 norm downdate: g2 lanes per column, all columns in flight
+      // trailing update + dlaqp2 norm downdate: g2 lanes per column, all columns in flight; column
+      // piv carries slot c's norms after the swap
       for (int j = c + 1 + gid2; j < p; j += ng2) {
         double *y = W + (int64_t)j * lq;
         double yc = y[c];
@@ -432,11 +430,12 @@ __global__ __launch_bounds__(1024) void svd_wg_kernel(const double *__restrict__
           yc -= w;
           if (gl2 == 0) y[c] = yc;
         }
-        const double a = vn1[j];
+        const int js = j == piv ? c : j;
+        const double a = vn1[js], a2 = vn2[js];
         if (a != 0.0) {
           double temp = fabs(yc) / a;
           temp = fmax(1.0 - temp * temp, 0.0);
-          const double r = a / vn2[j];
+          const double r = a / a2;
           if (temp * r * r <= 1.4901161193847656e-08) {
             __threadfence_block();  // the group reads back the updated column
             double acc = 0.0;
@@ -449,7 +448,11 @@ __global__ __launch_bounds__(1024) void svd_wg_kernel(const double *__restrict__
             }
           } else if (gl2 == 0) {
             vn1[j] = a * sqrt(temp);
+            vn2[j] = a2;
           }
+        } else if (gl2 == 0 && j == piv) {
+          vn1[j] = a;
+          vn2[j] = a2;
         }
       }
       __syncthreads();

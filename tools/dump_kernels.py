@@ -83,6 +83,31 @@ def main(path):
             out[f"env_{backward}_{shapes[0]}"] = D.read(tt_als.env_update_many(backward, items)[0])
     finally:
         lib.ttk_fused_set_mfma(old)
+    # one-workgroup SVDs (QRCP + Jacobi) on plain and graded matrices, tall and wide
+    for (m_, n_) in [(39, 52), (52, 39), (64, 63), (63, 64), (96, 80), (80, 96), (20, 17), (128, 40), (60, 90),
+                     (12, 8), (8, 12), (96, 96)]:
+        for graded in (0, 1):
+            M = rng.standard_normal((m_, n_))
+            if graded:
+                k = min(m_, n_)
+                Uq, _ = np.linalg.qr(rng.standard_normal((m_, k)))
+                Vq, _ = np.linalg.qr(rng.standard_normal((n_, k)))
+                M = (Uq * np.logspace(0, -15, k)) @ Vq.T
+            U_, S_, Vt_, _ = D.svd(D.from_numpy(M), host=False)
+            out[f"svd_{m_}_{n_}_{graded}"] = np.concatenate([D.read(U_).ravel(), D.read(S_).ravel(), D.read(Vt_).ravel()])
+    # Schur-reduced local KKT matvecs (VALU rows, side by side or not; MFMA rows), chained
+    from ttipm_amd import tt_ipm
+    for ineq in (False, True):
+        for (r_, R_, s_, S_) in [(12, 16, 10, 9), (3, 4, 5, 5), (16, 20, 12, 12), (14, 96, 10, 9)]:
+            cls = tt_ipm.IneqMatVecWrapper if ineq else tt_ipm.MatVecWrapper
+            Lb = {k: D.from_numpy(rng.standard_normal((r_, s_, r_)) * 0.1) for k in cls.keys}
+            Ab = {k: D.from_numpy(rng.standard_normal((s_, 4, 4, S_)) * 0.1) for k in cls.keys}
+            Rb = {k: D.from_numpy(rng.standard_normal((R_, S_, R_)) * 0.1) for k in cls.keys}
+            invI = D.from_numpy(rng.uniform(0.5, 2.0, (r_, 4, R_)))
+            v = D.from_numpy(rng.standard_normal((3 if ineq else 2) * r_ * 4 * R_))
+            op = cls(Lb, Ab, Rb, invI, (r_, 4, R_))
+            y = op.matvec(op.matvec(v))
+            out[f"schur_{int(ineq)}_{r_}_{R_}"] = D.read(y)
     torch.cuda.synchronize()
     import hashlib
     for k in list(out):  # big arrays as a SHA-256 digest (keeps gpurun_out small); bitwise comparison still
