@@ -83,6 +83,9 @@ void *ttk_ctx_stream(ttk_ctx ctx);
  *                   rows compute B21 x while the w = inv_I o B01^T y rows run, then take w over an
  *                   in-launch hand-off; 0: two launches (bit-identical either way; default from env
  *                   TTK_SCHUR_ONE, else 1)
+ *   ARNOLDI_ONE     1: a multi-workgroup LGMRES Arnoldi step (partial dots, basis update, norm +
+ *                   Hessenberg/Givens) is ONE launch over in-launch hand-offs; 0: three launches
+ *                   (bit-identical either way; default from env TTK_ARNOLDI_ONE, else 1)
  * ttk_ctx_set_knob stores value and returns the previous one in *old (may be NULL). */
 enum ttk_knob {
   TTK_KNOB_FUSED_APPLY = 0,
@@ -94,7 +97,8 @@ enum ttk_knob {
   TTK_KNOB_APPLY_DUAL = 6,
   TTK_KNOB_RCOND_EXACT = 7,
   TTK_KNOB_SCHUR_ONE = 8,
-  TTK_KNOB_COUNT = 9
+  TTK_KNOB_ARNOLDI_ONE = 9,
+  TTK_KNOB_COUNT = 10
 };
 int ttk_ctx_set_knob(ttk_ctx ctx, int knob, int value, int *old);
 int ttk_ctx_get_knob(ttk_ctx ctx, int knob, int *value);

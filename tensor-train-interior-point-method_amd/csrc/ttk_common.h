@@ -133,6 +133,49 @@ __device__ __forceinline__ double block_sum(double v, double *red) {
   return t;
 }
 
+// ---- in-launch hand-offs between the workgroups of ONE launch (MI355X_MICROARCH.md, inter-
+// workgroup visibility, first row of the measured hand-off table): the producer stores every
+// handed-off word with an sc1 (write-through) store, every storing wave drains with
+// s_waitcnt vmcnt(0), a workgroup barrier, then ONE lane adds 1 to an agent-scope counter
+// (dep_arrive); each consumer WAVE polls that counter with an sc1 load until it reaches the launch's
+// target and only then loads the words, each with an sc1 load.  The counter (dep[0], per context,
+// ttk::dep_counter) is monotonic: the host passes target = arrivals of every launch so far.
+// Producers sit at lower block indices than their consumers and never wait, so the grid drains
+// whatever the residency; a wait past DEP_SPIN_MAX polls gives up (counted in dep[1],
+// ttk_dep_timeouts) instead of hanging.
+constexpr long DEP_SPIN_MAX = 20000000;
+
+__device__ __forceinline__ double ld_sc1(const double *p) {
+  return __hip_atomic_load((const __attribute__((address_space(1))) double *)(p), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1(double *p, double v) {
+  __hip_atomic_store((__attribute__((address_space(1))) double *)(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// every wave for itself (lane 0 polls; the wave's other lanes are masked off meanwhile)
+__device__ __forceinline__ void dep_wait(const unsigned *dep, unsigned target) {
+  if ((threadIdx.x & 63) == 0) {
+    const __attribute__((address_space(1))) unsigned *d = (const __attribute__((address_space(1))) unsigned *)(dep);
+    long n = 0;
+    while ((int)(__hip_atomic_load(d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) < 0) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++n > DEP_SPIN_MAX) {
+        __hip_atomic_fetch_add(const_cast<unsigned *>(dep) + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+}
+// the workgroup's one arrival, after every wave's sc1 stores: drain, barrier, one lane adds
+__device__ __forceinline__ void dep_arrive(unsigned *dep) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(dep, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// the calling context's hand-off counter (allocated and zeroed on first use)
+int dep_counter(void *stream);
+
 }  // namespace ttk
 
 #define TTK_HIP(call)                                                                    \

@@ -571,43 +571,6 @@ __device__ unsigned long long g_mph[8];
 #define TTK_VPH(K)
 #endif
 
-// ---- in-launch hand-off of a task's output to another task's input (MI355X_MICROARCH.md, inter-
-// workgroup visibility, first row of the measured hand-off table): the producer stores every
-// handed-off word with an sc1 (write-through) store, every storing wave drains with
-// s_waitcnt vmcnt(0), a workgroup barrier, then ONE lane adds 1 to an agent-scope counter; each
-// consumer WAVE polls that counter with an sc1 load until it reaches the launch's target and only
-// then loads the words, each with an sc1 load.  The counter is monotonic per context (no reset):
-// the host passes target = arrivals of every launch so far.  Producers sit at the lowest block
-// indices and never wait, so the grid drains whatever the residency; a spin past DEP_SPIN_MAX
-// polls gives up (g_dep_timeout is set; ttk_dep_timeouts reads it) instead of hanging.
-__device__ unsigned g_dep_timeout;
-constexpr long DEP_SPIN_MAX = 20000000;
-
-__device__ __forceinline__ double ld_sc1(const double *p) {
-  return __hip_atomic_load((const __attribute__((address_space(1))) double *)(p), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_sc1(double *p, double v) {
-  __hip_atomic_store((__attribute__((address_space(1))) double *)(p), v, __ATOMIC_RELAXED,
-                     __HIP_MEMORY_SCOPE_AGENT);
-}
-// every wave for itself (lane 0 polls; the wave's other lanes are masked off meanwhile)
-__device__ __forceinline__ void dep_wait(const unsigned *dep, unsigned target) {
-  if ((threadIdx.x & 63) == 0) {
-    const __attribute__((address_space(1))) unsigned *d =
-        (const __attribute__((address_space(1))) unsigned *)(dep);
-    long n = 0;
-    while ((int)(__hip_atomic_load(d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) < 0) {
-      __builtin_amdgcn_s_sleep(2);
-      if (++n > DEP_SPIN_MAX) {
-        __hip_atomic_fetch_add(&g_dep_timeout, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-    }
-  }
-  __builtin_amdgcn_wave_barrier();
-}
-
 // tid / nt: this row's threads (the whole block, or one half of it when a task's two terms run side
 // by side, see fused_apply_multi_kernel); every output element is still one thread's sequential chain,
 // so the thread count never changes a result.  Three block barriers, unconditional.
@@ -618,7 +581,7 @@ __device__ void apply_row(const ApplyArgs &g, int a, double *sm, double *orow, i
   if (tid == 0) atomicAdd(&g_mph[7], 1ull);
 #endif
   const int nb = g.nb, nj = g.nj, nd = g.nd, nS = g.nS, ns = g.ns, ni = g.ni, nc = g.nc;
-  if (g.dep) dep_wait(g.dep, g.dep_target);
+  if (g.dep) ttk::dep_wait(g.dep, g.dep_target);
   double *X = sm;                       // nb*nj*nd     [b][j][d]
   double *Pa = X + nb * nj * nd;        // ns*nb        [s][b]   (P[a, s, b])
   double *As = Pa + ns * nb;            // ns*ni*nj*nS  [i][S][s][j]
@@ -638,7 +601,7 @@ __device__ void apply_row(const ApplyArgs &g, int a, double *sm, double *orow, i
     MixedIdx<3> ix(tid, nt, rx);
     if (g.dep)  // handed off inside this launch: sc1 loads (separate loop: no per-element branch)
       for (int e = tid; e < nb * nj * nd; e += nt, ix.step(rx))
-        X[e] = ld_sc1(g.x + ix.v[0] * g.xs[0] + ix.v[1] * g.xs[1] + ix.v[2] * g.xs[2]);
+        X[e] = ttk::ld_sc1(g.x + ix.v[0] * g.xs[0] + ix.v[1] * g.xs[1] + ix.v[2] * g.xs[2]);
     else
       for (int e = tid; e < nb * nj * nd; e += nt, ix.step(rx))
         X[e] = g.x[ix.v[0] * g.xs[0] + ix.v[1] * g.xs[1] + ix.v[2] * g.xs[2]];
@@ -824,7 +787,7 @@ __device__ void apply_row_mfma(const ApplyArgs &g, int a, double *sm, double *or
   const int tid = threadIdx.x, nt = blockDim.x;
   const int nb = g.nb, nj = g.nj, nd = g.nd, nS = g.nS, ns = g.ns, ni = g.ni, nc = g.nc;
   const int jd = nj * nd, sj = ns * nj;
-  if (g.dep) dep_wait(g.dep, g.dep_target);
+  if (g.dep) ttk::dep_wait(g.dep, g.dep_target);
   double *X = sm;                       // [b][j][d]
   double *Pa = X + nb * jd;             // [s][b]
   double *As = Pa + ns * nb;            // [(i,S)][(s,j)]
@@ -836,7 +799,7 @@ __device__ void apply_row_mfma(const ApplyArgs &g, int a, double *sm, double *or
     MixedIdx<3> ix(tid, nt, rx);
     if (g.dep)  // handed off inside this launch: sc1 loads
       for (int e = tid; e < nb * jd; e += nt, ix.step(rx))
-        X[e] = ld_sc1(g.x + ix.v[0] * g.xs[0] + ix.v[1] * g.xs[1] + ix.v[2] * g.xs[2]);
+        X[e] = ttk::ld_sc1(g.x + ix.v[0] * g.xs[0] + ix.v[1] * g.xs[1] + ix.v[2] * g.xs[2]);
     else
       for (int e = tid; e < nb * jd; e += nt, ix.step(rx))
         X[e] = g.x[ix.v[0] * g.xs[0] + ix.v[1] * g.xs[1] + ix.v[2] * g.xs[2]];
@@ -1014,14 +977,10 @@ __global__ __launch_bounds__(1024) void fused_apply_multi_kernel(ApplyLaunch L) 
     double v = orow[e];
     if (T.oscale) v = (1.0 * v) * T.oscale[oi];
     if (T.addv) v = 1.0 * T.addv[oi] + 1.0 * v;
-    if (pub) st_sc1(g0.out + oi, v);
+    if (pub) ttk::st_sc1(g0.out + oi, v);
     else g0.out[oi] = v;
   }
-  if (pub) {  // every storing wave drained, then one arrival for the workgroup
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) __hip_atomic_fetch_add(L.dep, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
+  if (pub) ttk::dep_arrive(L.dep);  // every storing wave drained, then one arrival for the workgroup
 }
 
 constexpr int64_t APPLY_LDS_DOUBLES = 20000;
@@ -1080,11 +1039,12 @@ static int choose_csplit(const ApplyArgs &g, int64_t rows_total) {
 }
 
 extern "C" int ttk_dep_timeouts(unsigned *out, int reset) {  // in-launch hand-off waits that gave up
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dep_timeout), sizeof(unsigned)) != hipSuccess) return TTK_ERR_HIP;
-  if (reset) {
-    const unsigned z = 0;
-    if (hipMemcpyToSymbol(HIP_SYMBOL(g_dep_timeout), &z, sizeof(z)) != hipSuccess) return TTK_ERR_HIP;
-  }
+  ttk::Ctx &cx = ttk::ctx();
+  *out = 0;
+  if (!cx.dep) return TTK_OK;
+  TTK_HIP(cx.stream ? hipStreamSynchronize(cx.stream) : hipDeviceSynchronize());
+  TTK_HIP(hipMemcpy(out, cx.dep + 1, sizeof(unsigned), hipMemcpyDeviceToHost));
+  if (reset) TTK_HIP(hipMemset(cx.dep + 1, 0, sizeof(unsigned)));
   return TTK_OK;
 }
 
@@ -1538,11 +1498,7 @@ int ttk::schur_apply(void *stream, int64_t handle, const double *v, double *out)
   const double *in[4] = {v, v + m, v + 2 * m, w};
   double *o[4] = {out, out + m, out + 2 * m, w};
   if (op.one_ok && cx.knob[TTK_KNOB_SCHUR_ONE]) {
-    if (!cx.dep) {
-      TTK_HIP(hipMalloc(reinterpret_cast<void **>(&cx.dep), 256));
-      TTK_HIP(hipMemsetAsync(cx.dep, 0, 256, TTK_STREAM(stream)));
-      cx.dep_total = 0;
-    }
+    if (int rc = ttk::dep_counter(stream)) return rc;
     ApplyLaunch L = op.one;
     const int nprod = L.off[1] - L.off[0];
     cx.dep_total += (unsigned)nprod;

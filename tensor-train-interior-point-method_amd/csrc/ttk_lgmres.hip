@@ -294,6 +294,100 @@ __global__ __launch_bounds__(1024) void arnoldi_finish_kernel(double *V, int n, 
   hess_update(H, it, col, cs, sn, hapend, cl);
 }
 
+// The three kernels above as ONE launch (in-launch hand-offs, ttk_common.h): blocks
+// [0, ndot) are the (chunk, vector) partial dots, [ndot, ndot + nblk) the update blocks, the last
+// block the finish.  Every role runs the same arithmetic as its kernel above with 256 threads (the
+// finish's reductions are serial or elementwise, so its thread count never changes a bit); the
+// words one role hands to the next in this launch (partials, w, the norm parts, the HH column) go
+// out with sc1 stores and come in with sc1 loads.  Stopped chunks still arrive, so the counter
+// stays in step with the host's targets.
+__global__ __launch_bounds__(256) void arnoldi_fused_kernel(double *__restrict__ V, int n, int it,
+                                                            double *__restrict__ partials, int nchunk,
+                                                            double *__restrict__ normpart, int nblk, double *base,
+                                                            int max_k, double haptol, Ctl cl, unsigned *dep,
+                                                            unsigned t_dots, unsigned t_upd) {
+  __shared__ double h[MAXV + 2];
+  __shared__ double red[16];
+  const bool stopped = ctl_stopped(cl);
+  const int tid = threadIdx.x, b = blockIdx.x;
+  const int ndot = nchunk * (it + 1);
+  double *w = V + (int64_t)(it + 1) * n;
+  if (b < ndot) {  // arnoldi_dot_kernel
+    if (!stopped) {
+      const int c = b % nchunk, j = b / nchunk;
+      const double *vj = V + (int64_t)j * n;
+      const int i0 = c * ARN_CHUNK, i1 = i0 + ARN_CHUNK < n ? i0 + ARN_CHUNK : n;
+      double acc = 0.0;
+#pragma unroll 4
+      for (int i = i0 + tid; i < i1; i += 256) acc = fma(vj[i], w[i], acc);
+      acc = ttk::block_sum(acc, red);
+      if (tid == 0) ttk::st_sc1(partials + (int64_t)j * nchunk + c, acc);
+    }
+    ttk::dep_arrive(dep);
+    return;
+  }
+  if (b < ndot + nblk) {  // arnoldi_update_kernel
+    const int blk = b - ndot;
+    ttk::dep_wait(dep, t_dots);
+    __syncthreads();
+    if (!stopped) {
+      for (int j = tid; j <= it; j += 256) {
+        double acc = 0.0;
+        for (int c = 0; c < nchunk; ++c) acc += ttk::ld_sc1(partials + (int64_t)j * nchunk + c);
+        h[j] = acc;
+      }
+      __syncthreads();
+      if (blk == 0) {
+        HH H(base, max_k);
+        for (int j = tid; j <= it; j += 256) {
+          ttk::st_sc1(H.hh + j * H.ld + it, h[j]);
+          H.hes[j * H.ld + it] = h[j];
+        }
+      }
+      double s2 = 0.0;
+      for (int ii = blk * ARN_UPD + tid; ii < n && ii < (blk + 1) * ARN_UPD; ii += 256) {
+        double acc = w[ii];
+        for (int j = 0; j <= it; ++j) acc -= h[j] * V[(int64_t)j * n + ii];
+        ttk::st_sc1(w + ii, acc);
+        s2 = fma(acc, acc, s2);
+      }
+      s2 = ttk::block_sum(s2, red);
+      if (tid == 0) ttk::st_sc1(normpart + blk, s2);
+    }
+    ttk::dep_arrive(dep);
+    return;
+  }
+  // arnoldi_finish_kernel
+  ttk::dep_wait(dep, t_upd);
+  __syncthreads();
+  if (stopped) return;
+  __shared__ double s_tt;
+  HH H(base, max_k);
+  if (tid == 0) {
+    double s2 = 0.0;
+    for (int q = 0; q < nblk; ++q) s2 += ttk::ld_sc1(normpart + q);
+    s_tt = sqrt(s2);
+  }
+  __syncthreads();
+  const double tt = s_tt;
+  const int ld = H.ld;
+  __shared__ double col[MAXV + 2], cs[MAXV + 2], sn[MAXV + 2];
+  for (int j = tid; j <= it; j += 256) col[j] = ttk::ld_sc1(H.hh + j * ld + it);
+  double hapbnd = fabs(tt / H.grs[it]);
+  if (hapbnd > haptol) hapbnd = haptol;
+  const bool hapend = !(tt > hapbnd);
+  if (!hapend) {
+    const double inv = 1.0 / tt;
+    for (int i = tid; i < n; i += 256) w[i] = ttk::ld_sc1(w + i) * inv;
+  }
+  if (tid == 0) {
+    H.hes[(it + 1) * ld + it] = tt;
+    col[it + 1] = tt;
+  }
+  __syncthreads();
+  hess_update(H, it, col, cs, sn, hapend, cl);
+}
+
 // y = HH \ GRS (back substitution in GRS), once, by a single thread (it <= 100)
 __global__ void build_solve_kernel(double *base, int max_k, int it) {
   HH H(base, max_k);
@@ -399,6 +493,17 @@ static int arnoldi_launch(hipStream_t st_, double *V, int n, int it, double *hh,
       return TTK_ERR_HIP;
     }
     double *normpart = partials + (int64_t)(it + 1) * nchunk;
+    ttk::Ctx &cx = ttk::ctx();
+    if (cx.knob[TTK_KNOB_ARNOLDI_ONE]) {  // one launch: dots -> update -> finish over hand-offs
+      if (int rc = ttk::dep_counter(st_)) return rc;
+      const unsigned ndot = (unsigned)(nchunk * (it + 1));
+      const unsigned t_dots = cx.dep_total + ndot, t_upd = t_dots + (unsigned)nblk;
+      cx.dep_total = t_upd;
+      hipLaunchKernelGGL(arnoldi_fused_kernel, dim3(ndot + nblk + 1), dim3(256), 0, st_, V, n, it, partials, nchunk,
+                         normpart, nblk, hh, max_k, haptol, cl, cx.dep, t_dots, t_upd);
+      TTK_LAUNCH_CHECK();
+      return TTK_OK;
+    }
     hipLaunchKernelGGL(arnoldi_dot_kernel, dim3(nchunk, it + 1), dim3(256), 0, st_, V, n, it, partials, nchunk, cl);
     hipLaunchKernelGGL(arnoldi_update_kernel, dim3(nblk), dim3(256), 0, st_, V, n, it, partials, nchunk, normpart,
                        hh, max_k, cl);

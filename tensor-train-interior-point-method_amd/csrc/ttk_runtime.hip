@@ -159,6 +159,15 @@ Ctx *ctx_swap(Ctx *c) {
 }
 }  // namespace ttk
 
+int ttk::dep_counter(void *stream) {
+  ttk::Ctx &cx = ttk::ctx();
+  if (cx.dep) return TTK_OK;
+  TTK_HIP(hipMalloc(reinterpret_cast<void **>(&cx.dep), 256));
+  TTK_HIP(hipMemsetAsync(cx.dep, 0, 256, TTK_STREAM(stream)));
+  cx.dep_total = 0;
+  return TTK_OK;
+}
+
 extern "C" {
 
 int ttk_ctx_create(void *stream, ttk_ctx *out) {

@@ -745,3 +745,49 @@ def test_schur_one_launch_bit_identical(dev, ineq, dims):
     for a, b in zip(outs[0], outs[1]):
         assert np.array_equal(a, b)
     assert _lib.lib.ttk_dep_timeouts(ctypes.byref(to), 0) == 0 and to.value == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ineq", [False, True])
+@pytest.mark.parametrize("mw_min", [0, 16384])
+def test_lgmres_one_launch_arnoldi_bit_identical(dev, ineq, mw_min):
+    """whole LGMRES solves on a Schur operator: the multi-workgroup Arnoldi step as ONE launch
+    (TTK_KNOB_ARNOLDI_ONE, the default) and as three launches give the same solution, residual and
+    iteration count bit for bit (mw_min 0: every step on the multi-workgroup path; 16384: the
+    default split), with the one-launch Schur matvec on and off, and no hand-off wait gives up"""
+    import ctypes
+    from ttipm_amd import _lib, lgmres, tt_ipm
+    rng = np.random.default_rng(17)
+    r, R, s, S, n = 9, 12, 4, 4, 4
+    cls = tt_ipm.IneqMatVecWrapper if ineq else tt_ipm.MatVecWrapper
+    L = {k: dev.from_numpy(rng.standard_normal((r, s, r)) * 0.3) for k in cls.keys}
+    Am = {k: dev.from_numpy(rng.standard_normal((s, n, n, S)) * 0.3) for k in cls.keys}
+    Rr = {k: dev.from_numpy(rng.standard_normal((R, S, R)) * 0.3) for k in cls.keys}
+    invI = dev.from_numpy(rng.uniform(0.5, 2.0, (r, n, R)))
+    nb = 3 if ineq else 2
+    b = dev.from_numpy(rng.standard_normal(nb * r * n * R))
+    m = r * n * R
+    to = ctypes.c_uint(0)
+    assert _lib.lib.ttk_dep_timeouts(ctypes.byref(to), 1) == 0
+    res = {}
+    old_mw = _set_knob(_lib.KNOB_LGMRES_MW_MIN, mw_min)
+    try:
+        for arn in (0, 1):
+            for one in (0, 1):
+                o1, o2 = _set_knob(_lib.KNOB_ARNOLDI_ONE, arn), _set_knob(_lib.KNOB_SCHUR_ONE, one)
+                try:
+                    op = cls(L, Am, Rr, invI, (r, n, R))
+                    info = {}
+                    x = lgmres.lgmres(op.matvec_into, b, rtol=1e-10, max_it=300, restart=min(m, 100),
+                                      augment=max(min(m, 100) // 10, 3), info=info, native=op.h)
+                    res[arn, one] = (dev.read(x), info["its"], info["res"], info["reason"])
+                finally:
+                    _set_knob(_lib.KNOB_ARNOLDI_ONE, o1)
+                    _set_knob(_lib.KNOB_SCHUR_ONE, o2)
+    finally:
+        _set_knob(_lib.KNOB_LGMRES_MW_MIN, old_mw)
+    ref = res[0, 0]
+    assert ref[1] > 10
+    for k, v in res.items():
+        assert np.array_equal(v[0], ref[0]) and v[1:] == ref[1:], k
+    assert _lib.lib.ttk_dep_timeouts(ctypes.byref(to), 0) == 0 and to.value == 0

@@ -108,6 +108,17 @@ def main(path):
             op = cls(Lb, Ab, Rb, invI, (r_, 4, R_))
             y = op.matvec(op.matvec(v))
             out[f"schur_{int(ineq)}_{r_}_{R_}"] = D.read(y)
+            if R_ < 50:  # whole LGMRES solves, every Arnoldi step on the multi-workgroup path
+                from ttipm_amd import lgmres
+                old = lib.ttk_lgmres_set_mw_threshold(0)
+                try:
+                    m_ = r_ * 4 * R_
+                    info = {}
+                    x = lgmres.lgmres(op.matvec_into, v, rtol=1e-10, max_it=300, restart=min(m_, 100),
+                                      augment=max(min(m_, 100) // 10, 3), info=info, native=op.h)
+                    out[f"lgmres_{int(ineq)}_{r_}_{R_}"] = np.concatenate([D.read(x), [info["its"], info["res"]]])
+                finally:
+                    lib.ttk_lgmres_set_mw_threshold(old)
     torch.cuda.synchronize()
     import hashlib
     for k in list(out):  # big arrays as a SHA-256 digest (keeps gpurun_out small); bitwise comparison still
