@@ -152,23 +152,48 @@ __global__ __launch_bounds__(1024) void arnoldi_kernel(double *V, int n, int it,
   hess_update(H, it, h, cs, sn, hapend, cl);
 }
 
+// KSPLGMRESBuildSoln's back substitution y = HH(0:it, 0:it) \ GRS in GRS, in its serial order, with
+// the triangle and GRS staged in LDS first by the whole block (hl: (it+1)^2 doubles, ys: it+1): the
+// dependent chain then waits on LDS loads instead of one L2 round trip per term (bit-identical)
+__device__ void hh_backsub(HH &H, int it, double *hl, double *ys) {
+  const int tid = threadIdx.x, nt = blockDim.x, ld = H.ld, w = it + 1;
+  for (int e = tid; e < w * w; e += nt) {
+    const int k = e / w, j = e - k * w;
+    hl[e] = j >= k ? H.hh[k * ld + j] : 0.0;
+  }
+  for (int j = tid; j <= it; j += nt) ys[j] = H.grs[j];
+  __syncthreads();
+  if (tid == 0) {
+    ys[it] = ys[it] / hl[it * w + it];
+    for (int k = it - 1; k >= 0; --k) {
+      double t0 = ys[k];
+      for (int j = k + 1; j <= it; ++j) t0 -= hl[k * w + j] * ys[j];
+      ys[k] = t0 / hl[k * w + k];
+    }
+  }
+  __syncthreads();
+  for (int j = tid; j <= it; j += nt) H.grs[j] = ys[j];
+}
+
+// avec = HES(0:it_total+1, 0:it_total) GRS: element jj sums its terms in the serial loop's order (ii
+// ascending from max(jj-1, 0)), one thread per element
+__device__ __forceinline__ void hes_times_grs(const HH &H, int it_total, double *avec) {
+  const int ld = H.ld;
+  for (int jj = threadIdx.x; jj <= it_total; jj += blockDim.x) {
+    double a = 0.0;
+    for (int ii = jj > 0 ? jj - 1 : 0; ii <= it_total; ++ii) a += H.hes[jj * ld + ii] * H.grs[ii];
+    avec[jj] = a;
+  }
+}
+
 // KSPLGMRESBuildSoln: back substitution in place in GRS, temp = sum y_j basis_j, x += temp.
 __global__ __launch_bounds__(1024) void build_kernel(double *base, int max_k, int it, PtrList basis, int nvec,
                                                      int n, double *x, double *aug_temp) {
+  extern __shared__ double hl[];  // (it+1)^2 triangle
   __shared__ double y[MAXV + 2];
   HH H(base, max_k);
-  const int ld = H.ld;
   const int tid = threadIdx.x, nt = blockDim.x;
-  if (tid == 0) {
-    H.grs[it] = H.grs[it] / H.hh[it * ld + it];
-    for (int k = it - 1; k >= 0; --k) {
-      double t0 = H.grs[k];
-      for (int j = k + 1; j <= it; ++j) t0 -= H.hh[k * ld + j] * H.grs[j];
-      H.grs[k] = t0 / H.hh[k * ld + k];
-    }
-    for (int j = 0; j <= it; ++j) y[j] = H.grs[j];
-  }
-  __syncthreads();
+  hh_backsub(H, it, hl, y);
   for (int i = tid; i < n; i += nt) {
     double t = 0.0;
     for (int j = 0; j < nvec; ++j) t += y[j] * basis.p[j][i];
@@ -185,11 +210,7 @@ __global__ __launch_bounds__(1024) void aug_kernel(const double *base_c, int max
   HH H(const_cast<double *>(base_c), max_k);
   const int ld = H.ld;
   const int tid = threadIdx.x, nt = blockDim.x;
-  if (tid == 0) {
-    for (int j = 0; j <= it_total; ++j) avec[j] = 0.0;
-    for (int ii = 0; ii <= it_total; ++ii)
-      for (int jj = 0; jj <= ii + 1 && jj <= it_total; ++jj) avec[jj] += H.hes[jj * ld + ii] * H.grs[ii];
-  }
+  hes_times_grs(H, it_total, avec);
   double s2 = 0.0;
   for (int i = tid; i < n; i += nt) s2 += aug_temp[i] * aug_temp[i];
   s2 = ttk::block_sum(s2, red);
@@ -389,15 +410,11 @@ __global__ __launch_bounds__(256) void arnoldi_fused_kernel(double *__restrict__
 }
 
 // y = HH \ GRS (back substitution in GRS), once, by a single thread (it <= 100)
-__global__ void build_solve_kernel(double *base, int max_k, int it) {
+__global__ __launch_bounds__(256) void build_solve_kernel(double *base, int max_k, int it) {
+  extern __shared__ double hl[];
+  __shared__ double ys[MAXV + 2];
   HH H(base, max_k);
-  const int ld = H.ld;
-  H.grs[it] = H.grs[it] / H.hh[it * ld + it];
-  for (int k = it - 1; k >= 0; --k) {
-    double t0 = H.grs[k];
-    for (int j = k + 1; j <= it; ++j) t0 -= H.hh[k * ld + j] * H.grs[j];
-    H.grs[k] = t0 / H.hh[k * ld + k];
-  }
+  hh_backsub(H, it, hl, ys);
 }
 
 // temp = sum_j y_j basis_j, x += temp (chunks over the chip; y = GRS after build_solve_kernel)
@@ -434,10 +451,8 @@ __global__ __launch_bounds__(256) void aug_apply_kernel(const double *base_c, in
   __shared__ double s_inv;
   HH H(const_cast<double *>(base_c), max_k);
   const int ld = H.ld, tid = threadIdx.x;
+  hes_times_grs(H, it_total, avec);
   if (tid == 0) {
-    for (int j = 0; j <= it_total; ++j) avec[j] = 0.0;
-    for (int ii = 0; ii <= it_total; ++ii)
-      for (int jj = 0; jj <= ii + 1 && jj <= it_total; ++jj) avec[jj] += H.hes[jj * ld + ii] * H.grs[ii];
     double s2 = 0.0;
     for (int b = 0; b < nblk; ++b) s2 += part[b];
     s_inv = 1.0 / sqrt(s2);
@@ -567,11 +582,19 @@ int ttk_lgmres_build(void *stream, double *hh, int max_k, int it, const double *
   PtrList pl;
   for (int j = 0; j < nvec; ++j) pl.p[j] = basis[j];
   if ((int64_t)nvec * n >= mw_min()) {
-    hipLaunchKernelGGL(build_solve_kernel, dim3(1), dim3(1), 0, TTK_STREAM(stream), hh, max_k, it);
+    const size_t shm = (size_t)(it + 1) * (it + 1) * sizeof(double);
+    if (shm > 65536)
+      (void)hipFuncSetAttribute(reinterpret_cast<const void *>(build_solve_kernel),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+    hipLaunchKernelGGL(build_solve_kernel, dim3(1), dim3(256), shm, TTK_STREAM(stream), hh, max_k, it);
     hipLaunchKernelGGL(build_axpy_kernel, dim3((n + 255) / 256), dim3(256), 0, TTK_STREAM(stream), hh, max_k, pl,
                        nvec, n, x, aug_temp);
   } else {
-    hipLaunchKernelGGL(build_kernel, dim3(1), dim3(1024), 0, TTK_STREAM(stream), hh, max_k, it, pl, nvec, n, x,
+    const size_t shm = (size_t)(it + 1) * (it + 1) * sizeof(double);
+    if (shm > 65536)
+      (void)hipFuncSetAttribute(reinterpret_cast<const void *>(build_kernel),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+    hipLaunchKernelGGL(build_kernel, dim3(1), dim3(1024), shm, TTK_STREAM(stream), hh, max_k, it, pl, nvec, n, x,
                        aug_temp);
   }
   TTK_LAUNCH_CHECK();
