@@ -1648,11 +1648,38 @@ __global__ __launch_bounds__(256) void tri_matvec_kernel(const double *__restric
   if (tid == 0) partials[blockIdx.x] = contrib;
 }
 
+// lds != 0: the finish's ten length-n vectors live in dynamic LDS (dv, ov, tv staged from gv first), so
+// the serial chains of the multisection, the inverse iteration and the back-transform wait on LDS,
+// not on L2 round trips; same operations in the same order either way
 __global__ __launch_bounds__(1024) void tri_finish_kernel(double *A, int n, int which, double *gv, double *ev_out,
-                                                          double *vec_out) {
+                                                          double *vec_out, int lds) {
+  extern __shared__ double fl[];
   double *dv = gv, *ov = dv + n, *ev2 = ov + n, *tv = ev2 + n, *z = tv + n;
   double *fd = z + n, *fdu = fd + n, *fdu2 = fdu + n, *fdl = fdu2 + n, *fpiv = fdl + n;
+  if (lds) {
+    double *ldv = fl, *lov = ldv + n, *lev2 = lov + n, *ltv = lev2 + n, *lz = ltv + n;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+      ldv[i] = dv[i];
+      lov[i] = ov[i];
+      ltv[i] = tv[i];
+    }
+    __syncthreads();
+    tridiag_extreme_finish(A, n, which, ldv, lov, lev2, ltv, lz, lz + n, lz + 2 * n, lz + 3 * n, lz + 4 * n,
+                           lz + 5 * n, ev_out, vec_out, n);
+    return;
+  }
   tridiag_extreme_finish(A, n, which, dv, ov, ev2, tv, z, fd, fdu, fdu2, fdl, fpiv, ev_out, vec_out, n);
+}
+
+static int tri_finish_launch(hipStream_t st, double *A, int n, int which, double *gv, double *ev, double *vec) {
+  const size_t shm = 10 * (size_t)n * sizeof(double);
+  const int lds = shm <= 150000;
+  if (lds && shm > 65536)
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(tri_finish_kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+  hipLaunchKernelGGL(tri_finish_kernel, dim3(1), dim3(1024), lds ? shm : 0, st, A, n, which, gv, ev, vec, lds);
+  TTK_LAUNCH_CHECK();
+  return TTK_OK;
 }
 
 // One launch per Householder step (replaces tri_update + tri_matvec): every block rebuilds row k
@@ -2695,9 +2722,8 @@ int ttk_syev_extreme(void *stream, const double *A, int n, int which, double *ev
       hipLaunchKernelGGL(tri_step_kernel, dim3(nblk), dim3(256), 0, st, Aw, n, k, tv, ov, dv, pvb, partb, vbuf, nblk,
                          rb);
     hipLaunchKernelGGL(tri_tail_kernel, dim3(1), dim3(256), 0, st, Aw, n, tv, pvb, partb, vbuf, nblk);
-    hipLaunchKernelGGL(tri_finish_kernel, dim3(1), dim3(1024), 0, st, Aw, n, which, gv, ev, vec);
     TTK_LAUNCH_CHECK();
-    return TTK_OK;
+    return tri_finish_launch(st, Aw, n, which, gv, ev, vec);
   }
   if (!use_lds && n > 2) {  // multi-workgroup tridiagonalisation, one-workgroup finish
     double *Aw = work, *gv = work + (int64_t)n * n;
@@ -2711,9 +2737,8 @@ int ttk_syev_extreme(void *stream, const double *A, int n, int which, double *ev
       TTK_LAUNCH_CHECK();
     }
     hipLaunchKernelGGL(tri_update_kernel, dim3(nblk), dim3(256), 0, st, Aw, n, n - 2, tv, ov, dv, pv, partials, nblk);
-    hipLaunchKernelGGL(tri_finish_kernel, dim3(1), dim3(1024), 0, st, Aw, n, which, gv, ev, vec);
     TTK_LAUNCH_CHECK();
-    return TTK_OK;
+    return tri_finish_launch(st, Aw, n, which, gv, ev, vec);
   }
   if (n >= 3 && n <= SYEV_SMALL_N && g_syev_small) {
     const size_t shm_s = (size_t)syev_small_need(n) * sizeof(double);
