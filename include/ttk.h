@@ -269,6 +269,11 @@ int ttk_dot_nd_dev(void *stream, const double *x, const double *y, int ndim, con
 /* batched sums of squares over `nb` contiguous slices of length n with stride `bstride`;
  * `out` is a device array of nb doubles (no sync). */
 int ttk_sumsq_batched(void *stream, const double *x, int64_t n, int nb, int64_t bstride, double *out);
+/* the same per-batch sums of squares over strided batches: element i (0 <= i < n) of batch b is
+ * x[b*bstride + (i/inner)*ostride + i%inner], summed in i order exactly as ttk_sumsq_batched sums a
+ * contiguous copy (per-block sums of a (r, B, n, R) core without the permuted copy). */
+int ttk_sumsq_batched_strided(void *stream, const double *x, int64_t n, int nb, int64_t bstride, int64_t inner,
+                              int64_t ostride, double *out);
 /* copy `n` device doubles to the host (blocking) */
 int ttk_read_sync(void *stream, const double *src, double *host_dst, int64_t n);
 /* n doubles from pageable host memory to the device, asynchronously on the stream (staged through

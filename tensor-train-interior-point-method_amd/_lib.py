@@ -46,6 +46,7 @@ _SIGS = {
     "ttk_dot_nd_sync": (i32, [vp, vp, vp, i32, c_i64p, c_i64p, c_i64p, c_dp]),
     "ttk_dot_nd_dev": (i32, [vp, vp, vp, i32, c_i64p, c_i64p, c_i64p, vp]),
     "ttk_sumsq_batched": (i32, [vp, vp, i64, i32, i64, vp]),
+    "ttk_sumsq_batched_strided": (i32, [vp, vp, i64, i32, i64, i64, i64, vp]),
     "ttk_read_sync": (i32, [vp, vp, c_dp, i64]),
     "ttk_upload": (i32, [vp, vp, vp, i64]),
     "ttk_svd_work": (i64, [i32, i32]),

@@ -591,6 +591,29 @@ __global__ void sumsq_batched_kernel(const double *__restrict__ x, int64_t n, in
   if (threadIdx.x == 0) out[blockIdx.x] = acc;
 }
 
+// the same sums over a strided batch: element i of batch b at x[b*bstride + (i/inner)*ostride + i%inner]
+// (each batch = an (outer, inner) slab), summed in i order by the same threads as sumsq_batched_kernel
+__global__ void sumsq_batched2_kernel(const double *__restrict__ x, int64_t n, int64_t bstride, int64_t inner,
+                                      int64_t ostride, double *out) {
+  __shared__ double red[16];
+  const double *xb = x + blockIdx.x * bstride;
+  double acc = 0.0;
+  int64_t o = threadIdx.x / inner, r = threadIdx.x - o * inner;
+  const int64_t so = blockDim.x / inner, sr = blockDim.x - so * inner;
+  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+    const double v = xb[o * ostride + r];
+    acc += v * v;
+    o += so;
+    r += sr;
+    if (r >= inner) {
+      r -= inner;
+      ++o;
+    }
+  }
+  acc = ttk::block_sum(acc, red);
+  if (threadIdx.x == 0) out[blockIdx.x] = acc;
+}
+
 int make_nd(ttk::NdDesc &d, int ndim, const int64_t *shape, const int64_t *s0, const int64_t *s1,
             const int64_t *s2) {
   if (ndim < 0 || ndim > ttk::MAXD) {
@@ -1099,6 +1122,20 @@ int ttk_sumsq_batched(void *stream, const double *x, int64_t n, int nb, int64_t 
   if (int brc = ttk::batch_barrier(stream)) return brc;  // an open einsum batch may feed this call
   if (nb <= 0) return TTK_OK;
   hipLaunchKernelGGL(sumsq_batched_kernel, dim3(nb), dim3(256), 0, TTK_STREAM(stream), x, n, bstride, out);
+  TTK_LAUNCH_CHECK();
+  return TTK_OK;
+}
+
+int ttk_sumsq_batched_strided(void *stream, const double *x, int64_t n, int nb, int64_t bstride, int64_t inner,
+                              int64_t ostride, double *out) {
+  if (int brc = ttk::batch_barrier(stream)) return brc;  // an open einsum batch may feed this call
+  if (nb <= 0) return TTK_OK;
+  if (inner <= 0) {
+    ttk::set_error("ttk_sumsq_batched_strided: inner %lld", (long long)inner);
+    return TTK_ERR_ARG;
+  }
+  hipLaunchKernelGGL(sumsq_batched2_kernel, dim3(nb), dim3(256), 0, TTK_STREAM(stream), x, n, bstride, inner, ostride,
+                     out);
   TTK_LAUNCH_CHECK();
   return TTK_OK;
 }

@@ -278,9 +278,10 @@ def axpby(src, src2, alpha, beta, gamma, out=None):
     return out
 
 
-def scale_axis_ss(src, axis, ss, invert):
-    """src * max(sqrt(ss), 1e-10)[i] (or its reciprocal) along `axis`; ss = device sums of squares."""
-    out = empty(*src.shape)
+def scale_axis_ss(src, axis, ss, invert, out=None):
+    """src * max(sqrt(ss), 1e-10)[i] (or its reciprocal) along `axis`; ss = device sums of squares;
+    into `out` (same shape, any strides) when given."""
+    out = empty(*src.shape) if out is None else out
     nd = src.dim()
     check(lib.ttk_scale_axis_ss(_stream(), _p(src), _p(out), nd, _arr(src.shape), _arr(src.stride()),
                                 _arr(out.stride()), int(axis), _p(ss), int(bool(invert))), "scale_axis_ss")

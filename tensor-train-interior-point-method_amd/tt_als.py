@@ -282,12 +282,15 @@ def truncated_svd(m, k):
 
 
 def _block_sumsq(sol):
-    """per-block sums of squares of a (r, B, n, R) core, left on the device (one kernel)."""
-    B = sol.shape[1]
-    perm = D.clone(sol.permute(1, 0, 2, 3))
+    """per-block sums of squares of a (r, B, n, R) core, left on the device: one kernel reading the
+    blocks in place (the sums of a contiguous (B, r, n, R) copy, bit for bit)."""
+    r, B = sol.shape[0], sol.shape[1]
     out = D.empty(B)
-    n = perm[0].numel()
-    D.check(D.lib.ttk_sumsq_batched(D._stream(), perm.data_ptr(), n, B, n, out.data_ptr()), "sumsq")
+    if not sol.is_contiguous():
+        sol = D.clone(sol)
+    inner = sol.shape[2] * sol.shape[3]
+    D.check(D.lib.ttk_sumsq_batched_strided(D._stream(), sol.data_ptr(), r * inner, B, inner, inner, B * inner,
+                                            out.data_ptr()), "sumsq")
     return out
 
 
@@ -298,9 +301,10 @@ def _scales(sol):
     return ss, ss, ss
 
 
-def _scale_blocks(t, ss):
-    """t * sc[b] along the block axis 1 of a (r, B, n, R) tensor -> new tensor."""
-    return D.scale_axis_ss(t, 1, ss, invert=False)
+def _scale_blocks(t, ss, out=None):
+    """t * sc[b] along the block axis 1 of a (r, B, n, R) tensor -> new tensor (or into `out`, any
+    strides)."""
+    return D.scale_axis_ss(t, 1, ss, invert=False, out=out)
 
 
 def _div_blocks_bdim(t, ss, axis):
@@ -336,8 +340,7 @@ def _sweep(c, backward, swp, last, dsf):
                 c.XAX[k], Ak, c.XAX[k + 1], c.Xb[k], bk, c.Xb[k + 1], prev, 3 * d, not dsf)
             local_res = max(local_res, res_old)
             if sol is not prev:
-                diff = D.clone(sol)
-                D.copy_(diff, prev, -1.0, 1.0)
+                diff = D.axpby(prev, sol, -1.0, 1.0, 1.0)  # sol - prev, one launch (= clone + copy_)
                 j = sum(1 for t in dx_seq if t is not None)
                 D.dot_into(diff, diff, dx_buf[2 * j:2 * j + 1])
                 D.dot_into(sol, sol, dx_buf[2 * j + 1:2 * j + 2])
@@ -364,11 +367,13 @@ def _sweep(c, backward, swp, last, dsf):
                     resz = D.contig(z[k]).view(rz[k] * B, N[k] * rz[k + 1]).t()
                 else:
                     resz = D.clone(z[k].permute(0, 2, 1, 3)).view(rz[k] * N[k], B * rz[k + 1])
-        scaled = _scale_blocks(sol, scd)
         if backward:
+            scaled = _scale_blocks(sol, scd)
             mat = scaled.view(rx[k] * B, N[k] * rx[k + 1]).t()
-        else:
-            mat = D.clone(scaled.permute(0, 2, 1, 3)).view(rx[k] * N[k], B * rx[k + 1])
+        else:  # scaled straight into (r, n, B, R) storage: the forward unfolding needs no copy
+            store = D.empty(rx[k], N[k], B, rx[k + 1])
+            scaled = _scale_blocks(sol, scd, out=store.permute(0, 2, 1, 3))
+            mat = store.view(rx[k] * N[k], B * rx[k + 1])
 
         interior = (k > 0) if backward else (k < d - 1)
         if not interior:
@@ -422,8 +427,9 @@ def _sweep(c, backward, swp, last, dsf):
                                    "lim": float(trunc_lim),
                                    "rat": [float(D.norm_of(ss[q]) / nrhs) for q in range(r0 - r + 1)] if cands else []})
             if backward:
-                u_new = D.clone(U[:, :r].t()).view(r, N[k], rx[k + 1])
                 v_new = D.clone(v[:r].t()).view(rx[k], B, r)
+                if not (amen and not last):
+                    u_new = D.clone(U[:, :r].t()).view(r, N[k], rx[k + 1])
                 if amen and not last:
                     sh = (rz[k], B, N[k], rx[k + 1])
                     rxz = D.zeros(*sh)
@@ -433,11 +439,12 @@ def _sweep(c, backward, swp, last, dsf):
                     D.copy_(rxz, Axz, -1.0, 1.0)
                     kr = min(c.kick_rank, rz[k] * B, N[k] * rx[k + 1])
                     uz, _ = truncated_svd(rxz.view(rz[k] * B, N[k] * rx[k + 1]).t(), kr)
-                    uzT = uz.t()  # (kr, N*rx1)
-                    cat = D.empty(r + kr, N[k] * rx[k + 1])
-                    D.copy_(cat[:r], u_new.view(r, -1))
-                    D.copy_(cat[r:], uzT)
-                    Qm, Rm = D.qr(D.clone(cat.t()))
+                    # [u_new; uz^T]^T = [U[:, :r], uz] built transposed in place (no clone of the
+                    # truncated left factor, no transpose copy before the QR)
+                    catT = D.empty(N[k] * rx[k + 1], r + kr)
+                    D.copy_(catT[:, :r], U[:, :r])
+                    D.copy_(catT[:, r:], uz)
+                    Qm, Rm = D.qr(catT)
                     u_new = D.clone(Qm.t()).view(-1, N[k], rx[k + 1])
                     v_new = einsum("Rdk,rk->Rdr", v_new, Rm[:, :v_new.shape[-1]])
                     r = u_new.shape[0]
@@ -705,8 +712,7 @@ def _tt_approx_product(A, Dm, x0, kick_rank, nswp, tol, verbose):
     rel_buf, rel_n = D.empty(2 * d), [0]
 
     def rel_change(sol, prev):
-        diff = D.clone(sol)
-        D.copy_(diff, prev, -1.0, 1.0)
+        diff = D.axpby(prev, sol, -1.0, 1.0, 1.0)  # sol - prev (= clone + copy_)
         i = rel_n[0]
         D.dot_into(diff, diff, rel_buf[2 * i:2 * i + 1])
         D.dot_into(sol, sol, rel_buf[2 * i + 1:2 * i + 2])

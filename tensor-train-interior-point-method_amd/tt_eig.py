@@ -111,13 +111,12 @@ def _split(sol, sh, trunc_tol, max_rank, bwd):
         U, S, Vt, s = D.svd(D.clone(sol.view(a, b).t()))
         v = einsum("r,rj->rj", S, Vt)
         r = min(T.prune_singular_vals(s, trunc_tol), max_rank)
-        s1, s2, r = _kick_rev(D.clone(v[:r].t()), D.clone(U[:, :r].t()), 4)
+        s1, s2, r = _kick_rev(v[:r].t(), U[:, :r].t(), 4)  # strided operands: no transpose copies
         return D.contig(s1).view(sh[0], sh[1], r), D.contig(s2).view(r, sh[2], sh[3])
     U, S, Vt, s = D.svd(sol.view(a, b))
     r = min(T.prune_singular_vals(s, trunc_tol), max_rank)
-    s1 = D.clone(U[:, :r])
     s2 = einsum("r,rj->rj", S[:r], Vt[:r])
-    s1, s2, r = _kick(s1, s2, 4)
+    s1, s2, r = _kick(U[:, :r], s2, 4)  # the kick copies the truncated factor itself
     return D.contig(s1).view(sh[0], sh[1], r), D.contig(s2).view(r, sh[2], sh[3])
 
 

@@ -277,6 +277,16 @@ class EmuLib:
             o[b] = np.dot(seg, seg)
         return 0
 
+    def ttk_sumsq_batched_strided(self, s, x, n, nb, bstride, inner, ostride, out):
+        outer = n // inner
+        xv = _dv(x, (nb - 1) * bstride + (outer - 1) * ostride + inner)
+        o = _dv(out, nb)
+        for b in range(nb):
+            idx = b * bstride + (np.arange(outer)[:, None] * ostride + np.arange(inner)[None, :]).reshape(-1)
+            seg = xv[idx]
+            o[b] = np.dot(seg, seg)
+        return 0
+
     def ttk_read_sync(self, s, src, dst, n):
         ctypes.memmove(dst, int(src), int(n) * 8)
         return 0
