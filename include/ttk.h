@@ -86,6 +86,10 @@ void *ttk_ctx_stream(ttk_ctx ctx);
  *   ARNOLDI_ONE     1: a multi-workgroup LGMRES Arnoldi step (partial dots, basis update, norm +
  *                   Hessenberg/Givens) is ONE launch over in-launch hand-offs; 0: three launches
  *                   (bit-identical either way; default from env TTK_ARNOLDI_ONE, else 1)
+ *   SCHUR_PREP      1: ttk_schur_build copies every term's A (and VALU rows' Q) once into the
+ *                   layout the apply rows stage in LDS, so a matvec stages them with contiguous
+ *                   copies instead of strided gathers (bit-identical; read at build; default
+ *                   from env TTK_SCHUR_PREP, else 1)
  * ttk_ctx_set_knob stores value and returns the previous one in *old (may be NULL). */
 enum ttk_knob {
   TTK_KNOB_FUSED_APPLY = 0,
@@ -98,7 +102,8 @@ enum ttk_knob {
   TTK_KNOB_RCOND_EXACT = 7,
   TTK_KNOB_SCHUR_ONE = 8,
   TTK_KNOB_ARNOLDI_ONE = 9,
-  TTK_KNOB_COUNT = 10
+  TTK_KNOB_SCHUR_PREP = 10,
+  TTK_KNOB_COUNT = 11
 };
 int ttk_ctx_set_knob(ttk_ctx ctx, int knob, int value, int *old);
 int ttk_ctx_get_knob(ttk_ctx ctx, int knob, int *value);

@@ -522,6 +522,9 @@ struct ApplyArgs {
   // every wave of this row waits until *dep >= dep_target, then loads x with sc1 loads
   const unsigned *dep = nullptr;
   unsigned dep_target = 0;
+  // operands pre-permuted into their LDS images once per Schur handle (schur_prep_kernel): As
+  // [i][S][s][j] and Qs [c][S|d] rows of stride (nS*nd)|1; staging then is a contiguous copy
+  const double *As_pre = nullptr, *Qs_pre = nullptr;
 };
 
 // Association follows the greedy pairwise plan the reference's opt_einsum picks for these shapes
@@ -591,26 +594,50 @@ __device__ void apply_row(const ApplyArgs &g, int a, double *sm, double *orow, i
   const int lq3 = (nS * nd) | 1;        // odd row stride: stage 3's lanes (one c each) on distinct banks
   if (g.qlds) {  // stage 3 reads every Q element once per row: one coalesced pass instead of a
                  // dependent FMA chain over global loads
-    const int rq[3] = {nc, nS, nd};
-    MixedIdx<3> iq(tid, nt, rq);
-    for (int e = tid; e < nc * nS * nd; e += nt, iq.step(rq))
-      Qs[iq.v[0] * lq3 + iq.v[1] * nd + iq.v[2]] = g.Q[iq.v[0] * g.qs[0] + iq.v[1] * g.qs[1] + iq.v[2] * g.qs[2]];
+    if (g.Qs_pre) {
+#pragma unroll 4
+      for (int e = tid; e < nc * lq3; e += nt) Qs[e] = g.Qs_pre[e];
+    } else {
+      const int rq[3] = {nc, nS, nd};
+      MixedIdx<3> iq(tid, nt, rq);
+      for (int e = tid; e < nc * nS * nd; e += nt, iq.step(rq))
+        Qs[iq.v[0] * lq3 + iq.v[1] * nd + iq.v[2]] = g.Q[iq.v[0] * g.qs[0] + iq.v[1] * g.qs[1] + iq.v[2] * g.qs[2]];
+    }
   }
-  {  // staging: multi-digit indices advanced by carries (MixedIdx) instead of divisions
-    const int rx[3] = {nb, nj, nd};
-    MixedIdx<3> ix(tid, nt, rx);
-    if (g.dep)  // handed off inside this launch: sc1 loads (separate loop: no per-element branch)
-      for (int e = tid; e < nb * nj * nd; e += nt, ix.step(rx))
-        X[e] = ttk::ld_sc1(g.x + ix.v[0] * g.xs[0] + ix.v[1] * g.xs[1] + ix.v[2] * g.xs[2]);
-    else
-      for (int e = tid; e < nb * nj * nd; e += nt, ix.step(rx))
-        X[e] = g.x[ix.v[0] * g.xs[0] + ix.v[1] * g.xs[1] + ix.v[2] * g.xs[2]];
+  {  // staging: multi-digit indices advanced by carries (MixedIdx) instead of divisions; contiguous
+     // operands (the Schur vectors, P rows, pre-permuted A) as straight coalesced copies
+    const int nx = nb * nj * nd;
+    const bool xc = g.xs[2] == 1 && g.xs[1] == nd && g.xs[0] == (int64_t)nj * nd;
+    if (xc && g.dep) {
+#pragma unroll 4
+      for (int e = tid; e < nx; e += nt) X[e] = ttk::ld_sc1(g.x + e);
+    } else if (xc) {
+#pragma unroll 4
+      for (int e = tid; e < nx; e += nt) X[e] = g.x[e];
+    } else {
+      const int rx[3] = {nb, nj, nd};
+      MixedIdx<3> ix(tid, nt, rx);
+      if (g.dep)  // handed off inside this launch: sc1 loads (separate loop: no per-element branch)
+        for (int e = tid; e < nx; e += nt, ix.step(rx))
+          X[e] = ttk::ld_sc1(g.x + ix.v[0] * g.xs[0] + ix.v[1] * g.xs[1] + ix.v[2] * g.xs[2]);
+      else
+        for (int e = tid; e < nx; e += nt, ix.step(rx))
+          X[e] = g.x[ix.v[0] * g.xs[0] + ix.v[1] * g.xs[1] + ix.v[2] * g.xs[2]];
+    }
   }
-  for (int e = tid; e < ns * nb; e += nt) {
-    const int s = e / nb, b = e - s * nb;
-    Pa[e] = g.P[a * g.ps[0] + s * g.ps[1] + b * g.ps[2]];
+  if (g.ps[2] == 1 && g.ps[1] == nb) {
+    const double *pa = g.P + a * g.ps[0];
+    for (int e = tid; e < ns * nb; e += nt) Pa[e] = pa[e];
+  } else {
+    for (int e = tid; e < ns * nb; e += nt) {
+      const int s = e / nb, b = e - s * nb;
+      Pa[e] = g.P[a * g.ps[0] + s * g.ps[1] + b * g.ps[2]];
+    }
   }
-  {  // As[i][S][s][j] = A[s, i, j, S]
+  if (g.As_pre) {
+#pragma unroll 4
+    for (int e = tid; e < ns * ni * nj * nS; e += nt) As[e] = g.As_pre[e];
+  } else {  // As[i][S][s][j] = A[s, i, j, S]
     const int ra[4] = {ni, nS, ns, nj};
     MixedIdx<4> ia(tid, nt, ra);
     for (int e = tid; e < ns * ni * nj * nS; e += nt, ia.step(ra))
@@ -808,7 +835,10 @@ __device__ void apply_row_mfma(const ApplyArgs &g, int a, double *sm, double *or
     const int s_ = e / nb, b = e - s_ * nb;
     Pa[e] = g.P[a * g.ps[0] + s_ * g.ps[1] + b * g.ps[2]];
   }
-  {
+  if (g.As_pre) {  // [(i,S)][(s,j)] = the VALU rows' [i][S][s][j], pre-permuted per Schur handle
+#pragma unroll 4
+    for (int e = tid; e < ni * nS * sj; e += nt) As[e] = g.As_pre[e];
+  } else {
     const int ra[4] = {ni, nS, ns, nj};  // As[(i,S)][(s,j)]
     MixedIdx<4> ia(tid, nt, ra);
     for (int e = tid; e < ni * nS * sj; e += nt, ia.step(ra))
@@ -981,6 +1011,41 @@ __global__ __launch_bounds__(1024) void fused_apply_multi_kernel(ApplyLaunch L) 
     else g0.out[oi] = v;
   }
   if (pub) ttk::dep_arrive(L.dep);  // every storing wave drained, then one arrival for the workgroup
+}
+
+// Pre-permuted operand images of a Schur handle's terms (one launch per ttk_schur_build): block q
+// copies job q, dst[i0][i1][i2][i3] (strides dst_st) = src[i0 * s0 + ...] over shape sh; dst_fill
+// doubles are zeroed first (the Q rows' odd-stride pad).  Pure copies: every staged value is the
+// operand value the gathers of apply_row / apply_row_mfma read.
+constexpr int PREP_MAX = 14;
+struct PrepJob {
+  const double *src;
+  double *dst;
+  int sh[4];
+  int64_t ss[4], ds[4];
+  int64_t fill;
+};
+struct PrepList {
+  PrepJob job[PREP_MAX];
+  int n;
+};
+
+__global__ __launch_bounds__(256) void schur_prep_kernel(PrepList L) {
+  const PrepJob &J = L.job[blockIdx.x];
+  for (int64_t e = threadIdx.x; e < J.fill; e += 256) J.dst[e] = 0.0;
+  __syncthreads();
+  const int64_t tot = (int64_t)J.sh[0] * J.sh[1] * J.sh[2] * J.sh[3];
+  for (int64_t e = threadIdx.x; e < tot; e += 256) {
+    int64_t r = e;
+    const int i3 = (int)(r % J.sh[3]);
+    r /= J.sh[3];
+    const int i2 = (int)(r % J.sh[2]);
+    r /= J.sh[2];
+    const int i1 = (int)(r % J.sh[1]);
+    const int i0 = (int)(r / J.sh[1]);
+    J.dst[i0 * J.ds[0] + i1 * J.ds[1] + i2 * J.ds[2] + i3 * J.ds[3]] =
+        J.src[i0 * J.ss[0] + i1 * J.ss[1] + i2 * J.ss[2] + i3 * J.ss[3]];
+  }
 }
 
 constexpr int64_t APPLY_LDS_DOUBLES = 20000;
@@ -1209,6 +1274,8 @@ struct SchurOp {
   std::vector<int64_t> desc;  // nblk x 36 words (ttk_einsum descriptors, x pointer patched per call)
   const double *inv_I;
   int64_t r, n, R;
+  double *pre = nullptr;  // pre-permuted operand images (per handle slot, grown, reused)
+  int64_t pre_cap = 0;
 };
 std::vector<SchurOp> &schur_ops() {  // the current context's handle table
   ttk::Ctx &c = ttk::ctx();
@@ -1258,6 +1325,13 @@ static int schur_store(SchurOp &op, int64_t m, int64_t *handle) {
   std::vector<SchurOp> &ops = schur_ops();
   size_t slot = 0;
   while (slot < ops.size() && ops[slot].used) ++slot;
+  if (slot < ops.size()) {  // the slot's operand-image buffer carries over to the new handle
+    op.pre = ops[slot].pre;
+    op.pre_cap = ops[slot].pre_cap;
+  } else {
+    op.pre = nullptr;
+    op.pre_cap = 0;
+  }
   if (slot == ops.size()) ops.push_back(op);
   else ops[slot] = op;
   *handle = (int64_t)slot + 1;
@@ -1326,6 +1400,82 @@ static int schur_apply_pairwise(void *stream, const SchurOp &op, const double *v
     if (!rc) rc = apply(6, t, o2, 1.0, 1.0);  // + B33 t
     rc2 = ttk_einsum_batch_end(stream);
     if (rc || rc2) return rc ? rc : rc2;
+  }
+  return TTK_OK;
+}
+
+// the operand images of a fused handle (PrepList above): one buffer per handle slot, one launch;
+// the staging of every VALU / MFMA row then copies them contiguously
+static int schur_prep(SchurOp &op) {
+  struct Ref {
+    int s, t, k;
+    int64_t aoff, qoff;
+  };
+  std::vector<Ref> refs;
+  int64_t need = 0;
+  int njob = 0;
+  for (int s = 0; s < 2; ++s)
+    for (int t = 0; t < op.st[s].ntask; ++t)
+      for (int k = 0; k < op.st[s].task[t].nterms; ++k) {
+        const ApplyArgs &g = op.st[s].task[t].t[k];
+        Ref r{s, t, k, need, -1};
+        need += (int64_t)g.ns * g.ni * g.nj * g.nS;
+        ++njob;
+        if (g.qlds && !g.mfma) {
+          r.qoff = need;
+          need += (int64_t)g.nc * ((g.nS * g.nd) | 1);
+          ++njob;
+        }
+        refs.push_back(r);
+      }
+  if (njob > PREP_MAX || need <= 0) return TTK_OK;  // staged by the gathers instead
+  ttk::Ctx &cx = ttk::ctx();
+  if (need > op.pre_cap) {
+    if (op.pre) {
+      TTK_HIP(cx.stream ? hipStreamSynchronize(cx.stream) : hipDeviceSynchronize());
+      (void)hipFree(op.pre);
+    }
+    op.pre = nullptr;
+    op.pre_cap = 0;
+    const int64_t want = need < 32768 ? 32768 : need;
+    TTK_HIP(hipMalloc(reinterpret_cast<void **>(&op.pre), want * sizeof(double)));
+    op.pre_cap = want;
+  }
+  PrepList L{};
+  L.n = 0;
+  for (const Ref &r : refs) {
+    const ApplyArgs &g = op.st[r.s].task[r.t].t[r.k];
+    PrepJob &A = L.job[L.n++];  // As[i][S][s][j] = A[s*as0 + i*as1 + j*as2 + S*as3]
+    A.src = g.A;
+    A.dst = op.pre + r.aoff;
+    A.sh[0] = g.ni, A.sh[1] = g.nS, A.sh[2] = g.ns, A.sh[3] = g.nj;
+    A.ss[0] = g.as[1], A.ss[1] = g.as[3], A.ss[2] = g.as[0], A.ss[3] = g.as[2];
+    A.ds[0] = (int64_t)g.nS * g.ns * g.nj, A.ds[1] = (int64_t)g.ns * g.nj, A.ds[2] = g.nj, A.ds[3] = 1;
+    A.fill = 0;
+    if (r.qoff >= 0) {  // Qs[c][S][d] in rows of stride (nS*nd)|1
+      const int lq3 = (g.nS * g.nd) | 1;
+      PrepJob &Q = L.job[L.n++];
+      Q.src = g.Q;
+      Q.dst = op.pre + r.qoff;
+      Q.sh[0] = g.nc, Q.sh[1] = g.nS, Q.sh[2] = g.nd, Q.sh[3] = 1;
+      Q.ss[0] = g.qs[0], Q.ss[1] = g.qs[1], Q.ss[2] = g.qs[2], Q.ss[3] = 0;
+      Q.ds[0] = lq3, Q.ds[1] = g.nd, Q.ds[2] = 1, Q.ds[3] = 0;
+      Q.fill = (int64_t)g.nc * lq3;
+    }
+  }
+  hipLaunchKernelGGL(schur_prep_kernel, dim3(L.n), dim3(256), 0, TTK_STREAM(cx.stream), L);
+  TTK_LAUNCH_CHECK();
+  for (const Ref &r : refs) {
+    ApplyArgs &g = op.st[r.s].task[r.t].t[r.k];
+    g.As_pre = op.pre + r.aoff;
+    g.Qs_pre = r.qoff >= 0 ? op.pre + r.qoff : nullptr;
+  }
+  for (int t = 0; t < op.one.ntask; ++t) {  // the one-launch form's copies of the same terms
+    const int s = op.one_src[t][0], tt = op.one_src[t][1];
+    for (int k = 0; k < op.one.task[t].nterms; ++k) {
+      op.one.task[t].t[k].As_pre = op.st[s].task[tt].t[k].As_pre;
+      op.one.task[t].t[k].Qs_pre = op.st[s].task[tt].t[k].Qs_pre;
+    }
   }
   return TTK_OK;
 }
@@ -1479,10 +1629,21 @@ int ttk_schur_build(ttk_ctx ctx, int ineq, int64_t m, const int64_t *descs, cons
       for (int k = 0; k < O.task[t].nterms; ++k) op.one_mfma = op.one_mfma || O.task[t].t[k].mfma;
     op.one_ok = nt_ >= 2 && O.off[nt_] <= 1024;  // producers are a small share of a small grid
   }
-  return schur_store(op, m, handle);
+  if (int rc = schur_store(op, m, handle)) return rc;
+  if (!ttk::ctx().knob[TTK_KNOB_SCHUR_PREP]) return TTK_OK;
+  return schur_prep(schur_ops()[*handle - 1]);
 }
 
 }  // extern "C"
+
+void ttk::schur_release(ttk::Ctx &c) {  // context teardown: the handle table and its operand images
+  if (!c.schur) return;
+  auto *ops = static_cast<std::vector<SchurOp> *>(c.schur);
+  for (SchurOp &op : *ops)
+    if (op.pre) (void)hipFree(op.pre);
+  delete ops;
+  c.schur = nullptr;
+}
 
 int ttk::schur_apply(void *stream, int64_t handle, const double *v, double *out) {
   std::vector<SchurOp> &ops = schur_ops();

@@ -57,10 +57,12 @@ struct Ctx {
                               env_int("TTK_SPLITK_MINK", 128) > 0 ? env_int("TTK_SPLITK_MINK", 128) : 128,
                               env_int("TTK_LGMRES_MW_MIN", 16384), env_int("TTK_MFMA_CSPLIT", 1) != 0 ? 1 : 0,
                               env_int("TTK_APPLY_DUAL", 1) != 0 ? 1 : 0, env_int("TTK_RCOND_EXACT", 0) != 0 ? 1 : 0,
-                              env_int("TTK_SCHUR_ONE", 1) != 0 ? 1 : 0, env_int("TTK_ARNOLDI_ONE", 1) != 0 ? 1 : 0};
+                              env_int("TTK_SCHUR_ONE", 1) != 0 ? 1 : 0, env_int("TTK_ARNOLDI_ONE", 1) != 0 ? 1 : 0,
+                              env_int("TTK_SCHUR_PREP", 1) != 0 ? 1 : 0};
 };
 Ctx &ctx();
-Ctx *ctx_swap(Ctx *c);  // bind c to the calling thread, return the previous binding
+Ctx *ctx_swap(Ctx *c);
+void schur_release(Ctx &c);  // ttk_einsum.hip: Schur handle table + operand images of a context  // bind c to the calling thread, return the previous binding
 }  // namespace ttk
 
 struct ttk_ctx_s {

@@ -234,6 +234,7 @@ int ttk_ctx_destroy(ttk_ctx h) {
   ttk::ctx_free_einsum(c);
   ttk::g_cur_ctx = prev == &c ? nullptr : prev;
   for (double *p : {c.scratch, c.splitk, c.dev_scalar, c.schur_w, c.lgmres, c.rcond}) if (p) (void)hipFree(p);
+  ttk::schur_release(c);
   if (c.status) (void)hipFree(c.status);
   if (c.dep) (void)hipFree(c.dep);
   if (c.mapped_h) (void)hipHostFree(c.mapped_h);

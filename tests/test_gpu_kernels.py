@@ -731,19 +731,22 @@ def test_schur_one_launch_bit_identical(dev, ineq, dims):
     assert _lib.lib.ttk_dep_timeouts(ctypes.byref(to), 1) == 0
     outs = {}
     for on in (0, 1):
-        old = _set_knob(_lib.KNOB_SCHUR_ONE, on)
-        try:
-            op = cls(L, Am, Rr, invI, (r, n, R))
-            assert op.h != 0
-            res = []
-            for v in vs:
-                y = op.matvec(v)
-                res.append(dev.read(op.matvec(y)))  # chained: each apply reads the previous output
-            outs[on] = res
-        finally:
-            _set_knob(_lib.KNOB_SCHUR_ONE, old)
-    for a, b in zip(outs[0], outs[1]):
-        assert np.array_equal(a, b)
+        for prep in (0, 1):  # operand images pre-permuted at build (TTK_KNOB_SCHUR_PREP) or gathered
+            old, oldp = _set_knob(_lib.KNOB_SCHUR_ONE, on), _set_knob(_lib.KNOB_SCHUR_PREP, prep)
+            try:
+                op = cls(L, Am, Rr, invI, (r, n, R))
+                assert op.h != 0
+                res = []
+                for v in vs:
+                    y = op.matvec(v)
+                    res.append(dev.read(op.matvec(y)))  # chained: each apply reads the previous output
+                outs[on, prep] = res
+            finally:
+                _set_knob(_lib.KNOB_SCHUR_ONE, old)
+                _set_knob(_lib.KNOB_SCHUR_PREP, oldp)
+    for key in outs:
+        for a, b in zip(outs[0, 0], outs[key]):
+            assert np.array_equal(a, b), key
     assert _lib.lib.ttk_dep_timeouts(ctypes.byref(to), 0) == 0 and to.value == 0
 
 
