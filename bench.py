@@ -27,8 +27,8 @@
   GPU.  `sec_per_iter_per_seed_median_inflight` is the same statistic over the timed (contended)
   solves.
 * `roofline` (contraction kernels: the MFMA GEMM `gemm_offs*`, the fused local apply and the Schur
-  multi-task apply): an untimed re-solve of rank 0's step-0 seed with every contraction launch
-  bracketed by HIP events on its stream.  achieved = ALGORITHMIC contraction FLOPs of that solve
+  multi-task apply): an untimed re-solve of each distinct seed rank 0 timed (the timed region's seed
+  mix) with every contraction launch bracketed by HIP events on its stream.  achieved = ALGORITHMIC contraction FLOPs of that solve
   (NumPy `einsum_path` greedy convention per einsum call plus the chained applies of every local
   KKT operator application; `dev.ALGO`) / summed contraction kernel time; peak =
   78.6 TFLOP/s fp64 matrix.
@@ -307,7 +307,7 @@ def _pmc_traffic():
     """HBM bytes per contraction launch (FETCH_SIZE + WRITE_SIZE, rocprofv3 KB x 1024) from the
     committed PMC passes over the same workload (counters need their own rocprofv3 runs, so they
     cannot be read live here); the newest round's file wins."""
-    for name in ("r03_pmc_maxcut10.json", "r02_pmc_maxcut10.json", "r01_pmc_maxcut10.json"):
+    for name in ("r04_pmc_maxcut10.json", "r03_pmc_maxcut10.json", "r02_pmc_maxcut10.json", "r01_pmc_maxcut10.json"):
         try:
             ks = json.load(open(os.path.join(HERE, "profiles", name)))["kernels"]
         except (OSError, KeyError, ValueError):
@@ -599,13 +599,19 @@ def main():
 
     roofline = None
     if not args.no_roofline and rank == 0:
+        # every distinct seed this rank timed, re-solved once with each contraction launch bracketed by
+        # HIP events on its stream (untimed for `value`): the same seed mix as the timed region, so a
+        # rocprofv3 --stats pass over the same command averages the same kernels
+        roof_seeds = list(dict.fromkeys(s for sl in slot_seeds for s in sl))
         st = (ctypes.c_double * 5)()
         lib.ttk_contract_stats(st, 1)
         lib.ttk_contract_timing(1)
         D.ALGO = {"flops": 0.0, "calls": 0, "by": {}}
         s0, l0 = lib.ttk_sync_count(), lib.ttk_launch_count()
+        its = 0
         try:
-            rr = solve(shard.unpack(*packed[mine_seeds[0]]))
+            for sd in roof_seeds:
+                its += solve(shard.unpack(*packed[sd]))["num_iters"]
             sync()
         finally:
             lib.ttk_contract_timing(0)
@@ -613,17 +619,18 @@ def main():
         syncs, all_launches = lib.ttk_sync_count() - s0, lib.ttk_launch_count() - l0
         lib.ttk_contract_stats(st, 1)
         flops, launches, tflops, tl, tms = list(st)
+        ns = max(len(roof_seeds), 1)
         if tms > 0:
             ach = algo["flops"] / (tms * 1e-3)
             roofline = {"bound": "mfma", "achieved": ach / 1e12, "peak": FP64_MATRIX_PEAK / 1e12,
                         "unit": "TFLOP/s", "frac": ach / FP64_MATRIX_PEAK, "traffic": _pmc_traffic(),
                         "kernel": "contraction kernels: gemm_offs* (fp64 MFMA offset-table GEMM), fused local "
                                   "apply, Schur multi-task apply; traffic = HBM bytes per gemm_offs launch",
-                        "seed": mine_seeds[0], "algorithmic_flops_per_solve": algo["flops"],
-                        "algorithmic_calls_per_solve": algo["calls"], "device_flops_per_solve": tflops,
-                        "launches_per_solve": int(tl), "kernel_ms_per_solve": tms,
-                        "all_launches_per_ipm_iter": all_launches / max(rr["num_iters"], 1),
-                        "host_syncs_per_ipm_iter": syncs / max(rr["num_iters"], 1),
+                        "seeds": roof_seeds, "algorithmic_flops_per_solve": algo["flops"] / ns,
+                        "algorithmic_calls_per_solve": algo["calls"] / ns, "device_flops_per_solve": tflops / ns,
+                        "launches_per_solve": tl / ns, "kernel_ms_per_solve": tms / ns,
+                        "all_launches_per_ipm_iter": all_launches / max(its, 1),
+                        "host_syncs_per_ipm_iter": syncs / max(its, 1),
                         "avg_launch_us": tms * 1e3 / max(tl, 1),
                         "algorithmic_flops_per_launch": algo["flops"] / max(tl, 1),
                         "algorithmic_by_op": dict(sorted(algo["by"].items(), key=lambda kv: -kv[1][1])[:10])}

@@ -31,19 +31,19 @@ for step in "$@"; do
              || { tail -20 gpurun_out/${tag}_smoke.log; exit 1; }
            tail -2 gpurun_out/${tag}_smoke.log ;;
     bench) args=${rest:-"--steps 5 --warmup 1"}
-           timeout -k 10 900 python bench.py $args > gpurun_out/${tag}_bench.json 2> gpurun_out/${tag}_bench.err \
+           timeout -k 10 900 python bench.py $args --detail gpurun_out/${tag}_bench_detail.json > gpurun_out/${tag}_bench.json 2> gpurun_out/${tag}_bench.err \
              || { tail -20 gpurun_out/${tag}_bench.err; exit 1; }
            cut -c1-600 gpurun_out/${tag}_bench.json ;;
     stats) args=${rest:-"--steps 5 --warmup 1 --no-cpu-baseline --inflight 1"}
            st=${tag}_s${idx}
            timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/${st}_stats -o run -- \
-             python3 bench.py $args > gpurun_out/${st}_stats.log 2>&1 || { tail -20 gpurun_out/${st}_stats.log; exit 1; }
+             python3 bench.py $args --detail gpurun_out/${st}_detail.json > gpurun_out/${st}_stats.log 2>&1 || { tail -20 gpurun_out/${st}_stats.log; exit 1; }
            # keep the summaries only (the full kernel trace exceeds what gpurun copies back)
            for f in $(find /tmp/${st}_stats -name "*stats.csv"); do cp $f gpurun_out/${st}_$(basename $f); done
            ls gpurun_out/ | grep "^${tag}_" ;;
     pmc)   cn=${rest%%:*}; args=${rest#*:}; [ "$args" = "$rest" ] && args="--steps 1 --warmup 0 --no-cpu-baseline --no-roofline --inflight 1"
            timeout -s KILL 300 rocprofv3 --pmc ${cn//,/ } --kernel-trace --output-format csv -d /tmp/${tag}_pmc_${cn%%,*} -o run -- \
-             python3 bench.py $args > gpurun_out/${tag}_pmc_${cn%%,*}.log 2>&1 || { tail -20 gpurun_out/${tag}_pmc_${cn%%,*}.log; exit 1; }
+             python3 bench.py $args --detail "" > gpurun_out/${tag}_pmc_${cn%%,*}.log 2>&1 || { tail -20 gpurun_out/${tag}_pmc_${cn%%,*}.log; exit 1; }
            # per-kernel summary only (the per-dispatch CSV is large)
            python tools/pmc_summary.py /tmp/${tag}_pmc_${cn%%,*} gpurun_out/${tag}_pmc_${cn%%,*}.json | tail -4 ;;
     py)    script=${rest%%:*}; args=${rest#*:}; [ "$args" = "$rest" ] && args=""
