@@ -319,7 +319,11 @@ if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "merge":  # merge KEY TMP: a run finished outside make_runs
         merge(sys.argv[2], sys.argv[3])
         sys.exit(0)
-    what = sys.argv[1] if len(sys.argv) > 1 else "all"
+    if len(sys.argv) < 2 or sys.argv[1] not in ("runs", "prims", "all"):
+        # no default: a bare invocation must not start regenerating (and rewriting) runs.json
+        sys.exit("usage: make_golden.py runs|prims|all [KEY ...] [-jN] | one PROB CFG SEED RANK FIXED OUT [NMAX]"
+                 " | merge KEY TMP")
+    what = sys.argv[1]
     rest = [a for a in sys.argv[2:] if not a.startswith("-j")]
     jobs = max([int(a[2:]) for a in sys.argv[2:] if a.startswith("-j")] or [1])
     if what in ("runs", "all"):
