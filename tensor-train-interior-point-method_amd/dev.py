@@ -576,10 +576,12 @@ _DUMP = {"min": int(os.environ.get("TTIPM_DUMP_SVD", "0")), "max": int(os.enviro
          "qmin": int(os.environ.get("TTIPM_DUMP_SVD_QMIN", "0")), "n": 0}
 
 
-def svd(A, defl=0.0, host=True):
+def svd(A, defl=0.0, host=True, S_out=None):
     """Thin SVD of a 2-D device matrix.  Returns (U, S, Vt, s_host).  `defl` > 0 lets the large-
     matrix path deflate directions whose total Frobenius norm is <= defl (S = 0 there).
-    host=False: no host copy of S (s_host None), so the call does not synchronise."""
+    host=False: no host copy of S (s_host None), so the call does not synchronise.  `S_out`: a
+    contiguous device slice of length min(m, n) that receives S (to be read together with other
+    device scalars in one host wait)."""
     t0 = _tic() if OPSTATS is not None else 0
     A = A.contiguous()
     m, n = A.shape
@@ -589,7 +591,7 @@ def svd(A, defl=0.0, host=True):
         np.save(f"gpurun_out/svd_in_{_DUMP['n']}.npy", read(A))
         _DUMP["n"] += 1
     k = min(m, n)
-    U, S, Vt = empty(m, k), empty(k), empty(k, n)
+    U, S, Vt = empty(m, k), (empty(k) if S_out is None else S_out), empty(k, n)
     work = empty(int(lib.ttk_svd_work(m, n)))
     check(lib.ttk_svd_tol(_stream(), _p(A), m, n, _p(U), _p(S), _p(Vt), _p(work), float(defl)), "svd")
     sh = read(S) if host else None
@@ -684,16 +686,20 @@ def syev(A):
     return ev, W, evh
 
 
-def syev_extreme(A, largest=False):
+def syev_extreme(A, largest=False, lam_out=None):
     """One extreme eigenpair of a symmetric device matrix (Householder tridiagonalisation +
-    multisection + inverse iteration, one launch).  Returns (eigenvalue float, unit vector)."""
+    multisection + inverse iteration, one launch).  Returns (eigenvalue float, unit vector); with
+    `lam_out` (a device slice of length 1) the eigenvalue stays there and is not read: (None, vector)."""
     t0 = _tic() if OPSTATS is not None else 0
     A = A.contiguous()
     n = A.shape[0]
-    buf = empty(n + 1)
+    buf = empty(n + 1) if lam_out is None else None
+    lam_p, vec = (buf[:1], buf[1:]) if lam_out is None else (lam_out, empty(n))
     work = empty(int(lib.ttk_syev_extreme_work(n)))
-    check(lib.ttk_syev_extreme(_stream(), _p(A), n, 1 if largest else 0, _p(buf), _p(buf[1:]), _p(work)),
+    check(lib.ttk_syev_extreme(_stream(), _p(A), n, 1 if largest else 0, _p(lam_p), _p(vec), _p(work)),
           "syev_extreme")
+    if lam_out is not None:
+        return None, vec
     lam = float(read(buf[:1])[0])
     if OPSTATS is not None:
         _stat("syev_extreme", n, t0, site_min=n >= 200)

@@ -333,49 +333,74 @@ def _sweep(c, backward, swp, last, dsf):
         Ak = c.A[k]
         bk = c.b.core(k)
         solving = swp > 0 and not last
-        resz = None
-        if solving:
-            prev = x[k]
-            sol, res_old, res_new, rhs, nrhs, dsf = c.local_solver(
-                c.XAX[k], Ak, c.XAX[k + 1], c.Xb[k], bk, c.Xb[k + 1], prev, 3 * d, not dsf)
-            local_res = max(local_res, res_old)
-            if sol is not prev:
-                diff = D.axpby(prev, sol, -1.0, 1.0, 1.0)  # sol - prev, one launch (= clone + copy_)
-                j = sum(1 for t in dx_seq if t is not None)
-                D.dot_into(diff, diff, dx_buf[2 * j:2 * j + 1])
-                D.dot_into(sol, sol, dx_buf[2 * j + 1:2 * j + 2])
-                dx_seq.append(j)
-            else:
-                dx_seq.append(None)
-            if amen:
-                zsh = (rz[k], B, N[k], rz[k + 1])
-                rz_ = D.zeros(*zsh)
-                rhs_local_product(bk, c.Zb[k], c.Zb[k + 1], rz_)
-                Az = D.zeros(*zsh)
-                Ak.compressed_block_local_product(c.ZAX[k], c.ZAX[k + 1], sol, Az)
-                D.copy_(rz_, Az, -1.0, 1.0)
-                if backward:
-                    resz = rz_.view(rz[k] * B, N[k] * rz[k + 1]).t()
+        interior = (k > 0) if backward else (k < d - 1)
+
+        def prep(sol, solved):
+            """everything of the core step between the local solve and the truncation SVD"""
+            resz = None
+            if solved:
+                if sol is not prev:
+                    diff = D.axpby(prev, sol, -1.0, 1.0, 1.0)  # sol - prev, one launch (= clone + copy_)
+                    j = sum(1 for t in dx_seq if t is not None)
+                    D.dot_into(diff, diff, dx_buf[2 * j:2 * j + 1])
+                    D.dot_into(sol, sol, dx_buf[2 * j + 1:2 * j + 2])
+                    dx_seq.append(j)
                 else:
-                    resz = D.clone(rz_.permute(0, 2, 1, 3)).view(rz[k] * N[k], B * rz[k + 1])
-            sc, scd, inv = _scales(sol)
-        else:
-            sol = x[k]
-            sc, scd, inv = _scales(sol)
-            if amen and not last:
+                    dx_seq.append(None)
+                if amen:
+                    zsh = (rz[k], B, N[k], rz[k + 1])
+                    rz_ = D.zeros(*zsh)
+                    rhs_local_product(bk, c.Zb[k], c.Zb[k + 1], rz_)
+                    Az = D.zeros(*zsh)
+                    Ak.compressed_block_local_product(c.ZAX[k], c.ZAX[k + 1], sol, Az)
+                    D.copy_(rz_, Az, -1.0, 1.0)
+                    if backward:
+                        resz = rz_.view(rz[k] * B, N[k] * rz[k + 1]).t()
+                    else:
+                        resz = D.clone(rz_.permute(0, 2, 1, 3)).view(rz[k] * N[k], B * rz[k + 1])
+            elif amen and not last:
                 if backward:
                     resz = D.contig(z[k]).view(rz[k] * B, N[k] * rz[k + 1]).t()
                 else:
                     resz = D.clone(z[k].permute(0, 2, 1, 3)).view(rz[k] * N[k], B * rz[k + 1])
-        if backward:
-            scaled = _scale_blocks(sol, scd)
-            mat = scaled.view(rx[k] * B, N[k] * rx[k + 1]).t()
-        else:  # scaled straight into (r, n, B, R) storage: the forward unfolding needs no copy
-            store = D.empty(rx[k], N[k], B, rx[k + 1])
-            scaled = _scale_blocks(sol, scd, out=store.permute(0, 2, 1, 3))
-            mat = store.view(rx[k] * N[k], B * rx[k + 1])
+            sc, scd, inv = _scales(sol)
+            if backward:
+                scaled = _scale_blocks(sol, scd)
+                mat = scaled.view(rx[k] * B, N[k] * rx[k + 1]).t()
+            else:  # scaled straight into (r, n, B, R) storage: the forward unfolding needs no copy
+                store = D.empty(rx[k], N[k], B, rx[k + 1])
+                scaled = _scale_blocks(sol, scd, out=store.permute(0, 2, 1, 3))
+                mat = store.view(rx[k] * N[k], B * rx[k + 1])
+            return resz, inv, scaled, mat
 
-        interior = (k > 0) if backward else (k < d - 1)
+        svd_out = None
+        if solving:
+            # the new local residual (`_ipm_local_solver`: keep prev if it got worse) comes back in
+            # ONE read with the truncation SVD's singular values: the core step is enqueued on the
+            # solver's solution, and redone on prev in the rare case the residual grew
+            prev = x[k]
+            kk = min(rx[k] * B, N[k] * rx[k + 1]) if backward else min(rx[k] * N[k], B * rx[k + 1])
+            comb = D.empty(1 + (kk if interior else 0))
+            sol, res_old, _, rhs, nrhs, dsf = c.local_solver(
+                c.XAX[k], Ak, c.XAX[k + 1], c.Xb[k], bk, c.Xb[k + 1], prev, 3 * d, not dsf, res_out=comb[:1])
+            local_res = max(local_res, res_old)
+            resz, inv, scaled, mat = prep(sol, True)
+            if interior:
+                svd_out = D.svd(D.contig(mat), host=False, S_out=comb[1:])
+            h = D.read(comb)
+            res_new = D.norm_of(h[0]) / nrhs
+            if res_old < res_new and sol is not prev:
+                dx_seq.pop()
+                sol = prev
+                resz, inv, scaled, mat = prep(sol, True)
+                svd_out = None
+            elif interior:
+                svd_out = svd_out[:3] + (h[1:],)
+            res_new = min(res_old, res_new)
+        else:
+            sol = x[k]
+            resz, inv, scaled, mat = prep(sol, False)
+
         if not interior:
             if backward:
                 x[k] = _div_blocks_bdim(scaled, inv, 1)
@@ -389,7 +414,7 @@ def _sweep(c, backward, swp, last, dsf):
                     z[k] = _div_blocks_bdim(zz, inv, 1)
             continue
 
-        U, S, Vt, s = D.svd(D.contig(mat))
+        U, S, Vt, s = D.svd(D.contig(mat)) if svd_out is None else svd_out
         v = einsum("r,rj->rj", S, Vt)  # s * v
         if not backward:
             u3 = U.view(rx[k], N[k], -1)

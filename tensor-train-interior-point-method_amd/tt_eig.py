@@ -105,15 +105,21 @@ def _kick_rev(u, v, r_add):
     return D.matmul(u, Rm[:old]), q, q.shape[0]
 
 
-def _split(sol, sh, trunc_tol, max_rank, bwd):
+def _split_svd(sol, sh, bwd, S_out=None):
+    """the SVD `_split` truncates (S into `S_out` without a host read when given)"""
     a, b = sh[0] * sh[1], sh[2] * sh[3]
+    mat = D.clone(sol.view(a, b).t()) if bwd else sol.view(a, b)
+    return D.svd(mat, host=S_out is None, S_out=S_out)
+
+
+def _split(sol, sh, trunc_tol, max_rank, bwd, pre=None):
+    """`pre`: the (U, S, Vt, s) of `_split_svd(sol, ...)` when already computed"""
+    U, S, Vt, s = _split_svd(sol, sh, bwd) if pre is None else pre
     if bwd:
-        U, S, Vt, s = D.svd(D.clone(sol.view(a, b).t()))
         v = einsum("r,rj->rj", S, Vt)
         r = min(T.prune_singular_vals(s, trunc_tol), max_rank)
         s1, s2, r = _kick_rev(v[:r].t(), U[:, :r].t(), 4)  # strided operands: no transpose copies
         return D.contig(s1).view(sh[0], sh[1], r), D.contig(s2).view(r, sh[2], sh[3])
-    U, S, Vt, s = D.svd(sol.view(a, b))
     r = min(T.prune_singular_vals(s, trunc_tol), max_rank)
     s2 = einsum("r,rj->rj", S[:r], Vt[:r])
     s1, s2, r = _kick(U[:, :r], s2, 4)  # the kick copies the truncated factor itself
@@ -303,14 +309,34 @@ class _EigThread(threading.local):
 _ET = _EigThread()  # per host thread: several solves may run at once in one process
 
 
-def _dense_step(prev, Am, Dm, step, eps, tag):
+def _dense_step(prev, Am, Dm, step, eps, tag, post=None):
     """dense branch of the step-size local solves: M = A/step + D, smallest eigenpair; if negative,
-    the largest lambda of -D v = lambda A v bounds the step (`src/tt_als.py:957-996,1060-1101`)."""
+    the largest lambda of -D v = lambda A v bounds the step (`src/tt_als.py:957-996,1060-1101`).
+
+    `post` = (k, fn): the caller's next device step on the solution -- fn(sol, S_out) enqueues the
+    truncation SVD (k singular values into S_out) and returns its (U, S, Vt, None).  It is enqueued
+    speculatively right behind the eigensolve, on the branch taken when ev >= 0, and the eigenvalue
+    and the k singular values come back in ONE host read; on ev < 0 that work is dropped (it has no
+    side effects) and the caller redoes it on the branch's solution.  Returns (sol, step, residual,
+    pre) with pre = the SVD tuple (host singular values filled in) or None."""
     M = _shifted(Am, Dm, step)
-    ev, sol = _min_eigpair(M)
+    pre = None
+    if post is not None:
+        k, fn = post
+        comb = D.empty(1 + k)
+        _, sol = D.syev_extreme(M, largest=False, lam_out=comb[:1])
+        if tag == "two-site":
+            sol = _normalise(sol)
+        U, S, Vt, _ = fn(sol, comb[1:])
+        h = D.read(comb)
+        ev = float(h[0])
+        if not ev < 0:
+            pre = (U, S, Vt, h[1:])
+    else:
+        ev, sol = _min_eigpair(M)
+        if tag == "two-site":
+            sol = _normalise(sol)
     step_in, branch = step, "keep"
-    if tag == "two-site":
-        sol = _normalise(sol)
     if ev < 0:
         try:
             lam, sol = _gen_max_eig(Dm, Am)
@@ -325,11 +351,11 @@ def _dense_step(prev, Am, Dm, step, eps, tag):
     df = _ET.defer if _FUSED_TAIL and prev.is_contiguous() else None
     if df == "skip":  # the caller discards the residual: only its 1/step (ZeroDivisionError at 0) matters
         1.0 / step
-        return sol, step, None
+        return sol, step, None, pre
     if df is not None:
-        return sol, step, df.rayleigh(Am, Dm, step, prev)
+        return sol, step, df.rayleigh(Am, Dm, step, prev), pre
     old_res = _rayleigh(Am, Dm, step, prev)[1]  # 1/step raises ZeroDivisionError at step 0, as the reference
-    return sol, step, old_res
+    return sol, step, old_res, pre
 
 
 def _iterative_step(prev, apply_A, apply_D, step, eps, tag):
@@ -392,7 +418,13 @@ def _step_size_local_solve(p1, p2, XAX_k, A_k, A_kp1, XAX_k2, XDX_k, D_k, D_kp1,
         pv = prev.view(-1)
         Dm = _sym(einsum(TWO_SITE, XDX_k, D_k, D_kp1, XDX_k2), m)
         Am = _sym(einsum(TWO_SITE, XAX_k, A_k, A_kp1, XAX_k2), m)
-        sol, step, old_res = _dense_step(pv, Am, Dm, step, eps, "two-site")
+        k = min(sh[0] * sh[1], sh[2] * sh[3])
+        sol, step, old_res, pre = _dense_step(
+            pv, Am, Dm, step, eps, "two-site",
+            post=(k, lambda v, S_out: _split_svd(_normalise(v), sh, bwd, S_out)) if _FUSED_TAIL else None)
+        if pre is not None:
+            s1, s2 = _split(None, sh, trunc_tol, max_rank, bwd, pre=pre)
+            return s1, s2, step, old_res
     else:
         pv = prev.view(-1)
         eq = "lsr,smnk,kptS,LSR,rntR->lmpL"
@@ -404,11 +436,12 @@ def _step_size_local_solve(p1, p2, XAX_k, A_k, A_kp1, XAX_k2, XDX_k, D_k, D_kp1,
     return s1, s2, step, old_res
 
 
-def _step_size_local_solve_last(prev, XDX_k, Dk, XDX_k1, XAX_k, Ak, XAX_k1, dense, step, eps):
+def _step_size_local_solve_last(prev, XDX_k, Dk, XDX_k1, XAX_k, Ak, XAX_k1, dense, step, eps, post=None):
     """`_step_size_local_solve_last` (`src/tt_als.py:1056-1129`); `dense` is the reference's
-    sqrt(r R) < size_limit flag."""
+    sqrt(r R) < size_limit flag.  Returns (sol, step, residual, pre): `post` / `pre` as in
+    `_dense_step` (dense branch only; pre is None otherwise)."""
     if (not np.isfinite(step)) or step <= 0:
-        return prev.reshape(-1) if prev.is_contiguous() else D.clone(prev).view(-1), 0.0, np.inf
+        return prev.reshape(-1) if prev.is_contiguous() else D.clone(prev).view(-1), 0.0, np.inf, None
     m = int(np.prod(prev.shape))
     xs = tuple(prev.shape)
     pv = D.contig(prev).view(-1)
@@ -416,10 +449,11 @@ def _step_size_local_solve_last(prev, XDX_k, Dk, XDX_k1, XAX_k, Ak, XAX_k1, dens
         _check_dense(m)
         Dm = _sym(einsum(ONE_SITE, XDX_k, Dk, XDX_k1), m)
         Am = _sym(einsum(ONE_SITE, XAX_k, Ak, XAX_k1), m)
-        return _dense_step(pv, Am, Dm, step, eps, "one-site")
+        return _dense_step(pv, Am, Dm, step, eps, "one-site", post=post if _FUSED_TAIL else None)
     eq = "lsr,smnS,LSR,rnR->lmL"
     return _iterative_step(pv, lambda v: einsum(eq, XAX_k, Ak, XAX_k1, v.view(*xs)).view(-1),
-                           lambda v: einsum(eq, XDX_k, Dk, XDX_k1, v.view(*xs)).view(-1), step, eps, "one-site")
+                           lambda v: einsum(eq, XDX_k, Dk, XDX_k1, v.view(*xs)).view(-1), step, eps,
+                           "one-site") + (None,)
 
 
 def _res_stalled(prev, res, tol):
@@ -466,11 +500,14 @@ def tt_max_generalised_eigen(A, Delta, x0=None, nswp=10, tol=1e-8, size_limit=25
         nonlocal step
         _ET.defer = "skip"  # the last local solves' residuals are discarded
         for k in range(d):
-            sol, step, _ = _step_size_local_solve_last(x[k], XDX[k], Delta[k], XDX[k + 1], XAX[k], A[k], XAX[k + 1],
-                                                       np.sqrt(rx[k] * rx[k + 1]) < size_limit, step, tol)
+            a, b = rx[k] * N[k], rx[k + 1]
+            post = (min(a, b), lambda v, S_out: D.svd(v.view(a, b), host=False, S_out=S_out)) if k < d - 1 else None
+            sol, step, _, pre = _step_size_local_solve_last(x[k], XDX[k], Delta[k], XDX[k + 1], XAX[k], A[k],
+                                                            XAX[k + 1], np.sqrt(rx[k] * rx[k + 1]) < size_limit,
+                                                            step, tol, post)
             sol = sol.view(rx[k] * N[k], rx[k + 1])
             if k < d - 1:
-                U, S, Vt, s = D.svd(sol)
+                U, S, Vt, s = D.svd(sol) if pre is None else pre
                 v = einsum("r,rj->rj", S, Vt)
                 r = min(T.prune_singular_vals(s, trunc_tol), max_rank)
                 x[k] = D.clone(U[:, :r]).view(rx[k], N[k], r)
@@ -486,11 +523,18 @@ def tt_max_generalised_eigen(A, Delta, x0=None, nswp=10, tol=1e-8, size_limit=25
         nonlocal step
         _ET.defer = "skip"  # the last local solves' residuals are discarded
         for k in range(d - 1, -1, -1):
-            sol, step, _ = _step_size_local_solve_last(x[k], XDX[k], Delta[k], XDX[k + 1], XAX[k], A[k], XAX[k + 1],
-                                                       np.sqrt(rx[k] * rx[k + 1]) < size_limit, step, tol)
+            a, b = rx[k], N[k] * rx[k + 1]
+            post = (min(a, b), lambda v, S_out: D.svd(D.clone(v.view(a, b).t()), host=False, S_out=S_out)) \
+                if k > 0 else None
+            sol, step, _, pre = _step_size_local_solve_last(x[k], XDX[k], Delta[k], XDX[k + 1], XAX[k], A[k],
+                                                            XAX[k + 1], np.sqrt(rx[k] * rx[k + 1]) < size_limit,
+                                                            step, tol, post)
             if k > 0:
-                mat = D.clone(sol.view(rx[k], N[k] * rx[k + 1]).t())
-                U, S, Vt, s = D.svd(mat)
+                if pre is None:
+                    mat = D.clone(sol.view(rx[k], N[k] * rx[k + 1]).t())
+                    U, S, Vt, s = D.svd(mat)
+                else:
+                    U, S, Vt, s = pre
                 v = einsum("r,rj->rj", S, Vt)
                 r = min(T.prune_singular_vals(s, trunc_tol), max_rank)
                 x[k] = D.clone(U[:, :r].t()).view(r, N[k], rx[k + 1])

@@ -172,22 +172,35 @@ def _local_rhs(Xb_k, b_k, Xb_k1, shape, nb):
     return rhs
 
 
-def _residual_norm(A_k, XAX_k, XAX_k1, x, rhs, nrhs):
+def _residual_norm(A_k, XAX_k, XAX_k1, x, rhs, nrhs, res_out=None):
+    """||A x - rhs|| / nrhs; with `res_out` (a device slice of length 1) ||A x - rhs||^2 is left there
+    unread (the caller reads it together with later device scalars) and None is returned."""
     res = D.scaled(rhs, -1.0)
     A_k.block_local_product(XAX_k, XAX_k1, x, out=res)
+    if res_out is not None:
+        D.dot_into(res, res, res_out)
+        return None
     return D.norm(res) / nrhs
+
+
+def _rhs_and_residual_dots(A_k, XAX_k, XAX_k1, x, rhs, buf):
+    """<rhs, rhs> and ||A x - rhs||^2 into the device slots buf[0:2] (no host read)."""
+    D.dot_into(rhs, rhs, buf[0:1])
+    res = D.scaled(rhs, -1.0)
+    A_k.block_local_product(XAX_k, XAX_k1, x, out=res)
+    D.dot_into(res, res, buf[1:2])
+
+
+def _norms_from_dots(v):
+    nrhs = max(D.norm_of(v[0]), 1e-10)
+    return nrhs, D.norm_of(v[1]) / nrhs
 
 
 def _rhs_and_residual_norms(A_k, XAX_k, XAX_k1, x, rhs):
     """(max(||rhs||, 1e-10), ||A x - rhs|| / that) with ONE host read (both dots on the device)."""
     buf = D.empty(2)
-    D.dot_into(rhs, rhs, buf[0:1])
-    res = D.scaled(rhs, -1.0)
-    A_k.block_local_product(XAX_k, XAX_k1, x, out=res)
-    D.dot_into(res, res, buf[1:2])
-    v = D.read(buf)
-    nrhs = max(D.norm_of(v[0]), 1e-10)
-    return nrhs, D.norm_of(v[1]) / nrhs
+    _rhs_and_residual_dots(A_k, XAX_k, XAX_k1, x, rhs, buf)
+    return _norms_from_dots(D.read(buf))
 
 
 def _assemble(XAX_k, A_k, XAX_k1, key, m):
@@ -286,14 +299,54 @@ def _dense_python(XAX_k, A_k, XAX_k1, rhs, inv_I, xs):
     return sol
 
 
-def _ipm_local_solver(XAX_k, A_k, XAX_k1, Xb_k, b_k, Xb_k1, prev, size_limit, dense_solve=True, rtol=1e-5):
-    """`_ipm_local_solver` (`src/tt_ipm.py:183-282`) on the device."""
+def _lgmres_prologue(XAX_k, A_k, XAX_k1, inv_I, rhs, prev, xs, nb2):
+    """the Schur operator, the reduced right-hand side and its residual at `prev` (the iterative
+    branch of `src/tt_ipm.py:224-262`); <lrhs, lrhs> and ||lrhs - S prev||^2 into the device slots
+    nb2[0:2] (unread)."""
+    r, n, R = xs[0], xs[2], xs[3]
+    m = r * n * R
+    op = MatVecWrapper(XAX_k, A_k, XAX_k1, inv_I, (r, n, R))
+    lrhs = D.empty(2 * m)
+    l0, l1 = lrhs[:m].view(r, n, R), lrhs[m:].view(r, n, R)
+    D.copy_(l0, rhs[:, 0])
+    D.copy_(l1, rhs[:, 2])
+    w = D.empty(r, n, R)
+    D.mul_(w, inv_I, rhs[:, 1])
+    einsum(APPLY, XAX_k[2, 2], A_k[2, 2], XAX_k1[2, 2], w, out=l1, alpha=-1.0, beta=1.0)
+    D.dot_into(lrhs, lrhs, nb2[0:1])
+    pv = D.empty(2 * m)
+    D.copy_(pv.view(2, r, n, R), prev[:, :2].permute(1, 0, 2, 3))
+    lvec = op.matvec(pv)
+    diff = D.clone(lrhs)
+    D.copy_(diff, lvec, -1.0, 1.0)
+    D.dot_into(diff, diff, nb2[1:2])
+    return op, lrhs, diff
+
+
+def _ipm_local_solver(XAX_k, A_k, XAX_k1, Xb_k, b_k, Xb_k1, prev, size_limit, dense_solve=True, rtol=1e-5,
+                      res_out=None):
+    """`_ipm_local_solver` (`src/tt_ipm.py:183-282`) on the device.
+
+    Host waits: when the dense branch is ruled out by size or by the caller, the iterative branch's
+    prologue is enqueued before ANY read and its two norms come back with ||rhs|| and the old
+    residual in one read.  `res_out` (a device slot): the new residual's square is left there unread
+    and the returned res_new is None -- the caller reads it with its next device scalars and applies
+    `if res_old < res_new: sol = prev` itself (`_finish_local`)."""
     xs = tuple(prev.shape)
     r, n, R = xs[0], xs[2], xs[3]
     m = r * n * R
     rhs = _local_rhs(Xb_k, b_k, Xb_k1, xs, 3)
     inv_I = D.recip(einsum(DIAG, XAX_k[1, 2], A_k[1, 2], XAX_k1[1, 2]))
-    nrhs, res_old = _rhs_and_residual_norms(A_k, XAX_k, XAX_k1, prev, rhs)
+    pro, nv = None, None
+    if (np.sqrt(r * R) <= size_limit) and dense_solve:
+        nrhs, res_old = _rhs_and_residual_norms(A_k, XAX_k, XAX_k1, prev, rhs)
+    else:  # iterative branch whatever res_old is: one read for all four dots
+        buf = D.empty(4)
+        _rhs_and_residual_dots(A_k, XAX_k, XAX_k1, prev, rhs, buf[0:2])
+        pro = _lgmres_prologue(XAX_k, A_k, XAX_k1, inv_I, rhs, prev, xs, buf[2:4])
+        h = D.read(buf)
+        nrhs, res_old = _norms_from_dots(h[0:2])
+        nv = h[2:4]
     dense_solve = (np.sqrt(r * R) <= size_limit) and dense_solve and (res_old >= rtol)
     failed = not dense_solve
     sol = None
@@ -306,23 +359,11 @@ def _ipm_local_solver(XAX_k, A_k, XAX_k1, Xb_k, b_k, Xb_k1, prev, size_limit, de
             _report(e)
             failed = True
     if not dense_solve or failed:
-        op = MatVecWrapper(XAX_k, A_k, XAX_k1, inv_I, (r, n, R))
-        lrhs = D.empty(2 * m)
-        l0, l1 = lrhs[:m].view(r, n, R), lrhs[m:].view(r, n, R)
-        D.copy_(l0, rhs[:, 0])
-        D.copy_(l1, rhs[:, 2])
-        w = D.empty(r, n, R)
-        D.mul_(w, inv_I, rhs[:, 1])
-        einsum(APPLY, XAX_k[2, 2], A_k[2, 2], XAX_k1[2, 2], w, out=l1, alpha=-1.0, beta=1.0)
-        nb2 = D.empty(2)
-        D.dot_into(lrhs, lrhs, nb2[0:1])
-        pv = D.empty(2 * m)
-        D.copy_(pv.view(2, r, n, R), prev[:, :2].permute(1, 0, 2, 3))
-        lvec = op.matvec(pv)
-        diff = D.clone(lrhs)
-        D.copy_(diff, lvec, -1.0, 1.0)
-        D.dot_into(diff, diff, nb2[1:2])
-        nv = D.read(nb2)
+        if pro is None:
+            nb2 = D.empty(2)
+            pro = _lgmres_prologue(XAX_k, A_k, XAX_k1, inv_I, rhs, prev, xs, nb2)
+            nv = D.read(nb2)
+        op, lrhs, diff = pro
         lnorm = D.norm_of(nv[0])
         use_prev = D.norm_of(nv[1]) < lnorm
         if use_prev:
@@ -343,6 +384,9 @@ def _ipm_local_solver(XAX_k, A_k, XAX_k1, Xb_k, b_k, Xb_k1, prev, size_limit, de
             zt = D.clone(rhs[:, 1])
             einsum(APPLY_T, XAX_k[0, 1], A_k[0, 1], XAX_k1[0, 1], sol[:, 0], out=zt, alpha=-1.0, beta=1.0)
             D.mul_(sol[:, 2], inv_I, zt)
+    if res_out is not None:
+        _residual_norm(A_k, XAX_k, XAX_k1, sol, rhs, nrhs, res_out)
+        return sol, res_old, None, rhs, nrhs, failed
     res_new = _residual_norm(A_k, XAX_k, XAX_k1, sol, rhs, nrhs)
     if _LOCAL_TRACE:
         print(f"  local m={m} dense={dense_solve} failed={failed} res_old={res_old:.6e} res_new={res_new:.6e}")
@@ -424,8 +468,10 @@ def _dense_native_ineq(XAX_k, A_k, XAX_k1, rhs, inv_I, xs):
     return sol
 
 
-def _ipm_local_solver_ineq(XAX_k, A_k, XAX_k1, Xb_k, b_k, Xb_k1, prev, size_limit, dense_solve=True, rtol=1e-5):
-    """`_ipm_local_solver_ineq` (`src/tt_ipm.py:284-401`) on the device."""
+def _ipm_local_solver_ineq(XAX_k, A_k, XAX_k1, Xb_k, b_k, Xb_k1, prev, size_limit, dense_solve=True, rtol=1e-5,
+                           res_out=None):
+    """`_ipm_local_solver_ineq` (`src/tt_ipm.py:284-401`) on the device (`res_out` as in
+    `_ipm_local_solver`)."""
     xs = tuple(prev.shape)
     r, n, R = xs[0], xs[2], xs[3]
     m = r * n * R
@@ -486,6 +532,9 @@ def _ipm_local_solver_ineq(XAX_k, A_k, XAX_k1, Xb_k, b_k, Xb_k1, prev, size_limi
             D.copy_(sol[:, 0], l3[0])
             D.copy_(sol[:, 1], l3[1])
             D.copy_(sol[:, 3], l3[2])
+    if res_out is not None:
+        _residual_norm(A_k, XAX_k, XAX_k1, sol, rhs, nrhs, res_out)
+        return sol, res_old, None, rhs, nrhs, failed
     res_new = _residual_norm(A_k, XAX_k, XAX_k1, sol, rhs, nrhs)
     if res_old < res_new:
         sol = prev
@@ -570,15 +619,12 @@ def tt_compute_centrality(X, Z, st):
 def tt_infeasible_newton_system(lhs, C, X, Y, Z, Tt, L, Ladj, b, mask, st):
     """`src/tt_ipm.py:429-475`"""
     rhs = TTBlockVector()
+    # the residual norms are read once, after every device step that does not depend on them (the
+    # same steps in the same order: the random core picks of tt_scale stay where they were); the
+    # centrality row is built there too when it is certain to be (not central), and its norm -- the
+    # KKT row scaling's (`_tt_kkt_row_scales`) -- comes back in the same read
     pf = tt_compute_primal_feasibility(L, b, X, st)
-    npf = T.tt_norm(pf)
-    st.primal_error = np.divide(npf, st.primal_error_normalisation)
-    st.is_primal_feasible = np.less(st.primal_error, st.feasibility_tol)
     df = tt_compute_dual_feasibility(C, Ladj, Z, Y, Tt, st)
-    ndf = T.tt_norm(df)
-    st.dual_error = np.divide(ndf, st.dual_error_normalisation)
-    st.is_dual_feasible = np.less(st.dual_error, (1 + (st.ineq_status is IneqStatus.ACTIVE)) * st.feasibility_tol)
-    st.is_last_iter = st.is_last_iter or (st.is_primal_feasible and st.is_dual_feasible and st.is_central)
     if st.aho_direction:
         lhs[2, 1] = T.tt_psd_rank_reduce(T.tt_scale(0.5, T.tt_add(T.tt_IkronM(Z), T.tt_MkronI(Z))),
                                          eps=0.1 * st.eta * st.dual_error_normalisation)
@@ -587,8 +633,16 @@ def tt_infeasible_newton_system(lhs, C, X, Y, Z, Tt, L, Ladj, b, mask, st):
     else:
         lhs[2, 1] = T.tt_psd_rank_reduce(T.tt_MkronI(Z), eps=0.1 * st.eta * st.dual_error_normalisation)
         lhs[2, 2] = T.tt_psd_rank_reduce(T.tt_IkronM(X), eps=0.1 * st.eta * st.primal_error_normalisation)
+    cen = None if st.is_central else tt_compute_centrality(X, Z, st)
+    ips = T.tt_scalars([("ip", pf, pf), ("ip", df, df)] + ([("ip", cen, cen)] if cen is not None else []))
+    npf, ndf = T.norm_from_ip(ips[0]), T.norm_from_ip(ips[1])
+    st.primal_error = np.divide(npf, st.primal_error_normalisation)
+    st.is_primal_feasible = np.less(st.primal_error, st.feasibility_tol)
+    st.dual_error = np.divide(ndf, st.dual_error_normalisation)
+    st.is_dual_feasible = np.less(st.dual_error, (1 + (st.ineq_status is IneqStatus.ACTIVE)) * st.feasibility_tol)
+    st.is_last_iter = st.is_last_iter or (st.is_primal_feasible and st.is_dual_feasible and st.is_central)
     # the row norms the KKT row scaling reads (`_tt_kkt_row_scales`) are these same values: kept with
-    # the row objects instead of being recomputed (one host read each)
+    # the row objects instead of being recomputed
     rhs._norms = {}
     if not st.is_primal_feasible or st.is_last_iter:
         rhs[0] = pf
@@ -596,7 +650,10 @@ def tt_infeasible_newton_system(lhs, C, X, Y, Z, Tt, L, Ladj, b, mask, st):
     if not st.is_dual_feasible or st.is_last_iter:
         rhs[1] = df
         rhs._norms[1] = (df, ndf)
-    if not st.is_central or st.is_last_iter:
+    if cen is not None:
+        rhs[2] = cen
+        rhs._norms[2] = (cen, T.norm_from_ip(ips[2]))
+    elif st.is_last_iter:
         rhs[2] = tt_compute_centrality(X, Z, st)
     if st.ineq_status is IneqStatus.ACTIVE:
         lhs[3, 1] = T.tt_diag_op(Tt, 0.1 * st.eta * st.dual_error_normalisation)
@@ -790,21 +847,24 @@ def _tt_ipm_newton_step(lhs, rhs, mask, X, Z, Tt, ZX, TX, st, solver):
             DT = T.tt_fast_hadamard(mask, T.tt_reshape(DT, (2, 2)), st.eps)
         xs, zs = _tt_get_step_sizes(X, Z, Tt, DX, DZ, DT, mask, st)
         if not st.is_central and not st.is_last_iter:
-            DXZ = T.tt_inner_prod(DX, DZ)
+            act = st.ineq_status is IneqStatus.ACTIVE
+            sv = T.tt_scalars([("ip", DX, DZ), ("ip", X, DZ), ("ip", DX, Z)]
+                              + ([("ip", DT, DX), ("ip", X, DT), ("sum", DT), ("ip", DX, Tt)] if act else []))
+            DXZ = sv[0]
             if st.verbose:
                 print("\n--- Centering-Corrector  step ---", flush=True)
-            if st.ineq_status is IneqStatus.ACTIVE:
-                mu_aff = (ZX + xs * zs * DXZ + zs * T.tt_inner_prod(X, DZ) + xs * T.tt_inner_prod(DX, Z)
-                          + TX + xs * zs * T.tt_inner_prod(DT, DX)
-                          + zs * (T.tt_inner_prod(X, DT) + st.ineq_boundary_val * T.tt_entrywise_sum(DT))
-                          + xs * T.tt_inner_prod(DX, Tt))
+            if act:
+                mu_aff = (ZX + xs * zs * DXZ + zs * sv[1] + xs * sv[2]
+                          + TX + xs * zs * sv[3]
+                          + zs * (sv[4] + st.ineq_boundary_val * sv[5])
+                          + xs * sv[6])
                 e = max(1, 3 * min(xs, zs) ** 2)
                 st.sigma = min(0.99, max(mu_aff / (ZX + TX), 0) ** e)
                 if st.sigma > 1e-4:
                     rhs[3] = T.tt_rank_reduce(T.tt_add(T.tt_scale(st.sigma * st.mu, T.tt_reshape(mask, (4,))),
                                                        rhs.get_row(3)), 0.1 * st.eta * st.centrl_error_normalisation)
             else:
-                mu_aff = ZX + xs * zs * DXZ + zs * T.tt_inner_prod(X, DZ) + xs * T.tt_inner_prod(DX, Z)
+                mu_aff = ZX + xs * zs * DXZ + zs * sv[1] + xs * sv[2]
                 e = max(1, 3 * min(xs, zs) ** 2)
                 st.sigma = min(0.99, max(mu_aff / ZX, 0) ** e)
             ce = 0.1 * st.eta * st.centrl_error_normalisation
@@ -951,11 +1011,13 @@ def tt_ipm(lag_maps, obj_tt, lin_op_tt, bias_tt, ineq_mask=None, max_iter=100, m
             print("============================================\n Maximum #iterations reached!\n"
                   "============================================")
             st.is_last_iter = True
-        ZX = T.tt_inner_prod(Z, X)
-        TX = (T.tt_inner_prod(X, Tt) + st.ineq_boundary_val * T.tt_entrywise_sum(Tt)) \
-            if st.ineq_status is IneqStatus.ACTIVE else 0
+        act = st.ineq_status is IneqStatus.ACTIVE
+        sv = T.tt_scalars([("ip", Z, X), ("ip", C, T.tt_reshape(X, (4,)))]
+                          + ([("ip", X, Tt), ("sum", Tt)] if act else []))  # one host read
+        ZX = sv[0]
+        TX = (sv[2] + st.ineq_boundary_val * sv[3]) if act else 0
         st.mu = np.divide(abs(ZX) + abs(TX), (2 ** dim + (st.ineq_status is IneqStatus.ACTIVE) * st.num_ineq_constraints))
-        st.centrl_error_normalisation = 1 + abs(T.tt_inner_prod(C, T.tt_reshape(X, (4,))))
+        st.centrl_error_normalisation = 1 + abs(sv[1])
         st.centrality_error = st.mu / st.centrl_error_normalisation
         st.is_central = np.less(st.centrality_error, st.centrality_tol)
         st.eta = max(min(st.eta, 2 * st.mu), st.op_tol)

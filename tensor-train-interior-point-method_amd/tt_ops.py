@@ -167,8 +167,34 @@ def tt_inner_prod(t1, t2):
 
 def tt_norm(tt):
     """`src/tt_ops.py:306-310`"""
-    ip = tt_inner_prod(tt, tt)
+    return norm_from_ip(tt_inner_prod(tt, tt))
+
+
+def norm_from_ip(ip):
+    """tt_norm's formula on a read-back <tt, tt>"""
     return float(np.sqrt(ip)) if ip > 0 else 0.0
+
+
+def tt_scalars(specs):
+    """Several TT scalars with ONE host read: ("ip", t1, t2) = tt_inner_prod(t1, t2), ("sum", tt) =
+    tt_entrywise_sum(tt).  Each contraction chain is the one of the single-value function (same
+    launches, same order); its last step writes straight into the chain's slot of one buffer."""
+    buf = D.empty(max(len(specs), 1))
+    for i, sp in enumerate(specs):
+        slot = buf[i:i + 1].view(1, 1)
+        if sp[0] == "ip":
+            t1, t2 = sp[1], sp[2]
+            res = _const("one11", np.ones((1, 1)))
+            for j, (c1, c2) in enumerate(zip(t1, t2)):
+                res = D.einsum(_inner_eq(c1.dim()), res, c1, c2, out=slot if j == len(t1) - 1 else None)
+        else:
+            tt = sp[1]
+            eq = "ab,aijm,bijn->mn" if tt[0].dim() == 4 else "ab,aim,bin->mn"
+            one = _const("ones_" + "x".join(map(str, tt[0].shape[1:-1])), np.ones((1, *tt[0].shape[1:-1], 1)))
+            res = _const("one11", np.ones((1, 1)))
+            for j, c in enumerate(tt):
+                res = D.einsum(eq, res, c, one, out=slot if j == len(tt) - 1 else None)
+    return [float(v) for v in D.read(buf[:len(specs)])] if specs else []
 
 
 def tt_normalise(tt, radius=1):
