@@ -13,12 +13,14 @@
   and at N=1 the steps cycle through the config's seeds.  `replica`: every rank solves step i's
   N=1 seed.  Problems are created once per distinct seed on rank 0 and delivered by ONE broadcast
   (RCCL over xGMI with the nccl backend) before the timed region; no collective inside the IPM loop.
-* Solves in flight per GPU (`--inflight P`, default 2 at every N, so the 1/2/4/8-GPU series is
+* Solves in flight per GPU (`--inflight P`, default 4 at every N, so the 1/2/4/8-GPU series is
   like-for-like): a solve is a chain of small dependent launches that leaves most of the chip idle,
-  so each GPU runs P seeds at once, one process per solve on its default stream -- this process plus
-  P-1 workers spawned before the GPU is touched (an 8-GPU node runs 16 solve processes).  All slots
-  warm up, then are released together at the start of the timed region.  A step is P solves per GPU:
-  step i, rank p, slot j solves seeds[(i*N*P + p*P + j) mod S].
+  so each GPU runs P seeds at once: P/T processes (this one plus workers spawned before the GPU is
+  touched) of T = `--threads` (default 2) slot threads, each slot on its own created stream and
+  libttk context (an 8-GPU node runs 16 solve processes).  The bench processes get 8 HIP hardware
+  queues (`GPU_MAX_HW_QUEUES`, recorded in `env_knobs`).  All slots warm up, then are released
+  together at the start of the timed region.  A step is P solves per GPU: step i, rank p, slot j
+  solves seeds[(i*N*P + p*P + j) mod S].
 * Timed region: barrier + device sync on both sides of the K steps, max over ranks.
   `value` = (max-over-ranks wall) / (IPM iterations of all ranks): whole-job s per IPM-iteration.
 * `sec_per_iter_per_seed_median`: SURVEY.md §8(d)'s statistic as the reference runner measures it
@@ -154,6 +156,8 @@ class _Slots:
 
     def __init__(self, slot_seeds, packed, solve, warmup, device):
         import threading
+        if len(slot_seeds) > 1:  # a slot waiting for the GIL asks for it after 0.5 ms, not 5 ms
+            sys.setswitchinterval(SLOT_SWITCH_INTERVAL)
         self.n = len(slot_seeds)
         self.ready = threading.Barrier(self.n + 1)
         self.go = threading.Event()
@@ -324,17 +328,21 @@ def _pmc_traffic():
     return None
 
 
-DEFAULT_THREADS = 1  # solves in flight per process (slot threads; >1: one created HIP stream each)
-DEFAULT_INFLIGHT = 2  # solves in flight per GPU, the same at every N (like-for-like 1->8 series)
+DEFAULT_THREADS = 2  # solves in flight per process (slot threads, one created HIP stream each)
+DEFAULT_INFLIGHT = 4  # solves in flight per GPU, the same at every N (like-for-like 1->8 series)
+SLOT_SWITCH_INTERVAL = 0.0005  # sys.setswitchinterval for processes with several slot threads
+HW_QUEUES = 8  # GPU_MAX_HW_QUEUES for the bench processes (HIP's default is 4)
 
 
 def default_inflight(world):
-    """Solves in flight per GPU: DEFAULT_INFLIGHT (one process each, on its default stream) at every
-    N up to 8, so the 1/2/4/8-GPU series carries the same per-GPU load (an 8-GPU node then runs 16
-    solve processes, the process guard's limit).  Round-2/3 sweeps on one MI355X (maxcut_10 whole
-    job, 1 -> 0.39, 2 -> 0.20, 4 -> 0.106 s/IPM-iter) put the knee at 4, which an 8-GPU node cannot
-    hold with one process per solve; slot threads would, but they need created streams, and solves
-    on created streams slow each other down (profiles/r03_inflight_layouts.txt)."""
+    """Solves in flight per GPU: DEFAULT_INFLIGHT at every N up to 8, so the 1/2/4/8-GPU series
+    carries the same per-GPU load: 2 processes per GPU x DEFAULT_THREADS slot threads each (an 8-GPU
+    node then runs 16 solve processes, the process guard's limit).  Why threads work since round 4:
+    the launch-only library calls keep the GIL (`_lib.py`), a slot waiting for the GIL asks for it
+    after 0.5 ms, and each process gets 8 HIP hardware queues -- with HIP's default 4, a process's
+    two slot streams plus their libttk side streams share queues and two such processes slowed each
+    other down (maxcut_10, whole job: 2 processes x 1 slot 0.190, 2 x 2 slots 0.209 with 4 queues,
+    0.117-0.131 with 8 or 16; 2 x 3: 0.155, 2 x 4: 0.128; profiles/r04_inflight_layouts.txt)."""
     return max(1, min(DEFAULT_INFLIGHT, DEFAULT_THREADS * (16 // max(world, 1))))
 
 
@@ -427,7 +435,7 @@ def compose_line(problem, config, cfg_name, rank_tt, world, P, T, n_procs, steps
     cb = None
     if cpu is not None:
         cb = {k: v for k, v in cpu.items() if k != "per_seed"}
-    knobs = {k: v for k, v in sorted(os.environ.items()) if k.startswith(("TTK_", "TTIPM_"))}
+    knobs = {k: v for k, v in sorted(os.environ.items()) if k.startswith(("TTK_", "TTIPM_", "GPU_MAX_HW_QUEUES"))}
     line = {"metric": METRIC, "value": value, "unit": "s/IPM-iter", "n_gpus": world,
             "steps": steps, "warmup": warmup, "ms_per_step": elapsed * 1e3 / max(steps, 1),
             "higher_is_better": False, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
@@ -491,6 +499,9 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if not _profiled() and int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < HW_QUEUES:
+        # before anything initialises HIP here (and inherited by the GPU worker processes)
+        os.environ["GPU_MAX_HW_QUEUES"] = str(HW_QUEUES)
     with open(args.config) as f:
         config = yaml.safe_load(f)
     P = args.inflight if args.inflight else default_inflight(world)

@@ -108,12 +108,30 @@ _SIGS = {
     "ttk_lgmres_set_mw_threshold": (i32, [i32]),
 }
 
+# Entry points that wait for the device (a stream synchronisation or a blocking copy inside): they
+# release the GIL while they wait, so another solve thread of the process runs its host code then.
+BLOCKING = frozenset(n for n in _SIGS if "sync" in n) | frozenset((
+    "ttk_lgmres", "ttk_round", "ttk_zipup", "ttk_dense_schur_solve", "ttk_dense_schur_solve_ineq",
+    "ttk_lgmres_chunk", "ttk_lgmres_build", "ttk_lgmres_aug", "ttk_schur_build", "ttk_schur_free",
+    "ttk_ctx_create", "ttk_ctx_destroy", "ttk_upload", "ttk_dep_timeouts", "ttk_debug_counters",
+    "ttk_mfma_profile", "ttk_contract_stats", "ttk_gemm_hist"))
+# Every other (launch-only, microseconds) entry point keeps the GIL (ctypes.PyDLL calling
+# convention; TTK_HOLD_GIL=0 releases it on every call, as plain ctypes does).  A thread that drops
+# the GIL for a 3 us launch and takes it straight back makes a second solve thread of the process
+# wait for the GIL hand-over on every launch; holding it, the threads switch where one of them
+# waits for the device (2 slot threads of one process,
+# maxcut_10 s41 + s235: whole job 0.153 -> 0.141 s/IPM-iter, 0.130 with a 0.5 ms switch interval;
+# profiles/r04_slot_threads.txt).
+_held = ctypes.PyDLL(LIB_PATH) if os.environ.get("TTK_HOLD_GIL", "1") == "1" else None
+
 for _name, (_res, _args) in _SIGS.items():
     if os.environ.get("TTK_LIB_PATH") and not hasattr(lib, _name):
         continue  # diagnostics: an older build loaded for a bit-identity comparison
-    _f = getattr(lib, _name)
+    _f = getattr(_held if _held is not None and _name not in BLOCKING else lib, _name)
     _f.restype = _res
     _f.argtypes = _args
+    if _held is not None and _name not in BLOCKING:
+        setattr(lib, _name, _f)
 
 EXPORTED = tuple(_SIGS)
 

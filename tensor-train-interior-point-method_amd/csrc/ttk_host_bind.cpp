@@ -27,6 +27,7 @@ mul_fn g_mul = nullptr;
 // one launch stream per host thread: a process may drive several solves at once, one per thread,
 // each on its own stream and libttk context (bind() is called once on each such thread)
 thread_local void *g_stream = nullptr;
+bool g_release_gil = true;
 
 void bind(int64_t einsum_addr, int64_t copy_addr, int64_t mul_addr, int64_t stream) {
   g_einsum = reinterpret_cast<einsum_fn>(einsum_addr);
@@ -116,8 +117,10 @@ at::Tensor einsum(const std::string &eq, const std::vector<at::Tensor> &ops, c10
   }
   double *rp = res.data_ptr<double>();
   int rc;
-  {  // the launch itself touches no Python object: other solve threads may run meanwhile
+  if (g_release_gil) {  // the launch itself touches no Python object: other solve threads may run meanwhile
     pybind11::gil_scoped_release nogil;
+    rc = g_einsum(g_stream, eq.c_str(), desc, rp, alpha, beta);
+  } else {  // TTK_HOLD_GIL: threads switch only where one waits for the device (dev.py)
     rc = g_einsum(g_stream, eq.c_str(), desc, rp, alpha, beta);
   }
   check(rc, "einsum");
@@ -164,7 +167,10 @@ at::Tensor mul_(at::Tensor dst, const at::Tensor &a, const at::Tensor &b, double
 
 }  // namespace
 
+void set_release_gil(bool on) { g_release_gil = on; }
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.def("set_release_gil", &set_release_gil);
   m.def("bind", &bind);
   m.def("einsum", &einsum);
   m.def("copy_", &copy_);

@@ -119,6 +119,8 @@ def _load_bind():
 
 
 _BIND = _load_bind()
+if _BIND is not None and os.environ.get("TTK_HOLD_GIL", "1") == "1" and hasattr(_BIND, "set_release_gil"):
+    _BIND.set_release_gil(False)  # as the launch-only libttk entry points (_lib.py)
 
 
 def _fast():
