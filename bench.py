@@ -64,9 +64,11 @@ METRIC = "sec/IPM-iter (AMEn KKT solve), maxcut dim=10 r=1; MFMA util% on core-c
 FP64_MATRIX_PEAK = 78.6e12  # MI355X spec, FLOP/s
 HOST_SHARE = 16  # CPU share of one GPU on the box (nproc shows the whole machine)
 
-# Seeds beyond a config's own list, vetted non-pathological with the oracle in the build container
-# (maxcut_12 r=2 lists 5 seeds, the 8-GPU run needs 8).  See DESIGN.md §5.
-EXTRA_SEEDS = {"maxcut_12.yaml": [20, 19, 9]}
+# Seeds beyond a config's own list (maxcut_12 r=2 lists 5 seeds, the 8-GPU run
+# needs 8), chosen by a rule fixed in advance that looks at nothing but the reference: the first
+# seeds in seed order, skipping the config's own, whose reference run as shipped (tests/golden/
+# runs.json, src/utils.py:67) is not pathological.  tests/test_bench_schedule.py re-derives them.
+EXTRA_SEEDS = {"maxcut_12.yaml": [1, 9, 11]}
 
 
 class _Stop(Exception):

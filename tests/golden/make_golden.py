@@ -225,18 +225,18 @@ RUNS = [
     # the bench's extra maxcut_12 seeds (configs[4] needs 8 distinct seeds for 8 ranks): vetted as
     # non-pathological by these reference runs (src/utils.py:67-84)
     ("maxcut", "maxcut_12", 0, 2, True, 0),  # pathological in the reference (29 iterations, gap 2.1e-2)
-    ("maxcut", "maxcut_12", 1, 2, True, 0),
+    ("maxcut", "maxcut_12", 1, 2, True, 0),  # 16 iterations, gap 9.2e-4 (hash twins: bounded_twins.json)
     ("maxcut", "maxcut_12", 2, 2, True, 0),  # pathological in the reference (29 iterations, gap 4.3e-2)
     ("maxcut", "maxcut_12", 3, 2, True, 0),  # pathological in the reference (14 iterations, gap 1.3e-2)
     ("maxcut", "maxcut_12", 4, 2, True, 0),  # pathological in the reference (13 iterations, gap 0.38)
     ("maxcut", "maxcut_12", 5, 2, True, 0),  # pathological in the reference (10 iterations, gap 4.7)
     ("maxcut", "maxcut_12", 6, 2, True, 0),  # pathological in the reference (29 iterations, gap 2.1e-2)
-    ("maxcut", "maxcut_12", 7, 2, True, 0),
+    ("maxcut", "maxcut_12", 7, 2, True, 0),  # pathological in the reference (24 iterations, gap 5.3)
     ("maxcut", "maxcut_12", 8, 2, True, 0),  # pathological in the reference (29 iterations, gap 6.0e-3)
     ("maxcut", "maxcut_12", 9, 2, True, 0),
-    ("maxcut", "maxcut_12", 10, 2, True, 0),
-    ("maxcut", "maxcut_12", 11, 2, True, 0),
-    ("maxcut", "maxcut_12", 13, 2, True, 0),
+    ("maxcut", "maxcut_12", 10, 2, True, 0),  # pathological in the reference (29 iterations, gap 2.2e-2)
+    ("maxcut", "maxcut_12", 11, 2, True, 0),  # 14 iterations, gap 2.6e-4 (hash twins: bounded_twins.json)
+    ("maxcut", "maxcut_12", 13, 2, True, 0),  # pathological in the reference (29 iterations, gap 0.66)
     ("maxcut", "maxcut_12", 16, 2, True, 0),  # pathological in the reference (12 iterations, gap 0.17)
     ("maxcut", "maxcut_12", 18, 2, True, 0),  # pathological in the reference (17 iterations, gap 1.16e-3)
     ("maxcut", "maxcut_12", 19, 2, True, 0),
@@ -294,10 +294,10 @@ def make_runs(only=None, jobs=1):
         merge(key, tmp)
 
 
-def merge(key, tmp):
-    """add one finished run's JSON (`one` mode output) to runs.json under `key`"""
+def merge(key, tmp, store="runs.json"):
+    """add one finished run's JSON (`one` mode output) to runs.json (or `store`) under `key`"""
     import fcntl
-    path = os.path.join(HERE, "runs.json")
+    path = os.path.join(HERE, store)
     res = json.load(open(tmp))
     print(key, {k: res.get(k) for k in ("num_iters", "gap", "feas", "dual_feas", "sec_per_iter")}, flush=True)
     with open(path + ".lock", "w") as lk:  # several make_runs invocations may merge at once
@@ -318,6 +318,9 @@ if __name__ == "__main__":
         sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "merge":  # merge KEY TMP: a run finished outside make_runs
         merge(sys.argv[2], sys.argv[3])
+        sys.exit(0)
+    if len(sys.argv) > 1 and sys.argv[1] == "merge_twin":  # merge_twin KEY TMP: a bounded hash twin
+        merge(sys.argv[2], sys.argv[3], "bounded_twins.json")
         sys.exit(0)
     if len(sys.argv) < 2 or sys.argv[1] not in ("runs", "prims", "all"):
         # no default: a bare invocation must not start regenerating (and rewriting) runs.json

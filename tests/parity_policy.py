@@ -170,3 +170,57 @@ def check_relaxed(key, r):
     lo, hi = min(x["num_iters"] for x in allruns), max(x["num_iters"] for x in allruns)
     assert not is_pathological(r), r
     assert lo - 2 <= r["num_iters"] <= hi + 2, (r["num_iters"], lo, hi)
+
+
+# ---- bounded hash twins (tests/golden/bounded_twins.json): seeds whose full reference runs take
+# hours (maxcut_12 r=2 at 10^2-10^3 s per iteration) get the golden's first assemblies re-run
+# under PYTHONHASHSEED 0..3 (keys KEY_b<n>_h<h>); they measure where the reference's own noise
+# branches, so the follow rule above can be applied up to that point without full twins.
+BOUNDED_TWINS = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden",
+                                            "bounded_twins.json")))
+
+
+def bounded_twins(key):
+    return {k[len(key) + 1:]: v for k, v in sorted(BOUNDED_TWINS.items()) if k.startswith(key + "_b")}
+
+
+def check_bounded_follow(key, trace):
+    """The follow rule over the golden and its bounded hash twins: noise n_i = the largest relative
+    difference between the golden and a twin at assembly i (cumulated); the device must follow ONE
+    of these runs, rel <= max(1e-12, 50 n_i), at every assembly before n_i > 1e-3 that all of them
+    reached.  Returns (name of the run followed, the assembly where the noise branches or the
+    twins end, per-assembly distances to it)."""
+    g = RUNS[key]
+    tw = bounded_twins(key)
+    runs = [("golden", g["trace"])] + [(n, r["trace"]) for n, r in tw.items()]
+    n = min(len(t) for _, t in runs)
+    noise, cum = [], 0.0
+    for i in range(n):
+        cum = max([cum] + [max(_rel(t[i][k], g["trace"][i][k]) for k in KEYS4) for _, t in runs[1:]])
+        noise.append(cum)
+    upto = next((i for i, v in enumerate(noise) if v > BRANCH), n)
+    upto = min(upto, len(trace))
+    best = None
+    for name, t in runs:
+        per = [max(_rel(trace[i][k], t[i][k]) for k in KEYS4) for i in range(upto)]
+        if all(p <= max(FLOOR, FACTOR * noise[i]) for i, p in enumerate(per)):
+            if best is None or max(per, default=0.0) < max(best[2], default=0.0):
+                best = (name, upto, per)
+    assert best is not None, (key, "follows none of the reference's runs before its noise branches",
+                              [(name, [f"{max(_rel(trace[i][k], t[i][k]) for k in KEYS4):.1e}"
+                                       for i in range(upto)]) for name, t in runs],
+                              [f"{v:.1e}" for v in noise[:upto]])
+    return best
+
+
+# Extra maxcut_12 r=2 seeds of bench.EXTRA_SEEDS whose device end point differs from the golden's
+# while the reference's own hash twins have already branched (full twin runs not computed: hours
+# each), with the mechanism found.
+KNOWN_EXTRA_DEPARTURES = {
+    "maxcut_12_r2_s1": "the reference's hash twins leave the golden at assembly 2 (4e-4) and by 0.6-0.8 at "
+                       "assembly 5; the device follows twin h3 within 4e-6 / 3e-5 / 6e-5 at assemblies 2-4 and "
+                       "ends pathological after 29 iterations (golden: 16, gap 9.2e-4)",
+    "maxcut_12_r2_s11": "the reference's hash twins split at assembly 1 (h0-h2: mu 7.56e-2; h3: 8.57e-2, 13 %); "
+                        "the device takes h3's branch (to 1e-6 through assembly 2) and ends pathological after "
+                        "11 iterations (golden: 14, gap 2.6e-4)",
+}

@@ -40,14 +40,24 @@ def test_maxcut12_eight_ranks_distinct_seeds_per_step():
     assert sorted(sched[0]) == sorted(seeds * 2)
 
 
-def test_extra_seeds_are_vetted_by_reference_runs():
-    """The extra seeds are non-pathological in the reference's own runs (src/utils.py:67-84)."""
+def test_extra_seeds_follow_the_fixed_rule():
+    """bench.EXTRA_SEEDS are the first seeds in seed order, skipping the config's own, whose reference
+    run as shipped is not pathological (src/utils.py:67) -- every seed before the last one chosen
+    has a reference run in runs.json, so the choice is re-derived here, not taken on trust."""
     runs = json.load(open(os.path.join(ROOT, "tests", "golden", "runs.json")))
-    for s in bench.EXTRA_SEEDS["maxcut_12.yaml"]:
-        if f"maxcut_12_r2_s{s}" not in runs:
-            pytest.skip(f"reference run maxcut_12_r2_s{s} not in runs.json")
-        r = runs[f"maxcut_12_r2_s{s}"]
-        assert r["num_iters"] is not None and r["gap"] <= 1e-3 and r["feas"] <= 1e-3, (s, r["gap"], r["feas"])
+    own = set(_cfg("maxcut_12.yaml")["seeds"])
+    want = bench.EXTRA_SEEDS["maxcut_12.yaml"]
+    got, s = [], 0
+    while len(got) < len(want):
+        if s not in own:
+            key = f"maxcut_12_r2_s{s}"
+            assert key in runs, f"the rule needs the reference run of seed {s}"
+            r = runs[key]
+            assert r["num_iters"] is not None
+            if not (r["gap"] > 1e-3 or r["feas"] > 1e-3):
+                got.append(s)
+        s += 1
+    assert got == want
 
 
 def test_replica_schedule():
