@@ -165,6 +165,17 @@ at::Tensor mul_(at::Tensor dst, const at::Tensor &a, const at::Tensor &b, double
   return dst;
 }
 
+// Tensor metadata helpers that keep the GIL: torch's own Python bindings release it around every
+// op (torch.empty, Tensor.view / .t / .permute), which costs ~2 us per call and, with a second
+// solve thread in the process, a GIL hand-over each time (2-2.5x per call, tools/gil_bench.py).
+at::Tensor empty(const at::Tensor &like, std::vector<int64_t> shape) { return at::empty(shape, like.options()); }
+
+at::Tensor view(const at::Tensor &t, std::vector<int64_t> shape) { return t.view(shape); }
+
+at::Tensor transpose2(const at::Tensor &t) { return t.t(); }
+
+at::Tensor permute(const at::Tensor &t, std::vector<int64_t> dims) { return t.permute(dims); }
+
 }  // namespace
 
 void set_release_gil(bool on) { g_release_gil = on; }
@@ -175,4 +186,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("einsum", &einsum);
   m.def("copy_", &copy_);
   m.def("mul_", &mul_);
+  m.def("empty", &empty);
+  m.def("view", &view);
+  m.def("t", &transpose2);
+  m.def("permute", &permute);
 }

@@ -134,14 +134,30 @@ def _fast():
     return tl.fast
 
 
+_LIKE = []
+_BIND_EMPTY = getattr(_BIND, "empty", None)
+
+
+def _like():
+    """a float64 tensor on DEV whose options `_ttkbind.empty` copies"""
+    if not _LIKE:
+        _LIKE.append(torch.empty(1, dtype=F64, device=DEV))
+    return _LIKE[0]
+
+
 def empty(*shape):
+    """a new float64 device tensor (the caching allocator, the thread's current stream).  Through
+    _ttkbind when built: at::empty with the GIL held, ~1 us instead of torch.empty's ~3 us, and no
+    GIL hand-over to a second solve thread on every allocation (tools/gil_bench.py)."""
+    if _BIND_EMPTY is not None and DEV.type == "cuda":
+        return _BIND_EMPTY(_like(), shape)
     return torch.empty(shape, dtype=F64, device=DEV)
 
 
 def zeros(*shape):
     """a zero-filled device tensor: libttk's fill kernel on the launch stream (torch.zeros would
     dispatch its own fill kernel through the torch runtime, ~3x the host cost)"""
-    out = torch.empty(shape, dtype=F64, device=DEV)
+    out = empty(*shape)
     if DEV.type == "cuda" and out.numel():
         check(lib.ttk_fill(_stream(), out.data_ptr(), out.numel(), 0.0), "fill")
     elif DEV.type != "cuda":
@@ -156,7 +172,7 @@ def from_numpy(a):
     h = np.array(a, dtype=np.float64, order="C", copy=True)
     if DEV.type != "cuda":
         return torch.from_numpy(h).to(DEV)
-    out = torch.empty(h.shape, dtype=F64, device=DEV)
+    out = empty(*h.shape)
     if h.size:
         check(lib.ttk_upload(_stream(), h.ctypes.data, out.data_ptr(), h.size), "upload")
     return out

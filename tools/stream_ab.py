@@ -71,5 +71,5 @@ for j in range(nthr):
     its += sum(i for _, i, _ in v)
     ok = all(g == solo[sd][0][2] for _, _, g in v)
     print(f"thread {j} seed {sd}: s/iter {[round(w / i, 4) for w, i, _ in v]} same gap as solo: {ok}", flush=True)
-print(f"threads {nthr} hold_gil {os.environ.get('TTK_HOLD_GIL', '0')} switch {sys.getswitchinterval()}: "
+print(f"threads {nthr} hold_gil {os.environ.get('TTK_HOLD_GIL', '1')} switch {sys.getswitchinterval()}: "
       f"whole job {wall / its:.4f} s/IPM-iter ({its} iters in {wall:.2f} s)", flush=True)
