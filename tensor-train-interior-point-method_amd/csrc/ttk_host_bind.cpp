@@ -21,7 +21,21 @@ using copy_fn = int (*)(void *, const double *, double *, int, const int64_t *, 
 using mul_fn = int (*)(void *, const double *, const double *, double *, int, const int64_t *, const int64_t *,
                        const int64_t *, const int64_t *, double, double);
 
+using axpby_fn = int (*)(void *, const double *, const double *, double *, int, const int64_t *, const int64_t *,
+                         const int64_t *, const int64_t *, double, double, double);
+using normalize_fn = int (*)(void *, const double *, double *, int, const int64_t *, const int64_t *);
+using scale_ss_fn = int (*)(void *, const double *, double *, int, const int64_t *, const int64_t *, const int64_t *,
+                            int, const double *, int);
+using dot_dev_fn = int (*)(void *, const double *, const double *, int, const int64_t *, const int64_t *,
+                           const int64_t *, double *);
+using fill_fn = int (*)(void *, double *, int64_t, double);
+
 einsum_fn g_einsum = nullptr;
+axpby_fn g_axpby = nullptr;
+normalize_fn g_normalize = nullptr;
+scale_ss_fn g_scale_ss = nullptr;
+dot_dev_fn g_dot_dev = nullptr;
+fill_fn g_fill = nullptr;
 copy_fn g_copy = nullptr;
 mul_fn g_mul = nullptr;
 // one launch stream per host thread: a process may drive several solves at once, one per thread,
@@ -34,6 +48,17 @@ void bind(int64_t einsum_addr, int64_t copy_addr, int64_t mul_addr, int64_t stre
   g_copy = reinterpret_cast<copy_fn>(copy_addr);
   g_mul = reinterpret_cast<mul_fn>(mul_addr);
   g_stream = reinterpret_cast<void *>(stream);
+}
+
+// the element-wise / reduction entry points of dev.py's hot wrappers (same libttk calls as its ctypes
+// path; one pybind call instead of ctypes argument packing)
+void bind2(int64_t axpby_addr, int64_t normalize_addr, int64_t scale_ss_addr, int64_t dot_dev_addr,
+           int64_t fill_addr) {
+  g_axpby = reinterpret_cast<axpby_fn>(axpby_addr);
+  g_normalize = reinterpret_cast<normalize_fn>(normalize_addr);
+  g_scale_ss = reinterpret_cast<scale_ss_fn>(scale_ss_addr);
+  g_dot_dev = reinterpret_cast<dot_dev_fn>(dot_dev_addr);
+  g_fill = reinterpret_cast<fill_fn>(fill_addr);
 }
 
 // output index string -> positions (operand, axis) of each output letter, per (equation)
@@ -165,6 +190,81 @@ at::Tensor mul_(at::Tensor dst, const at::Tensor &a, const at::Tensor &b, double
   return dst;
 }
 
+int geometry(const at::Tensor &t, int64_t *shp, int64_t *st) {
+  const int nd = (int)t.dim();
+  TORCH_CHECK(nd <= 16, "rank ", nd);
+  for (int i = 0; i < nd; ++i) {
+    shp[i] = t.size(i);
+    st[i] = t.stride(i);
+  }
+  return nd;
+}
+
+// out = alpha * src + beta * (gamma * src2) (dev.axpby)
+at::Tensor axpby(const at::Tensor &src, const at::Tensor &src2, double alpha, double beta, double gamma,
+                 c10::optional<at::Tensor> out_opt) {
+  at::Tensor out = out_opt.has_value() ? *out_opt : at::empty(src.sizes(), src.options());
+  int64_t shp[16], s1[16], s2[16], so[16];
+  const int nd = geometry(src, shp, s1);
+  TORCH_CHECK(src2.dim() == nd && out.dim() == nd, "axpby: rank mismatch");
+  for (int i = 0; i < nd; ++i) {
+    s2[i] = src2.stride(i);
+    so[i] = out.stride(i);
+  }
+  check(g_axpby(g_stream, src.data_ptr<double>(), src2.data_ptr<double>(), out.data_ptr<double>(), nd, shp, s1, s2,
+                so, alpha, beta, gamma),
+        "axpby_nd");
+  return out;
+}
+
+// src / ||src|| into a new contiguous tensor (dev.normalized)
+at::Tensor normalized(const at::Tensor &src) {
+  at::Tensor out = at::empty(src.sizes(), src.options());
+  int64_t shp[16], st[16];
+  int nd = geometry(src, shp, st);
+  if (nd == 0) {
+    nd = 1;
+    shp[0] = st[0] = 1;
+  }
+  check(g_normalize(g_stream, src.data_ptr<double>(), out.data_ptr<double>(), nd, shp, st), "normalize");
+  return out;
+}
+
+// src * f(ss[i_axis]) (dev.scale_axis_ss)
+at::Tensor scale_axis_ss(const at::Tensor &src, int64_t axis, const at::Tensor &ss, bool invert,
+                         c10::optional<at::Tensor> out_opt) {
+  at::Tensor out = out_opt.has_value() ? *out_opt : at::empty(src.sizes(), src.options());
+  int64_t shp[16], s1[16], so[16];
+  const int nd = geometry(src, shp, s1);
+  TORCH_CHECK(out.dim() == nd, "scale_axis_ss: rank mismatch");
+  for (int i = 0; i < nd; ++i) so[i] = out.stride(i);
+  check(g_scale_ss(g_stream, src.data_ptr<double>(), out.data_ptr<double>(), nd, shp, s1, so, (int)axis,
+                   ss.data_ptr<double>(), invert ? 1 : 0),
+        "scale_axis_ss");
+  return out;
+}
+
+// sum(x * y) into the device scalar `out` (dev.dot_into)
+void dot_into(const at::Tensor &x, const at::Tensor &y, at::Tensor out) {
+  TORCH_CHECK(x.sizes() == y.sizes(), "dot_into: shape mismatch ", x.sizes(), " vs ", y.sizes());
+  int64_t shp[16], xs[16], ys[16];
+  int nd = geometry(x, shp, xs);
+  for (int i = 0; i < nd; ++i) ys[i] = y.stride(i);
+  if (nd == 0) {
+    nd = 1;
+    shp[0] = xs[0] = ys[0] = 1;
+  }
+  check(g_dot_dev(g_stream, x.data_ptr<double>(), y.data_ptr<double>(), nd, shp, xs, ys, out.data_ptr<double>()),
+        "dot_nd_dev");
+}
+
+// a zero-filled tensor: at::empty + libttk's fill kernel (dev.zeros)
+at::Tensor zeros(const at::Tensor &like, std::vector<int64_t> shape) {
+  at::Tensor out = at::empty(shape, like.options());
+  if (out.numel()) check(g_fill(g_stream, out.data_ptr<double>(), out.numel(), 0.0), "fill");
+  return out;
+}
+
 // Tensor metadata helpers that keep the GIL: torch's own Python bindings release it around every
 // op (torch.empty, Tensor.view / .t / .permute), which costs ~2 us per call and, with a second
 // solve thread in the process, a GIL hand-over each time (2-2.5x per call, tools/gil_bench.py).
@@ -186,6 +286,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("einsum", &einsum);
   m.def("copy_", &copy_);
   m.def("mul_", &mul_);
+  m.def("bind2", &bind2);
+  m.def("axpby", &axpby);
+  m.def("normalized", &normalized);
+  m.def("scale_axis_ss", &scale_axis_ss);
+  m.def("dot_into", &dot_into);
+  m.def("zeros", &zeros);
   m.def("empty", &empty);
   m.def("view", &view);
   m.def("t", &transpose2);

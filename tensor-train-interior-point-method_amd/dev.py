@@ -130,12 +130,16 @@ def _fast():
         def addr(f):
             return ctypes.cast(f, ctypes.c_void_p).value
         _BIND.bind(addr(lib.ttk_einsum), addr(lib.ttk_copy_nd), addr(lib.ttk_mul_nd), _stream() or 0)
+        if _FAST2:
+            _BIND.bind2(addr(lib.ttk_axpby_nd), addr(lib.ttk_normalize), addr(lib.ttk_scale_axis_ss),
+                        addr(lib.ttk_dot_nd_dev), addr(lib.ttk_fill))
         tl.fast = _BIND
     return tl.fast
 
 
 _LIKE = []
 _BIND_EMPTY = getattr(_BIND, "empty", None)
+_FAST2 = hasattr(_BIND, "bind2")  # native packers of axpby / normalized / scale_axis_ss / dot_into / zeros
 
 
 def _like():
@@ -157,6 +161,8 @@ def empty(*shape):
 def zeros(*shape):
     """a zero-filled device tensor: libttk's fill kernel on the launch stream (torch.zeros would
     dispatch its own fill kernel through the torch runtime, ~3x the host cost)"""
+    if _FAST2 and DEV.type == "cuda":
+        return (_TL.fast or _fast()).zeros(_like(), shape)
     out = empty(*shape)
     if DEV.type == "cuda" and out.numel():
         check(lib.ttk_fill(_stream(), out.data_ptr(), out.numel(), 0.0), "fill")
@@ -289,6 +295,8 @@ def scale_axis(src, axis, scales, out=None):
 def axpby(src, src2, alpha, beta, gamma, out=None):
     """out = alpha * src + beta * (gamma * src2) (same shapes, any strides), one launch; rounds like
     scaled(src2, gamma) followed by copy_(out, src, alpha, beta)."""
+    if _FAST2 and DEV.type == "cuda":
+        return (_TL.fast or _fast()).axpby(src, src2, float(alpha), float(beta), float(gamma), out)
     out = empty(*src.shape) if out is None else out
     nd = src.dim()
     check(lib.ttk_axpby_nd(_stream(), _p(src), _p(src2), _p(out), nd, _arr(src.shape), _arr(src.stride()),
@@ -299,6 +307,8 @@ def axpby(src, src2, alpha, beta, gamma, out=None):
 def scale_axis_ss(src, axis, ss, invert, out=None):
     """src * max(sqrt(ss), 1e-10)[i] (or its reciprocal) along `axis`; ss = device sums of squares;
     into `out` (same shape, any strides) when given."""
+    if _FAST2 and DEV.type == "cuda":
+        return (_TL.fast or _fast()).scale_axis_ss(src, int(axis), ss, bool(invert), out)
     out = empty(*src.shape) if out is None else out
     nd = src.dim()
     check(lib.ttk_scale_axis_ss(_stream(), _p(src), _p(out), nd, _arr(src.shape), _arr(src.stride()),
@@ -308,6 +318,8 @@ def scale_axis_ss(src, axis, ss, invert, out=None):
 
 def normalized(src):
     """src / ||src|| as a new contiguous tensor, computed on the device (no host sync)."""
+    if _FAST2 and DEV.type == "cuda":
+        return (_TL.fast or _fast()).normalized(src)
     out = empty(*src.shape)
     nd = src.dim()
     if nd == 0:
@@ -367,6 +379,8 @@ def norm(x):
 
 def dot_into(x, y, out):
     """sum(x*y) into the device scalar `out` (a 1-element view), no host synchronisation."""
+    if _FAST2 and DEV.type == "cuda":
+        return (_TL.fast or _fast()).dot_into(x, y, out)
     assert tuple(x.shape) == tuple(y.shape)
     nd = x.dim()
     if nd == 0:
