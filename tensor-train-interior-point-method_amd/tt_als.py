@@ -57,7 +57,8 @@ class TTBlockVector:
 
     @property
     def norm(self):
-        return np.sqrt(sum(T.tt_inner_prod(v, v) for v in self._data.values()))
+        # every block's <v, v> in one host read, summed on the host in block order as before
+        return np.sqrt(sum(T.tt_scalars([("ip", v, v) for v in self._data.values()])))
 
     def __sub__(self, other):
         out = TTBlockVector()
