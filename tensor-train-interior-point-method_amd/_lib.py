@@ -123,6 +123,9 @@ BLOCKING = frozenset(n for n in _SIGS if "sync" in n) | frozenset((
 # maxcut_10 s41 + s235: whole job 0.153 -> 0.141 s/IPM-iter, 0.130 with a 0.5 ms switch interval;
 # profiles/r04_slot_threads.txt).
 _held = ctypes.PyDLL(LIB_PATH) if os.environ.get("TTK_HOLD_GIL", "1") == "1" else None
+# the same entry points, every one releasing the GIL: for calls whose host side is itself long
+# (e.g. the eigensolver's one launch per Householder reflector at n > 128, dev.syev_extreme)
+lib_release = ctypes.CDLL(LIB_PATH) if _held is not None else lib
 
 for _name, (_res, _args) in _SIGS.items():
     if os.environ.get("TTK_LIB_PATH") and not hasattr(lib, _name):
@@ -132,6 +135,9 @@ for _name, (_res, _args) in _SIGS.items():
     _f.argtypes = _args
     if _held is not None and _name not in BLOCKING:
         setattr(lib, _name, _f)
+        _g = getattr(lib_release, _name)
+        _g.restype = _res
+        _g.argtypes = _args
 
 EXPORTED = tuple(_SIGS)
 

@@ -19,7 +19,7 @@ from functools import lru_cache
 import numpy as np
 import torch
 
-from ._lib import LinAlgError, LinAlgWarning, c_dp, c_i64p, check, lib
+from ._lib import LinAlgError, LinAlgWarning, c_dp, c_i64p, check, lib, lib_release
 
 DEV = torch.device(os.environ.get("TTIPM_DEVICE", "cuda"))
 F64 = torch.float64
@@ -625,7 +625,9 @@ def svd(A, defl=0.0, host=True, S_out=None):
     k = min(m, n)
     U, S, Vt = empty(m, k), (empty(k) if S_out is None else S_out), empty(k, n)
     work = empty(int(lib.ttk_svd_work(m, n)))
-    check(lib.ttk_svd_tol(_stream(), _p(A), m, n, _p(U), _p(S), _p(Vt), _p(work), float(defl)), "svd")
+    # p > 96 takes the multi-launch path (host loops over Jacobi rounds): release the GIL meanwhile
+    L = lib_release if min(m, n) > 96 else lib
+    check(L.ttk_svd_tol(_stream(), _p(A), m, n, _p(U), _p(S), _p(Vt), _p(work), float(defl)), "svd")
     sh = read(S) if host else None
     if OPSTATS is not None:
         _stat("svd", (m, n), t0, site_min=min(m, n) >= 64)
@@ -640,7 +642,8 @@ def qr(A):
     k = min(m, n)
     Q, R = empty(m, k), empty(k, n)
     work = empty(int(lib.ttk_qr_work(m, n)))
-    check(lib.ttk_qr(_stream(), _p(A), m, n, _p(Q), _p(R), _p(work)), "qr")
+    L = lib_release if min(m, n) >= 48 else lib  # the blocked path's host loop over panels
+    check(L.ttk_qr(_stream(), _p(A), m, n, _p(Q), _p(R), _p(work)), "qr")
     if OPSTATS is not None:
         _stat("qr", (m, n), t0, site_min=min(m, n) >= 64)
     return Q, R
@@ -711,7 +714,7 @@ def syev(A):
     n = A.shape[0]
     ev, W = empty(n), empty(n, n)
     work = empty(int(lib.ttk_syev_work(n)))
-    check(lib.ttk_syev(_stream(), _p(A), n, _p(ev), _p(W), _p(work)), "syev")
+    check(lib_release.ttk_syev(_stream(), _p(A), n, _p(ev), _p(W), _p(work)), "syev")
     evh = read(ev)
     if OPSTATS is not None:
         _stat("syev", n, t0)
@@ -728,7 +731,9 @@ def syev_extreme(A, largest=False, lam_out=None):
     buf = empty(n + 1) if lam_out is None else None
     lam_p, vec = (buf[:1], buf[1:]) if lam_out is None else (lam_out, empty(n))
     work = empty(int(lib.ttk_syev_extreme_work(n)))
-    check(lib.ttk_syev_extreme(_stream(), _p(A), n, 1 if largest else 0, _p(lam_p), _p(vec), _p(work)),
+    # n > 128: one launch per Householder reflector from the host -- release the GIL meanwhile
+    L = lib_release if n > 128 else lib
+    check(L.ttk_syev_extreme(_stream(), _p(A), n, 1 if largest else 0, _p(lam_p), _p(vec), _p(work)),
           "syev_extreme")
     if lam_out is not None:
         return None, vec

@@ -504,8 +504,10 @@ def emulated_ttipm():
         del sys.modules[k]
     import ttipm_amd  # noqa: F401
     lib_mod = importlib.import_module("ttipm_amd._lib")
-    lib_mod.lib = EmuLib()
+    lib_mod.lib = lib_mod.lib_release = EmuLib()
     for name in ("dev", "lgmres", "tt_ipm"):
         m = importlib.import_module("ttipm_amd." + name)
         m.lib = lib_mod.lib
+        if hasattr(m, "lib_release"):
+            m.lib_release = lib_mod.lib
     return ttipm_amd
