@@ -11,6 +11,7 @@
 #include <cstdint>
 #include <string>
 #include <unordered_map>
+#include <tuple>
 #include <vector>
 
 namespace {
@@ -152,6 +153,21 @@ at::Tensor einsum(const std::string &eq, const std::vector<at::Tensor> &ops, c10
   return res;
 }
 
+// A run of einsums over block columns (the block local products of tt_als.py): item = (equation
+// index, operands, x column or -1, out column); operand list + x.select(1, xcol) -> out.select(1,
+// ocol), accumulated with (alpha, beta), in item order -- the same libttk calls, in the same order,
+// as one dev.einsum per item, without a Python slice and wrapper per block.
+void einsum_cols(const std::vector<std::string> &eqs,
+                 const std::vector<std::tuple<int64_t, std::vector<at::Tensor>, int64_t, int64_t>> &items,
+                 const at::Tensor &x, const at::Tensor &out, double alpha, double beta, int64_t flags) {
+  for (const auto &it : items) {
+    std::vector<at::Tensor> ops = std::get<1>(it);
+    const int64_t xc = std::get<2>(it), oc = std::get<3>(it);
+    if (xc >= 0) ops.push_back(x.select(1, xc));
+    einsum(eqs.at((size_t)std::get<0>(it)), ops, out.select(1, oc), alpha, beta, flags);
+  }
+}
+
 at::Tensor copy_(at::Tensor dst, const at::Tensor &src, double alpha, double beta) {
   TORCH_CHECK(dst.sizes() == src.sizes(), "copy_: shape mismatch ", dst.sizes(), " vs ", src.sizes());
   int nd = (int)dst.dim();
@@ -287,6 +303,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("copy_", &copy_);
   m.def("mul_", &mul_);
   m.def("bind2", &bind2);
+  m.def("einsum_cols", &einsum_cols);
   m.def("axpby", &axpby);
   m.def("normalized", &normalized);
   m.def("scale_axis_ss", &scale_axis_ss);

@@ -140,6 +140,7 @@ def _fast():
 _LIKE = []
 _BIND_EMPTY = getattr(_BIND, "empty", None)
 _FAST2 = hasattr(_BIND, "bind2")  # native packers of axpby / normalized / scale_axis_ss / dot_into / zeros
+_COLS = hasattr(_BIND, "einsum_cols")
 
 
 def _like():
@@ -536,6 +537,24 @@ def einsum(eq, *ops, out=None, alpha=1.0, beta=0.0, fused=False, algo=None):
     if _CHECK_FUSED and fused and eq in _FUSED_EQS:
         return _einsum_checked(eq, ops, out, alpha, beta)
     return _einsum_native(eq, *ops, out=out, alpha=alpha, beta=beta, fused=fused)
+
+
+def einsum_cols(eqs, items, x, out, alpha=1.0, beta=1.0):
+    """A run of einsums over block columns: item = (equation index into `eqs`, operands, x column or
+    -1, out column) computes out[:, ocol] = alpha * einsum(eq, *operands, x[:, xcol]) + beta *
+    out[:, ocol], in item order.  One native call (`_ttkbind.einsum_cols`: the same libttk einsum
+    calls, in the same order, as one `einsum` per item) instead of a Python slice and wrapper per
+    block; the per-item path when FLOPs are being counted or the native packer is absent."""
+    f = _TL.fast or _fast()
+    if f is None or not _COLS or ALGO is not None or OPSTATS is not None or _CHECK_FUSED:
+        for ei, ops, xc, oc in items:
+            einsum(eqs[ei], *ops, *((x[:, xc],) if xc >= 0 else ()), out=out[:, oc], alpha=alpha, beta=beta)
+        return out
+    tl = _TL
+    if tl.batch[0]:
+        tl.keep.append((items, x, out))
+    f.einsum_cols(eqs, items, x, out, float(alpha), float(beta), 256 if _FUSED_ALL else 0)
+    return out
 
 
 def _new_out(eq, ops):

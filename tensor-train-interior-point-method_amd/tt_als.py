@@ -154,32 +154,35 @@ class TTBlockMatrixView:
             return self._block_local_product(L, R, x, out)
 
     def _block_local_product(self, L, R, x, out):
+        items = []  # (equation, operands, x column, out column) in the reference's block order
         for (i, j) in self.bm._data:
-            A = self[i, j]
-            einsum(APPLY, L[i, j], A, R[i, j], x[:, j], out=out[:, i], beta=1.0)
+            ops = [L[i, j], self[i, j], R[i, j]]
+            items.append((0, ops, j, i))
             if (i, j) in self._transposes:
                 k, t = self._transposes[i, j]
-                einsum(APPLY_T, L[i, j], A, R[i, j], x[:, t], out=out[:, k], beta=1.0)
+                items.append((1, ops, t, k))
             if (i, j) in self._aliases:
                 k, t = self._aliases[i, j]
-                einsum(APPLY, L[i, j], A, R[i, j], x[:, t], out=out[:, k], beta=1.0)
-        return out
+                items.append((0, ops, t, k))
+        return D.einsum_cols((APPLY, APPLY_T), items, x, out)
 
     def _compressed(self, L, R, x, out, teq, tL, tR):
         with D.einsum_batch():
             return self._compressed_body(L, R, x, out, teq, tL, tR)
 
     def _compressed_body(self, L, R, x, out, teq, tL, tR):
+        items = []
         for (i, j) in self.bm._data:
             A = self[i, j]
-            einsum(APPLY, L[i, j], A, R[i, j], x[:, j], out=out[:, i], beta=1.0)
+            ops = [L[i, j], A, R[i, j]]
+            items.append((0, ops, j, i))
             if (i, j) in self._transposes:
                 k, t = self._transposes[i, j]
-                einsum(teq, L[k, t] if tL else L[i, j], A, R[k, t] if tR else R[i, j], x[:, t], out=out[:, k], beta=1.0)
+                items.append((1, [L[k, t] if tL else L[i, j], A, R[k, t] if tR else R[i, j]], t, k))
             if (i, j) in self._aliases:
                 k, t = self._aliases[i, j]
-                einsum(APPLY, L[i, j], A, R[i, j], x[:, t], out=out[:, k], beta=1.0)
-        return out
+                items.append((0, ops, t, k))
+        return D.einsum_cols((APPLY, teq), items, x, out)
 
     def compressed_block_local_product(self, ZL, ZR, x, out):
         """`:202-212` (accumulates into out)"""
@@ -197,8 +200,8 @@ class TTBlockMatrixView:
 def rhs_local_product(bcore, L, R, out, alpha=1.0):
     """`TTBlockVectorView.block_local_product` (`src/tt_als.py:79-83`), accumulated into out."""
     with D.einsum_batch():
-        for i, c in bcore.items():
-            einsum("br,bnB,BR->rnR", L[i], c, R[i], out=out[:, i], alpha=alpha, beta=1.0)
+        D.einsum_cols(("br,bnB,BR->rnR",), [(0, [L[i], c, R[i]], -1, i) for i, c in bcore.items()], out, out,
+                      alpha=alpha, beta=1.0)
     return out
 
 
