@@ -1,7 +1,7 @@
 """Diagnostics (GPU): solve a config for a range of seeds on the device and print which end
-non-pathological (`src/utils.py:67`: feasibility and gap <= 1e-3).  Used to pick the candidate extra
-seeds of configs[4] whose reference runs (tests/golden/make_golden.py) are then made in the build
-container -- the device only pre-selects, the reference run vets.
+non-pathological (`src/utils.py:67`: feasibility and gap <= 1e-3).  A diagnostic only: the extra
+seeds of configs[4] are chosen from the reference's own runs by a fixed rule (bench.EXTRA_SEEDS,
+DESIGN.md section 5), never from device results or timings.
 
     python tools/scan_seeds.py maxcut maxcut_12 2 7 30"""
 import json
