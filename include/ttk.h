@@ -90,6 +90,11 @@ void *ttk_ctx_stream(ttk_ctx ctx);
  *                   layout the apply rows stage in LDS, so a matvec stages them with contiguous
  *                   copies instead of strided gathers (bit-identical; read at build; default
  *                   from env TTK_SCHUR_PREP, else 1)
+ * TTK_KNOB_SPLITK_FUSED  1: a split-K GEMM is ONE launch -- the split blocks of a tile store their
+ *                   partial tiles write-through and count their arrival; the last one to arrive sums
+ *                   the partials in split order and writes C (the separate reduce launch's
+ *                   arithmetic, bit-identical); 0: split kernel + reduce kernel (default from env
+ *                   TTK_SPLITK_FUSED, else 1)
  * ttk_ctx_set_knob stores value and returns the previous one in *old (may be NULL). */
 enum ttk_knob {
   TTK_KNOB_FUSED_APPLY = 0,
@@ -103,7 +108,8 @@ enum ttk_knob {
   TTK_KNOB_SCHUR_ONE = 8,
   TTK_KNOB_ARNOLDI_ONE = 9,
   TTK_KNOB_SCHUR_PREP = 10,
-  TTK_KNOB_COUNT = 11
+  TTK_KNOB_SPLITK_FUSED = 11,
+  TTK_KNOB_COUNT = 12
 };
 int ttk_ctx_set_knob(ttk_ctx ctx, int knob, int value, int *old);
 int ttk_ctx_get_knob(ttk_ctx ctx, int knob, int *value);

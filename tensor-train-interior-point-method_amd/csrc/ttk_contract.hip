@@ -52,7 +52,8 @@ typedef double double4_t __attribute__((ext_vector_type(4)));
 // with 16-K stages (trailing all-zero K groups are skipped), so results are unchanged bit for bit.
 // out != nullptr: raw partial sums (no alpha/beta) to a dense [M][N] slab (split-K);
 // out == nullptr: alpha/beta epilogue into C through the output offset tables.
-template <int TS>  // K per LDS stage (16 / 32 / 64: picked per launch from K; LDS 8.4 / 17 / 34 KB)
+// SC1: the partial sums go out with write-through (sc1) stores, for a consumer on another CU.
+template <int TS, bool SC1 = false>  // K per LDS stage (16 / 32 / 64: picked per launch from K; LDS 8.4 / 17 / 34 KB)
 __device__ __forceinline__ void gemm_tile(const double *__restrict__ A, const double *__restrict__ B,
                                           double *__restrict__ C, const int64_t *__restrict__ offs,
                                           int nb, int M, int N, int K, double alpha, double beta,
@@ -147,7 +148,12 @@ __device__ __forceinline__ void gemm_tile(const double *__restrict__ A, const do
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int row = m0 + wr * 16 + (lane >> 4) + 4 * r;
-      if (row < M) out[(int64_t)row * N + col] = acc[r];
+      if (row < M) {
+        if (SC1)
+          ttk::st_sc1(out + (int64_t)row * N + col, acc[r]);
+        else
+          out[(int64_t)row * N + col] = acc[r];
+      }
     }
     return;
   }
@@ -290,6 +296,71 @@ __global__ __launch_bounds__(256) void gemm_offs_splitk_kernel(GemmArgs g, int n
   const int kb = sp * kc, ke = kb + kc < g.K ? kb + kc : g.K;
   double *out = part + ((int64_t)sp * g.nb + b) * g.M * g.N;
   gemm_tile<TS>(g.A, g.B, g.C, g.offs, g.nb, g.M, g.N, g.K, g.alpha, g.beta, b, m0, n0, kb, ke, out);
+}
+
+// Split-K in ONE launch: the split blocks of a tile store their partial tiles write-through (sc1),
+// drain, and count their arrival on the tile's counter (MI355X_MICROARCH.md's first measured
+// hand-off form: sc1 stores + s_waitcnt vmcnt(0) + workgroup barrier + one agent-scope atomic; the
+// consumer's loads are sc1).  The block whose arrival completes the count sums the tile's partials
+// in split order and writes C -- the reduce kernel's arithmetic below, element for element -- and
+// resets the counter for the next launch.  Nobody waits: a block that is not last just exits, so
+// the grid drains whatever the residency.
+template <int TS>
+__global__ __launch_bounds__(256) void gemm_offs_splitk_fused_kernel(GemmArgs g, int nsplit, int kc, double *part,
+                                                                     unsigned *cnt) {
+  __shared__ unsigned s_old;
+  const int n0 = blockIdx.x * TN, m0 = blockIdx.y * TM;
+  const int b = blockIdx.z / nsplit, sp = blockIdx.z % nsplit;
+  const int kb = sp * kc, ke = kb + kc < g.K ? kb + kc : g.K;
+  const int64_t mn = (int64_t)g.M * g.N;
+  gemm_tile<TS, true>(g.A, g.B, g.C, g.offs, g.nb, g.M, g.N, g.K, g.alpha, g.beta, b, m0, n0, kb, ke,
+                      part + ((int64_t)sp * g.nb + b) * mn);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  unsigned *c = cnt + ((int64_t)b * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+  if (threadIdx.x == 0) s_old = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  if (s_old != (unsigned)(nsplit - 1)) return;
+  const int64_t *a_b = g.offs;
+  const int64_t *c_b = a_b + g.nb + g.M + g.K + g.nb + g.K + g.N;
+  const int64_t *c_m = c_b + g.nb;
+  const int64_t *c_n = c_m + g.M;
+  // each thread owns EPT tile elements; the partials are loaded U splits at a time for all of them
+  // before any is added (sc1 loads in flight together), then added in split order per element
+  constexpr int EPT = TM * TN / 256, U = 8;
+  const int64_t slab = (int64_t)g.nb * mn;
+  const double *base = part + (int64_t)b * mn;
+  int64_t r[EPT];
+  bool ok[EPT];
+  double acc[EPT];
+#pragma unroll
+  for (int q = 0; q < EPT; ++q) {
+    const int e = threadIdx.x + q * 256, row = m0 + e / TN, col = n0 + e % TN;
+    ok[q] = row < g.M && col < g.N;
+    r[q] = ok[q] ? (int64_t)row * g.N + col : 0;
+    acc[q] = 0.0;
+  }
+  for (int s0 = 0; s0 < nsplit; s0 += U) {
+    double v[EPT][U];
+#pragma unroll
+    for (int q = 0; q < EPT; ++q)
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[q][u] = (ok[q] && s0 + u < nsplit) ? ttk::ld_sc1(base + (s0 + u) * slab + r[q]) : 0.0;
+#pragma unroll
+    for (int q = 0; q < EPT; ++q)
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (s0 + u < nsplit) acc[q] += v[q][u];
+  }
+#pragma unroll
+  for (int q = 0; q < EPT; ++q) {
+    if (!ok[q]) continue;
+    const int e = threadIdx.x + q * 256, row = m0 + e / TN, col = n0 + e % TN;
+    double *p = g.C + c_b[b] + c_m[row] + c_n[col];
+    const double v = g.alpha * acc[q];
+    *p = (g.beta == 0.0) ? v : v + g.beta * (*p);
+  }
+  if (threadIdx.x == 0) __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // C = alpha * sum_split part + beta * C (fixed summation order: deterministic)
@@ -711,6 +782,7 @@ extern "C" {
 namespace {
 // split-K on/off and K per split: per-context knobs (TTK_KNOB_SPLITK / _SPLITK_MINK)
 static inline bool splitk_on() { return ttk::ctx().knob[TTK_KNOB_SPLITK] != 0; }
+constexpr int SPLITK_TILES_MAX = 256;  // split-K runs only when the tile grid is below 256 tiles
 static inline int splitk_mink() {
   const int k = ttk::ctx().knob[TTK_KNOB_SPLITK_MINK];
   return k > 0 ? k : 128;  // the documented default (ttk_ctx_set_knob rejects <= 0)
@@ -804,11 +876,21 @@ int ttk_gemm_offs(void *stream, const double *A, const double *B, double *C, con
       return TTK_ERR_HIP;
     }
     dim3 gs(grid.x, grid.y, nb * nsplit);
-    hipExtLaunchKernelGGL(gemm_offs_splitk_kernel<64>, gs, dim3(256), 0, TTK_STREAM(stream), e0, nullptr, 0, g, nsplit,
-                          kc, part);
-    const int64_t tot = (int64_t)nb * M * N;
-    hipExtLaunchKernelGGL(gemm_splitk_reduce_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0,
-                          TTK_STREAM(stream), nullptr, e1, 0, g, nsplit, part);
+    ttk::Ctx &cx = ttk::ctx();
+    if (cx.knob[TTK_KNOB_SPLITK_FUSED] && tiles <= SPLITK_TILES_MAX) {
+      if (!cx.splitk_cnt) {  // per-tile counters, zero between launches (each launch's last blocks reset them)
+        TTK_HIP(hipMalloc(reinterpret_cast<void **>(&cx.splitk_cnt), SPLITK_TILES_MAX * sizeof(unsigned)));
+        TTK_HIP(hipMemsetAsync(cx.splitk_cnt, 0, SPLITK_TILES_MAX * sizeof(unsigned), TTK_STREAM(stream)));
+      }
+      hipExtLaunchKernelGGL(gemm_offs_splitk_fused_kernel<64>, gs, dim3(256), 0, TTK_STREAM(stream), e0, e1, 0, g,
+                            nsplit, kc, part, cx.splitk_cnt);
+    } else {
+      hipExtLaunchKernelGGL(gemm_offs_splitk_kernel<64>, gs, dim3(256), 0, TTK_STREAM(stream), e0, nullptr, 0, g,
+                            nsplit, kc, part);
+      const int64_t tot = (int64_t)nb * M * N;
+      hipExtLaunchKernelGGL(gemm_splitk_reduce_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0,
+                            TTK_STREAM(stream), nullptr, e1, 0, g, nsplit, part);
+    }
   } else if (M >= g_gemm64_min && N >= g_gemm64_min && K >= 64 &&
              (int64_t)((M + BM - 1) / BM) * ((N + BN - 1) / BN) * nb >= 512) {
     dim3 g64((N + BN - 1) / BN, (M + BM - 1) / BM, nb);

@@ -39,6 +39,7 @@ struct Ctx {
   int64_t schur_wcap = 0;
   unsigned *dep = nullptr;    // in-launch hand-off arrival counter (monotonic; ttk_einsum.hip)
   unsigned dep_total = 0;     // arrivals of every hand-off launch issued on this context so far
+  unsigned *splitk_cnt = nullptr;  // per-tile arrival counters of the one-launch split-K GEMM (reset by it)
   double *lgmres = nullptr;   // LGMRES partial sums
   int64_t lgmres_n = 0;
   int *status = nullptr;      // dense factorisation status words
@@ -58,7 +59,7 @@ struct Ctx {
                               env_int("TTK_LGMRES_MW_MIN", 16384), env_int("TTK_MFMA_CSPLIT", 1) != 0 ? 1 : 0,
                               env_int("TTK_APPLY_DUAL", 1) != 0 ? 1 : 0, env_int("TTK_RCOND_EXACT", 0) != 0 ? 1 : 0,
                               env_int("TTK_SCHUR_ONE", 1) != 0 ? 1 : 0, env_int("TTK_ARNOLDI_ONE", 1) != 0 ? 1 : 0,
-                              env_int("TTK_SCHUR_PREP", 1) != 0 ? 1 : 0};
+                              env_int("TTK_SCHUR_PREP", 1) != 0 ? 1 : 0, env_int("TTK_SPLITK_FUSED", 1) != 0 ? 1 : 0};
 };
 Ctx &ctx();
 Ctx *ctx_swap(Ctx *c);

@@ -794,3 +794,32 @@ def test_lgmres_one_launch_arnoldi_bit_identical(dev, ineq, mw_min):
     for k, v in res.items():
         assert np.array_equal(v[0], ref[0]) and v[1:] == ref[1:], k
     assert _lib.lib.ttk_dep_timeouts(ctypes.byref(to), 0) == 0 and to.value == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", [(212, 64, 2544), (60, 44, 2700), (116, 64, 1160), (33, 7, 300), (240, 60, 1000)])
+def test_splitk_one_launch_bit_identical(dev, shape):
+    """The one-launch split-K GEMM (TTK_KNOB_SPLITK_FUSED: partial tiles handed to the last-arriving
+    split block over write-through stores and an arrival counter) equals the split kernel + reduce
+    kernel bit for bit, with alpha / beta, on batched operands, and leaves its counters reset (the
+    same call repeated gives the same bits)."""
+    import torch
+    from ttipm_amd import _lib
+    from ttipm_amd import dev as D
+    M, N, K = shape
+    g = torch.Generator("cuda").manual_seed(M * N + K)
+    a = torch.randn(2, M, K, dtype=torch.float64, device="cuda", generator=g)
+    b = torch.randn(2, K, N, dtype=torch.float64, device="cuda", generator=g)
+    c0 = torch.randn(2, M, N, dtype=torch.float64, device="cuda", generator=g)
+    outs = []
+    for fused in (0, 1, 1):
+        old = _set_knob(_lib.KNOB_SPLITK_FUSED, fused)
+        try:
+            c = D.clone(c0)
+            D.einsum("bmk,bkn->bmn", a, b, out=c, alpha=0.75, beta=-1.25)
+            outs.append(D.read(c))
+        finally:
+            _set_knob(_lib.KNOB_SPLITK_FUSED, old)
+    assert np.array_equal(outs[0], outs[1]) and np.array_equal(outs[1], outs[2])
+    ref = 0.75 * np.einsum("bmk,bkn->bmn", D.read(a), D.read(b)) - 1.25 * D.read(c0)
+    assert np.allclose(outs[0], ref, rtol=1e-11, atol=1e-10)
