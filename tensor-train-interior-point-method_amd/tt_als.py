@@ -755,9 +755,16 @@ def _tt_approx_product(A, Dm, x0, kick_rank, nswp, tol, verbose):
             rel_n[0] = 0
         return m
 
-    def unit(t):
-        nn = D.norm(t)
-        return D.scaled(t, 1.0 / nn), nn
+    def unit_and_env(t, Pk):
+        """(t / ||t||, ||t||) and (Pk / nrm, nrm) of one core step: both norms in ONE host read (the
+        environment Pk does not depend on t; same values as two D.norm calls)"""
+        buf = D.empty(2)
+        D.dot_into(t, t, buf[0:1])
+        D.dot_into(Pk, Pk, buf[1:2])
+        h = D.read(buf)
+        nn, nrm = D.norm_of(h[0]), D.norm_of(h[1])
+        nrm = nrm if nrm > 0 else 1.0
+        return D.scaled(t, 1.0 / nn), nn, D.scaled(Pk, 1.0 / nrm), nrm
 
     last = False
     swp = 0
@@ -782,13 +789,11 @@ def _tt_approx_product(A, Dm, x0, kick_rank, nswp, tol, verbose):
                 nrmsc *= nx[k - 1] / nAD[k - 1]
                 x[k] = D.clone(u.t()).view(r, *modes[k], rx[k + 1])
                 prev = D.contig(x[k - 1]).view(-1, rx[k])
-                x[k - 1], nn = unit(einsum("ic,jc->ij", prev, v).view(rx[k - 1], *modes[k - 1], r))
+                t = einsum("ic,jc->ij", prev, v).view(rx[k - 1], *modes[k - 1], r)
+                Pk = einsum(e_bck, P[k + 1], A[k], Dm[k], x[k])
+                x[k - 1], nn, P[k], nrm = unit_and_env(t, Pk)
                 nx[k - 1] *= nn
                 rx[k] = r
-                Pk = einsum(e_bck, P[k + 1], A[k], Dm[k], x[k])
-                nrm = D.norm(Pk)
-                nrm = nrm if nrm > 0 else 1.0
-                P[k] = D.scaled(Pk, 1.0 / nrm)
                 nAD[k - 1] = nrm
                 nrmsc *= nAD[k - 1] / nx[k - 1]
             else:
@@ -813,13 +818,11 @@ def _tt_approx_product(A, Dm, x0, kick_rank, nswp, tol, verbose):
                     u, v = U[:, :r], v[:r]
                 x[k] = D.contig(u).view(rx[k], *modes[k], r)
                 nxt = D.contig(x[k + 1]).view(rx[k + 1], -1)
-                x[k + 1], nn = unit(einsum("ij,jk->ik", v, nxt).view(r, *modes[k + 1], rx[k + 2]))
+                t = einsum("ij,jk->ik", v, nxt).view(r, *modes[k + 1], rx[k + 2])
+                Pk = einsum(e_fwd, P[k], A[k], Dm[k], x[k])
+                x[k + 1], nn, P[k + 1], nrm = unit_and_env(t, Pk)
                 nx[k] *= nn
                 rx[k + 1] = r
-                Pk = einsum(e_fwd, P[k], A[k], Dm[k], x[k])
-                nrm = D.norm(Pk)
-                nrm = nrm if nrm > 0 else 1.0
-                P[k + 1] = D.scaled(Pk, 1.0 / nrm)
                 nAD[k] = nrm
                 nrmsc *= nAD[k] / nx[k]
             else:
