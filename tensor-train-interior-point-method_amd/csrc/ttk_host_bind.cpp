@@ -281,6 +281,51 @@ at::Tensor zeros(const at::Tensor &like, std::vector<int64_t> shape) {
   return out;
 }
 
+// ttk_env_update's block descriptor (include/ttk.h ttk_env_block, same layout)
+struct EnvBlock {
+  const double *phi, *x, *A, *y;
+  double *out;
+  int64_t phi_shape[3], x_shape[3], A_shape[4], y_shape[3];
+  int64_t a_strides[4];
+};
+using env_fn = int (*)(void *, int, int, const EnvBlock *);
+
+// all environment updates of one core step (tt_als.env_update_many): the outputs allocated and the
+// descriptors packed here, then ONE ttk_env_update call (fn = its address, ctx = the context)
+std::vector<at::Tensor> env_update(int64_t fn, int64_t ctx, bool backward,
+                                   const std::vector<std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor>> &items) {
+  const size_t n = items.size();
+  std::vector<EnvBlock> blocks(n);
+  std::vector<at::Tensor> outs;
+  outs.reserve(n);
+  for (size_t i = 0; i < n; ++i) {
+    const at::Tensor &P = std::get<0>(items[i]), &x = std::get<1>(items[i]), &A = std::get<2>(items[i]),
+                     &y = std::get<3>(items[i]);
+    TORCH_CHECK(P.dim() == 3 && x.dim() == 3 && A.dim() == 4 && y.dim() == 3, "env_update: operand ranks");
+    at::Tensor o = backward ? at::empty({x.size(0), A.size(0), y.size(0)}, P.options())
+                            : at::empty({x.size(2), A.size(3), y.size(2)}, P.options());
+    EnvBlock &e = blocks[i];
+    e.phi = P.data_ptr<double>();
+    e.x = x.data_ptr<double>();
+    e.A = A.data_ptr<double>();
+    e.y = y.data_ptr<double>();
+    e.out = o.data_ptr<double>();
+    for (int k = 0; k < 3; ++k) {
+      e.phi_shape[k] = P.size(k);
+      e.x_shape[k] = x.size(k);
+      e.y_shape[k] = y.size(k);
+    }
+    for (int k = 0; k < 4; ++k) {
+      e.A_shape[k] = A.size(k);
+      e.a_strides[k] = A.stride(k);
+    }
+    outs.push_back(o);
+  }
+  check(reinterpret_cast<env_fn>(fn)(reinterpret_cast<void *>(ctx), backward ? 1 : 0, (int)n, blocks.data()),
+        "env_update");
+  return outs;
+}
+
 // Tensor metadata helpers that keep the GIL: torch's own Python bindings release it around every
 // op (torch.empty, Tensor.view / .t / .permute), which costs ~2 us per call and, with a second
 // solve thread in the process, a GIL hand-over each time (2-2.5x per call, tools/gil_bench.py).
@@ -304,6 +349,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("mul_", &mul_);
   m.def("bind2", &bind2);
   m.def("einsum_cols", &einsum_cols);
+  m.def("env_update", &env_update);
   m.def("axpby", &axpby);
   m.def("normalized", &normalized);
   m.def("scale_axis_ss", &scale_axis_ss);

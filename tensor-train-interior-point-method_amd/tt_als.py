@@ -240,6 +240,9 @@ class _EnvBlock(ctypes.Structure):
 
 
 NATIVE_ENV = os.environ.get("TTIPM_NATIVE_ENV", "1") == "1"
+# _ttkbind.env_update and the address of ttk_env_update it calls (None: pack in Python)
+_ENV_NATIVE = ((D._BIND, ctypes.cast(D.lib.ttk_env_update, ctypes.c_void_p).value)
+               if D._BIND is not None and hasattr(D._BIND, "env_update") and D.DEV.type == "cuda" else (None, None))
 
 
 def env_update_many(backward, items):
@@ -250,6 +253,9 @@ def env_update_many(backward, items):
             not all(P.is_contiguous() and x.is_contiguous() and y.is_contiguous() for P, x, A, y in items):
         f = compute_phi_bck_A if backward else compute_phi_fwd_A
         return [f(P, x, A, y) for P, x, A, y in items]
+    if D.ALGO is None and _ENV_NATIVE[0] is not None:  # descriptors packed natively (same library call)
+        D._stream()
+        return _ENV_NATIVE[0].env_update(_ENV_NATIVE[1], D.ctx().value, bool(backward), items)
     arr = (_EnvBlock * len(items))()
     outs = []
     for e, (P, x, A, y) in zip(arr, items):
