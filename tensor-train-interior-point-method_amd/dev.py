@@ -416,6 +416,20 @@ def read(t):
     return out
 
 
+def check_handoffs():
+    """Raise if an in-launch hand-off wait of this thread's context gave up since the last check
+    (ttk_common.h dep_wait: after DEP_SPIN_MAX polls it counts a timeout and reads on, so the
+    one-launch Schur matvec / Arnoldi step / split-K reduce would have used stale words).  One
+    stream synchronisation; called once per solve (tt_ipm.tt_ipm) and by the kernel tests."""
+    if DEV.type != "cuda" or ctx() is None:
+        return
+    _stream()
+    n = ctypes.c_uint(0)
+    check(lib.ttk_dep_timeouts(ctypes.byref(n), 1), "dep_timeouts")
+    if n.value:
+        raise RuntimeError(f"{n.value} in-launch hand-off wait(s) timed out: results of this solve are invalid")
+
+
 # ------------------------------------------------------------------------ einsum planner
 def _ones_buf():
     t = _TL.ones.get("o")

@@ -1077,6 +1077,7 @@ def tt_ipm(lag_maps, obj_tt, lin_op_tt, bias_tt, ineq_mask=None, max_iter=100, m
         prev['centrality'] = st.centrality_error
         if iter_callback is not None:
             iter_callback(it)
+    D.check_handoffs()  # a timed-out in-launch hand-off (stale data) invalidates the solve
     rX, rZ, rY = T.tt_ranks(X), T.tt_ranks(Z), T.tt_ranks(Y)
     rT = T.tt_ranks(Tt) if Tt else [0] * (st.dim - 1)
     print("---Terminated---")

@@ -247,6 +247,11 @@ RUNS = [
     ("maxcut", "maxcut_12", 23, 2, True, 3),
     ("maxcut", "maxcut_12", 53, 2, True, 3),
     ("maxcut", "maxcut_12", 12, 2, True, 3),
+    # ... and their full runs (round 5: the device's end points on these seeds need a reference)
+    ("maxcut", "maxcut_12", 45, 2, True, 0),
+    ("maxcut", "maxcut_12", 23, 2, True, 0),
+    ("maxcut", "maxcut_12", 53, 2, True, 0),
+    ("maxcut", "maxcut_12", 12, 2, True, 0),
 ]
 
 
@@ -322,10 +327,14 @@ if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "merge_twin":  # merge_twin KEY TMP: a bounded hash twin
         merge(sys.argv[2], sys.argv[3], "bounded_twins.json")
         sys.exit(0)
+    if len(sys.argv) > 1 and sys.argv[1] == "local":  # dense local KKT solve fixtures (a6 / a7)
+        from tests.golden import make_local
+        make_local.main(_import_reference)
+        sys.exit(0)
     if len(sys.argv) < 2 or sys.argv[1] not in ("runs", "prims", "all"):
         # no default: a bare invocation must not start regenerating (and rewriting) runs.json
         sys.exit("usage: make_golden.py runs|prims|all [KEY ...] [-jN] | one PROB CFG SEED RANK FIXED OUT [NMAX]"
-                 " | merge KEY TMP")
+                 " | merge KEY TMP | local")
     what = sys.argv[1]
     rest = [a for a in sys.argv[2:] if not a.startswith("-j")]
     jobs = max([int(a[2:]) for a in sys.argv[2:] if a.startswith("-j")] or [1])
