@@ -58,7 +58,9 @@ def test_local_solver_matches_reference(dev, name, capsys):
         return
     tol = 1e-10 if not ex["failed"] else 1e-7  # LGMRES fallbacks: device vs restated PETSc reductions
     assert LC.rel(D.read(sol), ex["sol"]) <= tol, LC.rel(D.read(sol), ex["sol"])
-    assert abs(res_min - ex["res_min"]) <= max(1e-6 * ex["res_min"], 1e-11)
+    # a direct solve's new residual is at the rounding floor (~1e-10 of ||rhs||, set by summation
+    # order): absolute there
+    assert abs(res_min - ex["res_min"]) <= max(1e-6 * ex["res_min"], 1e-9)
 
 
 @pytest.mark.parametrize("name", [c for c in LC.CASES if "_dense" in c or c.endswith(("_chol", "_ill"))])

@@ -247,6 +247,6 @@ def test_local_solver_matches_reference(name, capsys):
         return
     tol = 1e-10 if not ex["failed"] else 1e-8
     assert LC.rel(sol, ex["sol"]) <= tol, LC.rel(sol, ex["sol"])
-    # the new residual of a dense solve sits at rounding level (||A x - rhs|| / ||rhs|| ~ 1e-10):
-    # compared in absolute terms there
-    assert abs(res_min - ex["res_min"]) <= max(1e-6 * ex["res_min"], 1e-11)
+    # the new residual of a dense solve sits at rounding level (||A x - rhs|| / ||rhs|| ~ 1e-10, set
+    # by summation order): compared in absolute terms there
+    assert abs(res_min - ex["res_min"]) <= max(1e-6 * ex["res_min"], 1e-9)
