@@ -95,6 +95,11 @@ void *ttk_ctx_stream(ttk_ctx ctx);
  *                   the partials in split order and writes C (the separate reduce launch's
  *                   arithmetic, bit-identical); 0: split kernel + reduce kernel (default from env
  *                   TTK_SPLITK_FUSED, else 1)
+ * TTK_KNOB_TRI_HOIST  1: each step of the multi-workgroup Householder tridiagonalisation of
+ *                   ttk_syev_extreme (128 < n <= 512) issues every global load of the step before
+ *                   its first use -- one L2 round trip per step instead of three; 0: the loads
+ *                   where they are used (same arithmetic in the same order: bit-identical; default
+ *                   from env TTK_TRI_HOIST, else 1)
  * ttk_ctx_set_knob stores value and returns the previous one in *old (may be NULL). */
 enum ttk_knob {
   TTK_KNOB_FUSED_APPLY = 0,
@@ -109,7 +114,8 @@ enum ttk_knob {
   TTK_KNOB_ARNOLDI_ONE = 9,
   TTK_KNOB_SCHUR_PREP = 10,
   TTK_KNOB_SPLITK_FUSED = 11,
-  TTK_KNOB_COUNT = 12
+  TTK_KNOB_TRI_HOIST = 12,
+  TTK_KNOB_COUNT = 13
 };
 int ttk_ctx_set_knob(ttk_ctx ctx, int knob, int value, int *old);
 int ttk_ctx_get_knob(ttk_ctx ctx, int knob, int *value);

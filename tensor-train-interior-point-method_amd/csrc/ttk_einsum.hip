@@ -525,6 +525,9 @@ struct ApplyArgs {
   // operands pre-permuted into their LDS images once per Schur handle (schur_prep_kernel): As
   // [i][S][s][j] and Qs [c][S|d] rows of stride (nS*nd)|1; staging then is a contiguous copy
   const double *As_pre = nullptr, *Qs_pre = nullptr;
+  // VALU rows: 1 stages the operands with the batched loads of stage_row_batched, 0 with the original
+  // per-operand loops (pure copies either way: bit-identical; env TTK_STAGE_BATCH, default 1)
+  int stage1 = 1;
 };
 
 // Association follows the greedy pairwise plan the reference's opt_einsum picks for these shapes
@@ -574,6 +577,144 @@ __device__ unsigned long long g_mph[8];
 #define TTK_VPH(K)
 #endif
 
+// Operand staging of apply_row with every thread's first batch of loads -- up to SC_* elements per
+// operand -- issued before any of its LDS stores: a maxcut-sized row (x <= 676, P row <= 130,
+// A <= 1600, Q <= 1700 doubles over 256 threads) waits for ONE L2 round trip instead of one per
+// operand and per unrolled group of four (a plain copy loop waits before each group's stores).
+// Elements beyond the caps follow in per-operand loops.  With x handed off inside the launch (g.dep)
+// the other operands are loaded first, so their loads overlap the hand-off wait.  Pure copies: the
+// staged values are exactly the original loops' (ApplyArgs::stage1 = 0 runs those).
+// VALU rows (256 threads): caps <4, 1, 8, 8>; MFMA rows (1024 threads, Q read in stage 3): <8, 1, 2, 1>.
+template <int SC_X, int SC_P, int SC_A, int SC_Q>
+__device__ void stage_row_batched(const ApplyArgs &g, int a, double *X, double *Pa, double *As, double *Qs, int lq3,
+                                  int tid, int nt) {
+  const int nb = g.nb, nj = g.nj, nd = g.nd, nS = g.nS, ns = g.ns, ni = g.ni, nc = g.nc;
+  const int nx = nb * nj * nd, np = ns * nb, na = ns * ni * nj * nS;
+  const int nq = g.qlds ? (g.Qs_pre ? nc * lq3 : nc * nS * nd) : 0;
+  const bool xc = g.xs[2] == 1 && g.xs[1] == nd && g.xs[0] == (int64_t)nj * nd;
+  const int rx[3] = {nb, nj, nd}, ra[4] = {ni, nS, ns, nj}, rq[3] = {nc, nS, nd};
+  const double *pa = g.P + a * g.ps[0];
+  double vp[SC_P], va[SC_A], vq[SC_Q], vx[SC_X];
+  int dq[SC_Q];
+  // ---- first batch: loads
+#pragma unroll
+  for (int u = 0; u < SC_P; ++u) {
+    const int e = tid + u * nt, s = e / nb, b = e - s * nb;
+    vp[u] = e < np ? pa[s * g.ps[1] + b * g.ps[2]] : 0.0;
+  }
+  if (g.As_pre) {
+#pragma unroll
+    for (int u = 0; u < SC_A; ++u) {
+      const int e = tid + u * nt;
+      va[u] = e < na ? g.As_pre[e] : 0.0;
+    }
+  } else {  // As[i][S][s][j] = A[s, i, j, S]
+    MixedIdx<4> ia(tid, nt, ra);
+#pragma unroll
+    for (int u = 0; u < SC_A; ++u, ia.step(ra)) {
+      const int e = tid + u * nt;
+      va[u] = e < na ? g.A[ia.v[2] * g.as[0] + ia.v[0] * g.as[1] + ia.v[3] * g.as[2] + ia.v[1] * g.as[3]] : 0.0;
+    }
+  }
+  if (g.Qs_pre) {
+#pragma unroll
+    for (int u = 0; u < SC_Q; ++u) {
+      const int e = tid + u * nt;
+      vq[u] = e < nq ? g.Qs_pre[e] : 0.0;
+      dq[u] = e;
+    }
+  } else {
+    MixedIdx<3> iq(tid, nt, rq);
+#pragma unroll
+    for (int u = 0; u < SC_Q; ++u, iq.step(rq)) {
+      const int e = tid + u * nt;
+      vq[u] = e < nq ? g.Q[iq.v[0] * g.qs[0] + iq.v[1] * g.qs[1] + iq.v[2] * g.qs[2]] : 0.0;
+      dq[u] = iq.v[0] * lq3 + iq.v[1] * nd + iq.v[2];
+    }
+  }
+  if (!g.dep) {
+    if (xc) {
+#pragma unroll
+      for (int u = 0; u < SC_X; ++u) {
+        const int e = tid + u * nt;
+        vx[u] = e < nx ? g.x[e] : 0.0;
+      }
+    } else {
+      MixedIdx<3> ix(tid, nt, rx);
+#pragma unroll
+      for (int u = 0; u < SC_X; ++u, ix.step(rx)) {
+        const int e = tid + u * nt;
+        vx[u] = e < nx ? g.x[ix.v[0] * g.xs[0] + ix.v[1] * g.xs[1] + ix.v[2] * g.xs[2]] : 0.0;
+      }
+    }
+  }
+  // ---- first batch: stores
+#pragma unroll
+  for (int u = 0; u < SC_P; ++u)
+    if (tid + u * nt < np) Pa[tid + u * nt] = vp[u];
+#pragma unroll
+  for (int u = 0; u < SC_A; ++u)
+    if (tid + u * nt < na) As[tid + u * nt] = va[u];
+#pragma unroll
+  for (int u = 0; u < SC_Q; ++u)
+    if (tid + u * nt < nq) Qs[dq[u]] = vq[u];
+  if (!g.dep) {
+#pragma unroll
+    for (int u = 0; u < SC_X; ++u)
+      if (tid + u * nt < nx) X[tid + u * nt] = vx[u];
+  }
+  // ---- the rest of large operands (the original loops from the first element past the caps)
+  for (int e = tid + SC_P * nt; e < np; e += nt) {
+    const int s = e / nb, b = e - s * nb;
+    Pa[e] = pa[s * g.ps[1] + b * g.ps[2]];
+  }
+  if (na > SC_A * nt) {
+    if (g.As_pre) {
+      for (int e = tid + SC_A * nt; e < na; e += nt) As[e] = g.As_pre[e];
+    } else {
+      MixedIdx<4> ia(tid + SC_A * nt, nt, ra);
+      for (int e = tid + SC_A * nt; e < na; e += nt, ia.step(ra))
+        As[e] = g.A[ia.v[2] * g.as[0] + ia.v[0] * g.as[1] + ia.v[3] * g.as[2] + ia.v[1] * g.as[3]];
+    }
+  }
+  if (nq > SC_Q * nt) {
+    if (g.Qs_pre) {
+      for (int e = tid + SC_Q * nt; e < nq; e += nt) Qs[e] = g.Qs_pre[e];
+    } else {
+      MixedIdx<3> iq(tid + SC_Q * nt, nt, rq);
+      for (int e = tid + SC_Q * nt; e < nq; e += nt, iq.step(rq))
+        Qs[iq.v[0] * lq3 + iq.v[1] * nd + iq.v[2]] = g.Q[iq.v[0] * g.qs[0] + iq.v[1] * g.qs[1] + iq.v[2] * g.qs[2]];
+    }
+  }
+  const int x0 = g.dep ? 0 : SC_X;  // first x element still to stage
+  if (g.dep) ttk::dep_wait(g.dep, g.dep_target);
+  if (nx > x0 * nt) {
+    if (xc && g.dep) {
+      // batched too: the hand-off is on the row's critical path
+      for (int b0 = tid; b0 < nx; b0 += SC_X * nt) {
+#pragma unroll
+        for (int u = 0; u < SC_X; ++u) {
+          const int e = b0 + u * nt;
+          vx[u] = e < nx ? ttk::ld_sc1(g.x + e) : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < SC_X; ++u)
+          if (b0 + u * nt < nx) X[b0 + u * nt] = vx[u];
+      }
+    } else if (xc) {
+      for (int e = tid + x0 * nt; e < nx; e += nt) X[e] = g.x[e];
+    } else {
+      MixedIdx<3> ix(tid + x0 * nt, nt, rx);
+      if (g.dep)
+        for (int e = tid + x0 * nt; e < nx; e += nt, ix.step(rx))
+          X[e] = ttk::ld_sc1(g.x + ix.v[0] * g.xs[0] + ix.v[1] * g.xs[1] + ix.v[2] * g.xs[2]);
+      else
+        for (int e = tid + x0 * nt; e < nx; e += nt, ix.step(rx))
+          X[e] = g.x[ix.v[0] * g.xs[0] + ix.v[1] * g.xs[1] + ix.v[2] * g.xs[2]];
+    }
+  }
+}
+
 // tid / nt: this row's threads (the whole block, or one half of it when a task's two terms run side
 // by side, see fused_apply_multi_kernel); every output element is still one thread's sequential chain,
 // so the thread count never changes a result.  Three block barriers, unconditional.
@@ -584,7 +725,6 @@ __device__ void apply_row(const ApplyArgs &g, int a, double *sm, double *orow, i
   if (tid == 0) atomicAdd(&g_mph[7], 1ull);
 #endif
   const int nb = g.nb, nj = g.nj, nd = g.nd, nS = g.nS, ns = g.ns, ni = g.ni, nc = g.nc;
-  if (g.dep) ttk::dep_wait(g.dep, g.dep_target);
   double *X = sm;                       // nb*nj*nd     [b][j][d]
   double *Pa = X + nb * nj * nd;        // ns*nb        [s][b]   (P[a, s, b])
   double *As = Pa + ns * nb;            // ns*ni*nj*nS  [i][S][s][j]
@@ -592,6 +732,11 @@ __device__ void apply_row(const ApplyArgs &g, int a, double *sm, double *orow, i
   double *T2 = T1 + ns * nj * nd;       // ni*nS*nd     [i][S][d]
   double *Qs = T2 + ni * nS * nd;       // nc rows of (nS*nd | 1)  [c][S][d]  (g.qlds)
   const int lq3 = (nS * nd) | 1;        // odd row stride: stage 3's lanes (one c each) on distinct banks
+  if (g.stage1) {
+    stage_row_batched<4, 1, 8, 8>(g, a, X, Pa, As, Qs, lq3, tid, nt);
+    __syncthreads();
+  } else {
+  if (g.dep) ttk::dep_wait(g.dep, g.dep_target);
   if (g.qlds) {  // stage 3 reads every Q element once per row: one coalesced pass instead of a
                  // dependent FMA chain over global loads
     if (g.Qs_pre) {
@@ -644,6 +789,7 @@ __device__ void apply_row(const ApplyArgs &g, int a, double *sm, double *orow, i
       As[e] = g.A[ia.v[2] * g.as[0] + ia.v[0] * g.as[1] + ia.v[3] * g.as[2] + ia.v[1] * g.as[3]];
   }
   __syncthreads();
+  }
   TTK_VPH(0)
   for (int e = tid; e < ns * nj * nd; e += nt) {  // t1[s][j][d] = sum_b P[a,s,b] x[b,j,d]
     const int s = e / (nj * nd), r = e - s * nj * nd;  // r = j*nd + d
@@ -814,13 +960,16 @@ __device__ void apply_row_mfma(const ApplyArgs &g, int a, double *sm, double *or
   const int tid = threadIdx.x, nt = blockDim.x;
   const int nb = g.nb, nj = g.nj, nd = g.nd, nS = g.nS, ns = g.ns, ni = g.ni, nc = g.nc;
   const int jd = nj * nd, sj = ns * nj;
-  if (g.dep) ttk::dep_wait(g.dep, g.dep_target);
   double *X = sm;                       // [b][j][d]
   double *Pa = X + nb * jd;             // [s][b]
   double *As = Pa + ns * nb;            // [(i,S)][(s,j)]
   double *T1 = As + ni * nS * sj;       // [(s,j)][d]
   double *T2 = T1 + sj * nd;            // [(i,S)][d]
   double *Qc = T2 + ni * nS * nd;       // [c][k], QCHUNK_MAX
+  if (g.stage1) {  // As [(i,S)][(s,j)] is the VALU rows' [i][S][s][j]; no Q staging (g.qlds = 0)
+    stage_row_batched<8, 1, 2, 1>(g, a, X, Pa, As, nullptr, 1, tid, nt);
+  } else {
+  if (g.dep) ttk::dep_wait(g.dep, g.dep_target);
   {  // staging: the gathers' multi-digit indices advance by carries instead of divisions
     const int rx[3] = {nb, nj, nd};
     MixedIdx<3> ix(tid, nt, rx);
@@ -843,6 +992,7 @@ __device__ void apply_row_mfma(const ApplyArgs &g, int a, double *sm, double *or
     MixedIdx<4> ia(tid, nt, ra);
     for (int e = tid; e < ni * nS * sj; e += nt, ia.step(ra))
       As[e] = g.A[ia.v[2] * g.as[0] + ia.v[0] * g.as[1] + ia.v[3] * g.as[2] + ia.v[1] * g.as[3]];
+  }
   }
   __syncthreads();
   TTK_MPH(0)
@@ -1083,6 +1233,7 @@ static int valu_threads_env() {
   return t < 64 ? 64 : (t > 512 ? 512 : t / 64 * 64);
 }
 static const int g_valu_threads = valu_threads_env();
+static const int g_stage_batch = getenv("TTK_STAGE_BATCH") ? (atoi(getenv("TTK_STAGE_BATCH")) != 0) : 1;
 
 // workgroups per MFMA output row (ApplyArgs::csplit): enough that each workgroup's share of the
 // stage-3 (tile, K block) pairs is about one round over its waves, but no more workgroups in the
@@ -1189,6 +1340,7 @@ static int apply_args(const char *eq, const int64_t *desc, double *out, double a
     g.os[0] = (int64_t)g.ni * g.nc;
   }
   g.mfma = 0;
+  g.stage1 = g_stage_batch;
   if (g.na < 1 || g.na > 65535) return 0;
   if (apply_lds(g.nb, g.nj, g.nd, g.nS, g.ns, g.ni) <= APPLY_LDS_DOUBLES) return 1;
   if (mfma_enabled() && apply_mfma_lds(g) <= APPLY_LDS_DOUBLES) {  // only the MFMA stages fit LDS

@@ -59,11 +59,12 @@ struct Ctx {
                               env_int("TTK_LGMRES_MW_MIN", 16384), env_int("TTK_MFMA_CSPLIT", 1) != 0 ? 1 : 0,
                               env_int("TTK_APPLY_DUAL", 1) != 0 ? 1 : 0, env_int("TTK_RCOND_EXACT", 0) != 0 ? 1 : 0,
                               env_int("TTK_SCHUR_ONE", 1) != 0 ? 1 : 0, env_int("TTK_ARNOLDI_ONE", 1) != 0 ? 1 : 0,
-                              env_int("TTK_SCHUR_PREP", 1) != 0 ? 1 : 0, env_int("TTK_SPLITK_FUSED", 1) != 0 ? 1 : 0};
+                              env_int("TTK_SCHUR_PREP", 1) != 0 ? 1 : 0, env_int("TTK_SPLITK_FUSED", 1) != 0 ? 1 : 0,
+                              env_int("TTK_TRI_HOIST", 1) != 0 ? 1 : 0};
 };
 Ctx &ctx();
-Ctx *ctx_swap(Ctx *c);
-void schur_release(Ctx &c);  // ttk_einsum.hip: Schur handle table + operand images of a context  // bind c to the calling thread, return the previous binding
+Ctx *ctx_swap(Ctx *c);       // bind c to the calling thread, return the previous binding
+void schur_release(Ctx &c);  // ttk_einsum.hip: Schur handle table + operand images of a context
 }  // namespace ttk
 
 struct ttk_ctx_s {

@@ -1783,6 +1783,148 @@ __global__ __launch_bounds__(256) void tri_step_kernel(double *A, int n, int k, 
   (void)s_tau;
 }
 
+// tri_step_kernel with every global load of the step issued up front into registers (the previous
+// step's partials, pivot row k, reflector k-1 and its p vector, the wave's own row): the loads do not
+// depend on each other, so a step waits for ONE round of L2 latency instead of three (partials ->
+// pivot row -> own row).  The arithmetic, its order and every stored value are tri_step_kernel's
+// at rb = 4 (bit-identical; TTK_KNOB_TRI_HOIST = 0 switches back).  NX * 256 >= n - k,
+// NP * 64 >= nblk, NR * 64 >= n - k - 1.
+template <int NX, int NP, int NR>
+__global__ __launch_bounds__(256) void tri_step_hoist_kernel(double *A, int n, int k, double *tv, double *ov,
+                                                             double *dv, double *pvb, double *partb, double *vbuf,
+                                                             int nblk) {
+  __shared__ double xs[NX * 256 + 1];
+  __shared__ double red[16];
+  __shared__ double s_k;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int r0 = blockIdx.x * 4, r1 = r0 + 4 < n ? r0 + 4 : n;
+  const int kp = k - 1;
+  const double *pvp = pvb + (kp & 1) * (int64_t)n, *ptp = partb + (kp & 1) * (int64_t)nblk;
+  const double *vp = vbuf + (kp & 1) * (int64_t)n;  // reflector k-1, relative index (vp[0] = 1)
+  double *pvc = pvb + (k & 1) * (int64_t)n, *ptc = partb + (k & 1) * (int64_t)nblk, *vc = vbuf + (k & 1) * (int64_t)n;
+  const int m = n - k - 1;
+  // ---- loads (values of buffers step k-1 did not write are read but never used: taup == 0 then)
+  const double taup = kp >= 0 ? tv[kp] : 0.0;
+  double pa[NP];
+#pragma unroll
+  for (int u = 0; u < NP; ++u) {
+    const int i = lane + 64 * u;
+    pa[u] = (wid == 0 && i < nblk) ? ptp[i] : 0.0;
+  }
+  const double v0 = vp[0], p0 = pvp[0];
+  double xa[NX], xv[NX], xp[NX];
+#pragma unroll
+  for (int u = 0; u < NX; ++u) {
+    const int j = k + tid + 256 * u, jj = j - kp - 1;
+    const bool ok = j < n;
+    xa[u] = ok ? A[(int64_t)k * n + j] : 0.0;
+    xv[u] = ok ? vp[jj] : 0.0;
+    xp[u] = ok ? pvp[jj] : 0.0;
+  }
+  const int rs = r0 > k + 1 ? r0 : k + 1;
+  const int r = rs + wid;  // this wave's own row (rb = 4: at most one per wave)
+  const bool has_row = r < r1;
+  double ra[NR], rv[NR], rp[NR], vi = 0.0, pi = 0.0;
+  if (has_row) {
+    const int ir = r - kp - 1;
+    vi = vp[ir];
+    pi = pvp[ir];
+    const double *ar = A + (int64_t)r * n;
+#pragma unroll
+    for (int u = 0; u < NR; ++u) {
+      const int j = k + 1 + lane + 64 * u, jj = j - kp - 1;
+      const bool ok = j < n;
+      ra[u] = ok ? ar[j] : 0.0;
+      rv[u] = ok ? vp[jj] : 0.0;
+      rp[u] = ok ? pvp[jj] : 0.0;
+    }
+  }
+  // ---- the step (tri_step_kernel's operations)
+  if (wid == 0) {
+    double acc = 0.0;
+    if (taup != 0.0) {
+#pragma unroll
+      for (int u = 0; u < NP; ++u)
+        if (lane + 64 * u < nblk) acc += pa[u];
+    }
+    acc = ttk::wave_sum(acc);
+    if (lane == 0) s_k = 0.5 * taup * acc;
+  }
+  __syncthreads();
+  const double K = s_k;
+  {
+    const double wk = taup != 0.0 ? p0 - K * v0 : 0.0, vk = taup != 0.0 ? v0 : 0.0;
+#pragma unroll
+    for (int u = 0; u < NX; ++u) {
+      const int j = k + tid + 256 * u;
+      if (j < n) {
+        double a = xa[u];
+        // tri_step_kernel's contraction of a -= vk * (p - K v) + wk * v, spelled out (the compiler
+        // contracts the expression differently in this kernel)
+        if (taup != 0.0) a -= fma(wk, xv[u], vk * fma(-K, xv[u], xp[u]));
+        xs[j - k] = a;
+      }
+    }
+  }
+  __syncthreads();
+  double part = 0.0;
+  for (int i = 2 + tid; i <= m; i += 256) part += xs[i] * xs[i];
+  const double sigma = ttk::block_sum(part, red);
+  const double alpha = xs[1];
+  double tau = 0.0, beta = alpha;
+  if (sigma > 0.0) {
+    beta = -copysign(sqrt(alpha * alpha + sigma), alpha);
+    tau = (beta - alpha) / beta;
+  }
+  const double sc = sigma > 0.0 ? 1.0 / (alpha - beta) : 1.0;
+  const bool owner_k = k >= r0 && k < r1;
+  __syncthreads();  // every thread has read xs[1] / the sigma partials
+  for (int i = 1 + tid; i <= m; i += 256) {
+    const double v = (i == 1) ? 1.0 : xs[i] * sc;
+    xs[i] = v;
+    if (owner_k) vc[i - 1] = v;
+  }
+  if (owner_k && tid == 0) {
+    tv[k] = tau;
+    ov[k] = beta;
+    dv[k] = xs[0];
+  }
+  if (kp >= 0 && kp >= r0 && kp < r1) {  // reflector k-1 into A's row k-1: the values loaded above
+#pragma unroll
+    for (int u = 0; u < NX; ++u) {
+      const int j = k + tid + 256 * u;
+      if (j < n) A[(int64_t)kp * n + j] = xv[u];
+    }
+  }
+  __syncthreads();
+  double contrib = 0.0;
+  if (has_row) {
+    double *ar = A + (int64_t)r * n;
+    const double wi = taup != 0.0 ? pi - K * vi : 0.0, vv = taup != 0.0 ? vi : 0.0;
+    double acc = 0.0;
+#pragma unroll
+    for (int u = 0; u < NR; ++u) {
+      const int j = k + 1 + lane + 64 * u;
+      if (j < n) {
+        double a = ra[u];
+        if (taup != 0.0) {
+          a -= fma(wi, rv[u], vv * fma(-K, rv[u], rp[u]));  // tri_step_kernel's contraction
+          ar[j] = a;
+        }
+        acc = fma(a, xs[j - k], acc);
+      }
+    }
+    acc = ttk::wave_sum(acc);
+    if (lane == 0) {
+      const double pr = tau * acc;
+      pvc[r - k - 1] = pr;
+      contrib += pr * xs[r - k];
+    }
+  }
+  contrib = ttk::block_sum(contrib, red);
+  if (tid == 0) ptc[blockIdx.x] = contrib;
+}
+
 // after the last step (k = n-3): pending update of step n-3 on the trailing 2 x 2 block and
 // reflector n-3 into A's row n-3 (one block)
 __global__ __launch_bounds__(256) void tri_tail_kernel(double *A, int n, double *tv, double *pvb, double *partb,
@@ -2718,9 +2860,18 @@ int ttk_syev_extreme(void *stream, const double *A, int n, int which, double *ev
     const int nblk = (n + rb - 1) / rb;
     double *pvb = gv + 11 * (int64_t)n, *vbuf = pvb + 2 * (int64_t)n, *partb = vbuf + 2 * (int64_t)n;
     TTK_HIP(hipMemcpyAsync(Aw, A, sizeof(double) * (size_t)n * n, hipMemcpyDeviceToDevice, st));
-    for (int k = 0; k + 2 < n; ++k)
-      hipLaunchKernelGGL(tri_step_kernel, dim3(nblk), dim3(256), 0, st, Aw, n, k, tv, ov, dv, pvb, partb, vbuf, nblk,
-                         rb);
+    const int hoist = rb == 4 && n <= 512 && ttk::ctx().knob[TTK_KNOB_TRI_HOIST] ? (n <= 256 ? 1 : 2) : 0;
+    for (int k = 0; k + 2 < n; ++k) {
+      if (hoist == 1)
+        hipLaunchKernelGGL((tri_step_hoist_kernel<1, 1, 4>), dim3(nblk), dim3(256), 0, st, Aw, n, k, tv, ov, dv, pvb,
+                           partb, vbuf, nblk);
+      else if (hoist == 2)
+        hipLaunchKernelGGL((tri_step_hoist_kernel<2, 2, 8>), dim3(nblk), dim3(256), 0, st, Aw, n, k, tv, ov, dv, pvb,
+                           partb, vbuf, nblk);
+      else
+        hipLaunchKernelGGL(tri_step_kernel, dim3(nblk), dim3(256), 0, st, Aw, n, k, tv, ov, dv, pvb, partb, vbuf, nblk,
+                           rb);
+    }
     hipLaunchKernelGGL(tri_tail_kernel, dim3(1), dim3(256), 0, st, Aw, n, tv, pvb, partb, vbuf, nblk);
     TTK_LAUNCH_CHECK();
     return tri_finish_launch(st, Aw, n, which, gv, ev, vec);
