@@ -528,7 +528,12 @@ struct ApplyArgs {
   // VALU rows: 1 stages the operands with the batched loads of stage_row_batched, 0 with the original
   // per-operand loops (pure copies either way: bit-identical; env TTK_STAGE_BATCH, default 1)
   int stage1 = 1;
+  // VALU rows: 1 runs the three stages' per-element FMA chains with the LDS operands loaded U steps
+  // ahead (lds_chain), 0 as plain loops (the same FMAs in the same order: bit-identical; env
+  // TTK_CHAIN_PREFETCH, default 1)
+  int chain = 1;
 };
+constexpr int CHAIN_U = 8;
 
 // Association follows the greedy pairwise plan the reference's opt_einsum picks for these shapes
 // (t1 = P x over r, t2 = A t1 over (s,n), out = Q t2 over (S,R)), so intermediates and rounding
@@ -687,7 +692,18 @@ __device__ void stage_row_batched(const ApplyArgs &g, int a, double *X, double *
     }
   }
   const int x0 = g.dep ? 0 : SC_X;  // first x element still to stage
+#ifdef TTK_VALU_PROFILE
+  if (g.dep) {  // hand-off wait ([4]) and waiting rows ([5]), inside the staging phase's time
+    const unsigned long long tw0 = wall_clock64();
+    ttk::dep_wait(g.dep, g.dep_target);
+    if (tid == 0) {
+      atomicAdd(&g_mph[4], wall_clock64() - tw0);
+      atomicAdd(&g_mph[5], 1ull);
+    }
+  }
+#else
   if (g.dep) ttk::dep_wait(g.dep, g.dep_target);
+#endif
   if (nx > x0 * nt) {
     if (xc && g.dep) {
       // batched too: the hand-off is on the row's critical path
@@ -715,10 +731,48 @@ __device__ void stage_row_batched(const ApplyArgs &g, int a, double *X, double *
   }
 }
 
+// acc <- fma(a[k*sa], b[k*sb], acc) for k = 0..K-1 in order -- a row's sequential chain -- with the
+// LDS operands of the next U steps loaded while the current U FMAs run: the chain then waits on FMA
+// latency instead of one LDS round trip per step (the same operations in the same order as the
+// plain loop: bit-identical)
+template <int U>
+__device__ __forceinline__ double lds_chain(const double *a, int sa, const double *b, int sb, int K, double acc) {
+  int k = 0;
+  if (K >= U) {
+    double x[U], y[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      x[u] = a[u * sa];
+      y[u] = b[u * sb];
+    }
+    for (k = U; k + U <= K; k += U) {
+      double nx[U], ny[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        nx[u] = a[(k + u) * sa];
+        ny[u] = b[(k + u) * sb];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) acc = fma(x[u], y[u], acc);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        x[u] = nx[u];
+        y[u] = ny[u];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc = fma(x[u], y[u], acc);
+  }
+  for (; k < K; ++k) acc = fma(a[k * sa], b[k * sb], acc);
+  return acc;
+}
+
 // tid / nt: this row's threads (the whole block, or one half of it when a task's two terms run side
 // by side, see fused_apply_multi_kernel); every output element is still one thread's sequential chain,
 // so the thread count never changes a result.  Three block barriers, unconditional.
-template <bool DIRECT>
+// CHAIN: compile the prefetched FMA chains (lds_chain; used when g.chain) -- off in the 1024-thread
+// launches, whose 128-VGPR budget they would exceed
+template <bool DIRECT, bool CHAIN = true>
 __device__ void apply_row(const ApplyArgs &g, int a, double *sm, double *orow, int tid, int nt) {
 #ifdef TTK_VALU_PROFILE
   unsigned long long t_vh_ = wall_clock64();
@@ -794,9 +848,11 @@ __device__ void apply_row(const ApplyArgs &g, int a, double *sm, double *orow, i
   for (int e = tid; e < ns * nj * nd; e += nt) {  // t1[s][j][d] = sum_b P[a,s,b] x[b,j,d]
     const int s = e / (nj * nd), r = e - s * nj * nd;  // r = j*nd + d
     const double *pr = Pa + s * nb;
-    double acc = 0.0;
-    for (int b = 0; b < nb; ++b) acc = fma(pr[b], X[b * nj * nd + r], acc);
-    T1[e] = acc;
+    T1[e] = CHAIN && g.chain ? lds_chain<CHAIN_U>(pr, 1, X + r, nj * nd, nb, 0.0) : [&] {
+      double acc = 0.0;
+      for (int b = 0; b < nb; ++b) acc = fma(pr[b], X[b * nj * nd + r], acc);
+      return acc;
+    }();
   }
   __syncthreads();
   TTK_VPH(1)
@@ -804,9 +860,11 @@ __device__ void apply_row(const ApplyArgs &g, int a, double *sm, double *orow, i
   for (int e = tid; e < ni * nS * nd; e += nt) {  // t2[i][S][d] = sum_{s,j} A[s,i,j,S] t1[s][j][d]
     const int iS = e / nd, d = e - iS * nd;
     const double *ar = As + iS * sj;
-    double acc = 0.0;
-    for (int k = 0; k < sj; ++k) acc = fma(ar[k], T1[k * nd + d], acc);
-    T2[e] = acc;
+    T2[e] = CHAIN && g.chain ? lds_chain<CHAIN_U>(ar, 1, T1 + d, nd, sj, 0.0) : [&] {
+      double acc = 0.0;
+      for (int k = 0; k < sj; ++k) acc = fma(ar[k], T1[k * nd + d], acc);
+      return acc;
+    }();
   }
   __syncthreads();
   TTK_VPH(2)
@@ -816,7 +874,10 @@ __device__ void apply_row(const ApplyArgs &g, int a, double *sm, double *orow, i
     double acc = 0.0;
     if (g.qlds) {
       const double *qr = Qs + c * lq3;
-      for (int k = 0; k < nS * nd; ++k) acc = fma(qr[k], tr[k], acc);  // k = (S, d): the same order
+      if (CHAIN && g.chain)
+        acc = lds_chain<CHAIN_U>(qr, 1, tr, 1, nS * nd, 0.0);  // k = (S, d): the same order
+      else
+        for (int k = 0; k < nS * nd; ++k) acc = fma(qr[k], tr[k], acc);
     } else {
       for (int S = 0; S < nS; ++S) {
         const double *qr = g.Q + c * g.qs[0] + S * g.qs[1];
@@ -1106,7 +1167,10 @@ struct ApplyLaunch {
   unsigned *dep = nullptr;
 };
 
-__global__ __launch_bounds__(1024) void fused_apply_multi_kernel(ApplyLaunch L) {
+// MF: the launch carries MFMA-stage rows (1024 threads, <= 128 VGPRs); otherwise VALU rows only (at
+// most 2 x 256 threads), whose register budget leaves room for the prefetched FMA chains
+template <bool MF>
+__global__ __launch_bounds__(MF ? 1024 : 512) void fused_apply_multi_kernel(ApplyLaunch L) {
   extern __shared__ double sm[];
   int t = 0;
   while (t + 1 < L.ntask && (int)blockIdx.x >= L.off[t + 1]) ++t;
@@ -1119,7 +1183,7 @@ __global__ __launch_bounds__(1024) void fused_apply_multi_kernel(ApplyLaunch L) 
     // the two terms side by side (independent until they are summed): half the block each, own LDS
     // stages; then the same two output updates as the sequential loop below, in the same order
     const int half = nt >> 1, k = tid >= half ? 1 : 0;
-    apply_row<false>(T.t[k], a, k ? work + T.work1 : work, k ? acc : orow, tid - k * half, half);
+    apply_row<false, !MF>(T.t[k], a, k ? work + T.work1 : work, k ? acc : orow, tid - k * half, half);
     __syncthreads();
     {
       const double al = g0.alpha;
@@ -1135,8 +1199,8 @@ __global__ __launch_bounds__(1024) void fused_apply_multi_kernel(ApplyLaunch L) 
     __syncthreads();
   } else
   for (int k = 0; k < T.nterms; ++k) {
-    if (T.t[k].mfma) apply_row_mfma<false>(T.t[k], a, work, k == 0 ? orow : acc, h);
-    else apply_row<false>(T.t[k], a, work, k == 0 ? orow : acc, tid, nt);
+    if (MF && T.t[k].mfma) apply_row_mfma<false>(T.t[k], a, work, k == 0 ? orow : acc, h);
+    else apply_row<false, !MF>(T.t[k], a, work, k == 0 ? orow : acc, tid, nt);
     __syncthreads();
     if (k > 0) {
       const double al = T.t[k].alpha;
@@ -1227,13 +1291,15 @@ static bool mfma_enabled() { return ttk::ctx().knob[TTK_KNOB_FUSED_MFMA] != 0; }
 static const int g_mfma_threads = getenv("TTK_MFMA_THREADS") ? atoi(getenv("TTK_MFMA_THREADS")) : 1024;
 // threads per workgroup of VALU apply rows (per term when a task's two terms run side by side):
 // every output element is one thread's sequential chain whatever the count, so results never change
-// (64..512 in steps of 64: a side-by-side launch doubles it and a workgroup holds at most 1024)
+// (64..256 in steps of 64: a side-by-side launch doubles it, and VALU-only launches are bounded at 512
+// threads so that the prefetched chains get their registers)
 static int valu_threads_env() {
   const int t = getenv("TTK_VALU_THREADS") ? atoi(getenv("TTK_VALU_THREADS")) : 256;
-  return t < 64 ? 64 : (t > 512 ? 512 : t / 64 * 64);
+  return t < 64 ? 64 : (t > 256 ? 256 : t / 64 * 64);  // <= 256: side by side 512, the VALU launches' bound
 }
 static const int g_valu_threads = valu_threads_env();
 static const int g_stage_batch = getenv("TTK_STAGE_BATCH") ? (atoi(getenv("TTK_STAGE_BATCH")) != 0) : 1;
+static const int g_chain_prefetch = getenv("TTK_CHAIN_PREFETCH") ? (atoi(getenv("TTK_CHAIN_PREFETCH")) != 0) : 1;
 
 // workgroups per MFMA output row (ApplyArgs::csplit): enough that each workgroup's share of the
 // stage-3 (tile, K block) pairs is about one round over its waves, but no more workgroups in the
@@ -1341,6 +1407,7 @@ static int apply_args(const char *eq, const int64_t *desc, double *out, double a
   }
   g.mfma = 0;
   g.stage1 = g_stage_batch;
+  g.chain = g_chain_prefetch;
   if (g.na < 1 || g.na > 65535) return 0;
   if (apply_lds(g.nb, g.nj, g.nd, g.nS, g.ns, g.ni) <= APPLY_LDS_DOUBLES) return 1;
   if (mfma_enabled() && apply_mfma_lds(g) <= APPLY_LDS_DOUBLES) {  // only the MFMA stages fit LDS
@@ -1829,14 +1896,19 @@ int ttk::schur_apply(void *stream, int64_t handle, const double *v, double *out)
       }
       if (s == 0 && tt == 1 && op.ineq) L.task[t].addv = v + 2 * m;  // w = inv_I o B01^T y + t
     }
+    const void *kern = op.one_mfma ? reinterpret_cast<const void *>(fused_apply_multi_kernel<true>)
+                                   : reinterpret_cast<const void *>(fused_apply_multi_kernel<false>);
     if (op.one_shm > 65536)
-      (void)hipFuncSetAttribute(reinterpret_cast<const void *>(fused_apply_multi_kernel),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)op.one_shm);
+      (void)hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)op.one_shm);
     hipEvent_t e0, e1;
     if (ttk::contract_events_ext(&e0, &e1) != TTK_OK) return TTK_ERR_HIP;
-    hipExtLaunchKernelGGL(fused_apply_multi_kernel, dim3(L.off[L.ntask]),
-                          dim3(op.one_mfma ? g_mfma_threads : (L.dual ? 2 * g_valu_threads : g_valu_threads)),
-                          op.one_shm, TTK_STREAM(stream), e0, e1, 0, L);
+    if (op.one_mfma)
+      hipExtLaunchKernelGGL(fused_apply_multi_kernel<true>, dim3(L.off[L.ntask]), dim3(g_mfma_threads), op.one_shm,
+                            TTK_STREAM(stream), e0, e1, 0, L);
+    else
+      hipExtLaunchKernelGGL(fused_apply_multi_kernel<false>, dim3(L.off[L.ntask]),
+                            dim3(L.dual ? 2 * g_valu_threads : g_valu_threads), op.one_shm, TTK_STREAM(stream), e0, e1,
+                            0, L);
     TTK_LAUNCH_CHECK();
     ttk::contract_count_ext(op.flops);
     return TTK_OK;
@@ -1850,17 +1922,21 @@ int ttk::schur_apply(void *stream, int64_t handle, const double *v, double *out)
       }
       if (s == 0 && t == 1 && op.ineq) L.task[t].addv = v + 2 * m;  // w = inv_I o B01^T y + t
     }
-    if (op.shm[s] > 65536)
-      (void)hipFuncSetAttribute(reinterpret_cast<const void *>(fused_apply_multi_kernel),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)op.shm[s]);
-    hipEvent_t e0, e1;
-    if (ttk::contract_events_ext(&e0, &e1) != TTK_OK) return TTK_ERR_HIP;
     bool mf = false;
     for (int t = 0; t < L.ntask; ++t)
       for (int k = 0; k < L.task[t].nterms; ++k) mf = mf || L.task[t].t[k].mfma;
-    hipExtLaunchKernelGGL(fused_apply_multi_kernel, dim3(L.off[L.ntask]), dim3(mf ? g_mfma_threads : (L.dual ? 2 * g_valu_threads : g_valu_threads)),
-                          op.shm[s],
-                          TTK_STREAM(stream), e0, e1, 0, L);
+    const void *kern = mf ? reinterpret_cast<const void *>(fused_apply_multi_kernel<true>)
+                          : reinterpret_cast<const void *>(fused_apply_multi_kernel<false>);
+    if (op.shm[s] > 65536) (void)hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)op.shm[s]);
+    hipEvent_t e0, e1;
+    if (ttk::contract_events_ext(&e0, &e1) != TTK_OK) return TTK_ERR_HIP;
+    if (mf)
+      hipExtLaunchKernelGGL(fused_apply_multi_kernel<true>, dim3(L.off[L.ntask]), dim3(g_mfma_threads), op.shm[s],
+                            TTK_STREAM(stream), e0, e1, 0, L);
+    else
+      hipExtLaunchKernelGGL(fused_apply_multi_kernel<false>, dim3(L.off[L.ntask]),
+                            dim3(L.dual ? 2 * g_valu_threads : g_valu_threads), op.shm[s], TTK_STREAM(stream), e0, e1,
+                            0, L);
     TTK_LAUNCH_CHECK();
   }
   ttk::contract_count_ext(op.flops);

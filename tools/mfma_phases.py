@@ -41,5 +41,9 @@ lib.ttk_mfma_profile(out, 0)
 rows = max(out[7], 1)
 names = ["staging", "stage1", "stage2", "stage3", "epilogue"]
 tot = sum(out[i] for i in range(5))
+if os.environ.get("TTK_VALU_PROFILE_WAIT"):  # VALU-profile build: [4] = hand-off wait inside staging, [5] = rows that waited
+    names = names[:4]
+    tot = sum(out[i] for i in range(4))
+    print(f"hand-off waits: {out[5]} rows, {out[4] / 100.0 / max(out[5], 1):.2f} us per waiting row (inside staging)")
 print(f"MFMA rows {out[7]}; per row (us): " + ", ".join(f"{n} {out[i] / 100.0 / rows:.2f}" for i, n in enumerate(names))
       + f"; total {tot / 100.0 / rows:.2f}")
