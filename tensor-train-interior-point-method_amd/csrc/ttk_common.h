@@ -27,6 +27,71 @@ struct NdDesc {
   int64_t s2[MAXD];
 };
 
+// acc <- fma(a(k), b(k), acc) (NEG: fma(-a(k), b(k), acc), the contraction of acc -= a * b) for
+// k = 0..count-1 in order, with the operands of the next U steps loaded while the current U FMAs
+// run.  A plain `for (...) s += x[i] * y[i]` over global memory compiles to load, wait, FMA per step
+// -- one L2 round trip per element; here the loop waits about once per U steps.  The same FMAs in the
+// same order as the plain loop: bit-identical.
+template <int U, bool NEG = false, class FA, class FB>
+__device__ __forceinline__ double chain_ahead(int count, FA fa, FB fb, double acc) {
+  int k = 0;
+  if (count >= U) {
+    double x[U], y[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      x[u] = fa(u);
+      y[u] = fb(u);
+    }
+    for (k = U; k + U <= count; k += U) {
+      double nx[U], ny[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        nx[u] = fa(k + u);
+        ny[u] = fb(k + u);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) acc = fma(NEG ? -x[u] : x[u], y[u], acc);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        x[u] = nx[u];
+        y[u] = ny[u];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc = fma(NEG ? -x[u] : x[u], y[u], acc);
+  }
+  for (; k < count; ++k) acc = fma(NEG ? -fa(k) : fa(k), fb(k), acc);
+  return acc;
+}
+// acc <- acc + f(k) for k = 0..count-1 in order, the next U terms loaded while the current U are
+// added (bit-identical to the plain loop)
+template <int U, class F>
+__device__ __forceinline__ double sum_ahead(int count, F f, double acc) {
+  int k = 0;
+  if (count >= U) {
+    double x[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) x[u] = f(u);
+    for (k = U; k + U <= count; k += U) {
+      double nx[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) nx[u] = f(k + u);
+#pragma unroll
+      for (int u = 0; u < U; ++u) acc = acc + x[u];
+#pragma unroll
+      for (int u = 0; u < U; ++u) x[u] = nx[u];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc = acc + x[u];
+  }
+  for (; k < count; ++k) acc = acc + f(k);
+  return acc;
+}
+// number of k with start + k * step < end (start < end not required)
+__device__ __forceinline__ int steps_below(int start, int end, int step) {
+  return start < end ? (end - start + step - 1) / step : 0;
+}
+
 // Cross-lane moves through DPP (ALU latency) instead of ds_bpermute (LDS round trip).
 template <int CTRL>
 __device__ __forceinline__ double dpp_mov(double v) {

@@ -117,21 +117,20 @@ __global__ __launch_bounds__(1024) void arnoldi_kernel(double *V, int n, int it,
   // h_j = <V_j, w>, j = 0..it (one wave per j)
   for (int j = wid; j <= it; j += nw) {
     const double *vj = V + (int64_t)j * n;
-    double s = 0.0;
-    for (int i = lane; i < n; i += 64) s += vj[i] * w[i];
+    double s = ttk::chain_ahead<8>(
+        ttk::steps_below(lane, n, 64), [&](int k) { return vj[lane + 64 * k]; }, [&](int k) { return w[lane + 64 * k]; },
+        0.0);
     s = ttk::wave_sum(s);
     if (lane == 0) h[j] = s;
   }
   __syncthreads();
   // w -= sum_j h_j V_j
-  for (int i = tid; i < n; i += nt) {
-    double acc = w[i];
-    for (int j = 0; j <= it; ++j) acc -= h[j] * V[(int64_t)j * n + i];
-    w[i] = acc;
-  }
+  for (int i = tid; i < n; i += nt)
+    w[i] = ttk::chain_ahead<8, true>(
+        it + 1, [&](int j) { return h[j]; }, [&](int j) { return V[(int64_t)j * n + i]; }, w[i]);
   __syncthreads();
-  double s2 = 0.0;
-  for (int i = tid; i < n; i += nt) s2 += w[i] * w[i];
+  double s2 = ttk::chain_ahead<8>(
+      ttk::steps_below(tid, n, nt), [&](int k) { return w[tid + nt * k]; }, [&](int k) { return w[tid + nt * k]; }, 0.0);
   s2 = ttk::block_sum(s2, red);
   const double tt = sqrt(s2);
   const int ld = H.ld;
@@ -195,8 +194,8 @@ __global__ __launch_bounds__(1024) void build_kernel(double *base, int max_k, in
   const int tid = threadIdx.x, nt = blockDim.x;
   hh_backsub(H, it, hl, y);
   for (int i = tid; i < n; i += nt) {
-    double t = 0.0;
-    for (int j = 0; j < nvec; ++j) t += y[j] * basis.p[j][i];
+    const double t = ttk::chain_ahead<8>(
+        nvec, [&](int j) { return y[j]; }, [&](int j) { return basis.p[j][i]; }, 0.0);
     aug_temp[i] = t;
     x[i] += t;
   }
@@ -211,14 +210,15 @@ __global__ __launch_bounds__(1024) void aug_kernel(const double *base_c, int max
   const int ld = H.ld;
   const int tid = threadIdx.x, nt = blockDim.x;
   hes_times_grs(H, it_total, avec);
-  double s2 = 0.0;
-  for (int i = tid; i < n; i += nt) s2 += aug_temp[i] * aug_temp[i];
+  double s2 = ttk::chain_ahead<8>(
+      ttk::steps_below(tid, n, nt), [&](int k) { return aug_temp[tid + nt * k]; },
+      [&](int k) { return aug_temp[tid + nt * k]; }, 0.0);
   s2 = ttk::block_sum(s2, red);
   const double inv = 1.0 / sqrt(s2);
   for (int i = tid; i < n; i += nt) {
     augvec[i] = aug_temp[i] * inv;
-    double t = 0.0;
-    for (int j = 0; j <= it_total; ++j) t += avec[j] * V[(int64_t)j * n + i];
+    const double t = ttk::chain_ahead<8>(
+        it_total + 1, [&](int j) { return avec[j]; }, [&](int j) { return V[(int64_t)j * n + i]; }, 0.0);
     a_augvec[i] = t * inv;
   }
 }
@@ -241,9 +241,9 @@ __global__ __launch_bounds__(256) void arnoldi_dot_kernel(const double *__restri
   const int c = blockIdx.x, j = blockIdx.y, tid = threadIdx.x;
   const double *vj = V + (int64_t)j * n, *w = V + (int64_t)(it + 1) * n;
   const int i0 = c * ARN_CHUNK, i1 = i0 + ARN_CHUNK < n ? i0 + ARN_CHUNK : n;
-  double s = 0.0;
-#pragma unroll 4
-  for (int i = i0 + tid; i < i1; i += 256) s = fma(vj[i], w[i], s);
+  double s = ttk::chain_ahead<8>(
+      ttk::steps_below(i0 + tid, i1, 256), [&](int k) { return vj[i0 + tid + 256 * k]; },
+      [&](int k) { return w[i0 + tid + 256 * k]; }, 0.0);
   s = ttk::block_sum(s, red);
   if (tid == 0) partials[(int64_t)j * nchunk + c] = s;
 }
@@ -256,11 +256,8 @@ __global__ __launch_bounds__(256) void arnoldi_update_kernel(double *__restrict_
   __shared__ double h[MAXV + 2];
   __shared__ double red[16];
   const int tid = threadIdx.x;
-  for (int j = tid; j <= it; j += 256) {
-    double acc = 0.0;
-    for (int c = 0; c < nchunk; ++c) acc += partials[(int64_t)j * nchunk + c];
-    h[j] = acc;
-  }
+  for (int j = tid; j <= it; j += 256)
+    h[j] = ttk::sum_ahead<8>(nchunk, [&](int c) { return partials[(int64_t)j * nchunk + c]; }, 0.0);
   __syncthreads();
   if (blockIdx.x == 0) {
     HH H(base, max_k);
@@ -273,8 +270,8 @@ __global__ __launch_bounds__(256) void arnoldi_update_kernel(double *__restrict_
   const int i = blockIdx.x * ARN_UPD + tid;
   double s2 = 0.0;
   for (int ii = i; ii < n && ii < (blockIdx.x + 1) * ARN_UPD; ii += 256) {
-    double acc = w[ii];
-    for (int j = 0; j <= it; ++j) acc -= h[j] * V[(int64_t)j * n + ii];
+    const double acc = ttk::chain_ahead<8, true>(
+        it + 1, [&](int j) { return h[j]; }, [&](int j) { return V[(int64_t)j * n + ii]; }, w[ii]);
     w[ii] = acc;
     s2 = fma(acc, acc, s2);
   }
@@ -290,9 +287,7 @@ __global__ __launch_bounds__(1024) void arnoldi_finish_kernel(double *V, int n, 
   HH H(base, max_k);
   const int tid = threadIdx.x, nt = blockDim.x;
   if (tid == 0) {
-    double s2 = 0.0;
-    for (int b = 0; b < nblk; ++b) s2 += normpart[b];
-    s_tt = sqrt(s2);
+    s_tt = sqrt(ttk::sum_ahead<8>(nblk, [&](int b) { return normpart[b]; }, 0.0));
   }
   __syncthreads();
   const double tt = s_tt;
@@ -338,9 +333,9 @@ __global__ __launch_bounds__(256) void arnoldi_fused_kernel(double *__restrict__
       const int c = b % nchunk, j = b / nchunk;
       const double *vj = V + (int64_t)j * n;
       const int i0 = c * ARN_CHUNK, i1 = i0 + ARN_CHUNK < n ? i0 + ARN_CHUNK : n;
-      double acc = 0.0;
-#pragma unroll 4
-      for (int i = i0 + tid; i < i1; i += 256) acc = fma(vj[i], w[i], acc);
+      double acc = ttk::chain_ahead<8>(
+          ttk::steps_below(i0 + tid, i1, 256), [&](int k) { return vj[i0 + tid + 256 * k]; },
+          [&](int k) { return w[i0 + tid + 256 * k]; }, 0.0);
       acc = ttk::block_sum(acc, red);
       if (tid == 0) ttk::st_sc1(partials + (int64_t)j * nchunk + c, acc);
     }
@@ -352,11 +347,8 @@ __global__ __launch_bounds__(256) void arnoldi_fused_kernel(double *__restrict__
     ttk::dep_wait(dep, t_dots);
     __syncthreads();
     if (!stopped) {
-      for (int j = tid; j <= it; j += 256) {
-        double acc = 0.0;
-        for (int c = 0; c < nchunk; ++c) acc += ttk::ld_sc1(partials + (int64_t)j * nchunk + c);
-        h[j] = acc;
-      }
+      for (int j = tid; j <= it; j += 256)
+        h[j] = ttk::sum_ahead<8>(nchunk, [&](int c) { return ttk::ld_sc1(partials + (int64_t)j * nchunk + c); }, 0.0);
       __syncthreads();
       if (blk == 0) {
         HH H(base, max_k);
@@ -367,8 +359,8 @@ __global__ __launch_bounds__(256) void arnoldi_fused_kernel(double *__restrict__
       }
       double s2 = 0.0;
       for (int ii = blk * ARN_UPD + tid; ii < n && ii < (blk + 1) * ARN_UPD; ii += 256) {
-        double acc = w[ii];
-        for (int j = 0; j <= it; ++j) acc -= h[j] * V[(int64_t)j * n + ii];
+        const double acc = ttk::chain_ahead<8, true>(
+            it + 1, [&](int j) { return h[j]; }, [&](int j) { return V[(int64_t)j * n + ii]; }, w[ii]);
         ttk::st_sc1(w + ii, acc);
         s2 = fma(acc, acc, s2);
       }
@@ -384,11 +376,7 @@ __global__ __launch_bounds__(256) void arnoldi_fused_kernel(double *__restrict__
   if (stopped) return;
   __shared__ double s_tt;
   HH H(base, max_k);
-  if (tid == 0) {
-    double s2 = 0.0;
-    for (int q = 0; q < nblk; ++q) s2 += ttk::ld_sc1(normpart + q);
-    s_tt = sqrt(s2);
-  }
+  if (tid == 0) s_tt = sqrt(ttk::sum_ahead<8>(nblk, [&](int q) { return ttk::ld_sc1(normpart + q); }, 0.0));
   __syncthreads();
   const double tt = s_tt;
   const int ld = H.ld;
