@@ -258,12 +258,17 @@ __device__ __forceinline__ void jacobi_round(double *X, int ldx, double *V, int 
     rr_pair(P, r, k, a, b);
     if (b >= p) continue;
     double *wa = X + a * ldx, *wb = X + b * ldx;
-    double xa[VPL], xb[VPL];
+    double *va = V + a * ldv, *vb = V + b * ldv;
+    double xa[VPL], xb[VPL], ya[VPL], yb[VPL];
+    // both columns of X and of V in one batch of LDS loads (the V columns used to be loaded after
+    // the X stores, one more LDS round trip per round; the pair owns all four columns this round)
 #pragma unroll
     for (int v = 0; v < VPL; ++v) {
       const int i = gl + v * G;
       xa[v] = i < L ? wa[i] : 0.0;
       xb[v] = i < L ? wb[i] : 0.0;
+      ya[v] = i < p ? va[i] : 0.0;
+      yb[v] = i < p ? vb[i] : 0.0;
     }
     double al = 0.0, be = 0.0, ga = 0.0;
 #pragma unroll
@@ -281,34 +286,38 @@ __device__ __forceinline__ void jacobi_round(double *X, int ldx, double *V, int 
     if (ga * ga <= tol2 * al * be) continue;  // |ga| <= tol sqrt(al be)
     double cs, sn;
     jacobi_rotation(al, be, ga, cs, sn);
+    // the rotations with the contractions the compiler chose for the previous form of this loop
+    // (wa, wb, va: the product of the second term first; vb: of the first), spelled out so that
+    // moving the loads cannot change them
 #pragma unroll
     for (int v = 0; v < VPL; ++v) {
       const int i = gl + v * G;
       if (i < L) {
-        wa[i] = cs * xa[v] - sn * xb[v];
-        wb[i] = sn * xa[v] + cs * xb[v];
+        wa[i] = fma(cs, xa[v], -(sn * xb[v]));
+        wb[i] = fma(cs, xb[v], sn * xa[v]);
       }
     }
-    double *va = V + a * ldv, *vb = V + b * ldv;
 #pragma unroll
     for (int v = 0; v < VPL; ++v) {
       const int i = gl + v * G;
       if (i < p) {
-        const double ya = va[i], yb = vb[i];
-        va[i] = cs * ya - sn * yb;
-        vb[i] = sn * ya + cs * yb;
+        va[i] = fma(cs, ya[v], -(sn * yb[v]));
+        vb[i] = fma(sn, ya[v], cs * yb[v]);
       }
     }
     if (gl == 0) *any_rot = 1;
   }
 }
 
-template <int G>
+// WL: W (and M) in LDS (w_in_lds), known at compile time so that their accesses are LDS
+// instructions, not flat ones (a flat access waits on both the LDS and the vector-memory counters)
+template <int G, bool WL>
 __global__ __launch_bounds__(1024) void svd_wg_kernel(const double *__restrict__ A, int m, int n,
                                                       double *__restrict__ U, double *__restrict__ S,
                                                       double *__restrict__ Vt, double *__restrict__ gwork,
                                                       int w_in_lds, int use_qr, int timing) {
   extern __shared__ double lds[];
+  constexpr int SU = WL ? 8 : 4;  // loads ahead in the dot chains (W in global memory: fewer registers left)
   __shared__ int s_piv, any_rot;
   __shared__ double red[16];
   const bool tall = m >= n;
@@ -334,7 +343,7 @@ __global__ __launch_bounds__(1024) void svd_wg_kernel(const double *__restrict__
   const int gl2 = tid & (g2 - 1), gid2 = tid / g2, ng2 = nt / g2;
   double *X = lds, *V = X + ldx * p, *tau = V + ldv * p, *vn1 = tau + p, *vn2 = vn1 + p, *sig = vn2 + p;
   int *perm = reinterpret_cast<int *>(sig + p), *rank = perm + p;
-  double *W = use_qr ? (w_in_lds ? reinterpret_cast<double *>(rank + p + (p & 1)) : gwork) : X;
+  double *W = use_qr ? (WL ? reinterpret_cast<double *>(rank + p + (p & 1)) : gwork) : X;
   // W / M column stride: odd, so the g2-lane groups of one wave (consecutive columns) start on
   // different LDS banks (an even q put every group of a wave on the same banks)
   const int lq = q | 1;
@@ -348,9 +357,9 @@ __global__ __launch_bounds__(1024) void svd_wg_kernel(const double *__restrict__
   if (use_qr) {
     for (int j = wid; j < p; j += nw) {
       const double *w = W + (int64_t)j * lq;
-      double acc = 0.0;
-      #pragma unroll 8
-      for (int i = lane; i < q; i += 64) acc += w[i] * w[i];
+      double acc = ttk::chain_ahead<SU>(
+          ttk::steps_below(lane, q, 64), [&](int k) { return w[lane + 64 * k]; },
+          [&](int k) { return w[lane + 64 * k]; }, 0.0);
       acc = sqrt(ttk::wave_sum(acc));
       if (lane == 0) {
         vn1[j] = acc;
@@ -390,9 +399,9 @@ __global__ __launch_bounds__(1024) void svd_wg_kernel(const double *__restrict__
             b[i] = t;
           }
         }
-        double part = 0.0;
-        #pragma unroll 8
-        for (int i = c + 1 + lane; i < q; i += 64) part += x[i] * x[i];
+        const double part = ttk::chain_ahead<SU>(
+            ttk::steps_below(c + 1 + lane, q, 64), [&](int k) { return x[c + 1 + lane + 64 * k]; },
+            [&](int k) { return x[c + 1 + lane + 64 * k]; }, 0.0);
         const double sigma = ttk::wave_sum(part);
         const double alpha = x[c];
         double t = 0.0, beta = alpha;
@@ -421,9 +430,9 @@ __global__ __launch_bounds__(1024) void svd_wg_kernel(const double *__restrict__
         double *y = W + (int64_t)j * lq;
         double yc = y[c];
         if (t != 0.0) {
-          double acc = 0.0;
-          #pragma unroll 8
-          for (int i = c + 1 + gl2; i < q; i += g2) acc += x[i] * y[i];
+          const double acc = ttk::chain_ahead<SU>(
+              ttk::steps_below(c + 1 + gl2, q, g2), [&](int k) { return x[c + 1 + gl2 + g2 * k]; },
+              [&](int k) { return y[c + 1 + gl2 + g2 * k]; }, 0.0);
           const double w = t * (ttk::group_sum_rt(acc, g2) + yc);
           #pragma unroll 8
           for (int i = c + 1 + gl2; i < q; i += g2) y[i] -= w * x[i];
@@ -438,9 +447,9 @@ __global__ __launch_bounds__(1024) void svd_wg_kernel(const double *__restrict__
           const double r = a / a2;
           if (temp * r * r <= 1.4901161193847656e-08) {
             __threadfence_block();  // the group reads back the updated column
-            double acc = 0.0;
-            #pragma unroll 8
-            for (int i = c + 1 + gl2; i < q; i += g2) acc += y[i] * y[i];
+            double acc = ttk::chain_ahead<SU>(
+                ttk::steps_below(c + 1 + gl2, q, g2), [&](int k) { return y[c + 1 + gl2 + g2 * k]; },
+                [&](int k) { return y[c + 1 + gl2 + g2 * k]; }, 0.0);
             acc = sqrt(ttk::group_sum_rt(acc, g2));
             if (gl2 == 0) {
               vn1[j] = acc;
@@ -550,9 +559,9 @@ __global__ __launch_bounds__(1024) void svd_wg_kernel(const double *__restrict__
         const double t = tau[c];
         if (t == 0.0) continue;
         const double *v = W + (int64_t)c * lq;
-        double acc = 0.0;
-        #pragma unroll 8
-        for (int i = c + 1 + gl2; i < q; i += g2) acc += v[i] * mc[i];
+        const double acc = ttk::chain_ahead<SU>(
+            ttk::steps_below(c + 1 + gl2, q, g2), [&](int k) { return v[c + 1 + gl2 + g2 * k]; },
+            [&](int k) { return mc[c + 1 + gl2 + g2 * k]; }, 0.0);
         const double w = t * (ttk::group_sum_rt(acc, g2) + mc[c]);
         #pragma unroll 8
         for (int i = c + 1 + gl2; i < q; i += g2) mc[i] -= w * v[i];
@@ -615,14 +624,17 @@ __global__ __launch_bounds__(1024) void svd_wg_kernel(const double *__restrict__
 
 // ------------------------------------------------------------------------------ QR
 // W: m x n column-major working copy; tau: k.
+// UL: the working copy in LDS (use_lds), at compile time: LDS instructions instead of flat ones
+template <bool UL>
 __global__ __launch_bounds__(1024) void qr_kernel(const double *__restrict__ A, int m, int n,
                                                   double *__restrict__ Q, double *__restrict__ R,
                                                   double *__restrict__ gwork, int use_lds) {
   extern __shared__ double lds[];
+  constexpr int CU = UL ? 8 : 4;  // loads ahead in the dot chains
   __shared__ double red[16];
   __shared__ double s_beta, s_tau, s_scale;
   const int k = m < n ? m : n;
-  double *W = use_lds ? lds : gwork;
+  double *W = UL ? lds : gwork;
   double *tau = W + (int64_t)m * n;
   double *Qc = tau + k;  // m x k column-major accumulation
   const int tid = threadIdx.x, nt = blockDim.x;
@@ -634,8 +646,9 @@ __global__ __launch_bounds__(1024) void qr_kernel(const double *__restrict__ A, 
   __syncthreads();
   for (int j = 0; j < k; ++j) {
     double *wj = W + (int64_t)j * m;
-    double s2 = 0.0;
-    for (int i = j + 1 + tid; i < m; i += nt) s2 += wj[i] * wj[i];
+    double s2 = ttk::chain_ahead<CU>(
+        ttk::steps_below(j + 1 + tid, m, nt), [&](int q) { return wj[j + 1 + tid + nt * q]; },
+        [&](int q) { return wj[j + 1 + tid + nt * q]; }, 0.0);
     s2 = ttk::block_sum(s2, red);
     if (tid == 0) {
       const double alpha = wj[j];
@@ -663,9 +676,9 @@ __global__ __launch_bounds__(1024) void qr_kernel(const double *__restrict__ A, 
     if (tj != 0.0) {
       for (int c = j + 1 + wid; c < n; c += nw) {
         double *wc = W + (int64_t)c * m;
-        double d = (lane == 0) ? wc[j] : 0.0;
-        #pragma unroll 8
-        for (int i = j + 1 + lane; i < m; i += 64) d += wj[i] * wc[i];
+        double d = ttk::chain_ahead<CU>(
+            ttk::steps_below(j + 1 + lane, m, 64), [&](int q) { return wj[j + 1 + lane + 64 * q]; },
+            [&](int q) { return wc[j + 1 + lane + 64 * q]; }, (lane == 0) ? wc[j] : 0.0);
         d = ttk::wave_sum(d) * tj;
         if (lane == 0) wc[j] -= d;
         #pragma unroll 8
@@ -691,9 +704,9 @@ __global__ __launch_bounds__(1024) void qr_kernel(const double *__restrict__ A, 
     const double *v = W + (int64_t)j * m;
     for (int c = j + wid; c < k; c += nw) {
       double *qc = Qc + (int64_t)c * m;
-      double d = (lane == 0) ? qc[j] : 0.0;
-      #pragma unroll 8
-      for (int i = j + 1 + lane; i < m; i += 64) d += v[i] * qc[i];
+      double d = ttk::chain_ahead<CU>(
+          ttk::steps_below(j + 1 + lane, m, 64), [&](int q) { return v[j + 1 + lane + 64 * q]; },
+          [&](int q) { return qc[j + 1 + lane + 64 * q]; }, (lane == 0) ? qc[j] : 0.0);
       d = ttk::wave_sum(d) * tj;
       if (lane == 0) qc[j] -= d;
       #pragma unroll 8
@@ -2619,11 +2632,17 @@ int ttk_svd_tol(void *stream, const double *A, int m, int n, double *U, double *
   if (use_qr && q * p > 2048) nt = 1024;  // column-parallel QR phases want a full block
   nt = nt < 64 ? 64 : (nt > 1024 ? 1024 : (nt + 63) / 64 * 64);
   (void)defl;  // no deflation on this path (every direction keeps an orthonormal vector)
-#define TTK_SVD_WG(GG)                                                                                    \
-  case GG:                                                                                                \
-    allow_big_lds(svd_wg_kernel<GG>, shm);                                                                \
-    hipLaunchKernelGGL(svd_wg_kernel<GG>, dim3(1), dim3(nt), shm, TTK_STREAM(stream), A, m, n, U, S, Vt, work, \
-                       w_in_lds, use_qr, g_svd_timing);                                                   \
+#define TTK_SVD_WG(GG)                                                                                      \
+  case GG:                                                                                                  \
+    if (w_in_lds) {                                                                                         \
+      allow_big_lds(svd_wg_kernel<GG, true>, shm);                                                          \
+      hipLaunchKernelGGL((svd_wg_kernel<GG, true>), dim3(1), dim3(nt), shm, TTK_STREAM(stream), A, m, n, U, S, Vt, \
+                         work, w_in_lds, use_qr, g_svd_timing);                                             \
+    } else {                                                                                                \
+      allow_big_lds(svd_wg_kernel<GG, false>, shm);                                                         \
+      hipLaunchKernelGGL((svd_wg_kernel<GG, false>), dim3(1), dim3(nt), shm, TTK_STREAM(stream), A, m, n, U, S,  \
+                         Vt, work, w_in_lds, use_qr, g_svd_timing);                                         \
+    }                                                                                                       \
     break;
   switch (g) {
     TTK_SVD_WG(1)
@@ -2665,8 +2684,13 @@ int ttk_qr(void *stream, const double *A, int m, int n, double *Q, double *R, do
   const int use_lds = need <= LDS_DOUBLES;
   if (k >= g_qr_big_k && (!use_lds || g_qr_big_k <= 2)) return qr_big(stream, A, m, n, Q, R, work);
   const size_t shm = use_lds ? need * sizeof(double) : 0;
-  allow_big_lds(qr_kernel, shm);
-  hipLaunchKernelGGL(qr_kernel, dim3(1), dim3(1024), shm, TTK_STREAM(stream), A, m, n, Q, R, work, use_lds);
+  if (use_lds) {
+    allow_big_lds(qr_kernel<true>, shm);
+    hipLaunchKernelGGL(qr_kernel<true>, dim3(1), dim3(1024), shm, TTK_STREAM(stream), A, m, n, Q, R, work, use_lds);
+  } else {
+    allow_big_lds(qr_kernel<false>, shm);
+    hipLaunchKernelGGL(qr_kernel<false>, dim3(1), dim3(1024), shm, TTK_STREAM(stream), A, m, n, Q, R, work, use_lds);
+  }
   TTK_LAUNCH_CHECK();
   return TTK_OK;
 }
