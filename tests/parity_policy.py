@@ -38,7 +38,9 @@ def is_pathological(r):
 #   never narrower than [min / 1.01, max * 1.01] -- the end-point resolution: the final feasibilities
 #   are squared residuals whose leading digits the last rounded update sets (maxcut_10 s35's five
 #   unmodified runs agree in gap to 1e-5 but spread 0.3 % in feas) -- and non-pathological
-#   (src/utils.py:67).
+#   (src/utils.py:67), unless one of the unmodified runs itself ends pathological: then a
+#   pathological device end point lands where that run lands (the basin is compared, not the
+#   stalled iterate; check_end_point).
 KEYS4 = ("mu", "primal_error", "dual_error", "centrality_error")
 FINAL_KEYS = ("gap", "feas", "dual_feas")
 ENVELOPE_KEYS = ("gap", "feas")
@@ -80,7 +82,10 @@ def reference_noise(key):
 
 def envelope(key):
     """the unmodified runs' end points widened 2x: {'num_iters': (lo, hi), 'gap': (lo, hi), 'feas': ...}"""
-    runs = [RUNS[key]] + _twins(key, NOISE_TWINS)
+    return envelope_of([RUNS[key]] + _twins(key, NOISE_TWINS))
+
+
+def envelope_of(runs):
     out = {}
     its = [x["num_iters"] for x in runs]
     w = max(its) - min(its)
@@ -136,12 +141,34 @@ def check_against_reference_runs(key, trace, r):
         for k in FINAL_KEYS:
             assert _rel(r[k], R[k]) <= max(FINAL_FLOOR, FACTOR * fin[k]), (k, r[k], R[k], fin[k])
     else:
-        assert not is_pathological(r), r
-        env = envelope(key)
-        assert env["num_iters"][0] <= r["num_iters"] <= env["num_iters"][1], ("num_iters", r["num_iters"], env)
-        for k in ENVELOPE_KEYS:
-            assert env[k][0] <= abs(r[k]) <= env[k][1], (k, r[k], env[k])
+        check_end_point(key, r)
     return name, best_per, cum
+
+
+def unmodified_runs(key):
+    return [RUNS[key]] + _twins(key, NOISE_TWINS)
+
+
+def check_end_point(key, r):
+    """End point of a key whose unmodified reference runs branch: the device must land where one of
+    those runs lands.
+    * non-pathological device end point: inside the envelope (widened 2x) of the unmodified runs --
+      of the non-pathological ones when some of them end pathological;
+    * pathological device end point (src/utils.py:67): allowed only when at least one of the
+      reference's own unmodified runs ends pathological too (maxcut_12 r=2: seeds 23, 1, ...); a
+      pathological end point has no meaningful envelope (stall / iteration-cap terminations), so
+      only the basin is compared."""
+    runs = unmodified_runs(key)
+    if is_pathological(r):
+        assert any(is_pathological(x) for x in runs), (
+            "pathological end point where every unmodified reference run converges", r,
+            [(x["num_iters"], x["gap"]) for x in runs])
+        return
+    good = [x for x in runs if not is_pathological(x)] or runs
+    env = envelope_of(good)
+    assert env["num_iters"][0] <= r["num_iters"] <= env["num_iters"][1], ("num_iters", r["num_iters"], env)
+    for k in ENVELOPE_KEYS:
+        assert env[k][0] <= abs(r[k]) <= env[k][1], (k, r[k], env[k])
 
 
 # Keys whose device run departs from every UNMODIFIED reference run under the rule above, with the
@@ -162,14 +189,24 @@ KNOWN_DEPARTURES = {
 }
 
 
+RELAXED_FACTOR = 4.0
+
+
 def check_relaxed(key, r):
-    """the pre-round-4 end-point rule, kept as the floor for KNOWN_DEPARTURES: non-pathological
-    (src/utils.py:67) and within 2 iterations of the range of ALL reference runs (diagnostic twins
-    included)"""
+    """the floor for KNOWN_DEPARTURES (the pre-round-4 end-point rule plus a bound on the end point):
+    non-pathological (src/utils.py:67), within 2 iterations of the range of ALL reference runs
+    (diagnostic twins included), and gap / feasibility within RELAXED_FACTOR of the range of the
+    reference's unmodified runs ([min / 4, max * 4]), so that a departure drifting further fails
+    instead of being an expected failure (maxcut_12 s80: 7.6e-4 against 5.8-5.9e-4; maxcut_10 s14:
+    feas 2.1e-7 against 0.9-6.2e-8)"""
     allruns = [RUNS[key]] + _twins(key)
     lo, hi = min(x["num_iters"] for x in allruns), max(x["num_iters"] for x in allruns)
     assert not is_pathological(r), r
     assert lo - 2 <= r["num_iters"] <= hi + 2, (r["num_iters"], lo, hi)
+    base = unmodified_runs(key)
+    for k in ENVELOPE_KEYS:
+        a, b = min(abs(x[k]) for x in base), max(abs(x[k]) for x in base)
+        assert a / RELAXED_FACTOR <= abs(r[k]) <= b * RELAXED_FACTOR, (k, r[k], a, b)
 
 
 # ---- bounded hash twins (tests/golden/bounded_twins.json): seeds whose full reference runs take

@@ -503,6 +503,31 @@ def test_maxcut_12_rank2_matches_reference_trajectory(dev):
     print("maxcut_12_r2_s80 follows", name, ["%.0e" % v for v in per], "noise", ["%.0e" % v for v in cum])
 
 
+YAML12_SEEDS = (45, 23, 53, 12)  # configs/maxcut_12.yaml's seeds besides 80 (BASELINE configs[4])
+
+
+@pytest.mark.parametrize("seed", YAML12_SEEDS)
+def test_maxcut_12_yaml_seeds_end_points(dev, seed):
+    """configs[4]'s own YAML seeds, whole solves, against the reference's full runs of them
+    (`make_golden.py`: golden + PYTHONHASHSEED twins): the device follows one unmodified reference run
+    until the reference's own noise branches, then lands where one of those runs lands
+    (tests/parity_policy.py check_end_point: inside the converged runs' envelope, or pathological only
+    where the reference's own run ends pathological too -- seed 23: golden gap 2.5e-3 and its hash
+    twin 4.5e-2 after 29 iterations each).  Keys whose full reference run is not committed yet fall
+    back to test_bounded_trace_matches_reference's first-assemblies check."""
+    key = f"maxcut_12_r2_s{seed}"
+    if key not in RUNS:
+        pytest.skip(f"{key}: no full reference run committed (bounded trace only)")
+    if not any(key + x in RUNS for x in ("_t8", "_h1", "_h2", "_h3")):
+        pytest.skip(f"{key}: no unmodified reference twin committed (the follow rule needs the reference's noise)")
+    trace = []
+    g, r = _run(key, trace)
+    assert max(_rel(trace[0][k], g["trace"][0][k]) for k in KEYS4) <= 1e-8
+    name, per, cum = _policy(key, trace, r)
+    print(key, "follows", name, ["%.0e" % v for v in per], "noise", ["%.0e" % v for v in cum],
+          "end", {k: r[k] for k in ("num_iters", "gap", "feas")}, "pathological" if is_pathological(r) else "")
+
+
 def _extra_seeds():
     import sys
     sys.path.insert(0, ROOT)
