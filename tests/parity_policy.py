@@ -176,10 +176,6 @@ def check_end_point(key, r):
 # of the strict rule, after asserting the relaxed one (check_relaxed) so that anything worse still
 # fails; a key that passes the strict rule passes.
 KNOWN_DEPARTURES = {
-    "maxcut_10_r1_s23": "AMEn truncation SVDs: the shipped reference (scipy's default gesdd) departs at "
-                        "assembly 2 (8e-6) from the same reference on its own gesvd driver, on LAPACK's "
-                        "Jacobi SVD and from the device, which follows the Jacobi-SVD twin _j6 to the end; "
-                        "the end point lies inside the unmodified envelope",
     "maxcut_10_r1_s14": "bimodal step-size eigen-ALS at assembly 5 (zs 0.5019 or 0.4057 depending only on "
                         "contraction summation order): the device takes the 0.4057 branch, as the reference's "
                         "own Jacobi-SVD twin _j4 does, and ends one iteration later than the unmodified runs",
@@ -190,6 +186,32 @@ KNOWN_DEPARTURES = {
 
 
 RELAXED_FACTOR = 4.0
+
+
+# Keys whose device run leaves every unmodified reference run at a noise-level decision of a kind the
+# reference's own code changes under its OTHER valid LAPACK driver, with the device following the
+# reference on that driver: the follow rule is replaced by (a) following that diagnostic twin within
+# the same noise-scaled bound and (b) the end point landing where the unmodified runs land
+# (check_end_point) -- both asserted, no expected failure.
+ENVELOPE_ONLY = {
+    "maxcut_10_r1_s23": ("_j6", "AMEn truncation SVDs: the shipped reference (scipy's default gesdd) and the same "
+                                "reference on its gesvd driver or LAPACK's one-sided Jacobi SVD part at assembly 2 "
+                                "(8e-6, the same step sizes to 1e-10); the device follows the Jacobi-SVD twin _j6"),
+}
+
+
+def check_envelope_only(key, trace, r):
+    """ENVELOPE_ONLY keys: the named diagnostic twin followed within max(1e-12, 50 x the unmodified
+    runs' noise) until that noise branches, and the end point checked by check_end_point"""
+    twin, _ = ENVELOPE_ONLY[key]
+    cum, checked, _ = reference_noise(key)
+    R = RUNS[key + twin]
+    per = _per(trace, R)
+    m = min(checked, len(per), len(R["trace"]))
+    ratio = max([per[i] / max(FLOOR, FACTOR * cum[i]) for i in range(m)] or [0.0])
+    assert ratio <= 1.0, (f"{key}: does not follow {twin}", ["%.0e" % v for v in per[:m]])
+    check_end_point(key, r)
+    return twin, per, cum
 
 
 def check_relaxed(key, r):

@@ -391,7 +391,7 @@ def _run(key, trace=None):
 # code's rounding noise until that noise branches, then end inside their envelope widened 2x).
 from tests.parity_policy import ALL_TWINS as TWIN_SUFFIXES  # noqa: E402
 from tests.parity_policy import KEYS4, KNOWN_DEPARTURES, _rel, check_against_reference_runs, check_relaxed  # noqa: E402,F401,E501
-from tests.parity_policy import diagnose, is_pathological  # noqa: E402,F401
+from tests.parity_policy import ENVELOPE_ONLY, check_envelope_only, diagnose, is_pathological  # noqa: E402,F401
 
 
 def _policy(key, trace, r):
@@ -402,6 +402,8 @@ def _policy(key, trace, r):
     print(key, "follows", d["follows"], "ratio %.3g" % d["follow_ratio"], "inside", d["inside"],
           "diagnostic", d["diagnostic_follows"], "%.3g" % d["diagnostic_ratio"],
           "result", {k: r[k] for k in ("num_iters", "gap", "feas")})
+    if key in ENVELOPE_ONLY:  # asserted: the named diagnostic twin followed, the end point in the envelope
+        return check_envelope_only(key, trace, r)
     try:
         return check_against_reference_runs(key, trace, r)
     except AssertionError as e:
