@@ -56,7 +56,8 @@ class _Wrap:
 
 # the _ttkbind packer holds raw pointers to these three: leave them, their launches are attributed to
 # the dev.* function that issued them
-BOUND = ("ttk_einsum", "ttk_copy_nd", "ttk_mul_nd")
+BOUND = ("ttk_einsum", "ttk_copy_nd", "ttk_mul_nd", "ttk_axpby_nd", "ttk_normalize", "ttk_scale_axis_ss", "ttk_dot_nd_dev",
+         "ttk_fill", "ttk_env_update")
 for n in [n for n in dir(_lib.lib) if n.startswith("ttk_") and n != "ttk_launch_count" and n not in BOUND]:
     try:
         setattr(_lib.lib, n, _Wrap(n, getattr(_lib.lib, n)))
