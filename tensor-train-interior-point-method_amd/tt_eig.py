@@ -416,8 +416,10 @@ def _step_size_local_solve(p1, p2, XAX_k, A_k, A_kp1, XAX_k2, XDX_k, D_k, D_kp1,
     if sh[0] * sh[-1] <= size_limit:
         _check_dense(m)
         pv = prev.view(-1)
-        Dm = _sym(einsum(TWO_SITE, XDX_k, D_k, D_kp1, XDX_k2), m)
-        Am = _sym(einsum(TWO_SITE, XAX_k, A_k, A_kp1, XAX_k2), m)
+        with D.einsum_batch():  # the two assemblies are independent: grouped launches, same arithmetic
+            Dr = einsum(TWO_SITE, XDX_k, D_k, D_kp1, XDX_k2)
+            Ar = einsum(TWO_SITE, XAX_k, A_k, A_kp1, XAX_k2)
+        Dm, Am = _sym(Dr, m), _sym(Ar, m)
         k = min(sh[0] * sh[1], sh[2] * sh[3])
         sol, step, old_res, pre = _dense_step(
             pv, Am, Dm, step, eps, "two-site",
@@ -447,8 +449,10 @@ def _step_size_local_solve_last(prev, XDX_k, Dk, XDX_k1, XAX_k, Ak, XAX_k1, dens
     pv = D.contig(prev).view(-1)
     if dense:
         _check_dense(m)
-        Dm = _sym(einsum(ONE_SITE, XDX_k, Dk, XDX_k1), m)
-        Am = _sym(einsum(ONE_SITE, XAX_k, Ak, XAX_k1), m)
+        with D.einsum_batch():
+            Dr = einsum(ONE_SITE, XDX_k, Dk, XDX_k1)
+            Ar = einsum(ONE_SITE, XAX_k, Ak, XAX_k1)
+        Dm, Am = _sym(Dr, m), _sym(Ar, m)
         return _dense_step(pv, Am, Dm, step, eps, "one-site", post=post if _FUSED_TAIL else None)
     eq = "lsr,smnS,LSR,rnR->lmL"
     return _iterative_step(pv, lambda v: einsum(eq, XAX_k, Ak, XAX_k1, v.view(*xs)).view(-1),

@@ -180,6 +180,12 @@ def tt_scalars(specs):
     tt_entrywise_sum(tt).  Each contraction chain is the one of the single-value function (same
     launches, same order); its last step writes straight into the chain's slot of one buffer."""
     buf = D.empty(max(len(specs), 1))
+    with D.einsum_batch():  # the chains are independent: their steps grouped level by level
+        _scalar_chains(specs, buf)
+    return [float(v) for v in D.read(buf[:len(specs)])] if specs else []
+
+
+def _scalar_chains(specs, buf):
     for i, sp in enumerate(specs):
         slot = buf[i:i + 1].view(1, 1)
         if sp[0] == "ip":
@@ -194,7 +200,6 @@ def tt_scalars(specs):
             res = _const("one11", np.ones((1, 1)))
             for j, c in enumerate(tt):
                 res = D.einsum(eq, res, c, one, out=slot if j == len(tt) - 1 else None)
-    return [float(v) for v in D.read(buf[:len(specs)])] if specs else []
 
 
 def tt_normalise(tt, radius=1):
