@@ -207,7 +207,16 @@ __device__ __forceinline__ double block_sum(double v, double *red) {
 // ttk::dep_counter) is monotonic: the host passes target = arrivals of every launch so far.
 // Producers sit at lower block indices than their consumers and never wait, so the grid drains
 // whatever the residency; a wait past DEP_SPIN_MAX polls gives up (counted in dep[1],
-// ttk_dep_timeouts) instead of hanging.
+// ttk_dep_timeouts, which every solve checks: dev.check_handoffs) instead of hanging.
+//
+// Memory model.  The arrival is an agent-scope release (lane 0: fence(release, agent) =
+// buffer_wbl2 sc1, drained, then the relaxed atomic add -- the adds of one launch form a release
+// sequence) and each consumer wave runs fence(acquire, agent) = buffer_inv sc1 after its poll, so
+// every hand-off is ordered under the HIP memory model itself, not only by the hardware behaviour of
+// the sc1 stores and loads (the guide's measured table, first row; that form alone is the diagnostic
+// build `python build.py -DTTK_HANDOFF_RELAXED --out=...`).  Cost of the two fences
+// (profiles/r05_handoff_fences.txt): the one-launch Schur matvec 21.70 -> 22.56 us at m = 676,
+// whole solves within run-to-run noise; results bit-identical on the 133 kernel cases.
 constexpr long DEP_SPIN_MAX = 20000000;
 
 __device__ __forceinline__ double ld_sc1(const double *p) {
@@ -231,12 +240,22 @@ __device__ __forceinline__ void dep_wait(const unsigned *dep, unsigned target) {
     }
   }
   __builtin_amdgcn_wave_barrier();
+#ifndef TTK_HANDOFF_RELAXED
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#endif
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);  // no load of the handed-off words moves above the poll
 }
 // the workgroup's one arrival, after every wave's sc1 stores: drain, barrier, one lane adds
 __device__ __forceinline__ void dep_arrive(unsigned *dep) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0) __hip_atomic_fetch_add(dep, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x == 0) {
+#ifndef TTK_HANDOFF_RELAXED
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+    __hip_atomic_fetch_add(dep, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 // the calling context's hand-off counter (allocated and zeroed on first use)
 int dep_counter(void *stream);

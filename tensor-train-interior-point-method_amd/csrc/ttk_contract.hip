@@ -299,9 +299,9 @@ __global__ __launch_bounds__(256) void gemm_offs_splitk_kernel(GemmArgs g, int n
 }
 
 // Split-K in ONE launch: the split blocks of a tile store their partial tiles write-through (sc1),
-// drain, and count their arrival on the tile's counter (MI355X_MICROARCH.md's first measured
-// hand-off form: sc1 stores + s_waitcnt vmcnt(0) + workgroup barrier + one agent-scope atomic; the
-// consumer's loads are sc1).  The block whose arrival completes the count sums the tile's partials
+// drain, and count their arrival on the tile's counter with an agent-scope release (sc1 stores +
+// s_waitcnt vmcnt(0) + workgroup barrier + release fence + one atomic add; the last arriver runs an
+// agent acquire and loads sc1 -- ttk_common.h, memory model).  The block whose arrival completes the count sums the tile's partials
 // in split order and writes C -- the reduce kernel's arithmetic below, element for element -- and
 // resets the counter for the next launch.  Nobody waits: a block that is not last just exits, so
 // the grid drains whatever the residency.
@@ -318,9 +318,18 @@ __global__ __launch_bounds__(256) void gemm_offs_splitk_fused_kernel(GemmArgs g,
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   unsigned *c = cnt + ((int64_t)b * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
-  if (threadIdx.x == 0) s_old = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x == 0) {  // ttk_common.h, memory model
+#ifndef TTK_HANDOFF_RELAXED
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+    s_old = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   __syncthreads();
   if (s_old != (unsigned)(nsplit - 1)) return;
+#ifndef TTK_HANDOFF_RELAXED
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#endif
   const int64_t *a_b = g.offs;
   const int64_t *c_b = a_b + g.nb + g.M + g.K + g.nb + g.K + g.N;
   const int64_t *c_m = c_b + g.nb;
@@ -806,6 +815,14 @@ double *splitk_scratch(int64_t n) {  // partial-sum slabs of the current context
   }
   return c.splitk;
 }
+
+}  // namespace
+
+// ttk_ctx_create: the slabs allocated with the context, so a launch-only entry point (which keeps
+// the GIL, _lib.py) does not stall the process's other solve thread on a sync + hipMalloc later
+int ttk::presize_splitk() { return splitk_scratch(1) ? TTK_OK : TTK_ERR_HIP; }
+
+namespace {
 
 // diagnostics: launch-shape histogram of the GEMM steps (ttk_gemm_hist)
 bool g_hist_on = false;

@@ -1527,6 +1527,15 @@ double term_flops(const ApplyArgs &g) {
 
 }  // namespace
 
+// the Schur operator's w buffer at its initial size (ttk_ctx_create; see ttk::presize_splitk)
+int ttk::presize_schur() {
+  ttk::Ctx &cx = ttk::ctx();
+  if (cx.schur_w) return TTK_OK;
+  TTK_HIP(hipMalloc(reinterpret_cast<void **>(&cx.schur_w), 65536 * sizeof(double)));
+  cx.schur_wcap = 65536;
+  return TTK_OK;
+}
+
 static int schur_store(SchurOp &op, int64_t m, int64_t *handle) {
   ttk::Ctx &cx = ttk::ctx();
   if (m > cx.schur_wcap) {

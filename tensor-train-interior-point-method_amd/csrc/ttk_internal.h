@@ -65,6 +65,11 @@ struct Ctx {
 Ctx &ctx();
 Ctx *ctx_swap(Ctx *c);       // bind c to the calling thread, return the previous binding
 void schur_release(Ctx &c);  // ttk_einsum.hip: Schur handle table + operand images of a context
+// scratch of the bound context at its initial sizes (ttk_ctx_create): split-K slabs, LGMRES partials,
+// the Schur operator's w buffer
+int presize_splitk();
+int presize_lgmres();
+int presize_schur();
 }  // namespace ttk
 
 struct ttk_ctx_s {

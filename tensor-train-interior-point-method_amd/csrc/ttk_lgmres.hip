@@ -473,6 +473,12 @@ double *lgmres_scratch(int64_t n) {  // partials / norm parts of the current con
   return c.lgmres;
 }
 
+}  // namespace
+
+int ttk::presize_lgmres() { return lgmres_scratch(1) ? TTK_OK : TTK_ERR_HIP; }  // see ttk::presize_splitk
+
+namespace {
+
 // (it+1)*n at or above which the multi-workgroup kernels run: per-context knob
 static inline int64_t mw_min() { return ttk::ctx().knob[TTK_KNOB_LGMRES_MW_MIN]; }
 

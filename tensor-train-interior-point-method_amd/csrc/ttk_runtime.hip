@@ -190,6 +190,20 @@ int ttk_ctx_create(void *stream, ttk_ctx *out) {
       return TTK_ERR_HIP;
     }
   }
+  {  // scratch at its initial sizes now (this entry point releases the GIL; the launch-only ones that
+     // would grow it later keep it, _lib.py), and the hand-off counter
+    ttk::Ctx *prev = ttk::ctx_swap(&h->c);
+    int rc = ttk::presize_splitk();
+    if (!rc) rc = ttk::presize_lgmres();
+    if (!rc) rc = ttk::presize_schur();
+    if (!rc) rc = ttk::dep_counter(stream);
+    if (!rc && hipStreamSynchronize(TTK_STREAM(stream)) != hipSuccess) rc = TTK_ERR_HIP;
+    ttk::ctx_swap(prev);
+    if (rc) {
+      ttk_ctx_destroy(h);
+      return rc;
+    }
+  }
   *out = h;
   return TTK_OK;
 }
