@@ -225,6 +225,11 @@ int ttk_gemm_set_splitk(int on);
 /* diagnostics: on > 0 records a (nb,M,N,K) histogram of ttk_gemm_offs launches, on < 0 clears it;
  * dump_path != NULL writes "nb M N K launches flops" lines */
 int ttk_gemm_hist(int on, const char *dump_path);
+/* diagnostics: on > 0 records a (kind, a, b, path) histogram of the dense factorisations (svd: a x b,
+ * qr: a x b, syev_extreme: n and which, lu / cholesky: n), each recorded call bracketed by two stream
+ * synchronisations and timed on the host; on < 0 clears it; dump_path != NULL writes
+ * "kind a b path calls total_us" lines.  Never on in a timed run. */
+int ttk_linalg_hist(int on, const char *dump_path);
 
 /* ---------------------------------------------------------------------------------------
  * Strided element-wise kernels (up to 6-D).  `shape`, `sstride`, `dstride` are host arrays.

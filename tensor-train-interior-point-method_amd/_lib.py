@@ -91,6 +91,7 @@ _SIGS = {
     "ttk_qr_set_big_threshold": (i32, [i32]),
     "ttk_contract_timing": (i32, [i32]),
     "ttk_gemm_hist": (i32, [i32, ctypes.c_char_p]),
+    "ttk_linalg_hist": (i32, [i32, ctypes.c_char_p]),
     "ttk_gemm_set_splitk": (i32, [i32]),
     "ttk_contract_stats": (i32, [vp, i32]),
     "ttk_syev_extreme": (i32, [vp, vp, i32, i32, vp, vp, vp]),
@@ -114,7 +115,7 @@ BLOCKING = frozenset(n for n in _SIGS if "sync" in n) | frozenset((
     "ttk_lgmres", "ttk_round", "ttk_zipup", "ttk_dense_schur_solve", "ttk_dense_schur_solve_ineq",
     "ttk_lgmres_chunk", "ttk_lgmres_build", "ttk_lgmres_aug", "ttk_schur_build", "ttk_schur_free",
     "ttk_ctx_create", "ttk_ctx_destroy", "ttk_upload", "ttk_dep_timeouts", "ttk_debug_counters",
-    "ttk_mfma_profile", "ttk_contract_stats", "ttk_gemm_hist"))
+    "ttk_mfma_profile", "ttk_contract_stats", "ttk_gemm_hist", "ttk_linalg_hist"))
 # Every other (launch-only, microseconds) entry point keeps the GIL (ctypes.PyDLL calling
 # convention; TTK_HOLD_GIL=0 releases it on every call, as plain ctypes does).  A thread that drops
 # the GIL for a 3 us launch and takes it straight back makes a second solve thread of the process

@@ -351,6 +351,155 @@ __global__ __launch_bounds__(1024) void getf2_panel_lds_kernel(double *A, int n,
   }
 }
 
+// The same panel factorisation with the panel in REGISTERS: thread t owns panel rows t, t + 1024, ...
+// (R of them, KB columns each, kb <= KB used), so a column step touches memory only for the
+// pivot search's 16 wave winners and the pivot row's broadcast -- two barriers per column, no
+// global or LDS round trip per element (getf2_panel_kernel: a strided global scan and update per
+// column; the LDS kernel: an LDS pass per column).  The same operations in the same order on every
+// element (idamax winner, swap of the whole panel row, l = a * (1 / d), a -= l * u): bit-identical
+// to both.  Double-buffered broadcast slots (column parity) leave the next column's writes behind
+// the current column's second barrier.
+// a copy the optimiser cannot look through (no instruction is emitted)
+__device__ __forceinline__ double opaque(double x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+
+template <int KB, int R>
+struct PanelRegs {
+  double r[R][KB];
+  double (*cv)[16];
+  int (*ci)[16];
+  double (*prow_s)[KB];
+  double (*crow_s)[KB];
+  double *A;
+  int n, k0, kb, rows, tid, lane, wid;
+  int *piv, *status;
+
+  // column C of the panel (C a template parameter: every r[][] index is compile-time)
+  template <int C>
+  __device__ __forceinline__ void column() {
+    if constexpr (C < KB) {
+      if (C < kb) {
+        constexpr int b = C & 1;
+        double best = -1.0;
+        int bi = C;
+#pragma unroll
+        for (int q = 0; q < R; ++q) {
+          const int i = tid + 1024 * q;
+          if (i >= C && i < rows) {
+            const double v = fabs(r[q][C]);
+            if (v > best) {
+              best = v;
+              bi = i;
+            }
+          }
+        }
+        ttk::wave_argmax(best, bi);
+        if (lane == 0) {
+          cv[b][wid] = best;
+          ci[b][wid] = bi;
+        }
+        __syncthreads();
+        double pb = lane < 16 ? cv[b][lane] : -2.0;
+        int p = lane < 16 ? ci[b][lane] : 0x7fffffff;
+        ttk::wave_argmax(pb, p);  // every wave reduces the 16 winners itself: uniform p, no third barrier
+        const int pt = p & 1023, pq = p >> 10;
+        if (tid == pt) {  // row pq of this thread, picked by value selects behind an opaque copy (a
+                          // select of two loads would fold into one load of a run-time index and
+                          // send r[][] to scratch)
+#pragma unroll
+          for (int cc = 0; cc < KB; ++cc) {
+            double v = opaque(r[0][cc]);
+#pragma unroll
+            for (int q = 1; q < R; ++q) v = q == pq ? opaque(r[q][cc]) : v;
+            prow_s[b][cc] = v;
+          }
+        }
+        if (p != C && tid == C) {
+#pragma unroll
+          for (int cc = 0; cc < KB; ++cc) crow_s[b][cc] = r[0][cc];
+        }
+        if (tid == 0) piv[k0 + C] = k0 + p;
+        __syncthreads();
+        if (p != C) {
+          if (tid == C) {
+#pragma unroll
+            for (int cc = 0; cc < KB; ++cc) r[0][cc] = prow_s[b][cc];
+          }
+          if (tid == pt) {
+#pragma unroll
+            for (int cc = 0; cc < KB; ++cc) {
+              const double v = crow_s[b][cc];
+#pragma unroll
+              for (int q = 0; q < R; ++q) r[q][cc] = q == pq ? v : opaque(r[q][cc]);
+            }
+          }
+        }
+        const double d = prow_s[b][C];
+        if (d == 0.0) {  // LAPACK: info = first zero pivot, no scaling, factorisation continues
+          if (tid == 0 && *status == 0) *status = k0 + C + 1;
+        } else {
+          const double inv = 1.0 / d;
+#pragma unroll
+          for (int q = 0; q < R; ++q) {
+            const int i = tid + 1024 * q;
+            if (i > C && i < rows) {
+              const double l = r[q][C] * inv;
+              r[q][C] = l;
+#pragma unroll
+              for (int cc = C + 1; cc < KB; ++cc)
+                if (cc < kb) r[q][cc] -= l * prow_s[b][cc];
+            }
+          }
+        }
+      }
+      column<C + 1>();
+    }
+  }
+};
+
+template <int KB, int R>
+__global__ __launch_bounds__(1024) void getf2_panel_reg_kernel(double *A, int n, int k0, int kb, int *piv,
+                                                               int *status) {
+  __shared__ double cv[2][16];
+  __shared__ int ci[2][16];
+  __shared__ double prow_s[2][KB], crow_s[2][KB];
+  PanelRegs<KB, R> P;
+  P.cv = cv;
+  P.ci = ci;
+  P.prow_s = prow_s;
+  P.crow_s = crow_s;
+  P.A = A;
+  P.n = n;
+  P.k0 = k0;
+  P.kb = kb;
+  P.rows = n - k0;
+  P.tid = threadIdx.x;
+  P.lane = threadIdx.x & 63;
+  P.wid = threadIdx.x >> 6;
+  P.piv = piv;
+  P.status = status;
+#pragma unroll
+  for (int q = 0; q < R; ++q) {
+    const int i = P.tid + 1024 * q;
+    const double *src = A + (int64_t)(k0 + i) * n + k0;
+#pragma unroll
+    for (int c = 0; c < KB; ++c) P.r[q][c] = (i < P.rows && c < kb) ? src[c] : 0.0;
+  }
+  P.template column<0>();
+#pragma unroll
+  for (int q = 0; q < R; ++q) {
+    const int i = P.tid + 1024 * q;
+    double *dst = A + (int64_t)(k0 + i) * n + k0;
+    if (i < P.rows) {
+#pragma unroll
+      for (int c = 0; c < KB; ++c)
+        if (c < kb) dst[c] = P.r[q][c];
+    }
+  }
+}
+
 // row swaps of panel [k0, k0+kb) on the columns outside it
 __global__ __launch_bounds__(256) void laswp_kernel(double *A, int n, int k0, int kb, const int *piv) {
   const int c = blockIdx.x * 256 + threadIdx.x;
@@ -734,6 +883,9 @@ __global__ __launch_bounds__(1024) void lu_solve_cols_kernel(const double *__res
 
 namespace ttk {
 
+// TTK_LU_REG_PANEL=0: the panels on the LDS / global-memory kernels (bit-identical; diagnostics)
+static const int g_lu_reg_panel = getenv("TTK_LU_REG_PANEL") ? atoi(getenv("TTK_LU_REG_PANEL")) : 1;
+
 int lu_blocked(hipStream_t st, double *A, int n, int *piv, double *work, int *status, double *rcond, int want_rcond) {
   TTK_HIP(hipMemsetAsync(status, 0, sizeof(int), st));
   double *colsum = work;  // n doubles
@@ -744,7 +896,17 @@ int lu_blocked(hipStream_t st, double *A, int n, int *piv, double *work, int *st
     while (kb > 8 && (size_t)(n - k0) * (kb + 1) * sizeof(double) > 150000) kb >>= 1;
     if (kb > n - k0) kb = n - k0;
     const size_t pshm = (size_t)(n - k0) * (kb + 1) * sizeof(double);
-    if (pshm <= 150000) {
+    const int rq = (n - k0 + 1023) / 1024;  // panel rows per thread of the register kernel
+    // panels that do not fit the LDS staging (kb = 8, more than 2083 rows) run in registers; where the
+    // LDS kernel applies it is the faster one (tools/bench_lu.py: n = 1000 4.38 vs 4.66 ms with every
+    // panel in registers; n = 3120 37.1 -> 24.0 ms, 3600 51.7 -> 31.6 ms with the global-memory panels
+    // replaced)
+    if (g_lu_reg_panel && pshm > 150000 && kb <= 8 && rq <= 4) {
+      if (rq == 3)  // rows > 2083 (pshm > 150000): 3 or 4 rows per thread
+        hipLaunchKernelGGL((getf2_panel_reg_kernel<8, 3>), dim3(1), dim3(1024), 0, st, A, n, k0, kb, piv, status);
+      else
+        hipLaunchKernelGGL((getf2_panel_reg_kernel<8, 4>), dim3(1), dim3(1024), 0, st, A, n, k0, kb, piv, status);
+    } else if (pshm <= 150000) {
       if (pshm > 65536)
         (void)hipFuncSetAttribute(reinterpret_cast<const void *>(getf2_panel_lds_kernel),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)pshm);

@@ -18,6 +18,12 @@
 #include <math.h>
 #include <stdlib.h>
 
+#include <array>
+#include <chrono>
+#include <cstdio>
+#include <map>
+#include <mutex>
+
 #include "ttk_common.h"
 #include "ttk_internal.h"
 
@@ -2470,6 +2476,51 @@ extern "C" {
 static int g_svd_big_p = 64;
 static int g_svd_timing = 0;  // phase timers of the one-workgroup SVD into the debug counters
 
+// diagnostics: shape histogram of the dense factorisations (ttk_linalg_hist).  While on, each
+// recorded call is bracketed by two stream synchronisations and its wall time (launch overhead
+// included) added to its (kind, a, b, path) entry -- a sizing tool, never on in a timed run.
+namespace {
+bool g_lhist_on = false;
+std::mutex g_lhist_mu;
+std::map<std::array<int, 4>, std::pair<long long, double>> g_lhist;
+const char *const LHIST_KIND[] = {"svd", "qr", "syev_extreme", "lu", "cholesky"};
+struct LinalgScope {
+  hipStream_t st;
+  std::array<int, 4> key;
+  std::chrono::steady_clock::time_point t0;
+  LinalgScope(hipStream_t s, int kind, int a, int b, int path) : st(s), key{kind, a, b, path} {
+    if (!g_lhist_on) return;
+    (void)hipStreamSynchronize(st);
+    t0 = std::chrono::steady_clock::now();
+  }
+  ~LinalgScope() {
+    if (!g_lhist_on) return;
+    (void)hipStreamSynchronize(st);
+    const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+    std::lock_guard<std::mutex> lk(g_lhist_mu);
+    auto &e = g_lhist[key];
+    e.first += 1;
+    e.second += us;
+  }
+};
+}  // namespace
+
+int ttk_linalg_hist(int on, const char *dump_path) {
+  std::lock_guard<std::mutex> lk(g_lhist_mu);
+  if (dump_path) {
+    FILE *f = std::fopen(dump_path, "w");
+    if (!f) return TTK_ERR_ARG;
+    std::fprintf(f, "kind a b path calls total_us\n");
+    for (const auto &kv : g_lhist)
+      std::fprintf(f, "%s %d %d %d %lld %.1f\n", LHIST_KIND[kv.first[0]], kv.first[1], kv.first[2], kv.first[3],
+                   kv.second.first, kv.second.second);
+    std::fclose(f);
+  }
+  if (on < 0) g_lhist.clear();
+  g_lhist_on = on > 0;
+  return TTK_OK;
+}
+
 int ttk_svd_set_timing(int on) {
   const int old = g_svd_timing;
   g_svd_timing = on;
@@ -2616,6 +2667,7 @@ int ttk_svd_tol(void *stream, const double *A, int m, int n, double *U, double *
   }
   const int p = m < n ? m : n, q = m < n ? n : m;
   const bool forced_big = g_svd_big_p <= 2;
+  LinalgScope scope_(TTK_STREAM(stream), 0, m, n, p > WG_P || forced_big ? 0 : -1);
   if (p > WG_P || forced_big) return svd_big(stream, A, m, n, U, S, Vt, work, defl);
   // small near-square problems converge fast without QR preconditioning; otherwise QRCP first
   const int use_qr = !(p <= 16 && q <= 2 * p);
@@ -2631,6 +2683,7 @@ int ttk_svd_tol(void *stream, const double *A, int m, int n, double *U, double *
   int nt = pairs * g;
   if (use_qr && q * p > 2048) nt = 1024;  // column-parallel QR phases want a full block
   nt = nt < 64 ? 64 : (nt > 1024 ? 1024 : (nt + 63) / 64 * 64);
+  scope_.key[3] = g * (use_qr ? 1 : -1) * (w_in_lds ? 1 : 100);  // path: svd_wg_kernel<g>, sign = QRCP, x100 = W global
   (void)defl;  // no deflation on this path (every direction keeps an orthonormal vector)
 #define TTK_SVD_WG(GG)                                                                                      \
   case GG:                                                                                                  \
@@ -2659,6 +2712,7 @@ int ttk_svd_tol(void *stream, const double *A, int m, int n, double *U, double *
   return TTK_OK;
 }
 
+static const int g_qr_narrow = getenv("TTK_QR_NARROW") ? atoi(getenv("TTK_QR_NARROW")) : 1;
 static int g_qr_big_k = 48;  // smallest min(m,n) that takes the blocked path (when it does not fit LDS)
 
 int ttk_qr_set_big_threshold(int k) {
@@ -2682,14 +2736,19 @@ int ttk_qr(void *stream, const double *A, int m, int n, double *Q, double *R, do
   const int64_t k = m < n ? m : n;
   const int64_t need = (int64_t)m * n + k + (int64_t)m * k + 16;
   const int use_lds = need <= LDS_DOUBLES;
+  LinalgScope scope_(TTK_STREAM(stream), 1, m, n, k >= g_qr_big_k && (!use_lds || g_qr_big_k <= 2) ? 0 : use_lds ? 1 : 2);
   if (k >= g_qr_big_k && (!use_lds || g_qr_big_k <= 2)) return qr_big(stream, A, m, n, Q, R, work);
   const size_t shm = use_lds ? need * sizeof(double) : 0;
+  // m <= 65: every thread's norm chain holds at most one element whatever the block size, and the
+  // per-column work is one wave's either way, so one wave per trailing column (<= 16) computes the
+  // same bits as the full 1024-thread block with fewer waves to synchronise (TTK_QR_NARROW=0: 1024)
+  const int nt = (g_qr_narrow && m <= 65) ? 64 * (n < 16 ? (n < 1 ? 1 : n) : 16) : 1024;
   if (use_lds) {
     allow_big_lds(qr_kernel<true>, shm);
-    hipLaunchKernelGGL(qr_kernel<true>, dim3(1), dim3(1024), shm, TTK_STREAM(stream), A, m, n, Q, R, work, use_lds);
+    hipLaunchKernelGGL(qr_kernel<true>, dim3(1), dim3(nt), shm, TTK_STREAM(stream), A, m, n, Q, R, work, use_lds);
   } else {
     allow_big_lds(qr_kernel<false>, shm);
-    hipLaunchKernelGGL(qr_kernel<false>, dim3(1), dim3(1024), shm, TTK_STREAM(stream), A, m, n, Q, R, work, use_lds);
+    hipLaunchKernelGGL(qr_kernel<false>, dim3(1), dim3(nt), shm, TTK_STREAM(stream), A, m, n, Q, R, work, use_lds);
   }
   TTK_LAUNCH_CHECK();
   return TTK_OK;
@@ -2710,6 +2769,7 @@ int ttk_cholesky_sync(void *stream, double *A, int n) {
     ttk::set_error("ttk_cholesky_sync: status alloc failed");
     return TTK_ERR_HIP;
   }
+  LinalgScope scope_(TTK_STREAM(stream), 4, n, n, n >= g_dense_block_min);
   if (n >= g_dense_block_min) {
     const int rc = ttk::cholesky_blocked(TTK_STREAM(stream), A, n, ttk::ctx().status);
     if (rc) return rc;
@@ -2743,6 +2803,7 @@ int ttk_lu_sync(void *stream, double *A, int n, int *piv, double *work, double *
     ttk::set_error("ttk_lu_sync: status alloc failed");
     return TTK_ERR_HIP;
   }
+  LinalgScope scope_(TTK_STREAM(stream), 3, n, n, n >= g_lu_block_min && n <= 7000);
   if (n >= g_lu_block_min && n <= 7000) {
     const int rc = ttk::lu_blocked(TTK_STREAM(stream), A, n, piv, work, ttk::ctx().status, ttk::ctx().rcond, 1);
     if (rc) return rc;
@@ -2772,6 +2833,7 @@ int lu_factor_fork_rcond(hipStream_t st, double *A, int n, int *piv, double *wor
     return TTK_ERR_HIP;
   }
   Ctx &c = ctx();
+  LinalgScope scope_(st, 3, n, n, n >= g_lu_block_min && n <= 7000 ? 2 : 3);  // 2 forked dgecon, 3 one kernel
   if (!(n >= g_lu_block_min && n <= 7000)) {  // one-kernel getrf + dgecon (ttk_lu_sync's small path)
     hipLaunchKernelGGL(lu_kernel, dim3(1), dim3(1024), 0, st, A, n, piv, work, c.status, c.rcond);
     TTK_LAUNCH_CHECK();
@@ -2877,6 +2939,10 @@ int ttk_syev_extreme(void *stream, const double *A, int n, int which, double *ev
   const int64_t need = syev_extreme_need(n);
   const int use_lds = need <= LDS_DOUBLES;
   hipStream_t st = TTK_STREAM(stream);
+  // path: 1 one launch per Householder step, 2 multi-workgroup, 3 small 1024, 4 small 256, 5 one kernel
+  LinalgScope scope_(st, 2, n, which,
+                     !use_lds && n > 2 ? (n <= g_syev_fused_max ? 1 : 2)
+                     : (n >= 3 && n <= SYEV_SMALL_N && g_syev_small) ? (n >= g_syev_small_wide ? 3 : 4) : 5);
   if (!use_lds && n > 2 && n <= g_syev_fused_max) {  // one launch per Householder step
     double *Aw = work, *gv = work + (int64_t)n * n;
     double *dv = gv, *ov = dv + n, *tv = ov + 2 * n;  // layout of tri_finish_kernel: dv ov ev2 tv ...

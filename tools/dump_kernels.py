@@ -33,7 +33,7 @@ def main(path):
         out[f"mmT_{M_}_{N_}_{K_}"] = D.read(D.matmul(b.t(), a.t()))
     # LU with the dgecon estimate (getrf + lu_rcond_kernel) and getrs
     import ctypes
-    for n in (40, 300, 1000, 2100, 4000):
+    for n in (40, 300, 600, 1000, 2100, 3120, 4000, 4500):
         M = rng.standard_normal((n, n)) + np.diag(np.linspace(0.0, 3.0, n))
         A = D.from_numpy(M)
         piv = torch.empty(n, dtype=torch.int32, device="cuda")
@@ -45,6 +45,11 @@ def main(path):
         out[f"lu_{n}"] = D.read(A)
         out[f"lu_rcond_{n}"] = np.array([rc.value])
         out[f"lu_sol_{n}"] = D.read(b)
+    # one-workgroup Householder QR (ttk_qr; the narrow launch for m <= 65) on the ranks' shapes
+    for (m_, n_) in [(10, 5), (24, 6), (16, 4), (8, 2), (4, 5), (2, 5), (48, 12), (56, 14), (128, 8), (16, 12),
+                     (65, 20), (64, 64), (66, 10), (1, 3), (3, 1), (40, 40)]:
+        Q_, R_ = D.qr(D.from_numpy(rng.standard_normal((m_, n_))))
+        out[f"qr_{m_}_{n_}"] = np.concatenate([D.read(Q_).ravel(), D.read(R_).ravel()])
     # VALU local-apply rows (maxcut-sized fused applies: single launches)
     old = lib.ttk_fused_set_mfma(0)
     try:
