@@ -87,6 +87,25 @@ __device__ __forceinline__ double sum_ahead(int count, F f, double acc) {
   for (; k < count; ++k) acc = acc + f(k);
   return acc;
 }
+// dst(e) <- src(e) for e = tid, tid + nt, ... < total, U loads issued before their U stores: a plain
+// `for (e = tid; e < total; e += nt) P[..] = A[..]` staging loop waits one global round trip per
+// element it moves (the loop is not unrolled at a run-time trip count).  A pure copy.
+template <int U, class LD, class ST>
+__device__ __forceinline__ void staged_copy(int total, int tid, int nt, LD ld, ST st) {
+  for (int e0 = tid; e0 < total; e0 += U * nt) {
+    double v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = e0 + u * nt;
+      v[u] = e < total ? ld(e) : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = e0 + u * nt;
+      if (e < total) st(e, v[u]);
+    }
+  }
+}
 // number of k with start + k * step < end (start < end not required)
 __device__ __forceinline__ int steps_below(int start, int end, int step) {
   return start < end ? (end - start + step - 1) / step : 0;

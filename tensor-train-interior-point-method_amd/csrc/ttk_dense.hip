@@ -89,10 +89,8 @@ __global__ __launch_bounds__(256) void potf2_block_kernel(double *A, int n, int 
   __shared__ int s_fail;
   const int tid = threadIdx.x;
   if (*status) return;  // an earlier panel failed: LAPACK stops there
-  for (int e = tid; e < kb * kb; e += 256) {
-    const int i = e / kb, j = e - i * kb;
-    Ls[i][j] = A[(int64_t)(k0 + i) * n + k0 + j];
-  }
+  ttk::staged_copy<4>(kb * kb, tid, 256, [&](int e) { return A[(int64_t)(k0 + e / kb) * n + k0 + e % kb]; },
+                      [&](int e, double v) { Ls[e / kb][e % kb] = v; });
   if (tid == 0) s_fail = 0;
   __syncthreads();
   for (int j = 0; j < kb; ++j) {
@@ -131,10 +129,8 @@ __global__ __launch_bounds__(256) void panel_trsm_kernel(double *A, int n, int k
   __shared__ double Ls[NB][NB + 1];
   if (*status) return;
   const int tid = threadIdx.x;
-  for (int e = tid; e < kb * kb; e += 256) {
-    const int i = e / kb, j = e - i * kb;
-    Ls[i][j] = A[(int64_t)(k0 + i) * n + k0 + j];
-  }
+  ttk::staged_copy<4>(kb * kb, tid, 256, [&](int e) { return A[(int64_t)(k0 + e / kb) * n + k0 + e % kb]; },
+                      [&](int e, double v) { Ls[e / kb][e % kb] = v; });
   __syncthreads();
   const int r = k0 + kb + blockIdx.x * 256 + tid;
   if (r >= n) return;
@@ -170,10 +166,13 @@ __global__ __launch_bounds__(256) void trsm_diag_kernel(const double *__restrict
                                                         int ldb, int r0, int kb, int trans) {
   __shared__ double Ls[NB][NB + 1];
   const int tid = threadIdx.x;
-  for (int e = tid; e < kb * kb; e += 256) {
-    const int i = e / kb, j = e - i * kb;
-    Ls[i][j] = trans ? L[(int64_t)(r0 + j) * n + r0 + i] : L[(int64_t)(r0 + i) * n + r0 + j];
-  }
+  ttk::staged_copy<4>(
+      kb * kb, tid, 256,
+      [&](int e) {
+        const int i = e / kb, j = e - i * kb;
+        return trans ? L[(int64_t)(r0 + j) * n + r0 + i] : L[(int64_t)(r0 + i) * n + r0 + j];
+      },
+      [&](int e, double v) { Ls[e / kb][e % kb] = v; });
   __syncthreads();
   const int c = blockIdx.x * 256 + tid;
   if (c >= nrhs) return;
@@ -221,9 +220,21 @@ __global__ __launch_bounds__(256) void trsm_diag_kernel(const double *__restrict
 __global__ __launch_bounds__(256) void colsum_kernel(const double *__restrict__ A, int n, double *__restrict__ out) {
   const int c = blockIdx.x * 256 + threadIdx.x;
   if (c >= n) return;
-  double s = 0.0;
-  for (int r = 0; r < n; ++r) s += fabs(A[(int64_t)r * n + c]);
-  out[c] = s;
+  // the plain loop's additions in its order, the next 8 rows' loads in flight (one L2 round trip per 8
+  // rows instead of per row: n = 1000 was ~0.25 ms on 4 workgroups)
+  out[c] = ttk::sum_ahead<8>(n, [&](int r) { return fabs(A[(int64_t)r * n + c]); }, 0.0);
+}
+
+// row i of a panel step: l = a_ic / d, a_ij -= l u_j for j in (c, kb) -- `pi` (row i) and `prow` (the
+// pivot row c < i) never overlap; saying so lets the u_j / a_ij loads issue ahead of the stores
+// (with possible aliasing every element waited for the previous element's store: one LDS or L2
+// round trip per element).  The same operations as the plain loop: bit-identical.
+__device__ __forceinline__ void panel_row_update(double *__restrict__ pi, const double *__restrict__ prow, int c,
+                                                 int kb, double inv) {
+  const double l = pi[c] * inv;
+  pi[c] = l;
+#pragma unroll 8
+  for (int cc = c + 1; cc < kb; ++cc) pi[cc] -= l * prow[cc];
 }
 
 __global__ __launch_bounds__(1024) void getf2_panel_kernel(double *A, int n, int k0, int kb, int *piv, int *status) {
@@ -275,34 +286,29 @@ __global__ __launch_bounds__(1024) void getf2_panel_kernel(double *A, int n, int
     }
     const double inv = 1.0 / d;
     const double *prow = A + (int64_t)j * n + k0;
-    for (int i = j + 1 + tid; i < n; i += 1024) {
-      double *ai = A + (int64_t)i * n + k0;
-      const double l = ai[c] * inv;
-      ai[c] = l;
-      for (int cc = c + 1; cc < kb; ++cc) ai[cc] -= l * prow[cc];
-    }
+    for (int i = j + 1 + tid; i < n; i += 1024) panel_row_update(A + (int64_t)i * n + k0, prow, c, kb, inv);
     __syncthreads();
   }
 }
 
-// the same panel factorisation with the (n-k0) x kb panel staged in LDS (row stride kb+1)
+// the same panel factorisation with the (n-k0) x kb panel staged in LDS (row stride kb+1); any block
+// size (a multiple of 64, <= 1024): lu_blocked launches one thread per panel row up to 1024, so a
+// short panel synchronises fewer waves (the pivot is the same idamax winner whatever the layout)
 __global__ __launch_bounds__(1024) void getf2_panel_lds_kernel(double *A, int n, int k0, int kb, int *piv,
                                                                int *status) {
   extern __shared__ double P[];
   __shared__ double wv[16];
   __shared__ int wi[16];
   __shared__ int s_p;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, nt = blockDim.x, nw = nt >> 6;
   const int rows = n - k0, ld = kb + 1;
-  for (int e = tid; e < rows * kb; e += 1024) {
-    const int i = e / kb, c = e - i * kb;
-    P[i * ld + c] = A[(int64_t)(k0 + i) * n + k0 + c];
-  }
+  ttk::staged_copy<8>(rows * kb, tid, nt, [&](int e) { return A[(int64_t)(k0 + e / kb) * n + k0 + e % kb]; },
+                      [&](int e, double v) { P[(e / kb) * ld + e % kb] = v; });
   __syncthreads();
   for (int c = 0; c < kb; ++c) {
     double best = -1.0;
     int bi = c;
-    for (int i = c + tid; i < rows; i += 1024) {
+    for (int i = c + tid; i < rows; i += nt) {
       const double v = fabs(P[i * ld + c]);
       if (v > best) {
         best = v;
@@ -315,9 +321,9 @@ __global__ __launch_bounds__(1024) void getf2_panel_lds_kernel(double *A, int n,
       wi[wid] = bi;
     }
     __syncthreads();
-    if (tid < 64) {  // wave 0: reduce the 16 wave winners, swap the two panel rows
-      double b = tid < 16 ? wv[tid] : -2.0;
-      int p = tid < 16 ? wi[tid] : 0x7fffffff;
+    if (tid < 64) {  // wave 0: reduce the nw wave winners, swap the two panel rows
+      double b = tid < nw ? wv[tid] : -2.0;
+      int p = tid < nw ? wi[tid] : 0x7fffffff;
       ttk::wave_argmax(b, p);  // uniform over the wave
       if (p != c && tid < kb) {
         const double t = P[c * ld + tid];
@@ -337,15 +343,10 @@ __global__ __launch_bounds__(1024) void getf2_panel_lds_kernel(double *A, int n,
     }
     const double inv = 1.0 / d;
     const double *prow = P + c * ld;
-    for (int i = c + 1 + tid; i < rows; i += 1024) {
-      double *pi = P + i * ld;
-      const double l = pi[c] * inv;
-      pi[c] = l;
-      for (int cc = c + 1; cc < kb; ++cc) pi[cc] -= l * prow[cc];
-    }
+    for (int i = c + 1 + tid; i < rows; i += nt) panel_row_update(P + i * ld, prow, c, kb, inv);
     __syncthreads();
   }
-  for (int e = tid; e < rows * kb; e += 1024) {
+  for (int e = tid; e < rows * kb; e += nt) {
     const int i = e / kb, c = e - i * kb;
     A[(int64_t)(k0 + i) * n + k0 + c] = P[i * ld + c];
   }
@@ -514,14 +515,54 @@ __global__ __launch_bounds__(256) void laswp_kernel(double *A, int n, int k0, in
   }
 }
 
+// laswp_kernel and lu_u12_kernel in one launch: thread idx owns column c (every column outside the
+// panel), applies the panel's row swaps to it, and -- right of the panel -- then solves its U12 column
+// against L11 (staged in LDS; the panel columns are not swapped here, so L11 is final).  Per column
+// the same operations as the two launches: bit-identical.
+__global__ __launch_bounds__(256) void lu_swap_u12_kernel(double *A, int n, int k0, int kb, const int *piv) {
+  __shared__ double Ls[NB][NB + 1];
+  const int tid = threadIdx.x;
+  const int idx = blockIdx.x * 256 + tid, c = idx < k0 ? idx : idx + kb;
+  const bool right = (int)(blockIdx.x * 256 + 255) >= k0;  // the block has columns right of the panel
+  if (right) {
+    ttk::staged_copy<4>(kb * kb, tid, 256, [&](int e) { return A[(int64_t)(k0 + e / kb) * n + k0 + e % kb]; },
+                        [&](int e, double v) { Ls[e / kb][e % kb] = v; });
+    __syncthreads();
+  }
+  if (c >= n) return;
+  for (int jj = k0; jj < k0 + kb; ++jj) {
+    const int p = piv[jj];
+    if (p != jj) {
+      const double t = A[(int64_t)jj * n + c];
+      A[(int64_t)jj * n + c] = A[(int64_t)p * n + c];
+      A[(int64_t)p * n + c] = t;
+    }
+  }
+  if (c < k0 + kb) return;
+  double x[NB];
+#pragma unroll
+  for (int q = 0; q < NB; ++q) x[q] = q < kb ? A[(int64_t)(k0 + q) * n + c] : 0.0;
+#pragma unroll
+  for (int q = 1; q < NB; ++q) {
+    if (q < kb) {
+      double v = x[q];
+#pragma unroll
+      for (int p = 0; p < NB; ++p)
+        if (p < q) v -= Ls[q][p] * x[p];
+      x[q] = v;
+    }
+  }
+#pragma unroll
+  for (int q = 1; q < NB; ++q)
+    if (q < kb) A[(int64_t)(k0 + q) * n + c] = x[q];
+}
+
 // U12 = L11^-1 A12 (L11 unit lower kb x kb), one thread per column c >= k0+kb
 __global__ __launch_bounds__(256) void lu_u12_kernel(double *A, int n, int k0, int kb) {
   __shared__ double Ls[NB][NB + 1];
   const int tid = threadIdx.x;
-  for (int e = tid; e < kb * kb; e += 256) {
-    const int i = e / kb, j = e - i * kb;
-    Ls[i][j] = A[(int64_t)(k0 + i) * n + k0 + j];
-  }
+  ttk::staged_copy<4>(kb * kb, tid, 256, [&](int e) { return A[(int64_t)(k0 + e / kb) * n + k0 + e % kb]; },
+                      [&](int e, double v) { Ls[e / kb][e % kb] = v; });
   __syncthreads();
   const int c = k0 + kb + blockIdx.x * 256 + tid;
   if (c >= n) return;
@@ -631,7 +672,7 @@ __device__ __forceinline__ void lu_solve_blk(const double *__restrict__ LU, int 
         double xq = hl < bs ? x[b0 + hl] : 0.0;
 #pragma unroll
         for (int p = 0; p < TB - 1; ++p) {
-          const double xp = __shfl(xq, p, 64);
+          const double xp = ttk::readlane_d(xq, p);  // p uniform: a scalar broadcast, no LDS trip
           xq -= lr[p] * xp;
         }
         if (half == 0 && hl < bs) x[b0 + hl] = xq;
@@ -653,7 +694,7 @@ __device__ __forceinline__ void lu_solve_blk(const double *__restrict__ LU, int 
         for (int p = TB - 1; p >= 0; --p) {
           if (p < bs) {
             if (hl == p) xq = xq / d;
-            const double xp = __shfl(xq, p, 64);
+            const double xp = ttk::readlane_d(xq, p);  // p uniform: a scalar broadcast, no LDS trip
             xq -= ur[p] * xp;
           }
         }
@@ -681,7 +722,7 @@ __device__ __forceinline__ void lu_solve_blk(const double *__restrict__ LU, int 
         for (int p = 0; p < TB; ++p) {
           if (p < bs) {
             if (hl == p) xq = xq / d;
-            const double xp = __shfl(xq, p, 64);
+            const double xp = ttk::readlane_d(xq, p);  // p uniform: a scalar broadcast, no LDS trip
             xq -= sg * uc[p] * xp;
           }
         }
@@ -705,7 +746,7 @@ __device__ __forceinline__ void lu_solve_blk(const double *__restrict__ LU, int 
         double xq = hl < bs ? x[b0 + hl] : 0.0;
 #pragma unroll
         for (int p = TB - 1; p >= 0; --p) {
-          const double xp = __shfl(xq, p, 64);
+          const double xp = ttk::readlane_d(xq, p);  // p uniform: a scalar broadcast, no LDS trip
           xq -= sg * lc[p] * xp;
         }
         if (half == 0 && hl < bs) x[b0 + hl] = xq;
@@ -884,6 +925,10 @@ __global__ __launch_bounds__(1024) void lu_solve_cols_kernel(const double *__res
 namespace ttk {
 
 // TTK_LU_REG_PANEL=0: the panels on the LDS / global-memory kernels (bit-identical; diagnostics)
+// TTK_LU_SWAP_U12=0: the row swaps and the U12 solve as two launches (bit-identical; diagnostics)
+static const int g_lu_swap_u12 = getenv("TTK_LU_SWAP_U12") ? atoi(getenv("TTK_LU_SWAP_U12")) : 1;
+// TTK_LU_PANEL_NARROW=0: the LDS panel kernel always at 1024 threads (bit-identical; diagnostics)
+static const int g_lu_panel_narrow = getenv("TTK_LU_PANEL_NARROW") ? atoi(getenv("TTK_LU_PANEL_NARROW")) : 1;
 static const int g_lu_reg_panel = getenv("TTK_LU_REG_PANEL") ? atoi(getenv("TTK_LU_REG_PANEL")) : 1;
 
 int lu_blocked(hipStream_t st, double *A, int n, int *piv, double *work, int *status, double *rcond, int want_rcond) {
@@ -910,14 +955,21 @@ int lu_blocked(hipStream_t st, double *A, int n, int *piv, double *work, int *st
       if (pshm > 65536)
         (void)hipFuncSetAttribute(reinterpret_cast<const void *>(getf2_panel_lds_kernel),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)pshm);
-      hipLaunchKernelGGL(getf2_panel_lds_kernel, dim3(1), dim3(1024), pshm, st, A, n, k0, kb, piv, status);
+      const int ntp = g_lu_panel_narrow ? ((n - k0 + 63) / 64 * 64 < 1024 ? (n - k0 + 63) / 64 * 64 : 1024) : 1024;
+      hipLaunchKernelGGL(getf2_panel_lds_kernel, dim3(1), dim3(ntp), pshm, st, A, n, k0, kb, piv, status);
     } else {
       hipLaunchKernelGGL(getf2_panel_kernel, dim3(1), dim3(1024), 0, st, A, n, k0, kb, piv, status);
     }
-    hipLaunchKernelGGL(laswp_kernel, dim3((n + 255) / 256), dim3(256), 0, st, A, n, k0, kb, piv);
     const int rest = n - k0 - kb;
+    if (g_lu_swap_u12) {
+      if (n - kb > 0)
+        hipLaunchKernelGGL(lu_swap_u12_kernel, dim3((n - kb + 255) / 256), dim3(256), 0, st, A, n, k0, kb, piv);
+    } else {
+      hipLaunchKernelGGL(laswp_kernel, dim3((n + 255) / 256), dim3(256), 0, st, A, n, k0, kb, piv);
+      if (rest > 0)
+        hipLaunchKernelGGL(lu_u12_kernel, dim3((rest + 255) / 256), dim3(256), 0, st, A, n, k0, kb);
+    }
     if (rest > 0) {
-      hipLaunchKernelGGL(lu_u12_kernel, dim3((rest + 255) / 256), dim3(256), 0, st, A, n, k0, kb);
       dim3 grid((rest + GT - 1) / GT, (rest + GT - 1) / GT);
       hipLaunchKernelGGL((gemm_strided_kernel<false, false>), grid, dim3(256), 0, st,
                          A + (int64_t)(k0 + kb) * n + k0, n, A + (int64_t)k0 * n + k0 + kb, n,
