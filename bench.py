@@ -20,7 +20,12 @@
   libttk context (an 8-GPU node runs 16 solve processes).  The bench processes get 8 HIP hardware
   queues (`GPU_MAX_HW_QUEUES`, recorded in `env_knobs`).  All slots warm up, then are released
   together at the start of the timed region.  A step is P solves per GPU: step i, rank p, slot j
-  solves seeds[(i*N*P + p*P + j) mod S].
+  solves seeds[(i*N*P + p*P + j) mod S] (`--balance static`, the default).  With K a multiple of the
+  seed count every slot solves every seed equally often at any N (maxcut_10, K = 5: slot loads equal),
+  which FIFO claiming cannot beat: `--balance dynamic` (the rank's K x P solves in that order go to
+  whichever slot is free next through one shared counter, `_claim`) measured 0.114 against static's
+  0.108 s/IPM-iter at K = 5 (its last claims are long seeds), and helps only when K leaves the
+  columns unequal.
 * Timed region: barrier + device sync on both sides of the K steps, max over ranks.
   `value` = (max-over-ranks wall) / (IPM iterations of all ranks): whole-job s per IPM-iteration.
 * `sec_per_iter_per_seed_median`: SURVEY.md §8(d)'s statistic as the reference runner measures it
@@ -149,6 +154,23 @@ def _cpu_worker(problem, cfg_path, seed, rank_tt, cap):
     print(json.dumps(out), flush=True)
 
 
+def _claim(path):
+    """Next index of a rank's work list: a counter in the file `path`, incremented under an exclusive
+    flock (shared by the rank's processes and slot threads; a claim costs tens of microseconds)."""
+    import fcntl
+    with open(path, "r+") as f:
+        fcntl.flock(f, fcntl.LOCK_EX)
+        try:
+            n = int(f.read().strip() or 0)
+            f.seek(0)
+            f.write(str(n + 1))
+            f.truncate()
+            f.flush()
+        finally:
+            fcntl.flock(f, fcntl.LOCK_UN)
+    return n
+
+
 class _Slots:
     """The solves in flight of one process: one host thread per slot, each with its own HIP stream,
     libttk context (`dev`'s per-thread state) and NumPy random stream (`ttipm_amd.rng`).  Every slot
@@ -156,11 +178,16 @@ class _Slots:
     seeds back to back and records its wall time (its own stream synchronised).  The launches
     themselves release the GIL, so the slots' host work overlaps while their kernels run."""
 
-    def __init__(self, slot_seeds, packed, solve, warmup, device):
+    def __init__(self, slot_seeds, packed, solve, warmup, device, queue=None):
+        """queue: None -- slot j solves slot_seeds[j] back to back (static); or (work, path) -- every
+        slot claims the next index of the rank's ordered work list from the cross-process counter
+        file `path` (`_claim`) until the list is exhausted (slot_seeds[j][0] is still its warm-up
+        seed)."""
         import threading
         if len(slot_seeds) > 1:  # a slot waiting for the GIL asks for it after 0.5 ms, not 5 ms
             sys.setswitchinterval(SLOT_SWITCH_INTERVAL)
         self.n = len(slot_seeds)
+        self.queue = queue
         self.ready = threading.Barrier(self.n + 1)
         self.go = threading.Event()
         self.out = [None] * self.n
@@ -184,7 +211,10 @@ class _Slots:
             rng.private()
             for _ in range(warmup):  # untimed: plans, this context's scratch, allocator, code pages
                 solve(shard.unpack(*packed[seeds[0]]))
-            preps = [shard.unpack(*packed[sd]) for sd in seeds]
+            # every problem this slot may solve, unpacked before the timed region (a dynamic slot may
+            # claim any entry of the work list: one fresh copy per entry)
+            work = seeds if self.queue is None else self.queue[0]
+            preps = [shard.unpack(*packed[sd]) for sd in work]
             if device is not None:
                 torch.cuda.current_stream().synchronize()
         except BaseException as e:  # noqa: BLE001 - re-raised by join()
@@ -194,9 +224,20 @@ class _Slots:
         if preps is None:
             return
         try:
-            traces = [[] for _ in seeds]
+            traces, res = [], []
             t0 = time.perf_counter()
-            res = [solve(pr, trace=tr) for pr, tr in zip(preps, traces)]
+            if self.queue is None:
+                for pr in preps:
+                    traces.append([])
+                    res.append(solve(pr, trace=traces[-1]))
+            else:
+                while True:
+                    idx = _claim(self.queue[1])
+                    if idx >= len(preps):
+                        break
+                    traces.append([])
+                    res.append(solve(preps[idx], trace=traces[-1]))
+                    preps[idx] = None  # solved: let the allocator reuse its cores
             if device is not None:
                 torch.cuda.current_stream().synchronize()
             elapsed = time.perf_counter() - t0
@@ -222,7 +263,7 @@ class _Slots:
         return [o[0] for o in self.out], [r for o in self.out for r in o[1]]
 
 
-def _gpu_worker(args, slot_seeds):
+def _gpu_worker(args, slot_seeds, queue=None):
     """Child process (more solves in flight on this rank's GPU): create its seeds' problems, start
     one slot thread per seed list (`_Slots`), print 'ready' once all have warmed up, wait for 'go'
     on stdin, run the solves, print one JSON line with the slots' elapsed wall times and the
@@ -237,13 +278,13 @@ def _gpu_worker(args, slot_seeds):
     config = yaml.safe_load(open(args.config))
     keep = ("seed", "num_iters", "runtime", "sec_per_iter", "gap", "feas", "dual_feas", "assembly_t")
     with contextlib.redirect_stdout(sys.stderr):  # once, around all slot threads (not thread-safe)
-        packed = {s: shard.pack(create(args.problem, config, s, args.rank, verbose=False))
-                  for sl in slot_seeds for s in sl}
+        need = [s for sl in slot_seeds for s in sl] + (list(queue[0]) if queue else [])
+        packed = {s: shard.pack(create(args.problem, config, s, args.rank, verbose=False)) for s in dict.fromkeys(need)}
 
         def solve(prep, trace=None):
             return _solve(prep, config, quiet=True, verbose=False, trace=trace)
 
-        slots = _Slots(slot_seeds, packed, solve, args.warmup, dev)
+        slots = _Slots(slot_seeds, packed, solve, args.warmup, dev, queue=queue)
         slots.wait_ready()
         print("ready", file=sys.__stdout__, flush=True)
         if sys.stdin.readline().strip() != "go":  # EOF: the parent is gone -- do not run as an orphan
@@ -253,15 +294,18 @@ def _gpu_worker(args, slot_seeds):
     print(json.dumps({"elapsed": elapsed, "results": [{k: r.get(k) for k in keep} for r in results]}), flush=True)
 
 
-def _spawn_gpu_workers(args, proc_slots):
+def _spawn_gpu_workers(args, proc_slots, queue=None):
     """Started BEFORE this process initialises the GPU; each prints 'ready' once warmed up.
-    proc_slots: per worker process, its slots' seed lists."""
+    proc_slots: per worker process, its slots' seed lists; queue: (work list, counter file) of the
+    dynamic schedule, or None."""
     procs = []
     for slots in proc_slots:
         cmd = [sys.executable, os.path.abspath(__file__), "--gpu-worker",
                ";".join(",".join(map(str, sl)) for sl in slots),
                "--problem", args.problem, "--config", args.config, "--rank", str(args.rank),
                "--warmup", str(args.warmup)]
+        if queue is not None:
+            cmd += ["--queue-work", ",".join(map(str, queue[0])), "--queue-file", queue[1]]
         procs.append(subprocess.Popen(cmd, stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=sys.stderr,
                                       text=True))
     _CHILDREN.extend(procs)
@@ -416,7 +460,7 @@ LINE_MAX = 4000  # the driver keeps a ~14.8 KB tail of stdout; the line stays fa
 
 
 def compose_line(problem, config, cfg_name, rank_tt, world, P, T, n_procs, steps, warmup, schedule, elapsed, iters,
-                 seeds, sched, all_results, solo, roofline, cpu, detail_path):
+                 seeds, sched, all_results, solo, roofline, cpu, detail_path, balance="static"):
     """(the ONE stdout JSON line, the detail dict for the side file).  The line holds the contract's
     keys plus the summary statistics and stays below LINE_MAX bytes at any N; everything per seed /
     per step / per op goes to the detail file."""
@@ -444,7 +488,7 @@ def compose_line(problem, config, cfg_name, rank_tt, world, P, T, n_procs, steps
             "data": "synthetic: the reference's generators (seeded MT19937 graph TT), problems broadcast from rank 0",
             "config": {"workload": f"{problem} dim={config['dim']} rank={rank_tt} ({cfg_name}), {P} concurrent "
                                    f"tt_ipm solves per GPU per step ({n_procs} processes x {T} slot threads)",
-                       "inflight_per_gpu": P, "seeds": seeds,
+                       "inflight_per_gpu": P, "seeds": seeds, "balance": balance,
                        "parallelism": f"seed-parallel x{world} GPUs x{P} in flight ({schedule})",
                        "solves": len(all_results), "total_ipm_iters": iters},
             # SURVEY.md section 8(d)'s statistic: each seed alone on the GPU, median over seeds
@@ -487,6 +531,11 @@ def main():
                     help=f"solves in flight per process (host threads; default {DEFAULT_THREADS})")
     ap.add_argument("--inflight", type=int, default=None,
                     help="solves in flight per GPU (default: default_inflight())")
+    ap.add_argument("--balance", choices=("dynamic", "static"), default="static",
+                    help="static (default): slot j solves its schedule column; dynamic: the rank's slots claim "
+                         "its solves one at a time from a shared counter, in schedule order")
+    ap.add_argument("--queue-work", default=None, help=argparse.SUPPRESS)
+    ap.add_argument("--queue-file", default=None, help=argparse.SUPPRESS)
     ap.add_argument("--cpu-worker", type=int, default=None, help=argparse.SUPPRESS)
     ap.add_argument("--gpu-worker", default=None, help=argparse.SUPPRESS)
     args = ap.parse_args()
@@ -496,7 +545,10 @@ def main():
     if args.cpu_worker is not None:
         return _cpu_worker(args.problem, args.config, args.cpu_worker, args.rank, args.cpu_cap)
     if args.gpu_worker is not None:
-        return _gpu_worker(args, [[int(x) for x in sl.split(",")] for sl in args.gpu_worker.split(";")])
+        q = None
+        if args.queue_file:
+            q = ([int(x) for x in args.queue_work.split(",")], args.queue_file)
+        return _gpu_worker(args, [[int(x) for x in sl.split(",")] for sl in args.gpu_worker.split(";")], q)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -519,8 +571,16 @@ def main():
     if _profiled():
         T = 1
     proc_slots = [slot_seeds[i:i + T] for i in range(0, P, T)]  # this process: proc_slots[0]
-    mine_seeds = slot_seeds[0]
-    gpu_procs = _spawn_gpu_workers(args, proc_slots[1:])  # before any GPU call
+    queue = None
+    if args.balance == "dynamic":
+        # the rank's K x P solves in schedule order (step by step, slot by slot), claimed one at a time
+        import tempfile
+        work = [sched[i][rank * P + j] for i in range(args.steps) for j in range(P)]
+        fd, qpath = tempfile.mkstemp(prefix=f"ttipm_bench_r{rank}_", suffix=".q")
+        os.write(fd, b"0")
+        os.close(fd)
+        queue = (work, qpath)
+    gpu_procs = _spawn_gpu_workers(args, proc_slots[1:], queue)  # before any GPU call
 
     cpu_seeds = list(dict.fromkeys(s for sl in slot_seeds for s in sl))  # the distinct seeds this (only) rank times
     cpu_procs, allcore_proc = [], []
@@ -571,7 +631,7 @@ def main():
 
     with contextlib.redirect_stdout(sys.stderr):
         sync()
-        slots = _Slots(proc_slots[0], packed, solve_quiet, args.warmup, dev_idx)
+        slots = _Slots(proc_slots[0], packed, solve_quiet, args.warmup, dev_idx, queue=queue)
         slots.wait_ready()
     for p in gpu_procs:  # every worker warmed up and waiting
         line = p.stdout.readline()
@@ -599,6 +659,8 @@ def main():
     sync()
     barrier()
     elapsed = time.perf_counter() - t0
+    if queue is not None:
+        os.unlink(queue[1])
     slot_elapsed = slot_elapsed + [e for w in worker_out for e in w["elapsed"]]
     results = results + [r for w in worker_out for r in w["results"]]
     iters = sum(r["num_iters"] for r in results)
@@ -675,7 +737,8 @@ def main():
             problem=args.problem, config=config, cfg_name=os.path.basename(args.config), rank_tt=args.rank,
             world=world, P=P, T=T, n_procs=len(proc_slots), steps=args.steps, warmup=args.warmup,
             schedule=args.schedule, elapsed=elapsed, iters=iters, seeds=seeds, sched=sched,
-            all_results=all_results, solo=solo, roofline=roofline, cpu=cpu, detail_path=args.detail)
+            all_results=all_results, solo=solo, roofline=roofline, cpu=cpu, detail_path=args.detail,
+            balance=args.balance)
         if args.detail:
             os.makedirs(os.path.dirname(os.path.abspath(args.detail)), exist_ok=True)
             with open(args.detail, "w") as f:

@@ -116,3 +116,43 @@ def test_bench_line_fits_the_driver_tail():
     assert {"value", "unit", "cores", "kind", "sample"} <= set(line["cpu_baseline"])
     assert len(detail["per_seed"]) == len(results) and detail["seeds_per_step"] == sched
     assert line["cpu_baseline"]["gpu_over_cpu_median_of_ratios"] is not None
+
+
+def _claim_many(path, n, out):
+    got = []
+    while True:
+        i = bench._claim(path)
+        if i >= n:
+            break
+        got.append(i)
+    out.extend(got)
+
+
+def _claim_proc(path, n, q):
+    got = []
+    _claim_many(path, n, got)
+    q.put(got)
+
+
+def test_dynamic_balance_claims_every_solve_once(tmp_path):
+    """`--balance dynamic`: the rank's processes and slot threads claim its work list through one
+    counter file; every index is handed out exactly once, whoever asks."""
+    import multiprocessing as mp
+    import threading
+    n = 200
+    path = tmp_path / "q"
+    path.write_text("0")
+    q = mp.get_context("spawn").Queue()
+    procs = [mp.get_context("spawn").Process(target=_claim_proc, args=(str(path), n, q)) for _ in range(2)]
+    for p in procs:
+        p.start()
+    outs = [[] for _ in range(3)]
+    ths = [threading.Thread(target=_claim_many, args=(str(path), n, outs[k])) for k in range(3)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    got = [i for o in outs for i in o] + [i for _ in procs for i in q.get(timeout=60)]
+    for p in procs:
+        p.join(timeout=60)
+    assert sorted(got) == list(range(n))
