@@ -1,0 +1,56 @@
+"""Aggregate kernel-dispatch rate of P processes (one stream each) launching tiny kernels back to
+back (ttk_fill of one double): is the GPU's dispatch rate what bounds several solves in flight?
+    python tools/launch_rate.py [launches_per_process] [P ...]"""
+import os
+import subprocess
+import sys
+import time
+
+
+def worker(n):
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import torch
+    from ttipm_amd import dev as D
+    from ttipm_amd._lib import lib
+    z = D.empty(1)
+    st = D._stream()
+    for _ in range(200):
+        lib.ttk_fill(st, D._p(z), 1, 0.0)
+    torch.cuda.synchronize()
+    print("ready", flush=True)
+    sys.stdin.readline()
+    t0 = time.perf_counter()
+    for _ in range(n):
+        lib.ttk_fill(st, D._p(z), 1, 0.0)
+    t1 = time.perf_counter()
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    print(f"{t1 - t0} {t2 - t0}", flush=True)
+
+
+def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "--worker":
+        return worker(int(sys.argv[2]))
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 20000
+    for P in [int(p) for p in (sys.argv[2:] or ["1", "2", "4", "8"])]:
+        env = dict(os.environ, GPU_MAX_HW_QUEUES="8")
+        ps = [subprocess.Popen([sys.executable, __file__, "--worker", str(n)], stdin=subprocess.PIPE,
+                               stdout=subprocess.PIPE, text=True, env=env) for _ in range(P)]
+        for p in ps:
+            while p.stdout.readline().strip() != "ready":
+                pass
+        t0 = time.perf_counter()
+        for p in ps:
+            p.stdin.write("go\n")
+            p.stdin.flush()
+        outs = [p.stdout.readline().split() for p in ps]
+        wall = time.perf_counter() - t0
+        for p in ps:
+            p.wait()
+        host = max(float(o[0]) for o in outs)
+        print(f"P={P}: {P * n} launches in {wall:.3f} s -> {P * n / wall / 1e3:.0f} k launches/s "
+              f"(per process {n / wall / 1e3:.0f} k/s; host enqueue {n / host / 1e3:.0f} k/s)", flush=True)
+
+
+if __name__ == "__main__":
+    main()
