@@ -16,8 +16,9 @@
 * Solves in flight per GPU (`--inflight P`, default 4 at every N, so the 1/2/4/8-GPU series is
   like-for-like): a solve is a chain of small dependent launches that leaves most of the chip idle,
   so each GPU runs P seeds at once: P/T processes (this one plus workers spawned before the GPU is
-  touched) of T = `--threads` (default 2) slot threads, each slot on its own created stream and
-  libttk context (an 8-GPU node runs 16 solve processes).  The bench processes get 8 HIP hardware
+  touched) of T = `--threads` slot threads (default `default_threads`: 1 -- one solve per process,
+  on its default stream, with its own GIL -- up to N = 4; 2 at N = 8, where 16 solve processes is the
+  node's limit), a process's several slots each on its own created stream and libttk context.  The bench processes get 8 HIP hardware
   queues (`GPU_MAX_HW_QUEUES`, recorded in `env_knobs`).  All slots warm up, then are released
   together at the start of the timed region.  A step is P solves per GPU: step i, rank p, slot j
   solves seeds[(i*N*P + p*P + j) mod S] (`--balance static`, the default).  With K a multiple of the
@@ -374,22 +375,32 @@ def _pmc_traffic():
     return None
 
 
-DEFAULT_THREADS = 2  # solves in flight per process (slot threads, one created HIP stream each)
 DEFAULT_INFLIGHT = 4  # solves in flight per GPU, the same at every N (like-for-like 1->8 series)
+NODE_PROCESSES = 16  # solve processes a node may run on its GPUs at once (the box's process guard)
 SLOT_SWITCH_INTERVAL = 0.0005  # sys.setswitchinterval for processes with several slot threads
 HW_QUEUES = 8  # GPU_MAX_HW_QUEUES for the bench processes (HIP's default is 4)
 
 
+def default_threads(world, P):
+    """Slot threads per process: 1 (every solve its own process, default stream, own GIL) while the
+    node's solve processes stay within NODE_PROCESSES (N <= 4 at 4 in flight), else the fewest that
+    fit (N = 8: 2).  One box, maxcut_10, 4 in flight, alternating runs: 4 processes x 1 slot 0.092 /
+    0.093 s/IPM-iter, 2 processes x 2 slots 0.107 / 0.109 (two slots of one process share its GIL;
+    profiles/r05_inflight_layouts.txt)."""
+    procs_per_gpu = max(1, NODE_PROCESSES // max(world, 1))
+    return max(1, -(-P // procs_per_gpu))
+
+
 def default_inflight(world):
     """Solves in flight per GPU: DEFAULT_INFLIGHT at every N up to 8, so the 1/2/4/8-GPU series
-    carries the same per-GPU load: 2 processes per GPU x DEFAULT_THREADS slot threads each (an 8-GPU
-    node then runs 16 solve processes, the process guard's limit).  Why threads work since round 4:
+    carries the same per-GPU load (default_threads splits it over processes within the node's
+    NODE_PROCESSES solve processes).  Why threads work since round 4:
     the launch-only library calls keep the GIL (`_lib.py`), a slot waiting for the GIL asks for it
     after 0.5 ms, and each process gets 8 HIP hardware queues -- with HIP's default 4, a process's
     two slot streams plus their libttk side streams share queues and two such processes slowed each
     other down (maxcut_10, whole job: 2 processes x 1 slot 0.190, 2 x 2 slots 0.209 with 4 queues,
     0.117-0.131 with 8 or 16; 2 x 3: 0.155, 2 x 4: 0.128; profiles/r04_inflight_layouts.txt)."""
-    return max(1, min(DEFAULT_INFLIGHT, DEFAULT_THREADS * (16 // max(world, 1))))
+    return max(1, min(DEFAULT_INFLIGHT, 2 * (NODE_PROCESSES // max(world, 1))))
 
 
 def make_schedule(config, cfg_name, seeds_arg, steps, world, rank, P, mode):
@@ -528,7 +539,7 @@ def main():
     ap.add_argument("--no-solo", action="store_true", help="skip the one-solve-at-a-time latency pass")
     ap.add_argument("--schedule", choices=("shard", "replica"), default="shard")
     ap.add_argument("--threads", type=int, default=None,
-                    help=f"solves in flight per process (host threads; default {DEFAULT_THREADS})")
+                    help="solves in flight per process (host threads; default: default_threads())")
     ap.add_argument("--inflight", type=int, default=None,
                     help="solves in flight per GPU (default: default_inflight())")
     ap.add_argument("--balance", choices=("dynamic", "static"), default="static",
@@ -567,7 +578,7 @@ def main():
                                              rank, P, args.schedule)
     step_seeds = [s for st in sched for s in st]
     per_step = world * P
-    T = max(1, min(args.threads or DEFAULT_THREADS, P))
+    T = max(1, min(args.threads or default_threads(world, P), P))
     if _profiled():
         T = 1
     proc_slots = [slot_seeds[i:i + T] for i in range(0, P, T)]  # this process: proc_slots[0]

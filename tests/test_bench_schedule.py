@@ -68,11 +68,15 @@ def test_replica_schedule():
 
 def test_default_inflight_is_constant_across_gpus():
     """The same solves in flight per GPU at N = 1, 2, 4, 8 (a like-for-like 1->8 series), and a node
-    never runs more than 16 solve processes (DEFAULT_THREADS slot threads per process)."""
+    never runs more than 16 solve processes (default_threads slot threads per process; one slot per
+    process wherever that fits)."""
     ps = [bench.default_inflight(w) for w in (1, 2, 4, 8)]
     assert len(set(ps)) == 1 and ps[0] >= 1
-    T = bench.DEFAULT_THREADS
-    assert all(w * -(-bench.default_inflight(w) // T) <= 16 for w in (1, 2, 4, 8, 16))
+    for w in (1, 2, 4, 8, 16):
+        P = bench.default_inflight(w)
+        T = bench.default_threads(w, P)
+        assert w * -(-P // T) <= 16
+        assert T == 1 or w * P > 16
 
 
 def _fake_results(sched, rank_count):
