@@ -551,6 +551,7 @@ __global__ __launch_bounds__(1024) void svd_wg_kernel(const double *__restrict__
     }
   }
   __syncthreads();
+  TTK_PHASE(6)
   for (int j = tid; j < p; j += nt) S[rank[j]] = sig[j];
   if (use_qr) {
     // left factor of W: M(:, rank[j]) = Q [V(:, j); 0]; g2 lanes per column, each column runs
@@ -578,7 +579,7 @@ __global__ __launch_bounds__(1024) void svd_wg_kernel(const double *__restrict__
     }
   }
   __syncthreads();
-  TTK_PHASE(6)
+  TTK_PHASE(7)
   // ---- outputs
   if (use_qr) {  // left = M (q x p), right(perm[i], rank[j]) = X(i, j)
     for (int e = tid; e < q * p; e += nt) {
@@ -616,9 +617,8 @@ __global__ __launch_bounds__(1024) void svd_wg_kernel(const double *__restrict__
         U[(int64_t)i * p + rank[j]] = v;
     }
   }
-  if (timing) {
+  if (timing) {  // (the output copies are not a phase of their own: a few us)
     __syncthreads();
-    TTK_PHASE(7)
     if (tid == 0) {
       atomicAdd(&g_dbg[0], 1ull);
       atomicAdd(&g_dbg[2], clock64() - t_c0);

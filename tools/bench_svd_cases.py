@@ -32,5 +32,5 @@ for f in sorted(glob.glob(sys.argv[1] if len(sys.argv) > 1 else ".svd_cases/*.np
           f"orthU {np.abs(U.T @ U - np.eye(U.shape[1])).max():.2e}", flush=True)
     lib.ttk_debug_counters(buf, 1)
     if buf[0]:
-        print(f"     phases us (qrcp, jacobi, vectors, out): {[round(buf[k] / 100.0, 1) for k in (4, 5, 6, 7)]} "
+        print(f"     phases us (qrcp, jacobi, post-jacobi, vectors): {[round(buf[k] / 100.0, 1) for k in (4, 5, 6, 7)]} "
               f"sweeps {buf[1]}  shader clock {buf[2] / max(buf[3], 1) * 0.1:.2f} GHz", flush=True)
