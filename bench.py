@@ -264,6 +264,20 @@ class _Slots:
         return [o[0] for o in self.out], [r for o in self.out for r in o[1]]
 
 
+def _hip_schedule():
+    """TTIPM_HIP_SCHED = spin | yield | blocking: hipSetDeviceFlags(hipDeviceSchedule*) before this
+    process's HIP context exists (how host threads wait in hipStreamSynchronize: a spinning wait holds
+    a core, a blocking one sleeps on an interrupt; diagnostics for solve processes that share the
+    box's cores).  Unset: HIP's default (auto)."""
+    mode = os.environ.get("TTIPM_HIP_SCHED")
+    if not mode:
+        return
+    flag = {"spin": 1, "yield": 2, "blocking": 4}[mode]
+    rc = ctypes.CDLL("libamdhip64.so").hipSetDeviceFlags(ctypes.c_uint(flag))
+    if rc != 0:
+        print(f"bench: hipSetDeviceFlags({mode}) returned {rc}", file=sys.stderr)
+
+
 def _gpu_worker(args, slot_seeds, queue=None):
     """Child process (more solves in flight on this rank's GPU): create its seeds' problems, start
     one slot thread per seed list (`_Slots`), print 'ready' once all have warmed up, wait for 'go'
@@ -272,6 +286,7 @@ def _gpu_worker(args, slot_seeds, queue=None):
     import torch
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dev = local % torch.cuda.device_count()
+    _hip_schedule()
     torch.cuda.set_device(dev)
     from ttipm_amd import shard
     from ttipm_amd.utils import create
@@ -608,6 +623,7 @@ def main():
 
     import torch
     import torch.distributed as dist
+    _hip_schedule()
     if torch.cuda.is_available():
         # one process per GPU; more ranks than GPUs only in rehearsals (TTIPM_BENCH_BACKEND=gloo)
         torch.cuda.set_device(local % torch.cuda.device_count())
