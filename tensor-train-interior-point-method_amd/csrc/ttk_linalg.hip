@@ -704,12 +704,16 @@ __global__ __launch_bounds__(1024) void qr_kernel(const double *__restrict__ A, 
     Qc[e] = (i == c) ? 1.0 : 0.0;
   }
   __syncthreads();
-  for (int j = k - 1; j >= 0; --j) {
-    const double tj = tau[j];
-    if (tj == 0.0) continue;
-    const double *v = W + (int64_t)j * m;
-    for (int c = j + wid; c < k; c += nw) {
-      double *qc = Qc + (int64_t)c * m;
+  // column c of Q only ever meets the reflectors j <= c, in the order j = c, c-1, ..., 0 -- so each
+  // wave takes whole columns through all their reflectors with no block barrier between reflectors
+  // (the per-column operations and their order are the reflector-by-reflector loop's: bit-identical;
+  // one wave's LDS / global accesses stay in program order behind the workgroup fence)
+  for (int c = wid; c < k; c += nw) {
+    double *qc = Qc + (int64_t)c * m;
+    for (int j = c; j >= 0; --j) {
+      const double tj = tau[j];
+      if (tj == 0.0) continue;
+      const double *v = W + (int64_t)j * m;
       double d = ttk::chain_ahead<CU>(
           ttk::steps_below(j + 1 + lane, m, 64), [&](int q) { return v[j + 1 + lane + 64 * q]; },
           [&](int q) { return qc[j + 1 + lane + 64 * q]; }, (lane == 0) ? qc[j] : 0.0);
@@ -717,9 +721,10 @@ __global__ __launch_bounds__(1024) void qr_kernel(const double *__restrict__ A, 
       if (lane == 0) qc[j] -= d;
       #pragma unroll 8
       for (int i = j + 1 + lane; i < m; i += 64) qc[i] -= d * v[i];
+      __threadfence_block();
     }
-    __syncthreads();
   }
+  __syncthreads();
   for (int64_t e = tid; e < (int64_t)m * k; e += nt) {
     const int i = (int)(e / k), c = (int)(e % k);
     Q[e] = Qc[(int64_t)c * m + i];
