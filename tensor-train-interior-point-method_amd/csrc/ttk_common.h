@@ -106,6 +106,15 @@ __device__ __forceinline__ void staged_copy(int total, int tid, int nt, LD ld, S
     }
   }
 }
+// y[i] -= w * x[i] for i = i0, i0 + step, ... < end, y and x never overlapping (different columns of
+// one working array): said so, the x / y loads of later elements issue ahead of the earlier stores
+// (with possible aliasing every element waited one LDS / L2 round trip for its predecessor's store).
+// The same operation per element: bit-identical.
+__device__ __forceinline__ void axpy_sub_strided(double *__restrict__ y, const double *__restrict__ x, double w,
+                                                 int i0, int end, int step) {
+#pragma unroll 8
+  for (int i = i0; i < end; i += step) y[i] -= w * x[i];
+}
 // number of k with start + k * step < end (start < end not required)
 __device__ __forceinline__ int steps_below(int start, int end, int step) {
   return start < end ? (end - start + step - 1) / step : 0;

@@ -440,8 +440,7 @@ __global__ __launch_bounds__(1024) void svd_wg_kernel(const double *__restrict__
               ttk::steps_below(c + 1 + gl2, q, g2), [&](int k) { return x[c + 1 + gl2 + g2 * k]; },
               [&](int k) { return y[c + 1 + gl2 + g2 * k]; }, 0.0);
           const double w = t * (ttk::group_sum_rt(acc, g2) + yc);
-          #pragma unroll 8
-          for (int i = c + 1 + gl2; i < q; i += g2) y[i] -= w * x[i];
+          ttk::axpy_sub_strided(y, x, w, c + 1 + gl2, q, g2);
           yc -= w;
           if (gl2 == 0) y[c] = yc;
         }
@@ -570,8 +569,7 @@ __global__ __launch_bounds__(1024) void svd_wg_kernel(const double *__restrict__
             ttk::steps_below(c + 1 + gl2, q, g2), [&](int k) { return v[c + 1 + gl2 + g2 * k]; },
             [&](int k) { return mc[c + 1 + gl2 + g2 * k]; }, 0.0);
         const double w = t * (ttk::group_sum_rt(acc, g2) + mc[c]);
-        #pragma unroll 8
-        for (int i = c + 1 + gl2; i < q; i += g2) mc[i] -= w * v[i];
+        ttk::axpy_sub_strided(mc, v, w, c + 1 + gl2, q, g2);
         __threadfence_block();
         if (gl2 == 0) mc[c] -= w;
         __threadfence_block();
@@ -687,8 +685,7 @@ __global__ __launch_bounds__(1024) void qr_kernel(const double *__restrict__ A, 
             [&](int q) { return wc[j + 1 + lane + 64 * q]; }, (lane == 0) ? wc[j] : 0.0);
         d = ttk::wave_sum(d) * tj;
         if (lane == 0) wc[j] -= d;
-        #pragma unroll 8
-        for (int i = j + 1 + lane; i < m; i += 64) wc[i] -= d * wj[i];
+        ttk::axpy_sub_strided(wc, wj, d, j + 1 + lane, m, 64);
       }
     }
     __syncthreads();
@@ -719,8 +716,7 @@ __global__ __launch_bounds__(1024) void qr_kernel(const double *__restrict__ A, 
           [&](int q) { return qc[j + 1 + lane + 64 * q]; }, (lane == 0) ? qc[j] : 0.0);
       d = ttk::wave_sum(d) * tj;
       if (lane == 0) qc[j] -= d;
-      #pragma unroll 8
-      for (int i = j + 1 + lane; i < m; i += 64) qc[i] -= d * v[i];
+      ttk::axpy_sub_strided(qc, v, d, j + 1 + lane, m, 64);
       __threadfence_block();
     }
   }
@@ -2031,8 +2027,7 @@ __global__ __launch_bounds__(1024) void qrb_panel_kernel(double *W, int m, int l
       #pragma unroll 8
       for (int i = c + 1 + lane; i < m; i += 64) acc += x[i] * y[i];
       const double w = t * (ttk::wave_sum(acc) + y[c]);
-      #pragma unroll 8
-      for (int i = c + 1 + lane; i < m; i += 64) y[i] -= w * x[i];
+      ttk::axpy_sub_strided(y, x, w, c + 1 + lane, m, 64);
       if (lane == 0) y[c] -= w;
     }
     // T(0:jj, jj) = -t T(0:jj, 0:jj) (Y(:, 0:jj)^T v)
@@ -2319,8 +2314,7 @@ __global__ __launch_bounds__(256) void qrcp_update_kernel(double *__restrict__ W
     #pragma unroll 8
     for (int i = c + 1 + lane; i < m; i += 64) acc += v[i] * y[i];
     const double w = t * (ttk::wave_sum(acc) + yc);
-    #pragma unroll 8
-    for (int i = c + 1 + lane; i < m; i += 64) y[i] -= w * v[i];
+    ttk::axpy_sub_strided(y, v, w, c + 1 + lane, m, 64);
     yc -= w;
     if (lane == 0) y[c] = yc;
   }
