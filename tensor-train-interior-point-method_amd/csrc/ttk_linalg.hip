@@ -349,7 +349,11 @@ __global__ __launch_bounds__(1024) void svd_wg_kernel(const double *__restrict__
   const int gl2 = tid & (g2 - 1), gid2 = tid / g2, ng2 = nt / g2;
   double *X = lds, *V = X + ldx * p, *tau = V + ldv * p, *vn1 = tau + p, *vn2 = vn1 + p, *sig = vn2 + p;
   int *perm = reinterpret_cast<int *>(sig + p), *rank = perm + p;
-  double *W = use_qr ? (WL ? reinterpret_cast<double *>(rank + p + (p & 1)) : gwork) : X;
+  // W right after the 2p ints of perm / rank: 8-byte aligned for any p (an extra int for odd p, as
+  // before round 5, put every double of W and M on a 4-byte boundary -- each ds_read/write_b64 then
+  // took the misaligned path: QRCP's trailing update and the left-vector pass ran 3-6x slower per
+  // element for odd p, SQ_LDS_IDX_ACTIVE 1.8M vs 0.34M cycles at 64 x 63 vs 144 x 48)
+  double *W = use_qr ? (WL ? reinterpret_cast<double *>(rank + p) : gwork) : X;
   // W / M column stride: odd, so the g2-lane groups of one wave (consecutive columns) start on
   // different LDS banks (an even q put every group of a wave on the same banks)
   const int lq = q | 1;
