@@ -315,15 +315,17 @@ __device__ __forceinline__ void jacobi_round(double *X, int ldx, double *V, int 
   }
 }
 
-// WL: W (and M) in LDS (w_in_lds), known at compile time so that their accesses are LDS
+// WM: where the QRCP working copy W and the left-vector buffer M live -- 2 both in LDS, 1 W in LDS and
+// M in global memory, 0 both global -- known at compile time so that their accesses are LDS
 // instructions, not flat ones (a flat access waits on both the LDS and the vector-memory counters)
-template <int G, bool WL>
+template <int G, int WM>
 __global__ __launch_bounds__(1024) void svd_wg_kernel(const double *__restrict__ A, int m, int n,
                                                       double *__restrict__ U, double *__restrict__ S,
                                                       double *__restrict__ Vt, double *__restrict__ gwork,
                                                       int w_in_lds, int use_qr, int timing) {
   extern __shared__ double lds[];
-  constexpr int SU = WL ? 8 : 4;  // loads ahead in the dot chains (W in global memory: fewer registers left)
+  constexpr bool WL = WM >= 1, ML = WM == 2;  // W in LDS; M in LDS too
+  constexpr int SU = ML ? 8 : 4;  // loads ahead in the dot chains (W or M in global memory: fewer registers left)
   __shared__ int s_piv, any_rot;
   __shared__ double red[16];
   const bool tall = m >= n;
@@ -339,7 +341,7 @@ __global__ __launch_bounds__(1024) void svd_wg_kernel(const double *__restrict__
     atomicAdd(&g_dbg[K], t1 - t_ph);                    \
     t_ph = t1;                                          \
   }
-  // LDS: X (ldx*p) | V (ldv*p) | tau, vn1, vn2, sig (4p) | perm, rank (2p ints) | [W, M if w_in_lds]
+  // LDS: X (ldx*p) | V (ldv*p) | tau, vn1, vn2, sig (4p) | perm, rank (2p ints) | [W (WM >= 1), M (WM == 2)]
   // odd leading dimensions: columns start on different LDS banks (even ones put every lane group
   // of a wave on the same banks)
   const int ldx = L | 1, ldv = p | 1;
@@ -358,7 +360,9 @@ __global__ __launch_bounds__(1024) void svd_wg_kernel(const double *__restrict__
   // different LDS banks (an even q put every group of a wave on the same banks)
   const int lq = q | 1;
   const int ldw = use_qr ? lq : ldx;
-  double *M = W + (int64_t)lq * p;
+  // M after W where both are in the same memory; WM = 1 (W fits LDS, W and M together do not): M is
+  // the global working buffer -- the QRCP then runs on LDS, only the left-vector pass on global memory
+  double *M = (ML || !WL) ? W + (int64_t)lq * p : gwork;
   for (int e = tid; e < q * p; e += nt) {
     const int j = e / q, i = e - j * q;
     W[(int64_t)j * ldw + i] = tall ? A[(int64_t)i * n + j] : A[(int64_t)j * n + i];
@@ -2677,8 +2681,10 @@ int ttk_svd_tol(void *stream, const double *A, int m, int n, double *U, double *
   const int L = use_qr ? p : q;
   const int64_t fixed = (int64_t)(L | 1) * p + (int64_t)(p | 1) * p + 5 * (int64_t)p + 2;  // X, V, vectors
   const int64_t wm = use_qr ? 2 * (int64_t)(q | 1) * p : 0;                    // W and M (odd stride)
-  const int w_in_lds = fixed + wm <= LDS_DOUBLES;
-  const size_t shm = (size_t)(fixed + (w_in_lds ? wm : 0)) * sizeof(double);
+  // W and M in LDS (2), W alone (1: M in the global working buffer), neither (0); mode 1 only for the
+  // instantiated lanes-per-pair counts (4, 8, 16: the p that overflow LDS with both)
+  int wmode = fixed + wm <= LDS_DOUBLES ? 2 : (use_qr && fixed + wm / 2 <= LDS_DOUBLES ? 1 : 0);
+  const int w_in_lds = wmode == 2;
 
   const int pairs = (p + 1) / 2;
   int g = 1;
@@ -2686,31 +2692,38 @@ int ttk_svd_tol(void *stream, const double *A, int m, int n, double *U, double *
   int nt = pairs * g;
   if (use_qr && q * p > 2048) nt = 1024;  // column-parallel QR phases want a full block
   nt = nt < 64 ? 64 : (nt > 1024 ? 1024 : (nt + 63) / 64 * 64);
-  scope_.key[3] = g * (use_qr ? 1 : -1) * (w_in_lds ? 1 : 100);  // path: svd_wg_kernel<g>, sign = QRCP, x100 = W global
+  if (wmode == 1 && !(g == 4 || g == 8 || g == 16)) wmode = 0;
+  const size_t shm = (size_t)(fixed + (wmode == 2 ? wm : wmode == 1 ? wm / 2 : 0)) * sizeof(double);
+  // path: svd_wg_kernel<g>, sign = QRCP, x100 = W global, x10 = W in LDS and M global
+  scope_.key[3] = g * (use_qr ? 1 : -1) * (wmode == 2 ? 1 : wmode == 1 ? 10 : 100);
   (void)defl;  // no deflation on this path (every direction keeps an orthonormal vector)
+#define TTK_SVD_WG_MODE(GG, MM)                                                                             \
+  {                                                                                                         \
+    allow_big_lds(svd_wg_kernel<GG, MM>, shm);                                                              \
+    hipLaunchKernelGGL((svd_wg_kernel<GG, MM>), dim3(1), dim3(nt), shm, TTK_STREAM(stream), A, m, n, U, S, Vt, \
+                       work, w_in_lds, use_qr, g_svd_timing);                                               \
+  }
 #define TTK_SVD_WG(GG)                                                                                      \
   case GG:                                                                                                  \
-    if (w_in_lds) {                                                                                         \
-      allow_big_lds(svd_wg_kernel<GG, true>, shm);                                                          \
-      hipLaunchKernelGGL((svd_wg_kernel<GG, true>), dim3(1), dim3(nt), shm, TTK_STREAM(stream), A, m, n, U, S, Vt, \
-                         work, w_in_lds, use_qr, g_svd_timing);                                             \
-    } else {                                                                                                \
-      allow_big_lds(svd_wg_kernel<GG, false>, shm);                                                         \
-      hipLaunchKernelGGL((svd_wg_kernel<GG, false>), dim3(1), dim3(nt), shm, TTK_STREAM(stream), A, m, n, U, S,  \
-                         Vt, work, w_in_lds, use_qr, g_svd_timing);                                         \
-    }                                                                                                       \
+    if (wmode == 2) TTK_SVD_WG_MODE(GG, 2) else TTK_SVD_WG_MODE(GG, 0)                                       \
+    break;
+#define TTK_SVD_WG3(GG)                                                                                     \
+  case GG:                                                                                                  \
+    if (wmode == 2) TTK_SVD_WG_MODE(GG, 2) else if (wmode == 1) TTK_SVD_WG_MODE(GG, 1) else TTK_SVD_WG_MODE(GG, 0) \
     break;
   switch (g) {
     TTK_SVD_WG(1)
     TTK_SVD_WG(2)
-    TTK_SVD_WG(4)
-    TTK_SVD_WG(8)
-    TTK_SVD_WG(16)
+    TTK_SVD_WG3(4)
+    TTK_SVD_WG3(8)
+    TTK_SVD_WG3(16)
     TTK_SVD_WG(32)
     default:
       TTK_SVD_WG(64)
   }
 #undef TTK_SVD_WG
+#undef TTK_SVD_WG3
+#undef TTK_SVD_WG_MODE
   TTK_LAUNCH_CHECK();
   return TTK_OK;
 }

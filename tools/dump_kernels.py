@@ -90,7 +90,8 @@ def main(path):
         lib.ttk_fused_set_mfma(old)
     # one-workgroup SVDs (QRCP + Jacobi) on plain and graded matrices, tall and wide
     for (m_, n_) in [(39, 52), (52, 39), (64, 63), (63, 64), (96, 80), (80, 96), (20, 17), (128, 40), (60, 90),
-                     (12, 8), (8, 12), (96, 96), (4, 3), (8, 6), (6, 6), (16, 16), (40, 10), (30, 33)]:
+                     (12, 8), (8, 12), (96, 96), (4, 3), (8, 6), (6, 6), (16, 16), (40, 10), (30, 33),
+                     (72, 72), (100, 75), (75, 100), (90, 70), (64, 65)]:
         for graded in (0, 1):
             M = rng.standard_normal((m_, n_))
             if graded:
