@@ -1487,6 +1487,23 @@ __global__ __launch_bounds__(1024) void syev_extreme_kernel(const double *__rest
 // syev_extreme_kernel, so both paths produce the same eigenpair to rounding.
 constexpr int SYEV_SMALL_N = 128;
 
+// the rank-2 update A22 -= v w^T + w v^T of syev_small_kernel, rows i = wid, wid + NW, ...: A22's rows,
+// the reflector v (row k of A, left of A22's rows) and p never overlap -- said so, a wave's next rows'
+// loads issue ahead of this row's stores (possible aliasing had each row wait for the previous row's
+// LDS stores).  The same operations per element: bit-identical.
+template <int NW>
+__device__ __forceinline__ void syev_rank2_rows(double *__restrict__ A22, int ld, const double *__restrict__ v,
+                                                const double *__restrict__ pv, int m, int wid, double K, int j0,
+                                                int j1, double v0, double v1, double w0, double w1) {
+#pragma unroll 4
+  for (int i = wid; i < m; i += NW) {
+    const double vi = v[i], wi = fma(-K, vi, pv[i]);
+    double *ai = A22 + i * ld;
+    if (j0 < m) ai[j0] -= fma(vi, w0, wi * v0);
+    if (j1 < m) ai[j1] -= fma(vi, w1, wi * v1);
+  }
+}
+
 template <int NT>
 __global__ __launch_bounds__(NT) void syev_small_kernel(const double *__restrict__ Ain, int n, int which,
                                                         double *__restrict__ ev_out, double *__restrict__ vec_out,
@@ -1563,13 +1580,7 @@ __global__ __launch_bounds__(NT) void syev_small_kernel(const double *__restrict
       const double p0 = j0 < m ? pv[j0] : 0.0, p1 = j1 < m ? pv[j1] : 0.0;
       const double K = 0.5 * tau * ttk::wave_sum(fma(p0, v0, p1 * v1));
       const double w0 = fma(-K, v0, p0), w1 = fma(-K, v1, p1);
-#pragma unroll 4
-      for (int i = wid; i < m; i += NW) {
-        const double vi = v[i], wi = fma(-K, vi, pv[i]);
-        double *ai = A + (k + 1 + i) * ld + k + 1;
-        if (j0 < m) ai[j0] -= fma(vi, w0, wi * v0);
-        if (j1 < m) ai[j1] -= fma(vi, w1, wi * v1);
-      }
+      syev_rank2_rows<NW>(A + (k + 1) * ld + k + 1, ld, v, pv, m, wid, K, j0, j1, v0, v1, w0, w1);
     }
     if (wid == 0 && k + 3 < n) {
       __threadfence_block();
