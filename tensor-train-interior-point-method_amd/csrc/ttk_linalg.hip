@@ -1151,6 +1151,9 @@ __global__ __launch_bounds__(1024) void syev_kernel(double *__restrict__ Ain, in
 // Phases 2-4 of the extreme eigenpair, shared by the one-workgroup kernel and the finish kernel of
 // the multi-workgroup tridiagonalisation: T from the reduced A (reflectors kept in A's rows), Sturm
 // multisection, inverse iteration, back-transform.
+// RA: the back-transform holds each reflector in registers, loaded one ahead (A in global memory: the
+// one-launch-per-step path's tri_finish_kernel); with A in LDS the plain loop is the faster one
+template <bool RA = false>
 __device__ __forceinline__ void tridiag_extreme_finish(double *A, int n, int which, double *dv, double *ov, double *ev2, double *tv,
                                        double *z, double *fd, double *fdu, double *fdu2, double *fdl, double *fpiv,
                                        double *__restrict__ ev_out, double *__restrict__ vec_out, int lda,
@@ -1379,8 +1382,40 @@ __device__ __forceinline__ void tridiag_extreme_finish(double *A, int n, int whi
   }
   __syncthreads();
   TTK_EPHASE(6)
-  // ---- 4. back-transform by wave 0 (no block barriers inside)
-  if (wid == 0) {
+  // ---- 4. back-transform by wave 0 (no block barriers inside).  Up to 8 elements per lane (n <= 514):
+  // each reflector is held in registers, loaded one reflector ahead -- the plain loop below waited
+  // one global round trip per reflector for A's row k, then read the row again for the update; the
+  // same FMAs in the same order (acc += v z, z -= acc v): bit-identical
+  constexpr int BT_VR = 8;
+  if (RA && wid == 0 && n - 1 <= 64 * BT_VR && n >= 3) {
+    double vc[BT_VR], vn[BT_VR];
+    auto load_row = [&](int k, double *dst) {
+      const double *v = A + (int64_t)k * lda + k + 1;
+      const int m = n - k - 1;
+#pragma unroll
+      for (int u = 0; u < BT_VR; ++u) dst[u] = lane + 64 * u < m ? v[lane + 64 * u] : 0.0;
+    };
+    load_row(n - 3, vc);
+    for (int k = n - 3; k >= 0; --k) {
+      if (k > 0) load_row(k - 1, vn);
+      const double tau = tv[k];
+      if (tau != 0.0) {
+        double *zk = z + k + 1;
+        const int m = n - k - 1;
+        double acc = 0.0;
+#pragma unroll
+        for (int u = 0; u < BT_VR; ++u)
+          if (lane + 64 * u < m) acc = fma(vc[u], zk[lane + 64 * u], acc);
+        acc = tau * ttk::wave_sum(acc);
+#pragma unroll
+        for (int u = 0; u < BT_VR; ++u)
+          if (lane + 64 * u < m) zk[lane + 64 * u] = fma(-acc, vc[u], zk[lane + 64 * u]);
+        __threadfence_block();
+      }
+#pragma unroll
+      for (int u = 0; u < BT_VR; ++u) vc[u] = vn[u];
+    }
+  } else if (wid == 0) {
     for (int k = n - 3; k >= 0; --k) {
       const double tau = tv[k];
       if (tau == 0.0) continue;
@@ -1703,11 +1738,11 @@ __global__ __launch_bounds__(1024) void tri_finish_kernel(double *A, int n, int 
       ltv[i] = tv[i];
     }
     __syncthreads();
-    tridiag_extreme_finish(A, n, which, ldv, lov, lev2, ltv, lz, lz + n, lz + 2 * n, lz + 3 * n, lz + 4 * n,
+    tridiag_extreme_finish<true>(A, n, which, ldv, lov, lev2, ltv, lz, lz + n, lz + 2 * n, lz + 3 * n, lz + 4 * n,
                            lz + 5 * n, ev_out, vec_out, n);
     return;
   }
-  tridiag_extreme_finish(A, n, which, dv, ov, ev2, tv, z, fd, fdu, fdu2, fdl, fpiv, ev_out, vec_out, n);
+  tridiag_extreme_finish<true>(A, n, which, dv, ov, ev2, tv, z, fd, fdu, fdu2, fdl, fpiv, ev_out, vec_out, n);
 }
 
 static int tri_finish_launch(hipStream_t st, double *A, int n, int which, double *gv, double *ev, double *vec) {
