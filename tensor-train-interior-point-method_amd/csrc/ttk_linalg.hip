@@ -656,6 +656,52 @@ __global__ __launch_bounds__(1024) void qr_kernel(const double *__restrict__ A, 
     W[e] = A[(int64_t)i * n + j];
   }
   __syncthreads();
+  if (m <= 65) {
+    // every lane holds at most one element of column j below the diagonal, so each wave can form the
+    // reflector itself: the norm is wave 0's wave sum in the block-wide path (the other waves add
+    // zeros), the scaled vector stays in registers, and each wave updates the columns it owns (c % nw
+    // == wid) -- one block barrier per column instead of four.  The same operations on every element
+    // in the same order as the block-wide loop below: bit-identical
+    for (int j = 0; j < k; ++j) {
+      double *wj = W + (int64_t)j * m;
+      const int i = j + 1 + lane;
+      const double x = i < m ? wj[i] : 0.0;
+      const double s2 = 0.0 + ttk::wave_sum(i < m ? fma(x, x, 0.0) : 0.0);
+      const double alpha = wj[j];
+      double tj, sc, beta;
+      if (s2 == 0.0) {
+        tj = 0.0;
+        beta = alpha;
+        sc = 0.0;
+      } else {
+        const double nrm = sqrt(alpha * alpha + s2);
+        beta = (alpha >= 0.0) ? -nrm : nrm;
+        tj = (beta - alpha) / beta;
+        sc = 1.0 / (alpha - beta);
+      }
+      const double v = x * sc;
+      if (tj != 0.0) {
+        for (int c = j + 1 + ((wid - (j + 1) % nw + nw) % nw); c < n; c += nw) {
+          double *wc = W + (int64_t)c * m;
+          const double init = (lane == 0) ? wc[j] : 0.0;
+          double d = i < m ? fma(v, wc[i], init) : init;
+          d = ttk::wave_sum(d) * tj;
+          if (lane == 0) wc[j] -= d;
+          if (i < m) wc[i] -= d * v;
+        }
+      }
+      __syncthreads();
+      if (wid == j % nw) {  // column j's owner stores the reflector, beta and tau (every wave has read
+                            // column j above; nobody reads it again before the loop ends)
+        if (i < m) wj[i] = v;
+        if (lane == 0) {
+          wj[j] = beta;
+          tau[j] = tj;
+        }
+      }
+    }
+    __syncthreads();
+  } else
   for (int j = 0; j < k; ++j) {
     double *wj = W + (int64_t)j * m;
     double s2 = ttk::chain_ahead<CU>(
