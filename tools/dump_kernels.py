@@ -47,7 +47,7 @@ def main(path):
         out[f"lu_sol_{n}"] = D.read(b)
     # one-workgroup Householder QR (ttk_qr; the narrow launch for m <= 65) on the ranks' shapes
     for (m_, n_) in [(10, 5), (24, 6), (16, 4), (8, 2), (4, 5), (2, 5), (48, 12), (56, 14), (128, 8), (16, 12),
-                     (65, 20), (64, 64), (66, 10), (1, 3), (3, 1), (40, 40)]:
+                     (65, 20), (64, 64), (66, 10), (1, 3), (3, 1), (40, 40), (20, 1200), (60, 400)]:
         Q_, R_ = D.qr(D.from_numpy(rng.standard_normal((m_, n_))))
         out[f"qr_{m_}_{n_}"] = np.concatenate([D.read(Q_).ravel(), D.read(R_).ravel()])
     # VALU local-apply rows (maxcut-sized fused applies: single launches)
