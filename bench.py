@@ -82,9 +82,13 @@ class _Stop(Exception):
 
 
 _CHILDREN = []  # every worker Popen; terminated on any early exit of main()
+_TEMP_FILES = []  # the dynamic schedule's counter files; removed on any exit of main()
 
 
 def _reap_children():
+    for f in _TEMP_FILES:
+        with contextlib.suppress(OSError):
+            os.unlink(f)
     for p in _CHILDREN:
         if p.poll() is None:
             p.terminate()
@@ -605,6 +609,7 @@ def main():
         fd, qpath = tempfile.mkstemp(prefix=f"ttipm_bench_r{rank}_", suffix=".q")
         os.write(fd, b"0")
         os.close(fd)
+        _TEMP_FILES.append(qpath)
         queue = (work, qpath)
     gpu_procs = _spawn_gpu_workers(args, proc_slots[1:], queue)  # before any GPU call
 
@@ -686,8 +691,6 @@ def main():
     sync()
     barrier()
     elapsed = time.perf_counter() - t0
-    if queue is not None:
-        os.unlink(queue[1])
     slot_elapsed = slot_elapsed + [e for w in worker_out for e in w["elapsed"]]
     results = results + [r for w in worker_out for r in w["results"]]
     iters = sum(r["num_iters"] for r in results)
