@@ -176,6 +176,31 @@ def _claim(path):
     return n
 
 
+def _cu_masked_stream(part, nparts):
+    """A HIP stream whose kernels run on one of `nparts` disjoint CU sets (hipExtStreamCreateWithCUMask):
+    TTIPM_CU_LAYOUT=block (default) gives part i the mask bits [i N/n, (i+1) N/n), stride the bits c
+    with c % n == i.  Diagnostics (TTIPM_CU_PARTS): do the solves in flight interfere through CU
+    occupancy -- a one-workgroup kernel that needs a whole CU's LDS waiting for CUs other solves'
+    multi-workgroup launches hold?  Measured no: 4 one-slot processes on 4 disjoint 64-CU sets ran
+    0.39-0.40 s/IPM-iter against 0.090 on their default streams (profiles/r05_inflight_layouts.txt) --
+    a created stream per process costs far more than any sharing of CUs."""
+    import torch
+    hip = ctypes.CDLL("libamdhip64.so")
+    ncu = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
+    words = (ncu + 31) // 32
+    mask = (ctypes.c_uint32 * words)()
+    stride = os.environ.get("TTIPM_CU_LAYOUT", "block") == "stride"
+    for c in range(ncu):
+        mine = (c % nparts == part) if stride else (c * nparts // ncu == part)
+        if mine:
+            mask[c // 32] |= 1 << (c % 32)
+    st = ctypes.c_void_p()
+    rc = hip.hipExtStreamCreateWithCUMask(ctypes.byref(st), ctypes.c_uint32(words), mask)
+    if rc != 0:
+        raise RuntimeError(f"hipExtStreamCreateWithCUMask returned {rc}")
+    return st.value
+
+
 class _Slots:
     """The solves in flight of one process: one host thread per slot, each with its own HIP stream,
     libttk context (`dev`'s per-thread state) and NumPy random stream (`ttipm_amd.rng`).  Every slot
@@ -183,7 +208,7 @@ class _Slots:
     seeds back to back and records its wall time (its own stream synchronised).  The launches
     themselves release the GIL, so the slots' host work overlaps while their kernels run."""
 
-    def __init__(self, slot_seeds, packed, solve, warmup, device, queue=None):
+    def __init__(self, slot_seeds, packed, solve, warmup, device, queue=None, slot_base=0):
         """queue: None -- slot j solves slot_seeds[j] back to back (static); or (work, path) -- every
         slot claims the next index of the rank's ordered work list from the cross-process counter
         file `path` (`_claim`) until the list is exhausted (slot_seeds[j][0] is still its warm-up
@@ -193,6 +218,7 @@ class _Slots:
             sys.setswitchinterval(SLOT_SWITCH_INTERVAL)
         self.n = len(slot_seeds)
         self.queue = queue
+        self.slot_base = slot_base
         self.ready = threading.Barrier(self.n + 1)
         self.go = threading.Event()
         self.out = [None] * self.n
@@ -211,7 +237,11 @@ class _Slots:
                 torch.cuda.set_device(device)
                 # one slot per process: the default stream (measured: two processes on created streams
                 # slow each other 2.6x, on their default streams not at all, profiles/r03_inflight_layouts.txt)
-                if self.n > 1 or os.environ.get("TTIPM_SLOT_STREAM", "default") != "default":
+                parts = int(os.environ.get("TTIPM_CU_PARTS", "0"))
+                if parts > 0:
+                    torch.cuda.set_stream(torch.cuda.ExternalStream(
+                        _cu_masked_stream((self.slot_base + j) % parts, parts)))
+                elif self.n > 1 or os.environ.get("TTIPM_SLOT_STREAM", "default") != "default":
                     torch.cuda.set_stream(torch.cuda.Stream())
             rng.private()
             for _ in range(warmup):  # untimed: plans, this context's scratch, allocator, code pages
@@ -304,7 +334,7 @@ def _gpu_worker(args, slot_seeds, queue=None):
         def solve(prep, trace=None):
             return _solve(prep, config, quiet=True, verbose=False, trace=trace)
 
-        slots = _Slots(slot_seeds, packed, solve, args.warmup, dev, queue=queue)
+        slots = _Slots(slot_seeds, packed, solve, args.warmup, dev, queue=queue, slot_base=args.slot_base)
         slots.wait_ready()
         print("ready", file=sys.__stdout__, flush=True)
         if sys.stdin.readline().strip() != "go":  # EOF: the parent is gone -- do not run as an orphan
@@ -314,16 +344,16 @@ def _gpu_worker(args, slot_seeds, queue=None):
     print(json.dumps({"elapsed": elapsed, "results": [{k: r.get(k) for k in keep} for r in results]}), flush=True)
 
 
-def _spawn_gpu_workers(args, proc_slots, queue=None):
+def _spawn_gpu_workers(args, proc_slots, queue=None, base=0):
     """Started BEFORE this process initialises the GPU; each prints 'ready' once warmed up.
     proc_slots: per worker process, its slots' seed lists; queue: (work list, counter file) of the
     dynamic schedule, or None."""
     procs = []
-    for slots in proc_slots:
+    for w, slots in enumerate(proc_slots):  # global slot ids: this process's own `base` slots first
         cmd = [sys.executable, os.path.abspath(__file__), "--gpu-worker",
                ";".join(",".join(map(str, sl)) for sl in slots),
                "--problem", args.problem, "--config", args.config, "--rank", str(args.rank),
-               "--warmup", str(args.warmup)]
+               "--warmup", str(args.warmup), "--slot-base", str(base + sum(len(x) for x in proc_slots[:w]))]
         if queue is not None:
             cmd += ["--queue-work", ",".join(map(str, queue[0])), "--queue-file", queue[1]]
         procs.append(subprocess.Popen(cmd, stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=sys.stderr,
@@ -565,6 +595,7 @@ def main():
                     help="static (default): slot j solves its schedule column; dynamic: the rank's slots claim "
                          "its solves one at a time from a shared counter, in schedule order")
     ap.add_argument("--queue-work", default=None, help=argparse.SUPPRESS)
+    ap.add_argument("--slot-base", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--queue-file", default=None, help=argparse.SUPPRESS)
     ap.add_argument("--cpu-worker", type=int, default=None, help=argparse.SUPPRESS)
     ap.add_argument("--gpu-worker", default=None, help=argparse.SUPPRESS)
@@ -611,7 +642,7 @@ def main():
         os.close(fd)
         _TEMP_FILES.append(qpath)
         queue = (work, qpath)
-    gpu_procs = _spawn_gpu_workers(args, proc_slots[1:], queue)  # before any GPU call
+    gpu_procs = _spawn_gpu_workers(args, proc_slots[1:], queue, base=len(proc_slots[0]))  # before any GPU call
 
     cpu_seeds = list(dict.fromkeys(s for sl in slot_seeds for s in sl))  # the distinct seeds this (only) rank times
     cpu_procs, allcore_proc = [], []
