@@ -1585,10 +1585,48 @@ __device__ __forceinline__ void syev_rank2_rows(double *__restrict__ A22, int ld
   }
 }
 
+// the same for rows first, first + S, ... (S wave-uniform; syev_small_kernel gives wave 0 row 0 alone
+// and the other waves the rest), in batches of B rows whose operands are loaded before any of their
+// stores.  Rows past m load row m - 1, lanes past m load column 0, and those lanes store into a
+// scratch slot (`dummy`, 32 doubles nobody reads), so a batch has no branches.  The same operations
+// per stored element: bit-identical.
+template <int B>
+__device__ __forceinline__ void syev_rank2_rows_b(double *__restrict__ A22, int ld, const double *__restrict__ v,
+                                                  const double *__restrict__ pv, int m, int first, int S, double K,
+                                                  int j0, int j1, double v0, double v1, double w0, double w1,
+                                                  double *__restrict__ dummy) {
+  // wide (m > 64): j0 < m on every lane, and column j0 + 64 past m still lies inside the LDS block
+  // (the next row, or the arrays after A), so x1 is read unguarded -- one ds_read2 with x0
+  const bool c0 = j0 < m, c1 = j1 < m, wide = m > 64;
+  const int l0 = c0 ? j0 : 0;
+  double *const d = dummy + (j0 & 31);
+  for (int i0 = first; i0 < m; i0 += S * B) {
+    double vi[B], pi[B], x0[B], x1[B];
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+      const int i = min(i0 + b * S, m - 1);
+      const double *ai = A22 + i * ld;
+      vi[b] = v[i];
+      pi[b] = pv[i];
+      x0[b] = ai[l0];
+      x1[b] = wide ? ai[l0 + 64] : 0.0;
+    }
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+      const int i = i0 + b * S;
+      const bool ok = i < m;
+      const double wi = fma(-K, vi[b], pi[b]);
+      double *ai = A22 + (ok ? i : 0) * ld;
+      *(ok && c0 ? ai + j0 : d) = x0[b] - fma(vi[b], w0, wi * v0);
+      if (wide) *(ok && c1 ? ai + j1 : d) = x1[b] - fma(vi[b], w1, wi * v1);
+    }
+  }
+}
+
 template <int NT>
 __global__ __launch_bounds__(NT) void syev_small_kernel(const double *__restrict__ Ain, int n, int which,
                                                         double *__restrict__ ev_out, double *__restrict__ vec_out,
-                                                        int timing) {
+                                                        int timing, int var) {
   constexpr int NW = NT / 64, G = NT / 128;  // waves; lanes per row in the symv (rows <= 127)
   extern __shared__ double lds[];
   const int ld = n | 1;
@@ -1604,7 +1642,11 @@ __global__ __launch_bounds__(NT) void syev_small_kernel(const double *__restrict
   __syncthreads();
   // two barriers per reflector: wave 0 owns A22's first row in the rank-2 update, so right after
   // updating it (same wave, LDS order) it builds the next reflector from that row while the other
-  // waves finish their rows; nobody else reads the row in that phase
+  // waves finish their rows; nobody else reads the row in that phase.  `var` (TTK_SYEV_VAR, A/B
+  // timing; every setting bit-identical): 4 = the symv's lane-group sums by DPP instead of LDS
+  // permutes, 8 (4 waves) / 16 (16 waves) = wave 0 updates row 0 only (it was the last to reach the
+  // step's second barrier: its share of the rows plus the reflector), the other waves the remaining
+  // rows -- n = 40 134.7 -> 126.2 us with 4 waves, slower with 16 (r05_syev_small.txt).
   auto reflector = [&](int k) {  // wave 0: dlarfg on row k (the sub-column by symmetry)
     double *v = A + k * ld + k + 1;
     const int m = n - k - 1;
@@ -1629,6 +1671,15 @@ __global__ __launch_bounds__(NT) void syev_small_kernel(const double *__restrict
   };
   if (wid == 0 && n > 2) reflector(0);
   __syncthreads();
+  // timing == 2: wave 0's cycles per step phase into the debug counters 0..5 (symv, barrier, K,
+  // rank-2 rows, reflector, barrier) -- diagnostics only, the stamps wait on outstanding LDS ops
+  unsigned long long t_s = timing == 2 ? clock64() : 0;
+#define TTK_SSTAMP(K)                                       \
+  if (timing == 2 && wid == 0) {                            \
+    const unsigned long long t1 = clock64();                \
+    if (lane == 0) atomicAdd(&g_dbg[K], t1 - t_s);          \
+    t_s = t1;                                               \
+  }
   for (int k = 0; k + 2 < n; ++k) {
     const double *v = A + k * ld + k + 1;
     const int m = n - k - 1;
@@ -1651,26 +1702,44 @@ __global__ __launch_bounds__(NT) void syev_small_kernel(const double *__restrict
           for (; j < m; j += G) acc = fma(ar[j], v[j], acc);
           acc = (acc + a1) + (a2 + a3);
         }
+        if (var & 4) {  // DPP: the xor-butterfly's sums (both lanes of a pair hold a + b), no LDS permutes
+          acc = ttk::group_sum<G>(acc);
+        } else {
 #pragma unroll
-        for (int o = 1; o < G; o <<= 1) acc += __shfl_xor(acc, o, 64);
+          for (int o = 1; o < G; o <<= 1) acc += __shfl_xor(acc, o, 64);
+        }
         if (h == 0 && r < m) pv[r] = tau * acc;
       }
+      TTK_SSTAMP(0)
       __syncthreads();
+      TTK_SSTAMP(1)
       const int j0 = lane, j1 = lane + 64;
       const double v0 = j0 < m ? v[j0] : 0.0, v1 = j1 < m ? v[j1] : 0.0;
       const double p0 = j0 < m ? pv[j0] : 0.0, p1 = j1 < m ? pv[j1] : 0.0;
       const double K = 0.5 * tau * ttk::wave_sum(fma(p0, v0, p1 * v1));
       const double w0 = fma(-K, v0, p0), w1 = fma(-K, v1, p1);
-      syev_rank2_rows<NW>(A + (k + 1) * ld + k + 1, ld, v, pv, m, wid, K, j0, j1, v0, v1, w0, w1);
+      TTK_SSTAMP(2)
+      if (var & (NT <= 256 ? 8 : 16)) {  // wave 0 updates row 0 only, then the next reflector
+        if (wid == 0)
+          syev_rank2_rows_b<1>(A + (k + 1) * ld + k + 1, ld, v, pv, m, 0, m, K, j0, j1, v0, v1, w0, w1, fpiv + n);
+        else
+          syev_rank2_rows_b<4>(A + (k + 1) * ld + k + 1, ld, v, pv, m, wid, NW - 1, K, j0, j1, v0, v1, w0, w1,
+                               fpiv + n);
+      } else
+        syev_rank2_rows<NW>(A + (k + 1) * ld + k + 1, ld, v, pv, m, wid, K, j0, j1, v0, v1, w0, w1);
+      TTK_SSTAMP(3)
     }
     if (wid == 0 && k + 3 < n) {
       __threadfence_block();
       reflector(k + 1);
     }
+    TTK_SSTAMP(4)
     __syncthreads();
+    TTK_SSTAMP(5)
   }
-  if (timing && tid == 0) atomicAdd(&g_dbg[4], wall_clock64() - t_ph0);
-  tridiag_extreme_finish(A, n, which, dv, ov, ev2, tv, z, fd, fdu, fdu2, fdl, fpiv, ev_out, vec_out, ld, timing);
+#undef TTK_SSTAMP
+  if (timing == 1 && tid == 0) atomicAdd(&g_dbg[4], wall_clock64() - t_ph0);
+  tridiag_extreme_finish(A, n, which, dv, ov, ev2, tv, z, fd, fdu, fdu2, fdl, fpiv, ev_out, vec_out, ld, timing == 1);
 }
 
 int64_t syev_small_need(int n) { return (int64_t)n * (n | 1) + 13 * (int64_t)n + 32; }
@@ -3029,6 +3098,7 @@ int64_t ttk_syev_extreme_work(int n) {
 }
 
 static int g_syev_fused_max = TRI_FUSED_MAX;
+static int g_syev_var = getenv("TTK_SYEV_VAR") ? atoi(getenv("TTK_SYEV_VAR")) : 12;  // syev_small_kernel variants
 static int g_syev_small_wide = getenv("TTK_SYEV_WIDE") ? atoi(getenv("TTK_SYEV_WIDE")) : 64;  // 16-wave small kernel from this n
 static int g_tri_rows = getenv("TTK_TRI_ROWS") ? atoi(getenv("TTK_TRI_ROWS")) : 4;  // largest n for the one-launch-per-step tridiagonalisation
 
@@ -3093,10 +3163,12 @@ int ttk_syev_extreme(void *stream, const double *A, int n, int which, double *ev
     const size_t shm_s = (size_t)syev_small_need(n) * sizeof(double);
     if (n >= g_syev_small_wide) {
       allow_big_lds(syev_small_kernel<1024>, shm_s);
-      hipLaunchKernelGGL(syev_small_kernel<1024>, dim3(1), dim3(1024), shm_s, st, A, n, which, ev, vec, g_svd_timing);
+      hipLaunchKernelGGL(syev_small_kernel<1024>, dim3(1), dim3(1024), shm_s, st, A, n, which, ev, vec, g_svd_timing,
+                         g_syev_var);
     } else {
       allow_big_lds(syev_small_kernel<256>, shm_s);
-      hipLaunchKernelGGL(syev_small_kernel<256>, dim3(1), dim3(256), shm_s, st, A, n, which, ev, vec, g_svd_timing);
+      hipLaunchKernelGGL(syev_small_kernel<256>, dim3(1), dim3(256), shm_s, st, A, n, which, ev, vec, g_svd_timing,
+                         g_syev_var);
     }
     TTK_LAUNCH_CHECK();
     return TTK_OK;

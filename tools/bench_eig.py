@@ -11,7 +11,50 @@ from ttipm_amd._lib import lib  # noqa: E402
 from tools.bench_linalg import timed  # noqa: E402
 
 
+def step_phases():
+    """syev_small_kernel's tridiagonalisation, wave 0's cycles per Householder step by phase (timing 2)."""
+    from tools.bench_linalg import counters
+    rng = np.random.default_rng(0)
+    st = D._stream()
+    lib.ttk_svd_set_timing(2)
+    print("cycles per step (wave 0): symv, barrier1, K, rank-2 rows, reflector, barrier2")
+    for n in [10, 40, 63, 64, 80, 100, 128]:
+        M = rng.standard_normal((n, n))
+        A = D.from_numpy(M + M.T)
+        wx = D.empty(int(lib.ttk_syev_extreme_work(n)))
+        buf = D.empty(n + 1)
+        f = lambda: lib.ttk_syev_extreme(st, D._p(A), n, 0, D._p(buf), D._p(buf[1:]), D._p(wx))  # noqa: E731
+        f()
+        torch.cuda.synchronize()
+        counters()
+        reps = 20
+        t = timed(f, reps=reps)
+        c = counters()
+        steps = (reps + 1) * (n - 2)
+        print(f"  n={n:4d} total {t:8.1f} us  " + " ".join(f"{c[k] / steps:7.0f}" for k in range(6)), flush=True)
+    lib.ttk_svd_set_timing(0)
+
+
+def totals():
+    """Default-path latency per n (no timers), for A/B across TTK_SYEV_VAR settings."""
+    rng = np.random.default_rng(0)
+    st = D._stream()
+    out = []
+    for n in [10, 20, 40, 63, 64, 80, 100, 128]:
+        M = rng.standard_normal((n, n))
+        A = D.from_numpy(M + M.T)
+        wx = D.empty(int(lib.ttk_syev_extreme_work(n)))
+        buf = D.empty(n + 1)
+        out.append(timed(lambda: lib.ttk_syev_extreme(st, D._p(A), n, 0, D._p(buf), D._p(buf[1:]), D._p(wx)),
+                         reps=20))
+    print("totals_us " + " ".join(f"{t:7.1f}" for t in out), flush=True)
+
+
 def main():
+    if "--steps" in sys.argv:
+        return step_phases()
+    if "--totals" in sys.argv:
+        return totals()
     rng = np.random.default_rng(0)
     st = D._stream()
     print("small eig phases (us per call): tridiag, multisection, inverse iteration, back-transform")
