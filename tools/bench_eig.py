@@ -60,7 +60,7 @@ def main():
     print("small eig phases (us per call): tridiag, multisection, inverse iteration, back-transform")
     from tools.bench_linalg import counters
     lib.ttk_svd_set_timing(1)
-    for n in [10, 40, 80, 100, 128]:
+    for n in [10, 40, 63, 64, 80, 100, 128]:
         M = rng.standard_normal((n, n))
         A = D.from_numpy(M + M.T)
         wx = D.empty(int(lib.ttk_syev_extreme_work(n)))
@@ -69,9 +69,11 @@ def main():
         t_x = timed(lambda: lib.ttk_syev_extreme(st, D._p(A), n, 0, D._p(buf), D._p(buf[1:]), D._p(wx)))
         c = counters()
         calls = max(c[2], 1)
-        print(f"  n={n:4d} total {t_x:8.1f}  phases {[round(c[k] / 100.0 / calls, 1) for k in (4, 5, 6, 7)]}",
-              flush=True)
+        print(f"  n={n:4d} total {t_x:8.1f}  phases {[round(c[k] / 100.0 / calls, 1) for k in (4, 5, 6, 7)]}"
+              f"  multisection rounds {c[3] / calls:.1f}", flush=True)
     lib.ttk_svd_set_timing(0)
+    if "--phases" in sys.argv:
+        return
     print("n      default_us   two_launch_us   lam_diff")
     for n in [4, 10, 20, 40, 80, 100, 128, 139, 160, 200, 288, 400, 504, 768, 1200]:
         M = rng.standard_normal((n, n))
