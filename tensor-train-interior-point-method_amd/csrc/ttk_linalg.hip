@@ -1205,7 +1205,7 @@ __device__ __forceinline__ void tridiag_extreme_finish(double *A, int n, int whi
                                        double *__restrict__ ev_out, double *__restrict__ vec_out, int lda,
                                        int timing = 0) {
   __shared__ double sh_a, sh_b;
-  __shared__ int sh_first;
+  __shared__ int sh_first[2];  // round r's first shift with count >= target, by round parity
   const int tid = threadIdx.x, nt = blockDim.x;
   unsigned long long t_ph = timing ? wall_clock64() : 0;
 #define TTK_EPHASE(K)                                   \
@@ -1243,18 +1243,17 @@ __device__ __forceinline__ void tridiag_extreme_finish(double *A, int n, int whi
   if (tid == 0) {
     sh_a = lo;
     sh_b = hi;
+    sh_first[0] = nt < 256 ? nt : 256;
   }
   __syncthreads();
-  // ---- 2. multisection
+  // ---- 2. multisection (two barriers per round: the next round's slot is reset with the update)
   // at most 4 waves evaluate shifts: the Sturm recurrence is issue-bound, more waves per SIMD only
   // stretch each round (the extra waves of a 16-wave block wait at the barriers)
   const int ns = nt < 256 ? nt : 256;
   for (int round = 0; round < 16; ++round) {
     const double a = sh_a, b = sh_b;
     if (b - a <= 2.0 * EPS * fmax(fabs(a), fabs(b)) + 2.0 * pivmin) break;
-    if (tid == 0) atomicAdd(&g_dbg[3], 1ull);
-    if (tid == 0) sh_first = ns;
-    __syncthreads();
+    if (timing == 1 && tid == 0) atomicAdd(&g_dbg[3], 1ull);  // rounds (diagnostics)
     if (tid < ns) {
       const double x = a + (b - a) * (double)(tid + 1) / (double)(ns + 1);
       int cnt = 0;
@@ -1283,18 +1282,19 @@ __device__ __forceinline__ void tridiag_extreme_finish(double *A, int n, int whi
         if (fabs(q) < pivmin) q = -pivmin;
         cnt += q < 0.0;
       }
-      if (cnt >= target) atomicMin(&sh_first, tid);
+      if (cnt >= target) atomicMin(&sh_first[round & 1], tid);
     }
     __syncthreads();
     if (tid == 0) {
-      const int f = sh_first;
+      const int f = sh_first[round & 1];
+      sh_first[(round + 1) & 1] = ns;
       sh_a = (f == 0) ? a : a + (b - a) * (double)f / (double)(ns + 1);
       sh_b = (f >= ns) ? b : a + (b - a) * (double)(f + 1) / (double)(ns + 1);
     }
     __syncthreads();
   }
   const double lam = 0.5 * (sh_a + sh_b);
-  if (tid == 0) atomicAdd(&g_dbg[2], 1ull);
+  if (timing == 1 && tid == 0) atomicAdd(&g_dbg[2], 1ull);  // calls
   TTK_EPHASE(5)
   // ---- 3. inverse iteration on T (thread 0, O(n) per solve).  The running pivot row, the next
   // diagonal and the solve recurrences are carried in registers; the LDS arrays are written once
