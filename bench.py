@@ -427,7 +427,7 @@ def _pmc_traffic():
 DEFAULT_INFLIGHT = 4  # solves in flight per GPU, the same at every N (like-for-like 1->8 series)
 NODE_PROCESSES = 16  # solve processes a node may run on its GPUs at once (the box's process guard)
 SLOT_SWITCH_INTERVAL = 0.0005  # sys.setswitchinterval for processes with several slot threads
-HW_QUEUES = 8  # GPU_MAX_HW_QUEUES for the bench processes (HIP's default is 4)
+HW_QUEUES = 8  # GPU_MAX_HW_QUEUES for the bench processes (HIP's default is 4; TTIPM_HW_QUEUES overrides)
 
 
 def default_threads(world, P):
@@ -614,9 +614,10 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if not _profiled() and int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < HW_QUEUES:
+    hwq = int(os.environ.get("TTIPM_HW_QUEUES", str(HW_QUEUES)))
+    if not _profiled() and int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) != hwq:
         # before anything initialises HIP here (and inherited by the GPU worker processes)
-        os.environ["GPU_MAX_HW_QUEUES"] = str(HW_QUEUES)
+        os.environ["GPU_MAX_HW_QUEUES"] = str(hwq)
     with open(args.config) as f:
         config = yaml.safe_load(f)
     P = args.inflight if args.inflight else default_inflight(world)

@@ -33,7 +33,7 @@ def main():
         return worker(int(sys.argv[2]))
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 20000
     for P in [int(p) for p in (sys.argv[2:] or ["1", "2", "4", "8"])]:
-        env = dict(os.environ, GPU_MAX_HW_QUEUES="8")
+        env = dict(os.environ, GPU_MAX_HW_QUEUES=os.environ.get("LR_HWQ", "8"))
         ps = [subprocess.Popen([sys.executable, __file__, "--worker", str(n)], stdin=subprocess.PIPE,
                                stdout=subprocess.PIPE, text=True, env=env) for _ in range(P)]
         for p in ps:
