@@ -250,3 +250,26 @@ def test_local_solver_matches_reference(name, capsys):
     # the new residual of a dense solve sits at rounding level (||A x - rhs|| / ||rhs|| ~ 1e-10, set
     # by summation order): compared in absolute terms there
     assert abs(res_min - ex["res_min"]) <= max(1e-6 * ex["res_min"], 1e-9)
+
+
+def test_extra_departure_floor_rule():
+    """The floor under a KNOWN_EXTRA_DEPARTURES xfail: following the named bounded
+    twin of the reference passes, a trace that leaves it (or a non-finite end point) fails."""
+    import copy
+
+    from tests.parity_policy import (BOUNDED_TWINS, EXTRA_DEPARTURE_FOLLOWS, KNOWN_EXTRA_DEPARTURES,
+                                     check_extra_departure_floor)
+    assert set(EXTRA_DEPARTURE_FOLLOWS) == set(KNOWN_EXTRA_DEPARTURES)
+    end = {"gap": 2.0, "feas": 1e-3}
+    for key, (twin, n, tol) in EXTRA_DEPARTURE_FOLLOWS.items():
+        t = BOUNDED_TWINS[f"{key}_{twin}"]["trace"]
+        check_extra_departure_floor(key, copy.deepcopy(t), end)
+        off = copy.deepcopy(t)
+        k0 = next(iter(off[n - 1]))
+        off[n - 1][k0] = off[n - 1][k0] * (1 + 100 * tol) + 100 * tol
+        with pytest.raises(AssertionError):
+            check_extra_departure_floor(key, off, end)
+        with pytest.raises(AssertionError):
+            check_extra_departure_floor(key, copy.deepcopy(t), {"gap": float("nan"), "feas": 1e-3})
+        with pytest.raises(AssertionError):
+            check_extra_departure_floor(key, copy.deepcopy(t)[:n - 1], end)
