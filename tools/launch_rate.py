@@ -1,5 +1,7 @@
 """Aggregate kernel-dispatch rate of P processes (one stream each) launching tiny kernels back to
 back (ttk_fill of one double): is the GPU's dispatch rate what bounds several solves in flight?
+LR_KERNEL=eig / gemm: the same with one-workgroup eigensolves / multi-workgroup GEMMs (do the
+processes' kernels run concurrently?); LR_HWQ: GPU_MAX_HW_QUEUES of the workers (default 8).
     python tools/launch_rate.py [launches_per_process] [P ...]"""
 import os
 import subprocess
@@ -12,16 +14,35 @@ def worker(n):
     import torch
     from ttipm_amd import dev as D
     from ttipm_amd._lib import lib
+    import numpy as np
     z = D.empty(1)
     st = D._stream()
-    for _ in range(200):
-        lib.ttk_fill(st, D._p(z), 1, 0.0)
+    kind = os.environ.get("LR_KERNEL", "fill")
+    if kind == "fill":  # tiny launches: the dispatch rate
+        def one():
+            lib.ttk_fill(st, D._p(z), 1, 0.0)
+    elif kind == "eig":  # one-workgroup ~0.45 ms kernels (syev_small n = 128): do processes overlap?
+        M = np.random.default_rng(0).standard_normal((128, 128))
+        A = D.from_numpy(M + M.T)
+        wx = D.empty(int(lib.ttk_syev_extreme_work(128)))
+        buf = D.empty(129)
+
+        def one():
+            lib.ttk_syev_extreme(st, D._p(A), 128, 0, D._p(buf), D._p(buf[1:]), D._p(wx))
+    else:  # "gemm": multi-workgroup fp64 GEMMs (700 x 650 x 520)
+        a = torch.randn(700, 520, dtype=torch.float64, device="cuda")
+        b = torch.randn(520, 650, dtype=torch.float64, device="cuda")
+
+        def one():
+            D.matmul(a, b)
+    for _ in range(20 if kind != "fill" else 200):
+        one()
     torch.cuda.synchronize()
     print("ready", flush=True)
     sys.stdin.readline()
     t0 = time.perf_counter()
     for _ in range(n):
-        lib.ttk_fill(st, D._p(z), 1, 0.0)
+        one()
     t1 = time.perf_counter()
     torch.cuda.synchronize()
     t2 = time.perf_counter()
