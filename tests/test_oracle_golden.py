@@ -126,19 +126,41 @@ def test_prune_singular_vals_rule():
 RUNS = json.load(open(os.path.join(HERE, "golden", "runs.json")))
 
 
+_ORACLE_RUN = """
+import json, sys
+import numpy as np
+import yaml
+sys.path.insert(0, sys.argv[1])
+from oracle.problems import run_and_record
+cfg = yaml.safe_load(open(sys.argv[2]))
+trace = []
+r = run_and_record("maxcut", cfg, int(sys.argv[3]), int(sys.argv[4]), trace=trace)
+conv = lambda o: o.item() if isinstance(o, np.generic) else (o.tolist() if isinstance(o, np.ndarray) else str(o))
+print(json.dumps({"trace": trace, "r": r}, default=conv))
+"""
+
+
 @pytest.mark.parametrize("key", ["maxcut_5_r1_s0", "maxcut_5_r1_s319"])
 def test_oracle_full_run_maxcut5(key):
     """Whole TT-IPM on maxcut_5 (configs[0]): the oracle must follow one of the reference's own runs
     (golden or twins) within 50x the reference's rounding noise -- the same policy the device's
-    whole-solve parity tests apply (tests/parity_policy.py)."""
-    import yaml
-    from oracle.problems import run_and_record
+    whole-solve parity tests apply (tests/parity_policy.py).  The oracle's path, like the reference's
+    (hence its PYTHONHASHSEED twins), depends on the interpreter's string-hash seed through set /
+    dict iteration order, so it runs in a child process under PYTHONHASHSEED=0: with a random seed
+    the test was flaky -- hash seeds 0-30 on s319: 28 follow the golden or one of its three committed
+    twins, 3 take a branch no committed reference run takes."""
+    import subprocess
+    import sys
+
     from tests.parity_policy import check_against_reference_runs
     g = RUNS[key]
-    cfg = yaml.safe_load(open(os.path.join(HERE, "..", "configs", g["config"] + ".yaml")))
-    trace = []
-    r = run_and_record("maxcut", cfg, g["seed"], g["rank"], trace=trace)
-    name, per, cum = check_against_reference_runs(key, trace, r)
+    root = os.path.join(HERE, "..")
+    env = dict(os.environ, PYTHONHASHSEED="0", OPENBLAS_NUM_THREADS="1")
+    out = subprocess.run([sys.executable, "-c", _ORACLE_RUN, root, os.path.join(root, "configs", g["config"] + ".yaml"),
+                          str(g["seed"]), str(g["rank"])], env=env, capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stderr[-2000:]
+    res = json.loads(out.stdout.strip().splitlines()[-1])
+    name, per, cum = check_against_reference_runs(key, res["trace"], res["r"])
     print(key, "follows", name, ["%.0e" % v for v in per])
 
 
