@@ -188,12 +188,12 @@ KNOWN_DEPARTURES = {
                         "follows _h1 within 0.035 of the noise bound and ends with it after 14 iterations at gap "
                         "8.7e-5 -- converged, 1 % below the widened envelope of the three converged runs "
                         "(8.74e-5 .. 1.3e-3)",
-    "maxcut_12_r2_s53": "chaotic from assembly 4 (configs[4] YAML seed): the reference's three unmodified runs agree "
+    "maxcut_12_r2_s53": "chaotic from assembly 4 (configs[4] YAML seed): the reference's four unmodified runs agree "
                         "to 3e-9 through assembly 3 and separate from assembly 4 (5e-4, then 0.15 at 5); the device "
-                        "follows the golden within 0.04 of that noise bound; golden and _h1 end barely pathological "
-                        "after 29 iterations (gap 2.9e-3 / 1.3e-3), _h2 converges after 29 at gap 4.0e-4, the "
-                        "device converges after 29 at 5.6e-4 -- _h2's basin, outside the envelope of a single "
-                        "converged run (3.98e-4 .. 4.06e-4); _h3 is running",
+                        "follows _h3 within 0.034 of that noise bound (the golden within 0.036); golden, _h1 and _h3 "
+                        "end barely pathological after 29 iterations (gap 2.9e-3 / 1.3e-3 / 2.7e-3), _h2 converges "
+                        "after 29 at gap 4.0e-4, the device converges after 29 at 5.6e-4 -- _h2's basin, outside "
+                        "the envelope of a single converged run (3.98e-4 .. 4.06e-4)",
 }
 
 
