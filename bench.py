@@ -115,9 +115,11 @@ class _BoundedTrace(list):
             raise _Stop
 
 
-def _cpu_worker(problem, cfg_path, seed, rank_tt, cap):
+def _cpu_worker(problem, cfg_path, seed, rank_tt, cap, cores=None):
     """Child process: wait for 'go' on stdin, run the oracle on one seed, print one JSON line."""
     import warnings
+    if cores:
+        os.sched_setaffinity(0, cores)
     from oracle import ipm as OI
     from oracle import problems as OP
     from oracle import tt as OT
@@ -153,7 +155,8 @@ def _cpu_worker(problem, cfg_path, seed, rank_tt, cap):
     n_it = len(trace.t) - 1
     out = {"seed": seed, "iters": n_it, "s_per_iter": (trace.t[n_it] - trace.t[0]) / max(n_it, 1),
            "work_s": trace.t[n_it] - t_start,
-           "assembly_t": [t - trace.t[0] for t in trace.t], "threads": os.environ.get("OPENBLAS_NUM_THREADS")}
+           "assembly_t": [t - trace.t[0] for t in trace.t], "threads": os.environ.get("OPENBLAS_NUM_THREADS"),
+           "cores": sorted(os.sched_getaffinity(0)), "hash_seed": os.environ.get("PYTHONHASHSEED")}
     if full is not None:
         out.update(full_solve_iters=full, full_solve_s_per_iter=wall / max(full, 1))
     print(json.dumps(out), flush=True)
@@ -362,14 +365,21 @@ def _spawn_gpu_workers(args, proc_slots, queue=None, base=0):
     return procs
 
 
-def _spawn_cpu_workers(args, seeds, threads, cap):
-    """Started BEFORE the GPU is initialised (no exec from a GPU process); each blocks on stdin."""
+def _spawn_cpu_workers(args, seeds, threads, cap, cores):
+    """Started BEFORE the GPU is initialised (no exec from a GPU process); each blocks on stdin.
+    Pinned: PYTHONHASHSEED=0, the golden's string-hash seed -- the oracle's
+    contraction order, like the reference's, follows set iteration (tests/golden/make_golden.py) --
+    and each worker on its own core(s) of `cores` (disjoint sched_setaffinity sets, `--cpu-cores`)."""
     procs = []
+    at = 0
     for s, th in zip(seeds, threads):
+        mine = cores[at:at + th] or cores[-th:]
+        at += th
         env = dict(os.environ, OPENBLAS_NUM_THREADS=str(th), OMP_NUM_THREADS=str(th), MKL_NUM_THREADS=str(th),
-                   CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+                   CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", PYTHONHASHSEED="0")
         cmd = [sys.executable, os.path.abspath(__file__), "--cpu-worker", str(s), "--problem", args.problem,
-               "--config", args.config, "--rank", str(args.rank), "--cpu-cap", str(cap)]
+               "--config", args.config, "--rank", str(args.rank), "--cpu-cap", str(cap),
+               "--cpu-cores", ",".join(str(c) for c in mine)]
         procs.append(subprocess.Popen(cmd, stdin=subprocess.PIPE, stdout=subprocess.PIPE,
                                       stderr=subprocess.DEVNULL, env=env, text=True))
     _CHILDREN.extend(procs)
@@ -477,7 +487,18 @@ def _median(xs):
     return float(np.median(xs)) if xs else None
 
 
-def cpu_summary(per, allc, gpu_runs, cap, workload, cores_avail):
+def reference_iters(cfg_name, rank_tt, seeds):
+    """the reference's own iteration count per seed (tests/golden/runs.json, the golden run: 1 BLAS
+    thread, PYTHONHASHSEED=0) -- a committed fixture, not the reference"""
+    try:
+        runs = json.load(open(os.path.join(HERE, "tests", "golden", "runs.json")))
+    except (OSError, ValueError):
+        return {}
+    stem = os.path.splitext(os.path.basename(cfg_name))[0]
+    return {s: runs[f"{stem}_r{rank_tt}_s{s}"]["num_iters"] for s in seeds if f"{stem}_r{rank_tt}_s{s}" in runs}
+
+
+def cpu_summary(per, allc, gpu_runs, cap, workload, cores_avail, ref_iters=None):
     """cpu_baseline from the oracle workers' lines (`_cpu_worker`) and the GPU's per-seed solves.
     Per seed, both sides are WHOLE-solve s/IPM-iter (solve wall / its iterations, the reference
     runner's statistic, src/utils.py:298-302); a CPU process stopped by the safety cap contributes
@@ -493,6 +514,7 @@ def cpu_summary(per, allc, gpu_runs, cap, workload, cores_avail):
         cs = c["full_solve_s_per_iter"] if full else c["s_per_iter"]
         gs = _median(gpu.get(c["seed"], []))
         rows.append({"seed": c["seed"], "cpu_iters": c.get("full_solve_iters", c["iters"]), "cpu_full_solve": full,
+                     "reference_iters": (ref_iters or {}).get(c["seed"]), "cpu_cores": c.get("cores"),
                      "cpu_s_per_iter": cs, "gpu_s_per_iter": gs,
                      "gpu_over_cpu": gs / cs if gs is not None and cs else None})
     cmed = _median([r["cpu_s_per_iter"] for r in rows])
@@ -505,6 +527,8 @@ def cpu_summary(per, allc, gpu_runs, cap, workload, cores_avail):
                       f"timed seed, all at once, each its seed's whole tt_ipm solve (safety cap {cap:g} s); "
                       f"value = median over seeds of solve wall / IPM iterations",
             "seeds_full_solve": sum(r["cpu_full_solve"] for r in rows), "seeds": len(rows),
+            "iters_cpu_vs_reference": {str(r["seed"]): [r["cpu_iters"], r["reference_iters"]] for r in rows},
+            "hash_seed": "0", "pinned": "one core per worker (sched_setaffinity)",
             "gpu_same_seeds_median": gmed,
             "gpu_over_cpu_ratio_of_medians": (gmed / cmed) if cmed and gmed else None,
             "gpu_over_cpu_median_of_ratios": _median([r["gpu_over_cpu"] for r in rows]),
@@ -598,13 +622,15 @@ def main():
     ap.add_argument("--slot-base", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--queue-file", default=None, help=argparse.SUPPRESS)
     ap.add_argument("--cpu-worker", type=int, default=None, help=argparse.SUPPRESS)
+    ap.add_argument("--cpu-cores", default=None, help=argparse.SUPPRESS)
     ap.add_argument("--gpu-worker", default=None, help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.problem is None:
         base = os.path.basename(args.config)
         args.problem = next(p for p in ("maxcut", "corr_clust", "graphm", "max_stable_set") if base.startswith(p))
     if args.cpu_worker is not None:
-        return _cpu_worker(args.problem, args.config, args.cpu_worker, args.rank, args.cpu_cap)
+        return _cpu_worker(args.problem, args.config, args.cpu_worker, args.rank, args.cpu_cap,
+                           [int(c) for c in args.cpu_cores.split(",")] if args.cpu_cores else None)
     if args.gpu_worker is not None:
         q = None
         if args.queue_file:
@@ -655,8 +681,11 @@ def main():
         # one single-thread oracle process per distinct timed seed, whole solves (the reference
         # runner's statistic, src/utils.py:298-302), plus one seed on all the share's cores as BLAS
         # threads (bounded: a side figure)
-        cpu_procs = _spawn_cpu_workers(args, cpu_seeds, [1] * len(cpu_seeds), args.cpu_cap)
-        allcore_proc = _spawn_cpu_workers(args, cpu_seeds[:1], [cores], min(args.cpu_cap or 60.0, 60.0))
+        # the share's last cores, one per seed (the GPU processes are done by the time they run: the
+        # workers are released after the GPU's timed region and solo solves)
+        share = sorted(os.sched_getaffinity(0))[-cores:]
+        cpu_procs = _spawn_cpu_workers(args, cpu_seeds, [1] * len(cpu_seeds), args.cpu_cap, share[::-1])
+        allcore_proc = _spawn_cpu_workers(args, cpu_seeds[:1], [cores], min(args.cpu_cap or 60.0, 60.0), share)
 
     import torch
     import torch.distributed as dist
@@ -792,7 +821,8 @@ def main():
             allc = _release(allcore_proc)[0]
         gpu_side = solo or results  # the GPU's one-at-a-time latency when measured
         cpu = cpu_summary(per, allc, gpu_side, args.cpu_cap,
-                          f"{args.problem} dim={config['dim']} rank={args.rank}", cores_avail=cores)
+                          f"{args.problem} dim={config['dim']} rank={args.rank}", cores_avail=cores,
+                          ref_iters=reference_iters(args.config, args.rank, cpu_seeds))
 
     if rank == 0:
         line, detail = compose_line(

@@ -331,6 +331,10 @@ if __name__ == "__main__":
         from tests.golden import make_local
         make_local.main(_import_reference)
         sys.exit(0)
+    if len(sys.argv) > 1 and sys.argv[1] == "step":  # step-size eigen-ALS fixtures (a19)
+        from tests.golden import make_step
+        make_step.main(_import_reference)
+        sys.exit(0)
     if len(sys.argv) < 2 or sys.argv[1] not in ("runs", "prims", "all"):
         # no default: a bare invocation must not start regenerating (and rewriting) runs.json
         sys.exit("usage: make_golden.py runs|prims|all [KEY ...] [-jN] | one PROB CFG SEED RANK FIXED OUT [NMAX]"

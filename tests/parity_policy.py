@@ -149,26 +149,48 @@ def unmodified_runs(key):
     return [RUNS[key]] + _twins(key, NOISE_TWINS)
 
 
+def _relaxed_box(runs):
+    """iterations within 2 of the runs' range, gap / feas within RELAXED_FACTOR of their range"""
+    return {"num_iters": (min(x["num_iters"] for x in runs) - 2, max(x["num_iters"] for x in runs) + 2),
+            **{k: (min(abs(x[k]) for x in runs) / RELAXED_FACTOR, max(abs(x[k]) for x in runs) * RELAXED_FACTOR)
+               for k in ENVELOPE_KEYS}}
+
+
+def _assert_inside(box, r, what):
+    assert box["num_iters"][0] <= r["num_iters"] <= box["num_iters"][1], (what, "num_iters", r["num_iters"], box)
+    for k in ENVELOPE_KEYS:
+        assert box[k][0] <= abs(r[k]) <= box[k][1], (what, k, r[k], box[k])
+
+
 def check_end_point(key, r):
     """End point of a key whose unmodified reference runs branch: the device must land where one of
-    those runs lands.
-    * non-pathological device end point: inside the envelope (widened 2x) of the unmodified runs --
-      of the non-pathological ones when some of them end pathological;
-    * pathological device end point (src/utils.py:67): allowed only when at least one of the
-      reference's own unmodified runs ends pathological too (maxcut_12 r=2: seeds 23, 1, ...); a
-      pathological end point has no meaningful envelope (stall / iteration-cap terminations), so
-      only the basin is compared."""
+    those runs lands (round 6: fixed before the round's device runs of the affected keys, ADVICE r5
+    medium / VERDICT r5 item 2).
+    * finite gap and feasibility, always;
+    * non-pathological device end point (src/utils.py:67): inside the envelope (widened 2x) of the
+      unmodified runs that converge when there are at least two of them; when exactly ONE unmodified
+      run converges (a single run has no spread to widen) within its relaxed box -- iterations within
+      2, gap and feas within RELAXED_FACTOR (the known-departure floor's factor); when none converges,
+      it fails (the reference never converges there);
+    * pathological device end point: only where some unmodified run ends pathological, and then
+      within the relaxed box of THOSE pathological runs (iterations within 2 of their range, gap and
+      feas within RELAXED_FACTOR of their range), so a stall at another iteration count or another
+      magnitude fails."""
+    assert np.isfinite(r["gap"]) and np.isfinite(r["feas"]), ("non-finite end point", r)
     runs = unmodified_runs(key)
+    path = [x for x in runs if is_pathological(x)]
+    good = [x for x in runs if not is_pathological(x)]
     if is_pathological(r):
-        assert any(is_pathological(x) for x in runs), (
-            "pathological end point where every unmodified reference run converges", r,
-            [(x["num_iters"], x["gap"]) for x in runs])
+        assert path, ("pathological end point where every unmodified reference run converges", r,
+                      [(x["num_iters"], x["gap"]) for x in runs])
+        _assert_inside(_relaxed_box(path), r, "pathological runs' relaxed box")
         return
-    good = [x for x in runs if not is_pathological(x)] or runs
-    env = envelope_of(good)
-    assert env["num_iters"][0] <= r["num_iters"] <= env["num_iters"][1], ("num_iters", r["num_iters"], env)
-    for k in ENVELOPE_KEYS:
-        assert env[k][0] <= abs(r[k]) <= env[k][1], (k, r[k], env[k])
+    assert good, ("converged end point where every unmodified reference run ends pathological", r,
+                  [(x["num_iters"], x["gap"]) for x in runs])
+    if len(good) == 1:
+        _assert_inside(_relaxed_box(good), r, "the single converged run's relaxed box")
+        return
+    _assert_inside(envelope_of(good), r, "converged runs' envelope")
 
 
 # Keys whose device run departs from every UNMODIFIED reference run under the rule above, with the
@@ -176,9 +198,14 @@ def check_end_point(key, r):
 # of the strict rule, after asserting the relaxed one (check_relaxed) so that anything worse still
 # fails; a key that passes the strict rule passes.
 KNOWN_DEPARTURES = {
-    "maxcut_10_r1_s14": "bimodal step-size eigen-ALS at assembly 5 (zs 0.5019 or 0.4057 depending only on "
-                        "contraction summation order): the device takes the 0.4057 branch, as the reference's "
-                        "own Jacobi-SVD twin _j4 does, and ends one iteration later than the unmodified runs",
+    "maxcut_10_r1_s14": "step-size eigen-ALS on degenerate local eigenproblems (tests/golden/step.npz, the "
+                        "reference's own calls): on the reference's inputs the device reproduces every step size "
+                        "(<= 4e-14) but assembly 4's dual predictor call (c17: clusters of 4 .. 112 equal smallest "
+                        "eigenvalues, tools/step_clusters.py) returns other eigenvectors of the same eigenspaces than "
+                        "ARPACK's Krylov vectors from v0 -- 4 of its 18 local solves truncate to other ranks, exactly "
+                        "as the oracle with exact eigensolves does (tests/test_oracle_step.py); warm-started from that "
+                        "solution the corrector's dual eigen-ALS (c19) settles at 0.5019 where the reference's goes on "
+                        "to 0.4057 (tests/test_gpu_step.py chain), and the run ends one iteration later",
     "maxcut_12_r2_s80": "noise-level final steps: the device follows the golden within 0.075 of the noise "
                         "bound through assembly 8, the reference's own runs separate there (> 1e-3), and the "
                         "device's last step ends at gap 7.6e-4 against 5.8-5.9e-4",
