@@ -542,18 +542,28 @@ def test_maxcut_12_extra_seeds_on_device(dev, seed):
     """The 8-GPU schedule's extra maxcut_12 r=2 seeds (bench.EXTRA_SEEDS: the first non-pathological
     reference runs in seed order): the device's first Newton system equals the reference's (1e-8);
     where the golden has hash twins (full: the whole-solve policy; bounded: `check_bounded_follow`)
-    the device follows one of the reference's runs until their own noise branches; the end point is
+    the device follows one of the reference's runs until their own noise branches; the end point lands
+    where one of the reference's unmodified runs lands (full twins: `check_end_point`, pathological
+    only within the relaxed box of the reference's pathological runs), or, with bounded twins only, is
     non-pathological (src/utils.py:67) within 2 iterations of the golden -- or, for a
     KNOWN_EXTRA_DEPARTURES key, an expected failure with its mechanism, after its floor
-    (`check_extra_departure_floor`: the device follows the named bounded twin, finite end point)."""
+    (`check_extra_follow_floor` / `check_extra_departure_floor`: the device follows the reference's
+    runs through their branch point, finite end point)."""
     from tests.parity_policy import (KNOWN_EXTRA_DEPARTURES, bounded_twins, check_bounded_follow,
-                                     check_extra_departure_floor)
+                                     check_extra_departure_floor, check_extra_follow_floor)
     key = f"maxcut_12_r2_s{seed}"
     trace = []
     g, r = _run(key, trace)
     assert max(_rel(trace[0][k], g["trace"][0][k]) for k in KEYS4) <= 1e-8
     if any(key + x in RUNS for x in ("_t8", "_h1", "_h2", "_h3")):
-        _policy(key, trace, r)
+        try:
+            _policy(key, trace, r)
+        except AssertionError as e:
+            if key not in KNOWN_EXTRA_DEPARTURES:
+                raise
+            name, per = check_extra_follow_floor(key, trace, r)
+            print(key, "follows", name, ["%.0e" % v for v in per])
+            pytest.xfail(f"{key}: iterations {r['num_iters']}, gap {r['gap']:.3e}: {KNOWN_EXTRA_DEPARTURES[key]} ({e})")
         return
     if bounded_twins(key):
         name, upto, per = check_bounded_follow(key, trace)
