@@ -100,6 +100,10 @@ void *ttk_ctx_stream(ttk_ctx ctx);
  *                   its first use -- one L2 round trip per step instead of three; 0: the loads
  *                   where they are used (same arithmetic in the same order: bit-identical; default
  *                   from env TTK_TRI_HOIST, else 1)
+ * TTK_KNOB_TRI_ONE    largest n (<= 513) whose Householder tridiagonalisation in ttk_syev_extreme runs
+ *                   as ONE one-workgroup launch (tri_wg_kernel: the per-step launches' arithmetic,
+ *                   bit-identical) instead of one launch per Householder step; 0: never (default from
+ *                   env TTK_TRI_ONE, else 512)
  * ttk_ctx_set_knob stores value and returns the previous one in *old (may be NULL). */
 enum ttk_knob {
   TTK_KNOB_FUSED_APPLY = 0,
@@ -115,7 +119,8 @@ enum ttk_knob {
   TTK_KNOB_SCHUR_PREP = 10,
   TTK_KNOB_SPLITK_FUSED = 11,
   TTK_KNOB_TRI_HOIST = 12,
-  TTK_KNOB_COUNT = 13
+  TTK_KNOB_TRI_ONE = 13,
+  TTK_KNOB_COUNT = 14
 };
 int ttk_ctx_set_knob(ttk_ctx ctx, int knob, int value, int *old);
 int ttk_ctx_get_knob(ttk_ctx ctx, int knob, int *value);

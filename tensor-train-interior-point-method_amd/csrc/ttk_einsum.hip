@@ -1165,6 +1165,7 @@ struct ApplyLaunch {
   // *dep); -1: none
   int prod = -1;
   unsigned *dep = nullptr;
+  unsigned tick_base = 0;  // with dep: workgroup roles by start order (ttk::ticket), base of this launch
 };
 
 // MF: the launch carries MFMA-stage rows (1024 threads, <= 128 VGPRs); otherwise VALU rows only (at
@@ -1172,11 +1173,14 @@ struct ApplyLaunch {
 template <bool MF>
 __global__ __launch_bounds__(MF ? 1024 : 512) void fused_apply_multi_kernel(ApplyLaunch L) {
   extern __shared__ double sm[];
+  // a hand-off launch numbers its workgroups by start order (the producer task's rows first), so a
+  // consumer only ever waits for workgroups that are already running (ttk::ticket)
+  const int blk = L.dep ? ttk::ticket(L.dep, L.tick_base) : (int)blockIdx.x;
   int t = 0;
-  while (t + 1 < L.ntask && (int)blockIdx.x >= L.off[t + 1]) ++t;
+  while (t + 1 < L.ntask && blk >= L.off[t + 1]) ++t;
   const ApplyTask &T = L.task[t];
   const ApplyArgs &g0 = T.t[0];
-  const int cs = g0.csplit, a = ((int)blockIdx.x - L.off[t]) / cs, h = ((int)blockIdx.x - L.off[t]) % cs;
+  const int cs = g0.csplit, a = (blk - L.off[t]) / cs, h = (blk - L.off[t]) % cs;
   const int ni = g0.ni, nc = g0.nc, tid = threadIdx.x, nt = blockDim.x;
   double *orow = sm, *acc = sm + ni * nc, *work = acc + ni * nc;
   if (L.dual && T.nterms == 2) {
@@ -1324,9 +1328,11 @@ extern "C" int ttk_dep_timeouts(unsigned *out, int reset) {  // in-launch hand-o
   ttk::Ctx &cx = ttk::ctx();
   *out = 0;
   if (!cx.dep) return TTK_OK;
-  TTK_HIP(cx.stream ? hipStreamSynchronize(cx.stream) : hipDeviceSynchronize());
-  TTK_HIP(hipMemcpy(out, cx.dep + 1, sizeof(unsigned), hipMemcpyDeviceToHost));
-  if (reset) TTK_HIP(hipMemset(cx.dep + 1, 0, sizeof(unsigned)));
+  // ordered on the context's stream: the read follows the solve's kernels, the reset
+  // precedes the next solve's, one stream wait for both
+  TTK_HIP(hipMemcpyAsync(out, cx.dep + 1, sizeof(unsigned), hipMemcpyDeviceToHost, cx.stream));
+  if (reset) TTK_HIP(hipMemsetAsync(cx.dep + 1, 0, sizeof(unsigned), cx.stream));
+  TTK_HIP(hipStreamSynchronize(cx.stream));
   return TTK_OK;
 }
 
@@ -1892,6 +1898,8 @@ int ttk::schur_apply(void *stream, int64_t handle, const double *v, double *out)
     const int nprod = L.off[1] - L.off[0];
     cx.dep_total += (unsigned)nprod;
     L.dep = cx.dep;
+    L.tick_base = cx.tick_total;
+    cx.tick_total += (unsigned)L.off[L.ntask];
     for (int t = 0; t < L.ntask; ++t) {
       const int s = op.one_src[t][0], tt = op.one_src[t][1];
       for (int k = 0; k < L.task[t].nterms; ++k) {

@@ -39,6 +39,7 @@ struct Ctx {
   int64_t schur_wcap = 0;
   unsigned *dep = nullptr;    // in-launch hand-off arrival counter (monotonic; ttk_einsum.hip)
   unsigned dep_total = 0;     // arrivals of every hand-off launch issued on this context so far
+  unsigned tick_total = 0;    // workgroup tickets (dep[2]) of every hand-off launch issued so far
   unsigned *splitk_cnt = nullptr;  // per-tile arrival counters of the one-launch split-K GEMM (reset by it)
   double *lgmres = nullptr;   // LGMRES partial sums
   int64_t lgmres_n = 0;
@@ -60,7 +61,7 @@ struct Ctx {
                               env_int("TTK_APPLY_DUAL", 1) != 0 ? 1 : 0, env_int("TTK_RCOND_EXACT", 0) != 0 ? 1 : 0,
                               env_int("TTK_SCHUR_ONE", 1) != 0 ? 1 : 0, env_int("TTK_ARNOLDI_ONE", 1) != 0 ? 1 : 0,
                               env_int("TTK_SCHUR_PREP", 1) != 0 ? 1 : 0, env_int("TTK_SPLITK_FUSED", 1) != 0 ? 1 : 0,
-                              env_int("TTK_TRI_HOIST", 1) != 0 ? 1 : 0};
+                              env_int("TTK_TRI_HOIST", 1) != 0 ? 1 : 0, env_int("TTK_TRI_ONE", 512)};
 };
 Ctx &ctx();
 Ctx *ctx_swap(Ctx *c);       // bind c to the calling thread, return the previous binding

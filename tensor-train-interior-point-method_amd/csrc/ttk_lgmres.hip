@@ -321,11 +321,13 @@ __global__ __launch_bounds__(256) void arnoldi_fused_kernel(double *__restrict__
                                                             double *__restrict__ partials, int nchunk,
                                                             double *__restrict__ normpart, int nblk, double *base,
                                                             int max_k, double haptol, Ctl cl, unsigned *dep,
-                                                            unsigned t_dots, unsigned t_upd) {
+                                                            unsigned t_dots, unsigned t_upd, unsigned tick_base) {
   __shared__ double h[MAXV + 2];
   __shared__ double red[16];
   const bool stopped = ctl_stopped(cl);
-  const int tid = threadIdx.x, b = blockIdx.x;
+  // roles by start order (ttk::ticket): the dot blocks first, the finish last -- every wait is on
+  // workgroups that are already running
+  const int tid = threadIdx.x, b = ttk::ticket(dep, tick_base);
   const int ndot = nchunk * (it + 1);
   double *w = V + (int64_t)(it + 1) * n;
   if (b < ndot) {  // arnoldi_dot_kernel
@@ -508,8 +510,10 @@ static int arnoldi_launch(hipStream_t st_, double *V, int n, int it, double *hh,
       const unsigned ndot = (unsigned)(nchunk * (it + 1));
       const unsigned t_dots = cx.dep_total + ndot, t_upd = t_dots + (unsigned)nblk;
       cx.dep_total = t_upd;
+      const unsigned tick = cx.tick_total;
+      cx.tick_total += ndot + (unsigned)nblk + 1u;
       hipLaunchKernelGGL(arnoldi_fused_kernel, dim3(ndot + nblk + 1), dim3(256), 0, st_, V, n, it, partials, nchunk,
-                         normpart, nblk, hh, max_k, haptol, cl, cx.dep, t_dots, t_upd);
+                         normpart, nblk, hh, max_k, haptol, cl, cx.dep, t_dots, t_upd, tick);
       TTK_LAUNCH_CHECK();
       return TTK_OK;
     }

@@ -2141,6 +2141,171 @@ __global__ __launch_bounds__(256) void tri_tail_kernel(double *A, int n, double 
   for (int j = kp + 1 + tid; j < n; j += 256) A[(int64_t)kp * n + j] = vp[j - kp - 1];
 }
 
+// The whole tridiagonalisation of tri_step_hoist_kernel + tri_tail_kernel in ONE workgroup (round 6,
+// one launch instead of one per Householder step).  The multi-workgroup form's
+// blocks of 4 rows become "virtual blocks": 16 waves take the rows > k round-robin, each row's pending
+// update, dot and p entry computed exactly as there (the same expressions, loops and wave reductions),
+// and the per-block partial sums of tau p.v are formed in block order from the rows' contributions --
+// every stored value and every reduction is the multi-launch path's, so the results are bit-identical
+// (tools/dump_kernels.py).  A stays in global memory (L2-resident); the reflector, p and partials live
+// in LDS, double-buffered per step as the global vectors were.  NR * 64 >= n - 1 (row elements per lane).
+// LDS (doubles): xs n+1 | vb 2n | pvb 2n | crow n.  Four block barriers per step.
+template <int NR, int QB>
+__global__ __launch_bounds__(1024) void tri_wg_kernel(double *A, int n, double *tv, double *ov, double *dv, int nblk) {
+  extern __shared__ double tl[];
+  __shared__ double red[16];
+  __shared__ double s_k, s_tau_prev;
+  double *xs = tl, *vb = xs + n + 1, *pvb = vb + 2 * n, *crow = pvb + 2 * n;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  if (tid == 0) {
+    s_k = 0.0;
+    s_tau_prev = 0.0;
+  }
+  __syncthreads();
+  for (int k = 0; k + 2 < n; ++k) {
+    const int kp = k - 1, m = n - k - 1;
+    const double *pvp = pvb + (kp & 1) * n, *vp = vb + (kp & 1) * n;
+    double *pvc = pvb + (k & 1) * n, *vc = vb + (k & 1) * n;
+    const double taup = s_tau_prev, K = s_k;
+    // ---- row k with step k-1's pending update (tri_step_hoist's expression) and the sigma partials
+    // of threads 0..255 (i = 2 + tid + 256 u, the multi-launch block's mapping), from registers
+    const double v0 = vp[0], p0 = pvp[0];
+    const double wk = taup != 0.0 ? p0 - K * v0 : 0.0, vk = taup != 0.0 ? v0 : 0.0;
+    auto rebuilt = [&](int i) {  // xs[i] = A[k, k + i] with the pending update
+      const int j = k + i, jj = j - kp - 1;
+      double a = A[(int64_t)k * n + j];
+      if (taup != 0.0) a -= fma(wk, vp[jj], vk * fma(-K, vp[jj], pvp[jj]));
+      return a;
+    };
+    double part = 0.0;
+    if (tid < 256) {
+      for (int i = 2 + tid; i <= m; i += 256) {
+        const double a = rebuilt(i);
+        xs[i] = a;
+        part += a * a;
+      }
+    } else if (tid < 258) {
+      xs[tid - 256] = rebuilt(tid - 256);
+    }
+    if (wid < 4) {
+      part = ttk::wave_sum(part);
+      if (lane == 0) red[wid] = part;
+    }
+    __syncthreads();
+    double sigma = 0.0;
+    for (int i = 0; i < 4; ++i) sigma += red[i];
+    const double alpha = xs[1];
+    double tau = 0.0, beta = alpha;
+    if (sigma > 0.0) {
+      beta = -copysign(sqrt(alpha * alpha + sigma), alpha);
+      tau = (beta - alpha) / beta;
+    }
+    const double sc = sigma > 0.0 ? 1.0 / (alpha - beta) : 1.0;
+    __syncthreads();  // every thread has read xs[1] and red
+    for (int i = 1 + tid; i <= m; i += 1024) {
+      const double v = (i == 1) ? 1.0 : xs[i] * sc;
+      xs[i] = v;
+      vc[i - 1] = v;
+    }
+    if (tid == 0) {
+      tv[k] = tau;
+      ov[k] = beta;
+      dv[k] = xs[0];
+    }
+    if (kp >= 0)  // reflector k-1 into A's row k-1 (nobody reads that row again)
+      for (int j = k + tid; j < n; j += 1024) A[(int64_t)kp * n + j] = vp[j - k];
+    __syncthreads();
+    // ---- rows r > k, round-robin over the 16 waves, QB rows' loads in flight per wave; the row-
+    // independent operands (reflector k-1, p, reflector k) in registers once per step
+    double rv[NR], rp[NR], rx[NR];
+#pragma unroll
+    for (int u = 0; u < NR; ++u) {
+      const int j = k + 1 + lane + 64 * u, jj = j - kp - 1;
+      rv[u] = j < n ? vp[jj] : 0.0;
+      rp[u] = j < n ? pvp[jj] : 0.0;
+      rx[u] = j < n ? xs[j - k] : 0.0;
+    }
+    for (int r0 = k + 1 + wid; r0 < n; r0 += 16 * QB) {
+      double ra[QB][NR];
+#pragma unroll
+      for (int q = 0; q < QB; ++q) {
+        const int r = r0 + 16 * q;
+#pragma unroll
+        for (int u = 0; u < NR; ++u) {
+          const int j = k + 1 + lane + 64 * u;
+          ra[q][u] = (r < n && j < n) ? A[(int64_t)r * n + j] : 0.0;
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < QB; ++q) {
+        const int r = r0 + 16 * q;
+        if (r >= n) break;
+        const int ir = r - kp - 1;
+        const double vi = vp[ir], pi = pvp[ir];
+        double *ar = A + (int64_t)r * n;
+        const double wi = taup != 0.0 ? pi - K * vi : 0.0, vv = taup != 0.0 ? vi : 0.0;
+        double acc = 0.0;
+#pragma unroll
+        for (int u = 0; u < NR; ++u) {
+          const int j = k + 1 + lane + 64 * u;
+          if (j < n) {
+            double a = ra[q][u];
+            if (taup != 0.0) {
+              a -= fma(wi, rv[u], vv * fma(-K, rv[u], rp[u]));  // tri_step_kernel's contraction
+              ar[j] = a;
+            }
+            acc = fma(a, rx[u], acc);
+          }
+        }
+        acc = ttk::wave_sum(acc);
+        if (lane == 0) {
+          const double pr = tau * acc;
+          pvc[r - k - 1] = pr;
+          double contrib = 0.0;
+          contrib += pr * xs[r - k];
+          crow[r] = contrib;
+        }
+      }
+    }
+    __syncthreads();
+    // ---- the blocks' partials (rows [4b, 4b+4) above k, in row order, as block_sum adds the waves'
+    // values) summed lane-strided in wave 0 for the next step's K, as tri_step_hoist's wave 0 does
+    if (wid == 0) {
+      double acc = 0.0;
+      if (tau != 0.0) {
+        for (int b = lane; b < nblk; b += 64) {
+          const int rb0 = 4 * b, rb1 = rb0 + 4 < n ? rb0 + 4 : n, rs = rb0 > k + 1 ? rb0 : k + 1;
+          double t = 0.0;
+          for (int w = 0; w < 4; ++w) {
+            const int r = rs + w;
+            t += r < rb1 ? crow[r] : 0.0;
+          }
+          acc += t;
+        }
+      }
+      acc = ttk::wave_sum(acc);
+      if (lane == 0) {
+        s_k = 0.5 * tau * acc;
+        s_tau_prev = tau;
+      }
+    }
+    __syncthreads();
+  }
+  // ---- tri_tail_kernel: step n-3's pending update of the trailing 2 x 2 block, reflector n-3 into row n-3
+  {
+    const int kp = n - 3;
+    const double *pvp = pvb + (kp & 1) * n, *vp = vb + (kp & 1) * n;
+    const double taup = s_tau_prev, K = s_k;
+    if (tid < 4 && taup != 0.0) {
+      const int r = n - 2 + (tid >> 1), j = n - 2 + (tid & 1);
+      const int ir = r - kp - 1, jj = j - kp - 1;
+      const double vi = vp[ir], wi = pvp[ir] - K * vi, vj = vp[jj];
+      A[(int64_t)r * n + j] -= vi * (pvp[jj] - K * vj) + wi * vj;
+    }
+    for (int j = kp + 1 + tid; j < n; j += 1024) A[(int64_t)kp * n + j] = vp[j - kp - 1];
+  }
+}
+
 template <typename K>
 void allow_big_lds(K kernel, size_t bytes) {
   if (bytes > 65536) (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kernel),
@@ -3128,6 +3293,16 @@ int ttk_syev_extreme(void *stream, const double *A, int n, int which, double *ev
     const int nblk = (n + rb - 1) / rb;
     double *pvb = gv + 11 * (int64_t)n, *vbuf = pvb + 2 * (int64_t)n, *partb = vbuf + 2 * (int64_t)n;
     TTK_HIP(hipMemcpyAsync(Aw, A, sizeof(double) * (size_t)n * n, hipMemcpyDeviceToDevice, st));
+    const int one_max = ttk::ctx().knob[TTK_KNOB_TRI_ONE];
+    if (rb == 4 && n <= 513 && n <= one_max) {  // the whole tridiagonalisation in one workgroup
+      const size_t shm = (size_t)(6 * n + 1) * sizeof(double);
+      if (n <= 257)
+        hipLaunchKernelGGL((tri_wg_kernel<4, 4>), dim3(1), dim3(1024), shm, st, Aw, n, tv, ov, dv, nblk);
+      else
+        hipLaunchKernelGGL((tri_wg_kernel<8, 1>), dim3(1), dim3(1024), shm, st, Aw, n, tv, ov, dv, nblk);
+      TTK_LAUNCH_CHECK();
+      return tri_finish_launch(st, Aw, n, which, gv, ev, vec);
+    }
     const int hoist = rb == 4 && n <= 512 && ttk::ctx().knob[TTK_KNOB_TRI_HOIST] ? (n <= 256 ? 1 : 2) : 0;
     for (int k = 0; k + 2 < n; ++k) {
       if (hoist == 1)

@@ -165,6 +165,7 @@ int ttk::dep_counter(void *stream) {
   TTK_HIP(hipMalloc(reinterpret_cast<void **>(&cx.dep), 256));
   TTK_HIP(hipMemsetAsync(cx.dep, 0, 256, TTK_STREAM(stream)));
   cx.dep_total = 0;
+  cx.tick_total = 0;
   return TTK_OK;
 }
 

@@ -449,6 +449,32 @@ def test_syev_fused_matches_two_launch(dev, n):
             assert min(np.abs(v1 - v2).max(), np.abs(v1 + v2).max()) <= 1e-8, name
 
 
+@pytest.mark.parametrize("n", [129, 150, 257, 258, 300, 513])
+def test_syev_tri_one_workgroup_bit_identical(dev, n):
+    """the one-workgroup tridiagonalisation (TTK_KNOB_TRI_ONE, one launch) and one launch per
+    Householder step give the same eigenpair bit for bit, on every case of _sym_cases (degenerate and
+    rank-deficient ones included), and the pair is an eigenpair (1e-10 residual)"""
+    from ttipm_amd import _lib
+    rng = _rng(17 * n)
+    for name, A in _sym_cases(n, rng):
+        for largest in (False, True):
+            out = []
+            for v in (513, 0):
+                old = _set_knob(_lib.KNOB_TRI_ONE, v)
+                try:
+                    l0 = dev.lib.ttk_launch_count()
+                    lam, vec = dev.syev_extreme(dev.from_numpy(A), largest=largest)
+                    launches = dev.lib.ttk_launch_count() - l0
+                finally:
+                    _set_knob(_lib.KNOB_TRI_ONE, old)
+                out.append((lam, dev.read(vec), launches))
+            (l1, v1, n1), (l2, v2, n2) = out
+            assert l1 == l2 and np.array_equal(v1, v2), (name, largest, l1, l2)
+            assert n1 < n2 and n1 <= 4, (n1, n2)  # copy + one tridiagonalisation + finish
+            scale = max(1.0, np.abs(A).max())
+            assert np.linalg.norm(A @ v1 - l1 * v1) <= 1e-10 * scale * np.sqrt(n), name
+
+
 def test_elementwise_and_reductions(dev):
     rng = _rng(5)
     a = rng.standard_normal((3, 4, 5))

@@ -50,7 +50,31 @@ def totals():
     print("totals_us " + " ".join(f"{t:7.1f}" for t in out), flush=True)
 
 
+def tri_one():
+    """One-workgroup tridiagonalisation (TTK_KNOB_TRI_ONE) against one launch per Householder step:
+    latency per n and the eigenpair bits (must be identical)."""
+    from ttipm_amd import _lib
+    rng = np.random.default_rng(0)
+    st = D._stream()
+    print("n      one_wg_us  per_step_us  identical")
+    for n in [129, 144, 160, 192, 224, 256, 257, 288, 320, 384, 448, 512]:
+        M = rng.standard_normal((n, n))
+        A = D.from_numpy(M + M.T)
+        wx = D.empty(int(lib.ttk_syev_extreme_work(n)))
+        res, ts = [], []
+        for v in (512, 0):
+            lib.ttk_ctx_set_knob(None, _lib.KNOB_TRI_ONE, v, None)
+            buf = D.empty(n + 1)
+            ts.append(timed(lambda: lib.ttk_syev_extreme(st, D._p(A), n, 0, D._p(buf), D._p(buf[1:]), D._p(wx)),
+                            reps=20))
+            res.append(D.read(buf))
+        lib.ttk_ctx_set_knob(None, _lib.KNOB_TRI_ONE, 512, None)
+        print(f"{n:5d} {ts[0]:10.1f} {ts[1]:12.1f}  {bool(np.array_equal(res[0], res[1]))}", flush=True)
+
+
 def main():
+    if "--tri" in sys.argv:
+        return tri_one()
     if "--steps" in sys.argv:
         return step_phases()
     if "--totals" in sys.argv:

@@ -18,7 +18,8 @@ def main(path):
     rng = np.random.default_rng(0)
     st = D._stream()
     out = {}
-    for n in [3, 5, 10, 17, 40, 63, 64, 80, 100, 127, 128, 139, 200, 513, 1000, 1900]:
+    for n in [3, 5, 10, 17, 40, 63, 64, 80, 100, 127, 128, 129, 139, 150, 192, 200, 256, 257, 258, 300, 384, 512, 513,
+              1000, 1900]:
         for which in (0, 1):
             M = rng.standard_normal((n, n))
             A = D.from_numpy(M + M.T)
