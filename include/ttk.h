@@ -103,7 +103,8 @@ void *ttk_ctx_stream(ttk_ctx ctx);
  * TTK_KNOB_TRI_ONE    largest n (<= 513) whose Householder tridiagonalisation in ttk_syev_extreme runs
  *                   as ONE one-workgroup launch (tri_wg_kernel: the per-step launches' arithmetic,
  *                   bit-identical) instead of one launch per Householder step; 0: never (default from
- *                   env TTK_TRI_ONE, else 512)
+ *                   env TTK_TRI_ONE, else 0: measured slower per call from n = 144 on -- one CU's L2
+ *                   bandwidth and serial latency against 64 workgroups per step)
  * ttk_ctx_set_knob stores value and returns the previous one in *old (may be NULL). */
 enum ttk_knob {
   TTK_KNOB_FUSED_APPLY = 0,

@@ -770,8 +770,10 @@ __device__ __forceinline__ double lds_chain(const double *a, int sa, const doubl
 // tid / nt: this row's threads (the whole block, or one half of it when a task's two terms run side
 // by side, see fused_apply_multi_kernel); every output element is still one thread's sequential chain,
 // so the thread count never changes a result.  Three block barriers, unconditional.
-// CHAIN: compile the prefetched FMA chains (lds_chain; used when g.chain) -- off in the 1024-thread
-// launches, whose 128-VGPR budget they would exceed
+// CHAIN: compile the prefetched FMA chains (lds_chain; used when g.chain) -- off in the MFMA-row
+// multi-task launch (fused_apply_multi_kernel<true>), which already sits at the 128 VGPRs of its
+// 1024-thread bound; the 1024-thread fused_apply_kernel / fused_apply_group_kernel keep them at 83 / 86
+// VGPRs without scratch (hipcc -Rpass-analysis=kernel-resource-usage, round 6)
 template <bool DIRECT, bool CHAIN = true>
 __device__ void apply_row(const ApplyArgs &g, int a, double *sm, double *orow, int tid, int nt) {
 #ifdef TTK_VALU_PROFILE

@@ -61,7 +61,7 @@ struct Ctx {
                               env_int("TTK_APPLY_DUAL", 1) != 0 ? 1 : 0, env_int("TTK_RCOND_EXACT", 0) != 0 ? 1 : 0,
                               env_int("TTK_SCHUR_ONE", 1) != 0 ? 1 : 0, env_int("TTK_ARNOLDI_ONE", 1) != 0 ? 1 : 0,
                               env_int("TTK_SCHUR_PREP", 1) != 0 ? 1 : 0, env_int("TTK_SPLITK_FUSED", 1) != 0 ? 1 : 0,
-                              env_int("TTK_TRI_HOIST", 1) != 0 ? 1 : 0, env_int("TTK_TRI_ONE", 512)};
+                              env_int("TTK_TRI_HOIST", 1) != 0 ? 1 : 0, env_int("TTK_TRI_ONE", 0)};
 };
 Ctx &ctx();
 Ctx *ctx_swap(Ctx *c);       // bind c to the calling thread, return the previous binding
