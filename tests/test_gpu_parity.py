@@ -497,8 +497,9 @@ def test_bounded_trace_matches_reference(dev, key):
 def test_maxcut_12_rank2_matches_reference_trajectory(dev):
     """BASELINE configs[4] (maxcut_12 r=2 seed 80) under the whole-solve parity policy
     (tests/parity_policy.py): the device follows one of the reference's unmodified runs (golden, hash
-    twin `_h1`) within 50x the reference's noise until that noise branches, then ends inside their
-    envelope (a KNOWN_DEPARTURES key: expected failure of the strict rule above the relaxed one)."""
+    twins `_h1` .. `_h3`) within 50x the reference's noise until that noise branches, then ends inside
+    their envelope (round 6: with the full twins `_h2` / `_h3` -- gap 5.86e-4 / 8.33e-4 -- the
+    reference's own end-point spread covers the device's 7.6e-4; asserted, no longer an expected failure)."""
     trace = []
     g, r = _run("maxcut_12_r2_s80", trace)
     name, per, cum = _policy("maxcut_12_r2_s80", trace, r)
@@ -549,8 +550,8 @@ def test_maxcut_12_extra_seeds_on_device(dev, seed):
     KNOWN_EXTRA_DEPARTURES key, an expected failure with its mechanism, after its floor
     (`check_extra_follow_floor` / `check_extra_departure_floor`: the device follows the reference's
     runs through their branch point, finite end point)."""
-    from tests.parity_policy import (KNOWN_EXTRA_DEPARTURES, bounded_twins, check_bounded_follow,
-                                     check_extra_departure_floor, check_extra_follow_floor)
+    from tests.parity_policy import (EXTRA_DEPARTURE_FOLLOWS, KNOWN_EXTRA_DEPARTURES, bounded_twins,
+                                     check_bounded_follow, check_extra_departure_floor, check_extra_follow_floor)
     key = f"maxcut_12_r2_s{seed}"
     trace = []
     g, r = _run(key, trace)
@@ -561,7 +562,10 @@ def test_maxcut_12_extra_seeds_on_device(dev, seed):
         except AssertionError as e:
             if key not in KNOWN_EXTRA_DEPARTURES:
                 raise
-            name, per = check_extra_follow_floor(key, trace, r)
+            if key in EXTRA_DEPARTURE_FOLLOWS:  # the device's branch is a bounded twin's (s11: h3)
+                name, per = check_extra_departure_floor(key, trace, r)
+            else:
+                name, per = check_extra_follow_floor(key, trace, r)
             print(key, "follows", name, ["%.0e" % v for v in per])
             pytest.xfail(f"{key}: iterations {r['num_iters']}, gap {r['gap']:.3e}: {KNOWN_EXTRA_DEPARTURES[key]} ({e})")
         return

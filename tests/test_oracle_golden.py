@@ -281,9 +281,11 @@ def test_extra_departure_floor_rule():
 
     from tests.parity_policy import (BOUNDED_TWINS, EXTRA_DEPARTURE_FOLLOWS, KNOWN_EXTRA_DEPARTURES, RUNS,
                                      check_extra_departure_floor)
-    # keys with full unmodified twins take check_extra_follow_floor instead (tests/test_parity_policy.py)
-    bounded_only = {k for k in KNOWN_EXTRA_DEPARTURES if not any(k + x in RUNS for x in ("_t8", "_h1", "_h2", "_h3"))}
-    assert set(EXTRA_DEPARTURE_FOLLOWS) == bounded_only
+    # every KNOWN_EXTRA_DEPARTURES key has a floor: a named bounded twin (EXTRA_DEPARTURE_FOLLOWS) or
+    # full unmodified twins for check_extra_follow_floor (tests/test_parity_policy.py)
+    full = {k for k in KNOWN_EXTRA_DEPARTURES if any(k + x in RUNS for x in ("_t8", "_h1", "_h2", "_h3"))}
+    assert set(EXTRA_DEPARTURE_FOLLOWS) <= set(KNOWN_EXTRA_DEPARTURES)
+    assert set(EXTRA_DEPARTURE_FOLLOWS) | full == set(KNOWN_EXTRA_DEPARTURES)
     end = {"gap": 2.0, "feas": 1e-3}
     for key, (twin, n, tol) in EXTRA_DEPARTURE_FOLLOWS.items():
         t = BOUNDED_TWINS[f"{key}_{twin}"]["trace"]
