@@ -164,6 +164,32 @@ def test_oracle_full_run_maxcut5(key):
     print(key, "follows", name, ["%.0e" % v for v in per])
 
 
+@pytest.mark.parametrize("hash_seed", [16, 24, 29])
+def test_oracle_maxcut5_hash_seed_departures(hash_seed):
+    """The hash seeds test_oracle_full_run_maxcut5 does not run (the pinned seed must not
+    hide them).  Over PYTHONHASHSEED 0..30 the oracle's maxcut_5 s319 run follows one of the committed
+    unmodified reference runs (golden, _h2, _h3) on 28 seeds; on these three it takes a contraction
+    order no committed reference run took and leaves them by more than 50x their noise
+    (profiles/r06_oracle_hash_scan_s319.txt) -- at the end-point level only: same iteration count, gap within 3e-5
+    relative of the golden's.  Asserted as such, so a change that makes them depart further fails."""
+    import subprocess
+    import sys
+
+    from tests.parity_policy import check_against_reference_runs
+    key = "maxcut_5_r1_s319"
+    g = RUNS[key]
+    root = os.path.join(HERE, "..")
+    env = dict(os.environ, PYTHONHASHSEED=str(hash_seed), OPENBLAS_NUM_THREADS="1")
+    out = subprocess.run([sys.executable, "-c", _ORACLE_RUN, root, os.path.join(root, "configs", g["config"] + ".yaml"),
+                          str(g["seed"]), str(g["rank"])], env=env, capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stderr[-2000:]
+    res = json.loads(out.stdout.strip().splitlines()[-1])
+    with pytest.raises(AssertionError):
+        check_against_reference_runs(key, res["trace"], res["r"])
+    assert res["r"]["num_iters"] == g["num_iters"]
+    assert abs(res["r"]["gap"] - g["gap"]) <= 3e-5 * g["gap"], (res["r"]["gap"], g["gap"])
+
+
 class _Bounded(Exception):
     pass
 
