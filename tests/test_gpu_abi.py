@@ -1,7 +1,13 @@
 """The C ABI driven from C++ alone (tests/c/test_abi.cpp): one local KKT solve (Schur operator
 handle + whole-solve PETSc LGMRES) on two library contexts with two streams from two host threads
 concurrently; both solutions bit-identical and equal to the oracle's to 1e-8 with the same
-iteration count.  Fixture: tests/golden/make_abi_fixture.py."""
+iteration count.  Fixture: tests/golden/make_abi_fixture.py.
+
+The `*_matches_python_steps` / `*_matches_python_sweep` / `*_composition` tests below are
+CONSISTENCY checks (one native C entry against the device's own step-by-step Python path, bit for
+bit), not parity: the parity of those rows against the reference's own output is
+tests/test_gpu_local.py (a6 / a7, tests/golden/local.npz), tests/test_gpu_parity.py's golden tests
+(a13-a15) and tests/test_gpu_step.py (a19)."""
 import os
 import subprocess
 

@@ -212,6 +212,10 @@ def _lgmres_case(dev, ci):
     _close(dev.read(x), xr, 1e-8)
 
 
+# ---- CONSISTENCY tests (device against device: knob variants and native handles against the
+# per-block applies, bit for bit).  Not parity: the Schur matvec's parity is test_schur_matvec above
+# (the reference's MatVecWrapper output, 1e-13), LGMRES's is test_lgmres_matches_petsc_restatement
+# (PETSc is absent: the builder's restatement, parity unpinned).
 @pytest.mark.parametrize("ci", range(3))
 def test_schur_operator_handle_is_bit_identical(dev, ci):
     """the native 2-launch Schur operator (ttk_schur_apply) reproduces the per-block fused applies

@@ -1,6 +1,10 @@
 """Seed sharding across ranks with the gloo backend, world_size 2, on CPU:
 rank 0 creates both problems, one broadcast delivers them, each rank solves its own seed through
-the product host path (libttk emulated), results are all-gathered and match the reference."""
+the product host path (libttk emulated), results are all-gathered and match the reference.
+This checks the sharding plumbing (broadcast, schedule, all-gather) on CPU; the gap tolerance (1e-4)
+is the emulated library's, not a parity claim -- the device's end points under sharding are
+checked on hardware by the 2-rank rehearsal (profiles/r06_rehearsal_maxcut10_n2_gloo_detail.json:
+every seed ends on its N = 1 result to the last digit)."""
 import json
 import os
 import socket
