@@ -54,13 +54,15 @@ def build(force=False, verbose=False, out=OUT, defines=()):
 
 
 BIND_SRC = os.path.join(CSRC, "ttk_host_bind.cpp")
+BIND_DEPS = [BIND_SRC, os.path.join(CSRC, "ttk_host_eig.inc")]
 BIND_OUT = os.path.join(HERE, "_ttkbind" + __import__("sysconfig").get_config_var("EXT_SUFFIX"))
 
 
 def build_bind(force=False, verbose=False):
     """Host-side argument packer (`csrc/ttk_host_bind.cpp`): a torch C++ extension compiled with
     g++ (no device code), loaded next to libttk.so by dev.py."""
-    if not force and os.path.exists(BIND_OUT) and os.path.getmtime(BIND_OUT) >= os.path.getmtime(BIND_SRC):
+    if not force and os.path.exists(BIND_OUT) and \
+            all(os.path.getmtime(BIND_OUT) >= os.path.getmtime(d) for d in BIND_DEPS):
         return BIND_OUT
     import sysconfig
     import torch
@@ -68,7 +70,9 @@ def build_bind(force=False, verbose=False):
     inc = ce.include_paths() + [sysconfig.get_paths()["include"]]
     libdir = ce.library_paths()[0]
     abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
-    cmd = (["g++", "-O2", "-fPIC", "-shared", "-std=c++17", "-w", f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
+    # -ffp-contract=off: the restated host arithmetic (NumPy's polar Gaussian, the pruning sums)
+    # must round like NumPy's own, never through fused multiply-adds
+    cmd = (["g++", "-O2", "-fPIC", "-shared", "-std=c++17", "-w", "-ffp-contract=off", f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
             "-DTORCH_EXTENSION_NAME=_ttkbind", "-DTORCH_API_INCLUDE_EXTENSION_H"] + [f"-I{i}" for i in inc] +
            [BIND_SRC, "-o", BIND_OUT, f"-L{libdir}", "-lc10", "-ltorch", "-ltorch_cpu", "-ltorch_python",
             f"-Wl,-rpath,{libdir}"])

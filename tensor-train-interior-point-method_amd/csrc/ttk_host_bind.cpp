@@ -5,10 +5,18 @@
 // ctypes array), more than the kernel itself.  This module reads them natively and calls the
 // same C ABI (`include/ttk.h`: ttk_einsum, ttk_copy_nd, ttk_mul_nd) through function pointers
 // handed over from the ctypes handle, so both paths share one libttk instance (plan cache,
-// event counters).  No arithmetic happens here.
+// event counters).  No device arithmetic happens here; ttk_host_eig.inc adds the step-size
+// eigen-ALS's orchestration (host decisions and NumPy's Gaussian stream restated, same libttk calls).
 #include <torch/extension.h>
 
+#include <pybind11/numpy.h>
+
+#include <array>
+#include <cmath>
 #include <cstdint>
+#include <cstring>
+#include <functional>
+#include <mutex>
 #include <string>
 #include <unordered_map>
 #include <tuple>
@@ -67,8 +75,10 @@ struct OutMap {
   std::vector<std::pair<int, int>> src;
 };
 std::unordered_map<std::string, OutMap> g_out;
+std::mutex g_out_mu;  // the native eigen-ALS calls this without the GIL, from several solve threads
 
 const OutMap &out_map(const std::string &eq) {
+  std::lock_guard<std::mutex> lock(g_out_mu);  // map nodes are stable: the reference outlives the lock
   auto it = g_out.find(eq);
   if (it != g_out.end()) return it->second;
   OutMap m;
@@ -98,9 +108,10 @@ const OutMap &out_map(const std::string &eq) {
 
 void check(int rc, const char *what) { TORCH_CHECK(rc == 0, "libttk ", what, " failed with status ", rc); }
 
-// out = alpha * einsum(eq, ops) + beta * out (out allocated when None); flags: 256 = fused opt-in
-at::Tensor einsum(const std::string &eq, const std::vector<at::Tensor> &ops, c10::optional<at::Tensor> out,
-                  double alpha, double beta, int64_t flags) {
+// out = alpha * einsum(eq, ops) + beta * out (out allocated when None); flags: 256 = fused opt-in.
+// release: drop the GIL around the launch (the caller holds it)
+at::Tensor einsum_impl(const std::string &eq, const std::vector<at::Tensor> &ops, c10::optional<at::Tensor> out,
+                       double alpha, double beta, int64_t flags, bool release) {
   TORCH_CHECK(g_einsum, "ttk_host_bind: bind() not called");
   const int nops = (int)ops.size();
   TORCH_CHECK(nops >= 1 && nops <= 8, "einsum: ", nops, " operands");
@@ -143,7 +154,7 @@ at::Tensor einsum(const std::string &eq, const std::vector<at::Tensor> &ops, c10
   }
   double *rp = res.data_ptr<double>();
   int rc;
-  if (g_release_gil) {  // the launch itself touches no Python object: other solve threads may run meanwhile
+  if (release) {  // the launch itself touches no Python object: other solve threads may run meanwhile
     pybind11::gil_scoped_release nogil;
     rc = g_einsum(g_stream, eq.c_str(), desc, rp, alpha, beta);
   } else {  // TTK_HOLD_GIL: threads switch only where one waits for the device (dev.py)
@@ -151,6 +162,11 @@ at::Tensor einsum(const std::string &eq, const std::vector<at::Tensor> &ops, c10
   }
   check(rc, "einsum");
   return res;
+}
+
+at::Tensor einsum(const std::string &eq, const std::vector<at::Tensor> &ops, c10::optional<at::Tensor> out,
+                  double alpha, double beta, int64_t flags) {
+  return einsum_impl(eq, ops, out, alpha, beta, flags, g_release_gil);
 }
 
 // A run of einsums over block columns (the block local products of tt_als.py): item = (equation
@@ -337,6 +353,8 @@ at::Tensor transpose2(const at::Tensor &t) { return t.t(); }
 
 at::Tensor permute(const at::Tensor &t, std::vector<int64_t> dims) { return t.permute(dims); }
 
+#include "ttk_host_eig.inc"
+
 }  // namespace
 
 void set_release_gil(bool on) { g_release_gil = on; }
@@ -359,4 +377,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("view", &view);
   m.def("t", &transpose2);
   m.def("permute", &permute);
+  m.def("bind_eig", &eig::bind_eig);
+  m.def("eig_als", &eig::eig_als);
+  m.def("legacy_randn", &eig::legacy_randn);
+  m.def("prune_singular_vals", &eig::prune_singular_vals);
 }

@@ -15,6 +15,7 @@ import numpy as np
 
 from . import dev as D
 from . import rng as _rng
+from . import tt_als as _TA
 from . import tt_ops as T
 from .dev import einsum
 from .tt_als import compute_phi_bck_A, compute_phi_fwd_A
@@ -25,6 +26,10 @@ MAX_DENSE = 4096
 _DEBUG = bool(os.environ.get("TTIPM_EIG_DEBUG"))
 # normalisation / Rayleigh residual on the device with one (or no) host read; same arithmetic
 _FUSED_TAIL = os.environ.get("TTIPM_EIG_FUSED_TAIL", "1") == "1"  # diagnostics: one line per local step-size solve
+# tt_max_generalised_eigen's sweeps orchestrated in C++ (_ttkbind.eig_als, csrc/ttk_host_eig.inc): the
+# same libttk calls in the same order as the Python below, bit-identical; "0" keeps the Python path
+_NATIVE = os.environ.get("TTIPM_NATIVE_EIG", "1") == "1"
+_NATIVE_BOUND = []
 
 
 def _sym(Mt, m):
@@ -480,6 +485,36 @@ def _svd_left(x, k, rx, N, trunc_tol, max_rank):
     return D.clone(U[:, :r].t()).view(r, N[k], rx[k + 1]), v[:r], r
 
 
+def _native_eig():
+    """_ttkbind (with eig_als) when this call can run natively: the device path with the fused
+    tails and environments, and no diagnostics that observe individual wrapper calls (FLOP
+    counting, op statistics, fused-kernel checks, debug prints); else None."""
+    B = D._BIND
+    if not _NATIVE or B is None or not hasattr(B, "eig_als") or D.DEV.type != "cuda":
+        return None
+    if _DEBUG or not _FUSED_TAIL or not _TA.FUSED_ENV or D.ALGO is not None or D.OPSTATS is not None \
+            or D._CHECK_FUSED or D._FUSED_ALL:
+        return None
+    if not _NATIVE_BOUND:
+        import ctypes
+        L = D.lib
+        B.bind_eig([ctypes.cast(f, ctypes.c_void_p).value for f in (
+            L.ttk_svd_work, L.ttk_svd_tol, L.ttk_qr_work, L.ttk_qr, L.ttk_syev_extreme_work, L.ttk_syev_extreme,
+            L.ttk_read_sync, L.ttk_upload, L.ttk_cholesky_sync, L.ttk_trsm_lower, L.ttk_rayleigh_tail_dev,
+            L.ttk_rayleigh_tail_sync, L.ttk_einsum_batch_begin, L.ttk_einsum_batch_end)])
+        _NATIVE_BOUND.append(True)
+    D._stream()
+    D._fast()  # binds this thread's launch stream in the binder
+    if D._TL.batch[0]:
+        return None
+    return B
+
+
+# per process: how tt_max_generalised_eigen calls ran (native; python; native bail-outs to Python:
+# a branch only Python takes, or a libttk failure the Python rerun reports with its own exception)
+NATIVE_CALLS = {"native": 0, "python": 0, "bail": 0, "error": 0}
+
+
 def tt_max_generalised_eigen(A, Delta, x0=None, nswp=10, tol=1e-8, size_limit=256, verbose=False):
     """`src/tt_als.py:1132-1283`: largest alpha with A + alpha*Delta >= 0 (two-site ALS)."""
     if verbose:
@@ -487,9 +522,30 @@ def tt_max_generalised_eigen(A, Delta, x0=None, nswp=10, tol=1e-8, size_limit=25
         t0 = time.time()
     x = T.tt_random_gaussian([2] * (len(A) - 1), (A[0].shape[2],)) if x0 is None else x0
     d = len(x)
+    o3 = T._const("one111", np.ones((1, 1, 1)))
+    B = _native_eig() if not verbose and d >= 2 else None
+    if B is not None:
+        # the sweeps below in C++; status 1 = a case only this Python handles (LOBPCG branch, dense cap,
+        # a zero step): nothing was changed, rerun here from the same random state
+        R = _rng.R()
+        st = R.get_state()
+        status, step, max_res, _, xs, key, pos, hg, g, why = B.eig_als(
+            list(A), list(Delta), list(x), o3, int(nswp), float(tol), int(size_limit), float(tol / np.sqrt(d)),
+            int(np.floor(2 ** (d / 2))), MAX_DENSE, st[1], st[2], st[3], st[4])
+        if status == 0:
+            NATIVE_CALLS["native"] += 1
+            R.set_state(("MT19937", key, pos, hg, g))
+            x[:] = xs
+            max_res = np.float64(max_res)
+            x = T.tt_normalise(x)
+            if max_res > tol:
+                print('\t Target Residual not reached!', flush=True)
+                step *= (tol / max_res)
+            return step, x
+        NATIVE_CALLS["bail" if status == 1 else "error"] += 1
+    NATIVE_CALLS["python"] += 1
     rx = np.array([1] + T.tt_ranks(x) + [1])
     N = np.array([c.shape[1] for c in x])
-    o3 = T._const("one111", np.ones((1, 1, 1)))
     XAX = [o3] + [None] * (d - 1) + [o3]
     XDX = [o3] + [None] * (d - 1) + [o3]
     step = 1

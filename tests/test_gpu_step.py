@@ -70,6 +70,34 @@ def test_step_size_local_solves_match_reference(dev, case):
     assert departures == SC.DEVICE_RANK_DEPARTURES.get(case, set()), departures
 
 
+@pytest.mark.parametrize("case", SC.CASES)
+def test_native_eigen_als_bit_identical_to_python(dev, case):
+    """_ttkbind.eig_als (csrc/ttk_host_eig.inc: the sweeps orchestrated in C++) against tt_eig.py's
+    Python orchestration of the same libttk calls, from the same inputs and MT19937 state: the same
+    step size, solution cores and random state afterwards, bit for bit, and the native path must
+    actually have run (no silent rerun in Python)."""
+    from ttipm_amd import tt_eig as E
+    D = dev
+    A, Dl, x0, st, ref, _ = SC.call(case)
+    out = {}
+    for native in (True, False):
+        E._NATIVE = native
+        try:
+            np.random.set_state(st)
+            n0 = E.NATIVE_CALLS["native"]
+            s, x = E.tt_max_generalised_eigen(_up(D, A), _up(D, Dl), x0=_up(D, x0), tol=1e-8)
+            ran = E.NATIVE_CALLS["native"] - n0
+        finally:
+            E._NATIVE = True
+        out[native] = (s, [D.read(c) for c in x], np.random.get_state(), ran)
+    (sn, xn, rn, ran_n), (sp, xp, rp, ran_p) = out[True], out[False]
+    assert ran_n == 1 and ran_p == 0
+    assert sn == sp, (sn, sp)
+    assert [c.shape for c in xn] == [c.shape for c in xp]
+    assert all(np.array_equal(a, b) for a, b in zip(xn, xp))
+    assert np.array_equal(rn[1], rp[1]) and rn[2:] == rp[2:]
+
+
 def test_step_size_chain_s14_assembly4(dev):
     """s14's assembly-4 step pairs as the IPM makes them: predictor (c16 x, c17 z), then the corrector
     (c18 x warm-started from c16's solution, c19 z from c17's), the MT19937 stream carried from c16's

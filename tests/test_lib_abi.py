@@ -106,3 +106,45 @@ def test_native_packer_matches_python_descriptor():
     dst = torch.zeros(4, 4, dtype=torch.float64)
     mod.copy_(dst, src, -1.0, 1.0)
     assert seen["cpy"] == (src.data_ptr(), dst.data_ptr(), [4, 4], [6, 1], [4, 1], -1.0, 1.0)
+
+
+def test_native_gaussian_stream_matches_numpy():
+    """csrc/ttk_host_eig.inc restates RandomState.randn (MT19937, polar Gaussian with its cached
+    second value) for the eigen-ALS kicks: the same draws and the same state afterwards as NumPy's,
+    from states with and without a cached value and across the 624-word regeneration."""
+    import numpy as np
+    mod = _bind_module()
+    for seed in range(24):
+        R = np.random.RandomState(seed)
+        R.randn(seed * 7 + 1)
+        st = R.get_state()
+        n = (1, 3, 700, 5000)[seed % 4]
+        out, key, pos, hg, g = mod.legacy_randn(st[1], st[2], st[3], st[4], n)
+        ref = R.randn(n)
+        st2 = R.get_state()
+        assert np.array_equal(out, ref), seed
+        assert np.array_equal(key, st2[1]) and (pos, hg, g) == (st2[2], st2[3], st2[4]), seed
+
+
+def test_native_prune_matches_host_rule():
+    """The native truncation rule equals tt_ops.prune_singular_vals (cy_src/tt_ops_cy.pyx:161-177) on
+    random spectra, exact zeros, empty input and tails straddling eps^2."""
+    import numpy as np
+
+    def rule(s, eps):  # tt_ops.prune_singular_vals, restated here to keep this test device-free
+        if np.linalg.norm(s) == 0.0:
+            return 1
+        sc = np.cumsum(np.abs(s[::-1]) ** 2)[::-1]
+        r = max(int(np.argmax(sc < eps ** 2)), 1)
+        return s.size if sc[-1] > eps ** 2 else r
+
+    mod = _bind_module()
+    rs = np.random.RandomState(3)
+    cases = [(np.zeros(4), 1e-9), (np.zeros(0), 1e-9), (np.array([1.0, 1e-5, 1e-9]), 1e-9),
+             (np.array([1.0, 1e-9]), 1e-9)]
+    for _ in range(3000):
+        n = rs.randint(1, 40)
+        s = np.sort(np.abs(rs.randn(n)) * 10.0 ** rs.uniform(-12, 1, n))[::-1].copy()
+        cases.append((s, 10.0 ** rs.uniform(-10, -2) / np.sqrt(rs.randint(2, 14))))
+    for s, eps in cases:
+        assert mod.prune_singular_vals(s, eps) == rule(s, eps), (s, eps)
