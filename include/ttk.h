@@ -105,6 +105,18 @@ void *ttk_ctx_stream(ttk_ctx ctx);
  *                   bit-identical) instead of one launch per Householder step; 0: never (default from
  *                   env TTK_TRI_ONE, else 0: measured slower per call from n = 144 on -- one CU's L2
  *                   bandwidth and serial latency against 64 workgroups per step)
+ * TTK_KNOB_SVD_SWEEP_ONE  1: the multi-workgroup one-sided Jacobi of ttk_svd (min(m,n) > 96) runs
+ *                   ONE launch per sweep -- the pair waves stay resident for every round and hand
+ *                   columns to the next round through per-column counters (in-launch hand-offs);
+ *                   0: one launch per round-robin round (the same rotations in the same order:
+ *                   bit-identical; default from env TTK_SVD_SWEEP_ONE, else 0: measured 1.3-1.8x
+ *                   slower per SVD -- a column hand-off through memory costs more than the launch
+ *                   boundary it replaces, profiles/r06_persist.txt)
+ * TTK_KNOB_TRI_PERSIST  1: the per-step launches of TTK_KNOB_TRI_HOIST (128 < n <= 512) become ONE
+ *                   launch whose resident workgroups run every step, handing each step's words to the
+ *                   next through the context's arrival counter (in-launch hand-offs); 0: one launch per
+ *                   step (the same step code: bit-identical; default from env TTK_TRI_PERSIST, else 0:
+ *                   measured 1.3-2.4x slower per eigenpair, profiles/r06_persist.txt)
  * ttk_ctx_set_knob stores value and returns the previous one in *old (may be NULL). */
 enum ttk_knob {
   TTK_KNOB_FUSED_APPLY = 0,
@@ -121,7 +133,9 @@ enum ttk_knob {
   TTK_KNOB_SPLITK_FUSED = 11,
   TTK_KNOB_TRI_HOIST = 12,
   TTK_KNOB_TRI_ONE = 13,
-  TTK_KNOB_COUNT = 14
+  TTK_KNOB_SVD_SWEEP_ONE = 14,
+  TTK_KNOB_TRI_PERSIST = 15,
+  TTK_KNOB_COUNT = 16
 };
 int ttk_ctx_set_knob(ttk_ctx ctx, int knob, int value, int *old);
 int ttk_ctx_get_knob(ttk_ctx ctx, int knob, int *value);

@@ -41,6 +41,8 @@ struct Ctx {
   unsigned dep_total = 0;     // arrivals of every hand-off launch issued on this context so far
   unsigned tick_total = 0;    // workgroup tickets (dep[2]) of every hand-off launch issued so far
   unsigned *splitk_cnt = nullptr;  // per-tile arrival counters of the one-launch split-K GEMM (reset by it)
+  unsigned *colr = nullptr;   // per-column round counters of the one-launch Jacobi sweep (ttk_linalg.hip)
+  int64_t colr_n = 0;
   double *lgmres = nullptr;   // LGMRES partial sums
   int64_t lgmres_n = 0;
   int *status = nullptr;      // dense factorisation status words
@@ -61,7 +63,8 @@ struct Ctx {
                               env_int("TTK_APPLY_DUAL", 1) != 0 ? 1 : 0, env_int("TTK_RCOND_EXACT", 0) != 0 ? 1 : 0,
                               env_int("TTK_SCHUR_ONE", 1) != 0 ? 1 : 0, env_int("TTK_ARNOLDI_ONE", 1) != 0 ? 1 : 0,
                               env_int("TTK_SCHUR_PREP", 1) != 0 ? 1 : 0, env_int("TTK_SPLITK_FUSED", 1) != 0 ? 1 : 0,
-                              env_int("TTK_TRI_HOIST", 1) != 0 ? 1 : 0, env_int("TTK_TRI_ONE", 0)};
+                              env_int("TTK_TRI_HOIST", 1) != 0 ? 1 : 0, env_int("TTK_TRI_ONE", 0),
+                              env_int("TTK_SVD_SWEEP_ONE", 0) != 0 ? 1 : 0, env_int("TTK_TRI_PERSIST", 0) != 0 ? 1 : 0};
 };
 Ctx &ctx();
 Ctx *ctx_swap(Ctx *c);       // bind c to the calling thread, return the previous binding

@@ -233,6 +233,99 @@ __global__ __launch_bounds__(256) void svd_big_round_kernel(double *__restrict__
   if (lane == 0) *flag = 1;
 }
 
+// One launch per Jacobi SWEEP instead of per round (TTK_KNOB_SVD_SWEEP_ONE): the P/2 pair waves of
+// svd_big_round_kernel stay resident for all P-1 rounds of the sweep, and a wave starts its pair of
+// round r as soon as its two columns have finished round r-1 -- per-column round counters `colr`
+// (in-launch hand-offs, ttk_common.h: sc1 stores, drain, agent-scope release; the consumer polls, then
+// acquires and loads with sc1), no grid-wide barrier.  Each column belongs to exactly one pair per
+// round, so a column's rounds are totally ordered through its counter, and every rotation is
+// svd_big_round_kernel's: the same expressions on the same values in the same round order
+// (bit-identical, tools/dump_kernels.py).  The wave's pair index is its workgroup's start ticket x 4
+// + its wave index.  A wave waits only for waves of the previous round, which wait only for earlier
+// rounds; round 0 never waits, so with every workgroup resident the launch drains -- the grid is
+// P/8 <= 256 workgroups of 256 threads, far below the chip's resident capacity, and a poll past
+// DEP_SPIN_MAX gives up and is counted (dep[1], ttk_dep_timeouts) instead of hanging.
+// colr[c] = base + (rounds of this sweep column c has finished); the host zeroes colr per SVD and
+// passes base = sweep * (P - 1).
+__device__ __forceinline__ void colr_wait(const unsigned *colr, int a, int b, unsigned target, unsigned *dep) {
+  if ((threadIdx.x & 63) == 0) {
+    const __attribute__((address_space(1))) unsigned *ca = (const __attribute__((address_space(1))) unsigned *)(colr + a);
+    const __attribute__((address_space(1))) unsigned *cb = (const __attribute__((address_space(1))) unsigned *)(colr + b);
+    long n = 0;
+    while ((int)(__hip_atomic_load(ca, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) < 0 ||
+           (int)(__hip_atomic_load(cb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) < 0) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++n > ttk::DEP_SPIN_MAX) {
+        __hip_atomic_fetch_add(dep + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+#ifndef TTK_HANDOFF_RELAXED
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#endif
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);  // no column load moves above the poll
+}
+
+__global__ __launch_bounds__(256) void svd_big_sweep_kernel(double *__restrict__ W, double *__restrict__ V, int p,
+                                                            int q, double tol, int *__restrict__ flag, unsigned *colr,
+                                                            unsigned base, unsigned *dep, unsigned tick_base) {
+  const int P = (p % 2) ? p + 1 : p;
+  const int k = ttk::ticket(dep, tick_base) * 4 + (int)(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (k >= P / 2) return;  // whole wave exits together (no pair: nobody waits for it)
+  bool rot = false;
+  for (int r = 0; r < P - 1; ++r) {
+    int a, b;
+    rr_pair(P, r, k, a, b);
+    colr_wait(colr, a, b, base + (unsigned)r, dep);
+    if (b < p) {
+      double *wa = W + (int64_t)a * q, *wb = W + (int64_t)b * q;
+      double al = 0.0, be = 0.0, ga = 0.0;
+#pragma unroll 8
+      for (int i = lane; i < q; i += 64) {
+        const double x = ttk::ld_sc1(wa + i), y = ttk::ld_sc1(wb + i);
+        al += x * x;
+        be += y * y;
+        ga += x * y;
+      }
+      al = ttk::wave_sum(al);
+      be = ttk::wave_sum(be);
+      ga = ttk::wave_sum(ga);
+      if (!(al < 1e-300 || be < 1e-300) && !(ga * ga <= tol * tol * al * be)) {
+        double c, s;
+        jacobi_rotation(al, be, ga, c, s);
+#pragma unroll 8
+        for (int i = lane; i < q; i += 64) {
+          const double x = ttk::ld_sc1(wa + i), y = ttk::ld_sc1(wb + i);
+          ttk::st_sc1(wa + i, c * x - s * y);
+          ttk::st_sc1(wb + i, s * x + c * y);
+        }
+        double *va = V + (int64_t)a * p, *vb = V + (int64_t)b * p;
+#pragma unroll 8
+        for (int i = lane; i < p; i += 64) {
+          const double x = ttk::ld_sc1(va + i), y = ttk::ld_sc1(vb + i);
+          ttk::st_sc1(va + i, c * x - s * y);
+          ttk::st_sc1(vb + i, s * x + c * y);
+        }
+        rot = true;
+      }
+    }
+    // publish both columns' round r: drain the sc1 stores, release, then the counters
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#ifndef TTK_HANDOFF_RELAXED
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+    if (lane == 0) {
+      __hip_atomic_store(colr + a, base + (unsigned)r + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(colr + b, base + (unsigned)r + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  if (rot && lane == 0) *flag = 1;
+}
+
 __global__ __launch_bounds__(1024) void svd_big_finish_kernel(double *W, double *V, double *sig, int *rank, int m,
                                                               int n, double *__restrict__ U, double *__restrict__ S,
                                                               double *__restrict__ Vt) {
@@ -1978,37 +2071,47 @@ __global__ __launch_bounds__(256) void tri_step_kernel(double *A, int n, int k, 
 // pivot row -> own row).  The arithmetic, its order and every stored value are tri_step_kernel's
 // at rb = 4 (bit-identical; TTK_KNOB_TRI_HOIST = 0 switches back).  NX * 256 >= n - k,
 // NP * 64 >= nblk, NR * 64 >= n - k - 1.
-template <int NX, int NP, int NR>
-__global__ __launch_bounds__(256) void tri_step_hoist_kernel(double *A, int n, int k, double *tv, double *ov,
-                                                             double *dv, double *pvb, double *partb, double *vbuf,
-                                                             int nblk) {
-  __shared__ double xs[NX * 256 + 1];
-  __shared__ double red[16];
-  __shared__ double s_k;
+// global accesses of a tridiagonalisation step: plain (one launch per step, the kernel boundary
+// orders the steps) or sc1 (tri_persist_kernel: the steps of one launch hand their words over)
+template <bool SC>
+__device__ __forceinline__ double gld(const double *p) {
+  if constexpr (SC) return ttk::ld_sc1(p);
+  else return *p;
+}
+template <bool SC>
+__device__ __forceinline__ void gst(double *p, double v) {
+  if constexpr (SC) ttk::st_sc1(p, v);
+  else *p = v;
+}
+
+template <int NX, int NP, int NR, bool SC>
+__device__ __forceinline__ void tri_hoist_step(double *A, int n, int k, double *tv, double *ov, double *dv,
+                                               double *pvb, double *partb, double *vbuf, int nblk, int blk,
+                                               double *xs, double *red, double &s_k) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int r0 = blockIdx.x * 4, r1 = r0 + 4 < n ? r0 + 4 : n;
+  const int r0 = blk * 4, r1 = r0 + 4 < n ? r0 + 4 : n;
   const int kp = k - 1;
   const double *pvp = pvb + (kp & 1) * (int64_t)n, *ptp = partb + (kp & 1) * (int64_t)nblk;
   const double *vp = vbuf + (kp & 1) * (int64_t)n;  // reflector k-1, relative index (vp[0] = 1)
   double *pvc = pvb + (k & 1) * (int64_t)n, *ptc = partb + (k & 1) * (int64_t)nblk, *vc = vbuf + (k & 1) * (int64_t)n;
   const int m = n - k - 1;
   // ---- loads (values of buffers step k-1 did not write are read but never used: taup == 0 then)
-  const double taup = kp >= 0 ? tv[kp] : 0.0;
+  const double taup = kp >= 0 ? gld<SC>(tv + kp) : 0.0;
   double pa[NP];
 #pragma unroll
   for (int u = 0; u < NP; ++u) {
     const int i = lane + 64 * u;
-    pa[u] = (wid == 0 && i < nblk) ? ptp[i] : 0.0;
+    pa[u] = (wid == 0 && i < nblk) ? gld<SC>(ptp + i) : 0.0;
   }
-  const double v0 = vp[0], p0 = pvp[0];
+  const double v0 = gld<SC>(vp), p0 = gld<SC>(pvp);
   double xa[NX], xv[NX], xp[NX];
 #pragma unroll
   for (int u = 0; u < NX; ++u) {
     const int j = k + tid + 256 * u, jj = j - kp - 1;
     const bool ok = j < n;
-    xa[u] = ok ? A[(int64_t)k * n + j] : 0.0;
-    xv[u] = ok ? vp[jj] : 0.0;
-    xp[u] = ok ? pvp[jj] : 0.0;
+    xa[u] = ok ? gld<SC>(A + (int64_t)k * n + j) : 0.0;
+    xv[u] = ok ? gld<SC>(vp + jj) : 0.0;
+    xp[u] = ok ? gld<SC>(pvp + jj) : 0.0;
   }
   const int rs = r0 > k + 1 ? r0 : k + 1;
   const int r = rs + wid;  // this wave's own row (rb = 4: at most one per wave)
@@ -2016,16 +2119,16 @@ __global__ __launch_bounds__(256) void tri_step_hoist_kernel(double *A, int n, i
   double ra[NR], rv[NR], rp[NR], vi = 0.0, pi = 0.0;
   if (has_row) {
     const int ir = r - kp - 1;
-    vi = vp[ir];
-    pi = pvp[ir];
+    vi = gld<SC>(vp + ir);
+    pi = gld<SC>(pvp + ir);
     const double *ar = A + (int64_t)r * n;
 #pragma unroll
     for (int u = 0; u < NR; ++u) {
       const int j = k + 1 + lane + 64 * u, jj = j - kp - 1;
       const bool ok = j < n;
-      ra[u] = ok ? ar[j] : 0.0;
-      rv[u] = ok ? vp[jj] : 0.0;
-      rp[u] = ok ? pvp[jj] : 0.0;
+      ra[u] = ok ? gld<SC>(ar + j) : 0.0;
+      rv[u] = ok ? gld<SC>(vp + jj) : 0.0;
+      rp[u] = ok ? gld<SC>(pvp + jj) : 0.0;
     }
   }
   // ---- the step (tri_step_kernel's operations)
@@ -2071,18 +2174,18 @@ __global__ __launch_bounds__(256) void tri_step_hoist_kernel(double *A, int n, i
   for (int i = 1 + tid; i <= m; i += 256) {
     const double v = (i == 1) ? 1.0 : xs[i] * sc;
     xs[i] = v;
-    if (owner_k) vc[i - 1] = v;
+    if (owner_k) gst<SC>(vc + i - 1, v);
   }
   if (owner_k && tid == 0) {
-    tv[k] = tau;
-    ov[k] = beta;
-    dv[k] = xs[0];
+    gst<SC>(tv + k, tau);
+    gst<SC>(ov + k, beta);
+    gst<SC>(dv + k, xs[0]);
   }
   if (kp >= 0 && kp >= r0 && kp < r1) {  // reflector k-1 into A's row k-1: the values loaded above
 #pragma unroll
     for (int u = 0; u < NX; ++u) {
       const int j = k + tid + 256 * u;
-      if (j < n) A[(int64_t)kp * n + j] = xv[u];
+      if (j < n) gst<SC>(A + (int64_t)kp * n + j, xv[u]);
     }
   }
   __syncthreads();
@@ -2098,7 +2201,7 @@ __global__ __launch_bounds__(256) void tri_step_hoist_kernel(double *A, int n, i
         double a = ra[u];
         if (taup != 0.0) {
           a -= fma(wi, rv[u], vv * fma(-K, rv[u], rp[u]));  // tri_step_kernel's contraction
-          ar[j] = a;
+          gst<SC>(ar + j, a);
         }
         acc = fma(a, xs[j - k], acc);
       }
@@ -2106,12 +2209,48 @@ __global__ __launch_bounds__(256) void tri_step_hoist_kernel(double *A, int n, i
     acc = ttk::wave_sum(acc);
     if (lane == 0) {
       const double pr = tau * acc;
-      pvc[r - k - 1] = pr;
+      gst<SC>(pvc + r - k - 1, pr);
       contrib += pr * xs[r - k];
     }
   }
   contrib = ttk::block_sum(contrib, red);
-  if (tid == 0) ptc[blockIdx.x] = contrib;
+  if (tid == 0) gst<SC>(ptc + blk, contrib);
+}
+
+
+template <int NX, int NP, int NR>
+__global__ __launch_bounds__(256) void tri_step_hoist_kernel(double *A, int n, int k, double *tv, double *ov,
+                                                             double *dv, double *pvb, double *partb, double *vbuf,
+                                                             int nblk) {
+  __shared__ double xs[NX * 256 + 1];
+  __shared__ double red[16];
+  __shared__ double s_k;
+  tri_hoist_step<NX, NP, NR, false>(A, n, k, tv, ov, dv, pvb, partb, vbuf, nblk, blockIdx.x, xs, red, s_k);
+}
+
+// Every step of tri_step_hoist_kernel in ONE launch (TTK_KNOB_TRI_PERSIST): the nblk workgroups stay
+// resident and run the steps in turn, each step's global words handed to the next step inside the
+// launch (ttk_common.h: sc1 stores, dep_arrive = drain + barrier + agent-scope release + one counter
+// add per workgroup; dep_wait = poll until all nblk workgroups arrived from step k-1, then acquire) --
+// step k reads only what step k-1 wrote (double-buffered by step parity, as the per-step launches),
+// and a workgroup writes step k's words only after every workgroup has finished step k-1, so the
+// launch boundary between steps becomes one counter.  The step itself is tri_hoist_step, the same
+// source as the per-step kernel: bit-identical (tools/dump_kernels.py, test_gpu_kernels.py).  Roles by
+// start ticket; nblk = n / 4 <= 128 workgroups of 256 threads, well inside the chip's resident capacity;
+// a wait past DEP_SPIN_MAX is counted (ttk_dep_timeouts) instead of hanging.
+template <int NX, int NP, int NR>
+__global__ __launch_bounds__(256) void tri_persist_kernel(double *A, int n, double *tv, double *ov, double *dv,
+                                                          double *pvb, double *partb, double *vbuf, int nblk,
+                                                          unsigned *dep, unsigned target, unsigned tick_base) {
+  __shared__ double xs[NX * 256 + 1];
+  __shared__ double red[16];
+  __shared__ double s_k;
+  const int blk = ttk::ticket(dep, tick_base);
+  for (int k = 0; k + 2 < n; ++k) {
+    if (k > 0) ttk::dep_wait(dep, target + (unsigned)nblk * (unsigned)k);
+    tri_hoist_step<NX, NP, NR, true>(A, n, k, tv, ov, dv, pvb, partb, vbuf, nblk, blk, xs, red, s_k);
+    ttk::dep_arrive(dep);
+  }
 }
 
 // after the last step (k = n-3): pending update of step n-3 on the trailing 2 x 2 block and
@@ -2925,10 +3064,30 @@ static int svd_big(void *stream, const double *A, int m, int n, double *U, doubl
   const double tol = EPS * (p > 16 ? (double)p : 16.0);
   const int P = (kk % 2) ? kk + 1 : kk;
   const int grid = (P / 2 * 64 + 255) / 256;
+  ttk::Ctx &cx = ttk::ctx();
+  const bool one = cx.knob[TTK_KNOB_SVD_SWEEP_ONE] != 0 && kk > 1;
+  if (one) {  // per-column round counters (zeroed per SVD) and the context's hand-off words
+    if (cx.colr_n < P) {
+      if (cx.colr) (void)hipFree(cx.colr);
+      cx.colr = nullptr;
+      cx.colr_n = 0;
+      TTK_HIP(hipMalloc(reinterpret_cast<void **>(&cx.colr), sizeof(unsigned) * (size_t)P));
+      cx.colr_n = P;
+    }
+    TTK_HIP(hipMemsetAsync(cx.colr, 0, sizeof(unsigned) * (size_t)P, st));
+    rc = ttk::dep_counter(stream);
+    if (rc != TTK_OK) return rc;
+  }
   for (int sweep = 0; sweep < 60 && kk > 1; ++sweep) {
     TTK_HIP(hipMemsetAsync(flag, 0, sizeof(int), st));
-    for (int r = 0; r < P - 1; ++r)
-      hipLaunchKernelGGL(svd_big_round_kernel, dim3(grid), dim3(256), 0, st, X, V, kk, p, r, tol, flag);
+    if (one) {
+      hipLaunchKernelGGL(svd_big_sweep_kernel, dim3(grid), dim3(256), 0, st, X, V, kk, p, tol, flag, cx.colr,
+                         (unsigned)sweep * (unsigned)(P - 1), cx.dep, cx.tick_total);
+      cx.tick_total += (unsigned)grid;
+    } else {
+      for (int r = 0; r < P - 1; ++r)
+        hipLaunchKernelGGL(svd_big_round_kernel, dim3(grid), dim3(256), 0, st, X, V, kk, p, r, tol, flag);
+    }
     TTK_LAUNCH_CHECK();
     int h = 0;
     TTK_HIP(hipMemcpyAsync(&h, flag, sizeof(int), hipMemcpyDeviceToHost, st));
@@ -3304,6 +3463,23 @@ int ttk_syev_extreme(void *stream, const double *A, int n, int which, double *ev
       return tri_finish_launch(st, Aw, n, which, gv, ev, vec);
     }
     const int hoist = rb == 4 && n <= 512 && ttk::ctx().knob[TTK_KNOB_TRI_HOIST] ? (n <= 256 ? 1 : 2) : 0;
+    ttk::Ctx &cx = ttk::ctx();
+    if (hoist && cx.knob[TTK_KNOB_TRI_PERSIST]) {  // every step in one launch (in-launch hand-offs)
+      int rc = ttk::dep_counter(stream);
+      if (rc != TTK_OK) return rc;
+      const unsigned target = cx.dep_total, tick = cx.tick_total;
+      cx.dep_total += (unsigned)nblk * (unsigned)(n - 2);
+      cx.tick_total += (unsigned)nblk;
+      if (hoist == 1)
+        hipLaunchKernelGGL((tri_persist_kernel<1, 1, 4>), dim3(nblk), dim3(256), 0, st, Aw, n, tv, ov, dv, pvb, partb,
+                           vbuf, nblk, cx.dep, target, tick);
+      else
+        hipLaunchKernelGGL((tri_persist_kernel<2, 2, 8>), dim3(nblk), dim3(256), 0, st, Aw, n, tv, ov, dv, pvb, partb,
+                           vbuf, nblk, cx.dep, target, tick);
+      hipLaunchKernelGGL(tri_tail_kernel, dim3(1), dim3(256), 0, st, Aw, n, tv, pvb, partb, vbuf, nblk);
+      TTK_LAUNCH_CHECK();
+      return tri_finish_launch(st, Aw, n, which, gv, ev, vec);
+    }
     for (int k = 0; k + 2 < n; ++k) {
       if (hoist == 1)
         hipLaunchKernelGGL((tri_step_hoist_kernel<1, 1, 4>), dim3(nblk), dim3(256), 0, st, Aw, n, k, tv, ov, dv, pvb,

@@ -253,6 +253,7 @@ int ttk_ctx_destroy(ttk_ctx h) {
   if (c.status) (void)hipFree(c.status);
   if (c.dep) (void)hipFree(c.dep);
   if (c.splitk_cnt) (void)hipFree(c.splitk_cnt);
+  if (c.colr) (void)hipFree(c.colr);
   if (c.mapped_h) (void)hipHostFree(c.mapped_h);
   if (c.side) {
     (void)hipStreamSynchronize(c.side);

@@ -472,6 +472,60 @@ def test_syev_tri_one_workgroup_bit_identical(dev, n):
             assert np.linalg.norm(A @ v1 - l1 * v1) <= 1e-10 * scale * np.sqrt(n), name
 
 
+@pytest.mark.parametrize("n", [129, 150, 256, 257, 300, 512])
+def test_syev_tri_persistent_launch_bit_identical(dev, n):
+    """the multi-workgroup tridiagonalisation with every Householder step in one launch
+    (TTK_KNOB_TRI_PERSIST: resident workgroups, steps handed over through the arrival counter) and
+    with one launch per step give the same eigenpair bit for bit on every case of _sym_cases; no
+    hand-off wait timed out"""
+    from ttipm_amd import _lib
+    rng = _rng(31 * n)
+    for name, A in _sym_cases(n, rng):
+        for largest in (False, True):
+            out = []
+            for v in (1, 0):
+                old = _set_knob(_lib.KNOB_TRI_PERSIST, v)
+                try:
+                    lam, vec = dev.syev_extreme(dev.from_numpy(A), largest=largest)
+                finally:
+                    _set_knob(_lib.KNOB_TRI_PERSIST, old)
+                out.append((lam, dev.read(vec)))
+            (l1, v1), (l2, v2) = out
+            assert l1 == l2 and np.array_equal(v1, v2), (name, largest, l1, l2)
+            scale = max(1.0, np.abs(A).max())
+            assert np.linalg.norm(A @ v1 - l1 * v1) <= 1e-10 * scale * np.sqrt(n), name
+    dev.check_handoffs()
+
+
+@pytest.mark.parametrize("m,n,graded", [(150, 120, 0), (120, 150, 1), (300, 200, 1), (97, 97, 0), (400, 130, 0),
+                                        (260, 255, 1)])
+def test_svd_sweep_one_launch_bit_identical(dev, m, n, graded):
+    """the multi-workgroup Jacobi SVD (min(m,n) > 96) with one launch per sweep (TTK_KNOB_SVD_SWEEP_ONE:
+    resident pair waves, per-column round hand-offs) and with one launch per round give the same U, S,
+    Vt bit for bit, and the factorisation holds; no hand-off wait timed out"""
+    from ttipm_amd import _lib
+    rng = _rng(7 * m + n)
+    k = min(m, n)
+    A = rng.standard_normal((m, n))
+    if graded:
+        Uq, _ = np.linalg.qr(rng.standard_normal((m, k)))
+        Vq, _ = np.linalg.qr(rng.standard_normal((n, k)))
+        A = (Uq * np.logspace(0, -15, k)) @ Vq.T
+    out = []
+    for v in (1, 0):
+        old = _set_knob(_lib.KNOB_SVD_SWEEP_ONE, v)
+        try:
+            U, S, Vt, s = dev.svd(dev.from_numpy(A))
+        finally:
+            _set_knob(_lib.KNOB_SVD_SWEEP_ONE, old)
+        out.append((dev.read(U), dev.read(S), dev.read(Vt)))
+    for a, b in zip(*out):
+        assert np.array_equal(a, b)
+    U, S, Vt = out[0]
+    assert np.abs((U * S) @ Vt - A).max() <= 1e-12 * max(1.0, np.abs(A).max()) * np.sqrt(k)
+    dev.check_handoffs()
+
+
 def test_elementwise_and_reductions(dev):
     rng = _rng(5)
     a = rng.standard_normal((3, 4, 5))

@@ -1,0 +1,7 @@
+set -o pipefail
+for i in 1 2; do
+  for nat in 1 0; do
+    TTIPM_NATIVE_EIG=$nat timeout -k 10 240 python -u bench.py --steps 10 --warmup 1 --no-cpu-baseline --no-roofline --no-solo --detail '' > gpurun_out/ab_bench_n${nat}_$i.json 2> gpurun_out/ab_bench_n${nat}_$i.err || exit 1
+    echo "native=$nat rep $i: $(python -c "import json;d=json.load(open('gpurun_out/ab_bench_n${nat}_$i.json'));print(d['value'], d['ms_per_step'])")"
+  done
+done

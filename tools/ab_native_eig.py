@@ -16,20 +16,23 @@ from ttipm_amd import tt_ipm as I  # noqa: E402
 from ttipm_amd.utils import run_and_record  # noqa: E402
 
 EIG_T = [0.0]
-_orig = I.tt_max_generalised_eigen
+AMEN_T = [0.0]
 
 
-def _timed(*a, **k):  # device-synchronised wall time inside the step-size eigen-ALS calls
-    torch.cuda.synchronize()
-    t = time.perf_counter()
-    try:
-        return _orig(*a, **k)
-    finally:
+def _timed(f, acc):  # device-synchronised wall time inside the calls of f
+    def g(*a, **k):
         torch.cuda.synchronize()
-        EIG_T[0] += time.perf_counter() - t
+        t = time.perf_counter()
+        try:
+            return f(*a, **k)
+        finally:
+            torch.cuda.synchronize()
+            acc[0] += time.perf_counter() - t
+    return g
 
 
-I.tt_max_generalised_eigen = _timed
+I.tt_max_generalised_eigen = _timed(I.tt_max_generalised_eigen, EIG_T)
+I.tt_restarted_block_amen = _timed(I.tt_restarted_block_amen, AMEN_T)
 
 prob, cfg_name = sys.argv[1], sys.argv[2]
 seeds = [int(s) for s in sys.argv[3].split(",")]
@@ -44,14 +47,14 @@ for seed in seeds:
         for native in (True, False):
             E._NATIVE = native
             c0 = dict(E.NATIVE_CALLS)
-            EIG_T[0] = 0.0
+            EIG_T[0] = AMEN_T[0] = 0.0
             t0 = time.time()
             r = run_and_record(prob, cfg, seed, 1, verbose=False)
             dt = time.time() - t0
             calls = {k: E.NATIVE_CALLS[k] - c0[k] for k in c0}
             res[native] = r
             print(f"seed {seed} rep {rep} {'native' if native else 'python'}: {dt:.3f} s, {r['num_iters']} iters, "
-                  f"{dt / r['num_iters']:.4f} s/iter (eigen-ALS {EIG_T[0]:.3f} s), gap {r['gap']:.12e}, eig calls {calls}", flush=True)
+                  f"{dt / r['num_iters']:.4f} s/iter (eigen-ALS {EIG_T[0]:.3f} s, AMEn {AMEN_T[0]:.3f} s), gap {r['gap']:.12e}, eig calls {calls}", flush=True)
         E._NATIVE = True
         same = all(repr(res[True][k]) == repr(res[False][k]) for k in keys)
         print(f"seed {seed} rep {rep}: end points identical: {same}", flush=True)

@@ -102,6 +102,18 @@ def main(path):
                 M = (Uq * np.logspace(0, -15, k)) @ Vq.T
             U_, S_, Vt_, _ = D.svd(D.from_numpy(M), host=False)
             out[f"svd_{m_}_{n_}_{graded}"] = np.concatenate([D.read(U_).ravel(), D.read(S_).ravel(), D.read(Vt_).ravel()])
+    # multi-workgroup SVDs (QRCP launches + Jacobi sweeps), min(m, n) > 96
+    for (m_, n_) in [(150, 120), (120, 150), (300, 200), (97, 97), (400, 130), (260, 255)]:
+        for graded in (0, 1):
+            M = rng.standard_normal((m_, n_))
+            if graded:
+                k = min(m_, n_)
+                Uq, _ = np.linalg.qr(rng.standard_normal((m_, k)))
+                Vq, _ = np.linalg.qr(rng.standard_normal((n_, k)))
+                M = (Uq * np.logspace(0, -15, k)) @ Vq.T
+            U_, S_, Vt_, _ = D.svd(D.from_numpy(M), host=False)
+            out[f"svdbig_{m_}_{n_}_{graded}"] = np.concatenate([D.read(U_).ravel(), D.read(S_).ravel(),
+                                                                 D.read(Vt_).ravel()])
     # Schur-reduced local KKT matvecs (VALU rows, side by side or not; MFMA rows), chained
     from ttipm_amd import tt_ipm
     for ineq in (False, True):
