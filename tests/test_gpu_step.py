@@ -121,3 +121,52 @@ def test_step_size_chain_s14_assembly4(dev):
         assert abs(s - 0.5018947125927) <= 1e-9, s  # the documented other optimum, nothing else
         pytest.xfail(f"s14 c19 chained: {s:.10f} against the reference's {ref:.10f} (warm start from the device's "
                      "c17 eigenvectors on degenerate local eigenproblems; maxcut_10 s14 KNOWN_DEPARTURES)")
+
+
+def test_native_eigen_als_slot_threads(dev):
+    """Two solve threads of one process (bench.py's slot threads, the layout at N = 8: each with its own
+    stream, libttk context and private MT19937) run the native eigen-ALS at the same time -- it releases
+    the GIL for the whole call: every call's step, cores and random state equal the same call run alone
+    on this thread, bit for bit, and every call ran natively."""
+    import threading
+
+    import torch
+
+    from ttipm_amd import rng
+    from ttipm_amd import tt_eig as E
+    D = dev
+    cases = [c for c in SC.CASES if c.startswith("s41")][:4]
+
+    def run(c, R):
+        A, Dl, x0, st, _, _ = SC.call(c)
+        R.set_state(st)
+        s, x = E.tt_max_generalised_eigen(_up(D, A), _up(D, Dl), x0=_up(D, x0), tol=1e-8)
+        return s, [D.read(t) for t in x], R.get_state()
+
+    n0 = E.NATIVE_CALLS["native"]
+    ref = {c: run(c, np.random.mtrand._rand) for c in cases}
+    out, errs = {}, []
+
+    def work(mine):
+        try:
+            torch.cuda.set_stream(torch.cuda.Stream())
+            R = rng.private()
+            for c in mine:
+                out[c] = run(c, R)
+            torch.cuda.current_stream().synchronize()
+        except BaseException as e:  # noqa: BLE001 - reported below
+            errs.append(e)
+
+    threads = [threading.Thread(target=work, args=(cases[i::2],)) for i in range(2)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=240)
+    assert not errs, errs
+    assert E.NATIVE_CALLS["native"] - n0 == 2 * len(cases)
+    for c in cases:
+        (s0, x0, r0), (s1, x1, r1) = ref[c], out[c]
+        assert s0 == s1, (c, s0, s1)
+        assert all(np.array_equal(a, b) for a, b in zip(x0, x1)), c
+        assert np.array_equal(r0[1], r1[1]) and r0[2:] == r1[2:], c
+    D.check_handoffs()
