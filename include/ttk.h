@@ -85,7 +85,9 @@ void *ttk_ctx_stream(ttk_ctx ctx);
  *                   TTK_SCHUR_ONE, else 1)
  *   ARNOLDI_ONE     1: a multi-workgroup LGMRES Arnoldi step (partial dots, basis update, norm +
  *                   Hessenberg/Givens) is ONE launch over in-launch hand-offs; 0: three launches
- *                   (bit-identical either way; default from env TTK_ARNOLDI_ONE, else 1)
+ *                   (bit-identical either way; default from env TTK_ARNOLDI_ONE, else 0 since round 6:
+ *                   the three launches measured 7.5 % faster per graphm_3 r=2 solve, maxcut within
+ *                   noise -- profiles/r06_ab_knobs_graphm3.txt)
  *   SCHUR_PREP      1: ttk_schur_build copies every term's A (and VALU rows' Q) once into the
  *                   layout the apply rows stage in LDS, so a matvec stages them with contiguous
  *                   copies instead of strided gathers (bit-identical; read at build; default

@@ -61,7 +61,7 @@ struct Ctx {
                               env_int("TTK_SPLITK_MINK", 128) > 0 ? env_int("TTK_SPLITK_MINK", 128) : 128,
                               env_int("TTK_LGMRES_MW_MIN", 16384), env_int("TTK_MFMA_CSPLIT", 1) != 0 ? 1 : 0,
                               env_int("TTK_APPLY_DUAL", 1) != 0 ? 1 : 0, env_int("TTK_RCOND_EXACT", 0) != 0 ? 1 : 0,
-                              env_int("TTK_SCHUR_ONE", 1) != 0 ? 1 : 0, env_int("TTK_ARNOLDI_ONE", 1) != 0 ? 1 : 0,
+                              env_int("TTK_SCHUR_ONE", 1) != 0 ? 1 : 0, env_int("TTK_ARNOLDI_ONE", 0) != 0 ? 1 : 0,
                               env_int("TTK_SCHUR_PREP", 1) != 0 ? 1 : 0, env_int("TTK_SPLITK_FUSED", 1) != 0 ? 1 : 0,
                               env_int("TTK_TRI_HOIST", 1) != 0 ? 1 : 0, env_int("TTK_TRI_ONE", 0),
                               env_int("TTK_SVD_SWEEP_ONE", 0) != 0 ? 1 : 0, env_int("TTK_TRI_PERSIST", 0) != 0 ? 1 : 0};

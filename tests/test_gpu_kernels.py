@@ -832,7 +832,7 @@ def test_schur_one_launch_bit_identical(dev, ineq, dims):
 @pytest.mark.parametrize("mw_min", [0, 16384])
 def test_lgmres_one_launch_arnoldi_bit_identical(dev, ineq, mw_min):
     """whole LGMRES solves on a Schur operator: the multi-workgroup Arnoldi step as ONE launch
-    (TTK_KNOB_ARNOLDI_ONE, the default) and as three launches give the same solution, residual and
+    (TTK_KNOB_ARNOLDI_ONE) and as three launches (the default since round 6) give the same solution, residual and
     iteration count bit for bit (mw_min 0: every step on the multi-workgroup path; 16384: the
     default split), with the one-launch Schur matvec on and off, and no hand-off wait gives up"""
     import ctypes
