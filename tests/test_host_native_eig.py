@@ -43,7 +43,8 @@ def native(pkg):
 
     def cb(name, fn=None):
         res, args = L._SIGS[name]
-        c = ctypes.CFUNCTYPE(res, *args)(fn or getattr(lib, name))
+        # looked up at call time, so a test that patches the emulator patches both paths
+        c = ctypes.CFUNCTYPE(res, *args)(fn or (lambda *a: getattr(lib, name)(*a)))
         keep.append(c)
         return ctypes.cast(c, ctypes.c_void_p).value
 
@@ -118,3 +119,68 @@ def test_native_eigen_als_bails_out_to_python(pkg, native):
     nat = _run(E, D, "s41_c0", native(), size_limit=1)
     assert E.NATIVE_CALLS["bail"] == b0 + 1 and E.NATIVE_CALLS["native"] == n0
     _same(py, nat)
+
+
+def test_native_eigen_als_generalised_branch_failure(pkg, native):
+    """The generalised-eigenproblem branch's failure path (`_gen_max_eig` raising: A not positive
+    definite -> keep the previous vector, step *= 1 - eps; `src/tt_als.py:986-996`): with the emulated
+    Cholesky failing every time, every negative-eigenvalue local solve of s41_c0 takes it (109 of them
+    once the first failures have changed the path), in both orchestrations, bit for bit."""
+    from ttipm_amd import _lib as L
+    from ttipm_amd import dev as D
+    from ttipm_amd import tt_eig as E
+    lib = L.lib
+    real = type(lib).ttk_cholesky_sync
+
+    def fail(self, s, A, n):
+        self.err = b"not positive definite (forced)"
+        return 3
+
+    type(lib).ttk_cholesky_sync = fail
+    try:
+        calls = []
+        og = E._gen_max_eig
+
+        def counted(*a):
+            calls.append(1)
+            return og(*a)
+
+        E._gen_max_eig = counted
+        try:
+            py = _run(E, D, "s41_c0", None)
+        finally:
+            E._gen_max_eig = og
+        assert len(calls) >= 9  # every negative-eigenvalue solve fails over (the path then changes)
+        nat = _run(E, D, "s41_c0", native())
+    finally:
+        type(lib).ttk_cholesky_sync = real
+    _same(py, nat)
+
+
+def test_native_eigen_als_zero_step_raises_like_python(pkg, native):
+    """A generalised eigenvalue of the wrong sign makes the step max(0, 1/lam) = 0, and the residual's
+    A / step then raises ZeroDivisionError in the Python orchestration (as in the reference).  The native
+    call bails out on it (status 1, nothing changed) and the Python rerun raises the same exception."""
+    from ttipm_amd import _lib as L
+    from ttipm_amd import dev as D
+    from ttipm_amd import tt_eig as E
+    lib = L.lib
+    real = type(lib).ttk_syev_extreme
+
+    def flipped(self, s, A, n, which, ev, vec, work):
+        rc = real(self, s, A, n, which, ev, vec, work)
+        if which:  # the largest eigenpair: only _gen_max_eig asks for it
+            from tests.emu_ttk import _dv
+            _dv(ev, 1)[0] = -abs(_dv(ev, 1)[0]) - 1.0
+        return rc
+
+    type(lib).ttk_syev_extreme = flipped
+    try:
+        with pytest.raises(ZeroDivisionError):
+            _run(E, D, "s41_c0", None)
+        b0 = E.NATIVE_CALLS["bail"]
+        with pytest.raises(ZeroDivisionError):
+            _run(E, D, "s41_c0", native())
+        assert E.NATIVE_CALLS["bail"] == b0 + 1
+    finally:
+        type(lib).ttk_syev_extreme = real
