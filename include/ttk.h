@@ -119,6 +119,10 @@ void *ttk_ctx_stream(ttk_ctx ctx);
  *                   next through the context's arrival counter (in-launch hand-offs); 0: one launch per
  *                   step (the same step code: bit-identical; default from env TTK_TRI_PERSIST, else 0:
  *                   measured 1.3-2.4x slower per eigenpair, profiles/r06_persist.txt)
+ * TTK_KNOB_SYEV_WAVES8  1: the small extreme-eigenpair kernel (n < 64) runs 8 waves -- the same symv
+ *                   (2 lanes per row), the rank-2 row updates spread over 7 waves instead of 3; 0: 4
+ *                   waves (bit-identical; default from env TTK_SYEV_WAVES8, else 1: 4-9 % faster per call
+ *                   from n = 32 on, equal below, profiles/r06_syev_small.txt)
  * ttk_ctx_set_knob stores value and returns the previous one in *old (may be NULL). */
 enum ttk_knob {
   TTK_KNOB_FUSED_APPLY = 0,
@@ -137,7 +141,8 @@ enum ttk_knob {
   TTK_KNOB_TRI_ONE = 13,
   TTK_KNOB_SVD_SWEEP_ONE = 14,
   TTK_KNOB_TRI_PERSIST = 15,
-  TTK_KNOB_COUNT = 16
+  TTK_KNOB_SYEV_WAVES8 = 16,
+  TTK_KNOB_COUNT = 17
 };
 int ttk_ctx_set_knob(ttk_ctx ctx, int knob, int value, int *old);
 int ttk_ctx_get_knob(ttk_ctx ctx, int knob, int *value);

@@ -1716,11 +1716,14 @@ __device__ __forceinline__ void syev_rank2_rows_b(double *__restrict__ A22, int 
   }
 }
 
-template <int NT>
+// GG: lanes per row in the symv (NT / 128 by default: rows <= 127); <512, 2> keeps the 4-wave kernel's
+// symv (2 lanes per row, rows <= 255) and spreads only the rank-2 rows over 8 waves -- every value the
+// same expression in the same order as <256> (bit-identical; TTK_KNOB_SYEV_WAVES8 selects it)
+template <int NT, int GG = NT / 128>
 __global__ __launch_bounds__(NT) void syev_small_kernel(const double *__restrict__ Ain, int n, int which,
                                                         double *__restrict__ ev_out, double *__restrict__ vec_out,
                                                         int timing, int var) {
-  constexpr int NW = NT / 64, G = NT / 128;  // waves; lanes per row in the symv (rows <= 127)
+  constexpr int NW = NT / 64, G = GG;  // waves; lanes per row in the symv
   extern __shared__ double lds[];
   const int ld = n | 1;
   double *A = lds;
@@ -1812,7 +1815,7 @@ __global__ __launch_bounds__(NT) void syev_small_kernel(const double *__restrict
       const double K = 0.5 * tau * ttk::wave_sum(fma(p0, v0, p1 * v1));
       const double w0 = fma(-K, v0, p0), w1 = fma(-K, v1, p1);
       TTK_SSTAMP(2)
-      if (var & (NT <= 256 ? 8 : 16)) {  // wave 0 updates row 0 only, then the next reflector
+      if (var & (NT <= 512 ? 8 : 16)) {  // wave 0 updates row 0 only, then the next reflector
         if (wid == 0)
           syev_rank2_rows_b<1>(A + (k + 1) * ld + k + 1, ld, v, pv, m, 0, m, K, j0, j1, v0, v1, w0, w1, fpiv + n);
         else
@@ -3516,6 +3519,10 @@ int ttk_syev_extreme(void *stream, const double *A, int n, int which, double *ev
       allow_big_lds(syev_small_kernel<1024>, shm_s);
       hipLaunchKernelGGL(syev_small_kernel<1024>, dim3(1), dim3(1024), shm_s, st, A, n, which, ev, vec, g_svd_timing,
                          g_syev_var);
+    } else if (ttk::ctx().knob[TTK_KNOB_SYEV_WAVES8]) {
+      allow_big_lds(syev_small_kernel<512, 2>, shm_s);
+      hipLaunchKernelGGL((syev_small_kernel<512, 2>), dim3(1), dim3(512), shm_s, st, A, n, which, ev, vec,
+                         g_svd_timing, g_syev_var);
     } else {
       allow_big_lds(syev_small_kernel<256>, shm_s);
       hipLaunchKernelGGL(syev_small_kernel<256>, dim3(1), dim3(256), shm_s, st, A, n, which, ev, vec, g_svd_timing,

@@ -472,6 +472,28 @@ def test_syev_tri_one_workgroup_bit_identical(dev, n):
             assert np.linalg.norm(A @ v1 - l1 * v1) <= 1e-10 * scale * np.sqrt(n), name
 
 
+@pytest.mark.parametrize("n", [3, 8, 17, 32, 40, 63])
+def test_syev_small_eight_waves_bit_identical(dev, n):
+    """the small extreme-eigenpair kernel with 8 waves (TTK_KNOB_SYEV_WAVES8: the same symv, the rank-2
+    rows over 7 waves) and with 4 give the same eigenpair bit for bit on every case of _sym_cases"""
+    from ttipm_amd import _lib
+    rng = _rng(41 * n)
+    for name, A in _sym_cases(n, rng):
+        for largest in (False, True):
+            out = []
+            for v in (1, 0):
+                old = _set_knob(_lib.KNOB_SYEV_WAVES8, v)
+                try:
+                    lam, vec = dev.syev_extreme(dev.from_numpy(A), largest=largest)
+                finally:
+                    _set_knob(_lib.KNOB_SYEV_WAVES8, old)
+                out.append((lam, dev.read(vec)))
+            (l1, v1), (l2, v2) = out
+            assert l1 == l2 and np.array_equal(v1, v2), (name, largest, l1, l2)
+            scale = max(1.0, np.abs(A).max())
+            assert np.linalg.norm(A @ v1 - l1 * v1) <= 1e-10 * scale * np.sqrt(n), name
+
+
 @pytest.mark.parametrize("n", [129, 150, 256, 257, 300, 512])
 def test_syev_tri_persistent_launch_bit_identical(dev, n):
     """the multi-workgroup tridiagonalisation with every Householder step in one launch
