@@ -123,6 +123,11 @@ void *ttk_ctx_stream(ttk_ctx ctx);
  *                   (2 lanes per row), the rank-2 row updates spread over 7 waves instead of 3; 0: 4
  *                   waves (bit-identical; default from env TTK_SYEV_WAVES8, else 1: 4-9 % faster per call
  *                   from n = 32 on, equal below, profiles/r06_syev_small.txt)
+ * TTK_KNOB_BT_STAGE  1: the back-transform of the multi-launch extreme eigenpair (128 < n <= 513) reads
+ *                   its reflectors from LDS blocks that the finish kernel's idle waves stage while wave
+ *                   0 applies the previous block; 0: each reflector loaded from global memory one ahead
+ *                   (bit-identical; default from env TTK_BT_STAGE, else 1: 3-5 % faster per eigenpair,
+ *                   profiles/r06_bt_stage.txt)
  * ttk_ctx_set_knob stores value and returns the previous one in *old (may be NULL). */
 enum ttk_knob {
   TTK_KNOB_FUSED_APPLY = 0,
@@ -142,7 +147,8 @@ enum ttk_knob {
   TTK_KNOB_SVD_SWEEP_ONE = 14,
   TTK_KNOB_TRI_PERSIST = 15,
   TTK_KNOB_SYEV_WAVES8 = 16,
-  TTK_KNOB_COUNT = 17
+  TTK_KNOB_BT_STAGE = 17,
+  TTK_KNOB_COUNT = 18
 };
 int ttk_ctx_set_knob(ttk_ctx ctx, int knob, int value, int *old);
 int ttk_ctx_get_knob(ttk_ctx ctx, int knob, int *value);

@@ -146,7 +146,7 @@ TTK_OK, TTK_ERR_ARG, TTK_ERR_HIP, TTK_ERR_NOT_PD, TTK_ERR_SINGULAR, TTK_ERR_NOT_
 # per-context numerics knobs (include/ttk.h enum ttk_knob)
 (KNOB_FUSED_APPLY, KNOB_FUSED_MFMA, KNOB_SPLITK, KNOB_SPLITK_MINK, KNOB_LGMRES_MW_MIN, KNOB_MFMA_CSPLIT, KNOB_APPLY_DUAL,
  KNOB_RCOND_EXACT, KNOB_SCHUR_ONE, KNOB_ARNOLDI_ONE, KNOB_SCHUR_PREP, KNOB_SPLITK_FUSED, KNOB_TRI_HOIST,
- KNOB_TRI_ONE, KNOB_SVD_SWEEP_ONE, KNOB_TRI_PERSIST, KNOB_SYEV_WAVES8) = range(17)
+ KNOB_TRI_ONE, KNOB_SVD_SWEEP_ONE, KNOB_TRI_PERSIST, KNOB_SYEV_WAVES8, KNOB_BT_STAGE) = range(18)
 
 
 class TTKError(RuntimeError):

@@ -65,7 +65,7 @@ struct Ctx {
                               env_int("TTK_SCHUR_PREP", 1) != 0 ? 1 : 0, env_int("TTK_SPLITK_FUSED", 1) != 0 ? 1 : 0,
                               env_int("TTK_TRI_HOIST", 1) != 0 ? 1 : 0, env_int("TTK_TRI_ONE", 0),
                               env_int("TTK_SVD_SWEEP_ONE", 0) != 0 ? 1 : 0, env_int("TTK_TRI_PERSIST", 0) != 0 ? 1 : 0,
-                              env_int("TTK_SYEV_WAVES8", 1) != 0 ? 1 : 0};
+                              env_int("TTK_SYEV_WAVES8", 1) != 0 ? 1 : 0, env_int("TTK_BT_STAGE", 1) != 0 ? 1 : 0};
 };
 Ctx &ctx();
 Ctx *ctx_swap(Ctx *c);       // bind c to the calling thread, return the previous binding

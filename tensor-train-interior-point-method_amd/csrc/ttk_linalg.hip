@@ -1292,11 +1292,14 @@ __global__ __launch_bounds__(1024) void syev_kernel(double *__restrict__ Ain, in
 // multisection, inverse iteration, back-transform.
 // RA: the back-transform holds each reflector in registers, loaded one ahead (A in global memory: the
 // one-launch-per-step path's tri_finish_kernel); with A in LDS the plain loop is the faster one
+// stage (RA only): 2 x BT_RB x 512 doubles of LDS -- the back-transform's reflectors then come from
+// LDS, staged BT_RB rows at a time by waves 1..BT_RB while wave 0 applies the previous block
+constexpr int BT_RB = 8;
 template <bool RA = false>
 __device__ __forceinline__ void tridiag_extreme_finish(double *A, int n, int which, double *dv, double *ov, double *ev2, double *tv,
                                        double *z, double *fd, double *fdu, double *fdu2, double *fdl, double *fpiv,
                                        double *__restrict__ ev_out, double *__restrict__ vec_out, int lda,
-                                       int timing = 0) {
+                                       int timing = 0, double *stage = nullptr) {
   __shared__ double sh_a, sh_b;
   __shared__ int sh_first[2];  // round r's first shift with count >= target, by round parity
   const int tid = threadIdx.x, nt = blockDim.x;
@@ -1526,7 +1529,53 @@ __device__ __forceinline__ void tridiag_extreme_finish(double *A, int n, int whi
   // one global round trip per reflector for A's row k, then read the row again for the update; the
   // same FMAs in the same order (acc += v z, z -= acc v): bit-identical
   constexpr int BT_VR = 8;
-  if (RA && wid == 0 && n - 1 <= 64 * BT_VR && n >= 3) {
+  if (RA && stage && n - 1 <= 64 * BT_VR && n >= 3 && nt >= 64 * (BT_RB + 1)) {
+    // the same steps as the register loop below, each reflector read from an LDS block that waves
+    // 1..BT_RB filled from global memory while wave 0 worked through the previous block: wave 0's
+    // global round trip per reflector becomes one block barrier per BT_RB reflectors.  The values and
+    // the FMAs, in their order, are the register loop's (bit-identical)
+    const int ktop = n - 3, nblk = (ktop + BT_RB) / BT_RB;
+    auto stage_row = [&](int b, int r) {  // row r of block b into its slot (zeros past the reflector)
+      const int k = ktop - b * BT_RB - r;
+      if (k < 0) return;
+      const double *v = A + (int64_t)k * lda + k + 1;
+      const int m = n - k - 1;
+      double *dst = stage + ((int64_t)(b & 1) * BT_RB + r) * (64 * BT_VR);
+#pragma unroll
+      for (int u = 0; u < BT_VR; ++u) dst[lane + 64 * u] = lane + 64 * u < m ? v[lane + 64 * u] : 0.0;
+    };
+    if (wid < BT_RB) stage_row(0, wid);
+    __syncthreads();
+    for (int b = 0; b < nblk; ++b) {
+      if (wid == 0) {
+        for (int r = 0; r < BT_RB; ++r) {
+          const int k = ktop - b * BT_RB - r;
+          if (k < 0) break;
+          const double tau = tv[k];
+          if (tau != 0.0) {
+            const double *vs = stage + ((int64_t)(b & 1) * BT_RB + r) * (64 * BT_VR);
+            double vc[BT_VR];
+#pragma unroll
+            for (int u = 0; u < BT_VR; ++u) vc[u] = vs[lane + 64 * u];
+            double *zk = z + k + 1;
+            const int m = n - k - 1;
+            double acc = 0.0;
+#pragma unroll
+            for (int u = 0; u < BT_VR; ++u)
+              if (lane + 64 * u < m) acc = fma(vc[u], zk[lane + 64 * u], acc);
+            acc = tau * ttk::wave_sum(acc);
+#pragma unroll
+            for (int u = 0; u < BT_VR; ++u)
+              if (lane + 64 * u < m) zk[lane + 64 * u] = fma(-acc, vc[u], zk[lane + 64 * u]);
+            __threadfence_block();
+          }
+        }
+      } else if (wid <= BT_RB && b + 1 < nblk) {
+        stage_row(b + 1, wid - 1);
+      }
+      __syncthreads();
+    }
+  } else if (RA && wid == 0 && n - 1 <= 64 * BT_VR && n >= 3) {
     double vc[BT_VR], vn[BT_VR];
     auto load_row = [&](int k, double *dst) {
       const double *v = A + (int64_t)k * lda + k + 1;
@@ -1950,15 +1999,18 @@ __global__ __launch_bounds__(1024) void tri_finish_kernel(double *A, int n, int 
     }
     __syncthreads();
     tridiag_extreme_finish<true>(A, n, which, ldv, lov, lev2, ltv, lz, lz + n, lz + 2 * n, lz + 3 * n, lz + 4 * n,
-                           lz + 5 * n, ev_out, vec_out, n);
+                           lz + 5 * n, ev_out, vec_out, n, 0, lds == 2 ? fl + 10 * n : nullptr);
     return;
   }
   tridiag_extreme_finish<true>(A, n, which, dv, ov, ev2, tv, z, fd, fdu, fdu2, fdl, fpiv, ev_out, vec_out, n);
 }
 
+// TTK_KNOB_BT_STAGE (default 1): the back-transform's reflectors staged through LDS (lds = 2, n <= 513);
+// 0: held in registers, loaded one ahead (bit-identical either way)
 static int tri_finish_launch(hipStream_t st, double *A, int n, int which, double *gv, double *ev, double *vec) {
-  const size_t shm = 10 * (size_t)n * sizeof(double);
-  const int lds = shm <= 150000;
+  const bool stg = ttk::ctx().knob[TTK_KNOB_BT_STAGE] && n - 1 <= 512;
+  const size_t shm = (10 * (size_t)n + (stg ? 2 * (size_t)BT_RB * 512 : 0)) * sizeof(double);
+  const int lds = shm <= 150000 ? (stg ? 2 : 1) : 0;
   if (lds && shm > 65536)
     (void)hipFuncSetAttribute(reinterpret_cast<const void *>(tri_finish_kernel),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);

@@ -494,6 +494,28 @@ def test_syev_small_eight_waves_bit_identical(dev, n):
             assert np.linalg.norm(A @ v1 - l1 * v1) <= 1e-10 * scale * np.sqrt(n), name
 
 
+@pytest.mark.parametrize("n", [129, 150, 256, 300, 448, 513])
+def test_syev_staged_back_transform_bit_identical(dev, n):
+    """the multi-launch extreme eigenpair's back-transform with its reflectors staged through LDS
+    (TTK_KNOB_BT_STAGE) and loaded from global memory one ahead give the same eigenpair bit for bit"""
+    from ttipm_amd import _lib
+    rng = _rng(43 * n)
+    for name, A in _sym_cases(n, rng):
+        for largest in (False, True):
+            out = []
+            for v in (1, 0):
+                old = _set_knob(_lib.KNOB_BT_STAGE, v)
+                try:
+                    lam, vec = dev.syev_extreme(dev.from_numpy(A), largest=largest)
+                finally:
+                    _set_knob(_lib.KNOB_BT_STAGE, old)
+                out.append((lam, dev.read(vec)))
+            (l1, v1), (l2, v2) = out
+            assert l1 == l2 and np.array_equal(v1, v2), (name, largest, l1, l2)
+            scale = max(1.0, np.abs(A).max())
+            assert np.linalg.norm(A @ v1 - l1 * v1) <= 1e-10 * scale * np.sqrt(n), name
+
+
 @pytest.mark.parametrize("n", [129, 150, 256, 257, 300, 512])
 def test_syev_tri_persistent_launch_bit_identical(dev, n):
     """the multi-workgroup tridiagonalisation with every Householder step in one launch
