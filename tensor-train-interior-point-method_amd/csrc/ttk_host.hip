@@ -13,12 +13,30 @@
 
 namespace {
 
-// stream-ordered scratch released when the call returns
+// Stream-ordered scratch released when the call returns.  With a capacity (in doubles) it is one
+// hipMallocAsync carved into 256-byte slots: an allocation per buffer costs the host several us each,
+// which lands on the critical path right after a host read, while the device waits.  A request past
+// the capacity gets its own allocation, so the capacity is a hint, never a correctness bound.
 struct Scratch {
   hipStream_t st;
   std::vector<void *> ptrs;
-  explicit Scratch(hipStream_t s) : st(s) {}
+  double *base = nullptr;
+  int64_t cap = 0, used = 0;
+  static int64_t slot(int64_t n) { return ((n > 0 ? n : 1) + 31) & ~(int64_t)31; }
+  explicit Scratch(hipStream_t s, int64_t capacity = 0) : st(s) {
+    void *p = nullptr;
+    if (capacity > 0 && hipMallocAsync(&p, (size_t)capacity * sizeof(double), st) == hipSuccess) {
+      ptrs.push_back(p);
+      base = static_cast<double *>(p);
+      cap = capacity;
+    }
+  }
   double *get(int64_t n) {
+    if (base && used + slot(n) <= cap) {
+      double *p = base + used;
+      used += slot(n);
+      return p;
+    }
     void *p = nullptr;
     if (hipMallocAsync(&p, (size_t)(n > 0 ? n : 1) * sizeof(double), st) != hipSuccess) return nullptr;
     ptrs.push_back(p);
@@ -130,7 +148,7 @@ int ttk_dense_schur_solve(ttk_ctx ctx, int64_t r, int64_t n, int64_t R, const tt
                            View{q.A, 4, {q.s, n, n, q.S}, {q.a_strides[0], q.a_strides[1], q.a_strides[2], q.a_strides[3]}},
                            v3(q.R, R, q.S, R));
   };
-  Scratch sc(st);
+  Scratch sc(st, 7 * Scratch::slot(m) + 5 * Scratch::slot(m * m) + Scratch::slot(2 * m + 16) + Scratch::slot(m / 2 + 1));
   double *rd = sc.get(m), *rc = sc.get(m), *rp = sc.get(m), *LXI = sc.get(m * m), *Leq = sc.get(m * m),
          *LZ = sc.get(m * m), *t = sc.get(m), *bvec = sc.get(m), *T1 = sc.get(m * m), *Am = sc.get(m * m),
          *t2 = sc.get(m), *t3 = sc.get(m), *work = sc.get(2 * m + 16);
@@ -244,7 +262,8 @@ int ttk_dense_schur_solve_ineq(ttk_ctx ctx, int64_t r, int64_t n, int64_t R, con
                            View{q.A, 4, {q.s, n, n, q.S}, {q.a_strides[0], q.a_strides[1], q.a_strides[2], q.a_strides[3]}},
                            v3(q.R, R, q.S, R));
   };
-  Scratch sc(st);
+  Scratch sc(st, 12 * Scratch::slot(m) + 12 * Scratch::slot(m * m) + Scratch::slot(2 * m + 16) +
+                     2 * Scratch::slot(m / 2 + 1));
   double *rp = sc.get(m), *rd = sc.get(m), *rc = sc.get(m), *rt = sc.get(m), *LZ = sc.get(m * m),
          *LZ_rc = sc.get(m), *LZ_LX = sc.get(m * m), *Leq = sc.get(m * m), *Top = sc.get(m * m),
          *LZ_LXI = sc.get(m * m), *w = sc.get(m), *u = sc.get(m), *v = sc.get(m), *Am = sc.get(m * m),
@@ -365,39 +384,73 @@ int ttk_round(ttk_ctx ctx, int d, double *const *cores, const int64_t *inner, in
   if (track) eps = eps / 2.0;
   eps = eps / std::sqrt((double)(d - 1));
   std::vector<int64_t> r(ranks, ranks + d + 1);
-  Scratch sc(st);
+  // Scratch for the whole call in one allocation (Scratch above), sized up front: the QR sweep's
+  // shapes follow from the ranks alone, the SVD sweep's are bounded by them (rank <= r[idx] after
+  // the QR sweep).
+  int64_t total = 0;
+  {
+    const auto words = Scratch::slot;
+    std::vector<int64_t> q(r);
+    for (int i = d - 1; i >= 1; --i) {
+      const int64_t m = inner[i] * q[i + 1], n = q[i], k = m < n ? m : n;
+      total += words(m * n) + words(m * k) + words(k * n) + words(ttk_qr_work((int)m, (int)n)) +
+               words(q[i - 1] * inner[i - 1] * k);
+      q[i] = k;
+    }
+    int64_t rank = 1;
+    for (int idx = 0; idx + 1 < d; ++idx) {
+      const int64_t n = q[idx + 1], mb = rank * inner[idx], kb = mb < n ? mb : n;
+      int64_t wb = 0;
+      for (int64_t rr = 1; rr <= rank; ++rr) {
+        const int64_t w = ttk_svd_work((int)(rr * inner[idx]), (int)n);
+        wb = w > wb ? w : wb;
+      }
+      total += words(mb * kb) + words(kb) + words(kb * n) + words(wb) + words(kb * inner[idx + 1] * q[idx + 2]);
+      rank = kb;
+    }
+  }
+  Scratch sc(st, total);
+  bool oom = false;
+  auto get = [&](int64_t n) {
+    double *p = sc.get(n);
+    oom = oom || !p;
+    return p;
+  };
   int rc = TTK_OK;
-  // ---- right-to-left QR sweep (tt_rl_orthogonalise, cy_src/tt_ops_cy.pyx:132-159)
+  // ---- right-to-left QR sweep (tt_rl_orthogonalise, cy_src/tt_ops_cy.pyx:132-159).  Core i-1's
+  // update (cores[i-1] R^T) stays in scratch: the next step and the SVD sweep read it from there
+  // and only ever write the core's final value, so no copy back is needed.
+  const double *cur = cores[d - 1];
   for (int i = d - 1; i >= 1 && rc == TTK_OK; --i) {
     const int64_t m = inner[i] * r[i + 1], n = r[i], k = m < n ? m : n;
-    double *At = sc.get(m * n), *Q = sc.get(m * k), *R = sc.get(k * n), *w = sc.get(ttk_qr_work((int)m, (int)n));
+    double *At = get(m * n), *Q = get(m * k), *R = get(k * n), *w = get(ttk_qr_work((int)m, (int)n));
     const int64_t lead = r[i - 1] * inner[i - 1];
-    double *prev = sc.get(lead * k);
-    if (!At || !Q || !R || !w || !prev) {
+    double *prev = get(lead * k);
+    if (oom) {
       ttk::set_error("ttk_round: scratch allocation failed");
       return TTK_ERR_HIP;
     }
-    rc = copy2(st, cores[i], m, n, 1, m, At);  // unfolding (r_i, n_i R_i) transposed
+    rc = copy2(st, cur, m, n, 1, m, At);  // unfolding (r_i, n_i R_i) transposed
     if (!rc) rc = ttk_qr(st, At, (int)m, (int)n, Q, R, w);
     if (!rc) rc = copy2(st, Q, k, m, 1, k, cores[i]);  // Q^T -> core i (k, n_i, R_i)
     if (!rc) rc = einsum(st, "ij,kj->ik", {mat(cores[i - 1], lead, n), mat(R, k, n)}, prev);
-    if (!rc) rc = hipMemcpyAsync(cores[i - 1], prev, lead * k * sizeof(double), hipMemcpyDeviceToDevice, st) ? TTK_ERR_HIP : 0;
+    cur = prev;
     r[i] = k;
   }
-  // ---- left-to-right truncated-SVD sweep (cy_src/tt_ops_cy.pyx:200-222)
+  // ---- left-to-right truncated-SVD sweep (cy_src/tt_ops_cy.pyx:200-222); `cur` holds core idx
   double tail = 0.0;
   int64_t rank = 1;
   std::vector<double> s;
   for (int idx = 0; idx + 1 < d && rc == TTK_OK; ++idx) {
     const int64_t m = rank * inner[idx], n = r[idx + 1], k = m < n ? m : n;
-    double *U = sc.get(m * k), *S = sc.get(k), *Vt = sc.get(k * n), *w = sc.get(ttk_svd_work((int)m, (int)n));
+    double *U = get(m * k), *S = get(k), *Vt = get(k * n), *w = get(ttk_svd_work((int)m, (int)n));
     const int64_t rest = inner[idx + 1] * r[idx + 2];
-    double *nxt = sc.get(k * rest);
-    if (!U || !S || !Vt || !w || !nxt) {
+    double *nxt = get(k * rest);
+    if (oom) {
       ttk::set_error("ttk_round: scratch allocation failed");
       return TTK_ERR_HIP;
     }
-    rc = ttk_svd_tol(st, cores[idx], (int)m, (int)n, U, S, Vt, w, track ? 0.0 : 1e-3 * eps);
+    rc = ttk_svd_tol(st, cur, (int)m, (int)n, U, S, Vt, w, track ? 0.0 : 1e-3 * eps);
     s.assign(k, 0.0);
     if (!rc) rc = ttk_read_sync(st, S, s.data(), k);
     if (rc) break;
@@ -407,7 +460,9 @@ int ttk_round(ttk_ctx ctx, int d, double *const *cores, const int64_t *inner, in
     rc = copy2(st, U, m, nr, k, 1, cores[idx]);  // U[:, :nr] -> core idx (rank, n_idx, nr)
     const View sv{S, 1, {nr}, {1}}, vv{Vt, 2, {nr, n}, {n, 1}};
     if (!rc) rc = einsum(st, "r,rj,jk->rk", {sv, vv, mat(cores[idx + 1], n, rest)}, nxt);
-    if (!rc) rc = hipMemcpyAsync(cores[idx + 1], nxt, nr * rest * sizeof(double), hipMemcpyDeviceToDevice, st) ? TTK_ERR_HIP : 0;
+    if (!rc && idx + 2 == d)
+      rc = hipMemcpyAsync(cores[idx + 1], nxt, nr * rest * sizeof(double), hipMemcpyDeviceToDevice, st) ? TTK_ERR_HIP : 0;
+    cur = nxt;
     r[idx + 1] = nr;
     rank = nr;
   }

@@ -1,0 +1,18 @@
+#!/bin/bash
+# ttk_round before/after on one box: HEAD's library (ab/libttk_head.so) and the working tree's,
+# alternating, then the rounding parity tests and an s41 solve pair on each.
+set -o pipefail
+mkdir -p gpurun_out
+for i in 1 2; do
+  for lib in ab/libttk_head.so tensor-train-interior-point-method_amd/libttk.so; do
+    echo "== $lib ($i)"
+    TTK_LIB_PATH=$PWD/$lib timeout -k 10 120 python3 -u tools/bench_round.py 300 || exit $?
+  done
+done
+timeout -k 10 300 python3 -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_abi.py || exit $?
+for i in 1 2; do
+  for lib in ab/libttk_head.so tensor-train-interior-point-method_amd/libttk.so; do
+    echo "== s41 $lib ($i)"
+    TTK_LIB_PATH=$PWD/$lib timeout -k 10 120 python3 -u tools/solve_twice.py maxcut maxcut_10 41 1 2>&1 | grep -E "Convergence in|first" || exit $?
+  done
+done
