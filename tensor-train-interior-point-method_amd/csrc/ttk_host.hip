@@ -430,9 +430,18 @@ int ttk_round(ttk_ctx ctx, int d, double *const *cores, const int64_t *inner, in
       ttk::set_error("ttk_round: scratch allocation failed");
       return TTK_ERR_HIP;
     }
-    rc = copy2(st, cur, m, n, 1, m, At);  // unfolding (r_i, n_i R_i) transposed
-    if (!rc) rc = ttk_qr(st, At, (int)m, (int)n, Q, R, w);
-    if (!rc) rc = copy2(st, Q, k, m, 1, k, cores[i]);  // Q^T -> core i (k, n_i, R_i)
+    // core i as (r_i, n_i R_i) row-major is the unfolding's transpose: the QR kernel takes it, and
+    // leaves Q^T (core i's new (k, n_i, R_i)), in that layout; into scratch when it would overwrite
+    // its own input.  Shapes the blocked QR takes go through the transposing copies and ttk_qr.
+    double *qt = cur == cores[i] ? Q : cores[i];
+    rc = ttk::qr_colmajor(st, cur, (int)m, (int)n, qt, R, w);
+    if (rc == TTK_OK && qt != cores[i])
+      rc = hipMemcpyAsync(cores[i], qt, k * m * sizeof(double), hipMemcpyDeviceToDevice, st) ? TTK_ERR_HIP : 0;
+    if (rc == TTK_ERR_ARG) {
+      rc = copy2(st, cur, m, n, 1, m, At);  // unfolding (r_i, n_i R_i) transposed
+      if (!rc) rc = ttk_qr(st, At, (int)m, (int)n, Q, R, w);
+      if (!rc) rc = copy2(st, Q, k, m, 1, k, cores[i]);  // Q^T -> core i (k, n_i, R_i)
+    }
     if (!rc) rc = einsum(st, "ij,kj->ik", {mat(cores[i - 1], lead, n), mat(R, k, n)}, prev);
     cur = prev;
     r[i] = k;

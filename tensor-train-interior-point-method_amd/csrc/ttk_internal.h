@@ -111,6 +111,10 @@ int lu_factor_fork_rcond(hipStream_t st, double *A, int n, int *piv, double *wor
 int lu_rcond_join(hipStream_t st);
 // getrs for nrhs columns of B (one workgroup per column, n <= 12000)
 int lu_solve_cols(hipStream_t st, const double *LU, int n, const int *piv, double *B, int nrhs, int ldb);
+// ttk_linalg.hip: ttk_qr of A given column-major (At, n x m row-major) returning Q^T (k x m
+// row-major) and R as ttk_qr does, bit for bit; TTK_ERR_ARG, nothing launched, for shapes that
+// take the blocked QR (the caller transposes and calls ttk_qr)
+int qr_colmajor(void *stream, const double *At, int m, int n, double *Qt, double *R, double *work);
 
 // ttk_contract.hip: grouped launches of independent offset-table GEMM problems (the einsum
 // engine's batches).  gemm_groupable(): the problem runs on the plain 32x32-tile kernel when

@@ -731,9 +731,12 @@ __global__ __launch_bounds__(1024) void svd_wg_kernel(const double *__restrict__
 // W: m x n column-major working copy; tau: k.
 // UL: the working copy in LDS (use_lds), at compile time: LDS instructions instead of flat ones
 template <bool UL>
+// colmajor: A arrives column-major (A^T row-major) and Q leaves as Q^T row-major -- the layouts the
+// TT rounding's right-to-left sweep holds, so it needs no transposing copies around the call; only
+// the loads and stores differ, the arithmetic is the same
 __global__ __launch_bounds__(1024) void qr_kernel(const double *__restrict__ A, int m, int n,
                                                   double *__restrict__ Q, double *__restrict__ R,
-                                                  double *__restrict__ gwork, int use_lds) {
+                                                  double *__restrict__ gwork, int use_lds, int colmajor) {
   extern __shared__ double lds[];
   constexpr int CU = UL ? 8 : 4;  // loads ahead in the dot chains
   __shared__ double red[16];
@@ -746,7 +749,7 @@ __global__ __launch_bounds__(1024) void qr_kernel(const double *__restrict__ A, 
   const int lane = tid & 63, wid = tid >> 6, nw = nt >> 6;
   for (int64_t e = tid; e < (int64_t)m * n; e += nt) {
     const int j = (int)(e / m), i = (int)(e % m);
-    W[e] = A[(int64_t)i * n + j];
+    W[e] = colmajor ? A[e] : A[(int64_t)i * n + j];
   }
   __syncthreads();
   if (m <= 65) {
@@ -868,6 +871,10 @@ __global__ __launch_bounds__(1024) void qr_kernel(const double *__restrict__ A, 
     }
   }
   __syncthreads();
+  if (colmajor) {
+    for (int64_t e = tid; e < (int64_t)m * k; e += nt) Q[e] = Qc[e];
+    return;
+  }
   for (int64_t e = tid; e < (int64_t)m * k; e += nt) {
     const int i = (int)(e / k), c = (int)(e % k);
     Q[e] = Qc[(int64_t)c * m + i];
@@ -3283,7 +3290,25 @@ int64_t ttk_qr_work(int m, int n) {
   return small > big ? small : big;
 }
 
+static int qr_impl(void *stream, const double *A, int m, int n, double *Q, double *R, double *work,
+                   int colmajor);
+
 int ttk_qr(void *stream, const double *A, int m, int n, double *Q, double *R, double *work) {
+  return qr_impl(stream, A, m, n, Q, R, work, 0);
+}
+
+}  // extern "C"
+namespace ttk {
+// ttk_qr on A^T (row-major n x m, i.e. A column-major) returning Q^T (k x m row-major) and R as
+// ttk_qr does; TTK_ERR_ARG without launching anything when the shape takes the blocked path
+int qr_colmajor(void *stream, const double *At, int m, int n, double *Qt, double *R, double *work) {
+  return qr_impl(stream, At, m, n, Qt, R, work, 1);
+}
+}  // namespace ttk
+extern "C" {
+
+static int qr_impl(void *stream, const double *A, int m, int n, double *Q, double *R, double *work,
+                   int colmajor) {
   if (int brc = ttk::batch_barrier(stream)) return brc;  // an open einsum batch may feed this call
   if (m <= 0 || n <= 0) {
     ttk::set_error("ttk_qr: empty matrix %dx%d", m, n);
@@ -3292,6 +3317,7 @@ int ttk_qr(void *stream, const double *A, int m, int n, double *Q, double *R, do
   const int64_t k = m < n ? m : n;
   const int64_t need = (int64_t)m * n + k + (int64_t)m * k + 16;
   const int use_lds = need <= LDS_DOUBLES;
+  if (colmajor && k >= g_qr_big_k && (!use_lds || g_qr_big_k <= 2)) return TTK_ERR_ARG;  // caller transposes
   LinalgScope scope_(TTK_STREAM(stream), 1, m, n, k >= g_qr_big_k && (!use_lds || g_qr_big_k <= 2) ? 0 : use_lds ? 1 : 2);
   if (k >= g_qr_big_k && (!use_lds || g_qr_big_k <= 2)) return qr_big(stream, A, m, n, Q, R, work);
   const size_t shm = use_lds ? need * sizeof(double) : 0;
@@ -3301,10 +3327,10 @@ int ttk_qr(void *stream, const double *A, int m, int n, double *Q, double *R, do
   const int nt = (g_qr_narrow && m <= 65) ? 64 * (n < 16 ? (n < 1 ? 1 : n) : 16) : 1024;
   if (use_lds) {
     allow_big_lds(qr_kernel<true>, shm);
-    hipLaunchKernelGGL(qr_kernel<true>, dim3(1), dim3(nt), shm, TTK_STREAM(stream), A, m, n, Q, R, work, use_lds);
+    hipLaunchKernelGGL(qr_kernel<true>, dim3(1), dim3(nt), shm, TTK_STREAM(stream), A, m, n, Q, R, work, use_lds, colmajor);
   } else {
     allow_big_lds(qr_kernel<false>, shm);
-    hipLaunchKernelGGL(qr_kernel<false>, dim3(1), dim3(nt), shm, TTK_STREAM(stream), A, m, n, Q, R, work, use_lds);
+    hipLaunchKernelGGL(qr_kernel<false>, dim3(1), dim3(nt), shm, TTK_STREAM(stream), A, m, n, Q, R, work, use_lds, colmajor);
   }
   TTK_LAUNCH_CHECK();
   return TTK_OK;
