@@ -415,7 +415,8 @@ template <int G, int WM>
 __global__ __launch_bounds__(1024) void svd_wg_kernel(const double *__restrict__ A, int m, int n,
                                                       double *__restrict__ U, double *__restrict__ S,
                                                       double *__restrict__ Vt, double *__restrict__ gwork,
-                                                      int w_in_lds, int use_qr, int timing) {
+                                                      int w_in_lds, int use_qr, int timing,
+                                                      double *__restrict__ host_s) {
   extern __shared__ double lds[];
   constexpr bool WL = WM >= 1, ML = WM == 2;  // W in LDS; M in LDS too
   constexpr int SU = ML ? 8 : 4;  // loads ahead in the dot chains (W or M in global memory: fewer registers left)
@@ -653,6 +654,8 @@ __global__ __launch_bounds__(1024) void svd_wg_kernel(const double *__restrict__
   __syncthreads();
   TTK_PHASE(6)
   for (int j = tid; j < p; j += nt) S[rank[j]] = sig[j];
+  if (host_s)  // the caller's host-coherent copy of S (a rank decision waits on it; no read kernel)
+    for (int j = tid; j < p; j += nt) host_s[rank[j]] = sig[j];
   if (use_qr) {
     // left factor of W: M(:, rank[j]) = Q [V(:, j); 0]; g2 lanes per column, each column runs
     // through all reflectors independently (no block barriers)
@@ -3212,8 +3215,27 @@ int ttk_svd(void *stream, const double *A, int m, int n, double *U, double *S, d
   return ttk_svd_tol(stream, A, m, n, U, S, Vt, work, 0.0);
 }
 
+static int svd_tol_impl(void *stream, const double *A, int m, int n, double *U, double *S, double *Vt,
+                        double *work, double defl, double *host_s);
+
 int ttk_svd_tol(void *stream, const double *A, int m, int n, double *U, double *S, double *Vt, double *work,
                 double defl) {
+  return svd_tol_impl(stream, A, m, n, U, S, Vt, work, defl, nullptr);
+}
+
+}  // extern "C"
+namespace ttk {
+// ttk_svd_tol that also stores S into `host_s` (a device pointer to host-coherent memory) from the
+// SVD kernel itself; TTK_ERR_ARG, nothing launched, for shapes that take the multi-workgroup SVD
+int svd_tol_host(void *stream, const double *A, int m, int n, double *U, double *S, double *Vt, double *work,
+                 double defl, double *host_s) {
+  return svd_tol_impl(stream, A, m, n, U, S, Vt, work, defl, host_s);
+}
+}  // namespace ttk
+extern "C" {
+
+static int svd_tol_impl(void *stream, const double *A, int m, int n, double *U, double *S, double *Vt,
+                        double *work, double defl, double *host_s) {
   if (int brc = ttk::batch_barrier(stream)) return brc;  // an open einsum batch may feed this call
   if (m <= 0 || n <= 0) {
     ttk::set_error("ttk_svd: empty matrix %dx%d", m, n);
@@ -3221,6 +3243,7 @@ int ttk_svd_tol(void *stream, const double *A, int m, int n, double *U, double *
   }
   const int p = m < n ? m : n, q = m < n ? n : m;
   const bool forced_big = g_svd_big_p <= 2;
+  if (host_s && (p > WG_P || forced_big)) return TTK_ERR_ARG;  // the caller reads S itself
   LinalgScope scope_(TTK_STREAM(stream), 0, m, n, p > WG_P || forced_big ? 0 : -1);
   if (p > WG_P || forced_big) return svd_big(stream, A, m, n, U, S, Vt, work, defl);
   // small near-square problems converge fast without QR preconditioning; otherwise QRCP first
@@ -3248,7 +3271,7 @@ int ttk_svd_tol(void *stream, const double *A, int m, int n, double *U, double *
   {                                                                                                         \
     allow_big_lds(svd_wg_kernel<GG, MM>, shm);                                                              \
     hipLaunchKernelGGL((svd_wg_kernel<GG, MM>), dim3(1), dim3(nt), shm, TTK_STREAM(stream), A, m, n, U, S, Vt, \
-                       work, w_in_lds, use_qr, g_svd_timing);                                               \
+                       work, w_in_lds, use_qr, g_svd_timing, host_s);                                          \
   }
 #define TTK_SVD_WG(GG)                                                                                      \
   case GG:                                                                                                  \
