@@ -353,6 +353,13 @@ int ttk_svd(void *stream, const double *A, int m, int n, double *U, double *S, d
  * (`cy_src/tt_ops_cy.pyx:161-177`).  defl = 0: exact. */
 int ttk_svd_tol(void *stream, const double *A, int m, int n, double *U, double *S, double *Vt,
                 double *work, double defl);
+/* ttk_svd_tol followed by the host read of S (blocking): `s_host` receives the min(m,n) singular
+ * values, as ttk_read_sync(S) would.  On the one-workgroup path the SVD kernel stores them into
+ * host-coherent memory itself, so the host's wait follows the SVD with no read kernel between --
+ * the rank decisions of the truncated-SVD sweeps (`cy_src/tt_ops_cy.pyx:200-222`,
+ * `src/tt_als.py:269-274,457`) wait on exactly this. */
+int ttk_svd_tol_read(void *stream, const double *A, int m, int n, double *U, double *S, double *Vt,
+                     double *work, double defl, double *s_host);
 /* min(m,n) <= 96: one-workgroup kernel (column-pivoted QR + one-sided Jacobi on R^T in LDS);
  * larger: the multi-workgroup path (pivoted QR launches + one launch per Jacobi round).
  * ttk_svd_set_big_threshold(p <= 2) forces the multi-workgroup path for every size (tests);

@@ -67,6 +67,7 @@ _SIGS = {
     "ttk_svd_set_timing": (i32, [i32]),
     "ttk_svd_set_big_threshold": (i32, [i32]),
     "ttk_svd_tol": (i32, [vp, vp, i32, i32, vp, vp, vp, vp, f64]),
+    "ttk_svd_tol_read": (i32, [vp, vp, i32, i32, vp, vp, vp, vp, f64, c_dp]),
     "ttk_einsum": (i32, [vp, ctypes.c_char_p, vp, vp, f64, f64]),
     "ttk_einsum_stats": (i32, [vp]),
     "ttk_einsum_batch_begin": (i32, [vp]),
@@ -112,7 +113,7 @@ _SIGS = {
 # Entry points that wait for the device (a stream synchronisation or a blocking copy inside): they
 # release the GIL while they wait, so another solve thread of the process runs its host code then.
 BLOCKING = frozenset(n for n in _SIGS if "sync" in n) | frozenset((
-    "ttk_lgmres", "ttk_round", "ttk_zipup", "ttk_dense_schur_solve", "ttk_dense_schur_solve_ineq",
+    "ttk_lgmres", "ttk_round", "ttk_zipup", "ttk_svd_tol_read", "ttk_dense_schur_solve", "ttk_dense_schur_solve_ineq",
     "ttk_lgmres_chunk", "ttk_lgmres_build", "ttk_lgmres_aug", "ttk_schur_build", "ttk_schur_free",
     "ttk_ctx_create", "ttk_ctx_destroy", "ttk_upload", "ttk_dep_timeouts", "ttk_debug_counters",
     "ttk_mfma_profile", "ttk_contract_stats", "ttk_gemm_hist", "ttk_linalg_hist"))

@@ -459,20 +459,9 @@ int ttk_round(ttk_ctx ctx, int d, double *const *cores, const int64_t *inner, in
       ttk::set_error("ttk_round: scratch allocation failed");
       return TTK_ERR_HIP;
     }
-    // the singular values reach the host from the SVD kernel's own stores into mapped memory (no
-    // read kernel between it and the host's wait); the multi-workgroup SVD takes ttk_read_sync
-    const double defl = track ? 0.0 : 1e-3 * eps;
+    // the singular values reach the host from the SVD kernel's own stores (ttk_svd_tol_read)
     s.assign(k, 0.0);
-    double *hdev = nullptr, *h = k <= 65536 ? ttk::mapped_stage((size_t)k, &hdev) : nullptr;
-    rc = h ? ttk::svd_tol_host(st, cur, (int)m, (int)n, U, S, Vt, w, defl, hdev) : TTK_ERR_ARG;
-    if (rc == TTK_OK) {
-      ttk::note_sync();
-      rc = hipStreamSynchronize(st) ? TTK_ERR_HIP : TTK_OK;
-      if (!rc) std::memcpy(s.data(), h, (size_t)k * sizeof(double));
-    } else if (rc == TTK_ERR_ARG) {
-      rc = ttk_svd_tol(st, cur, (int)m, (int)n, U, S, Vt, w, defl);
-      if (!rc) rc = ttk_read_sync(st, S, s.data(), k);
-    }
+    rc = ttk_svd_tol_read(st, cur, (int)m, (int)n, U, S, Vt, w, track ? 0.0 : 1e-3 * eps, s.data());
     if (rc) break;
     double t = 0.0;
     const int64_t nr = truncation_rank(s, eps, track, &t);

@@ -115,10 +115,6 @@ int lu_solve_cols(hipStream_t st, const double *LU, int n, const int *piv, doubl
 // row-major) and R as ttk_qr does, bit for bit; TTK_ERR_ARG, nothing launched, for shapes that
 // take the blocked QR (the caller transposes and calls ttk_qr)
 int qr_colmajor(void *stream, const double *At, int m, int n, double *Qt, double *R, double *work);
-// ttk_linalg.hip: ttk_svd_tol whose one-workgroup kernel also stores S into host_s (device pointer
-// of host-coherent memory, mapped_stage); TTK_ERR_ARG, nothing launched, on the multi-workgroup path
-int svd_tol_host(void *stream, const double *A, int m, int n, double *U, double *S, double *Vt, double *work,
-                 double defl, double *host_s);
 
 // ttk_contract.hip: grouped launches of independent offset-table GEMM problems (the einsum
 // engine's batches).  gemm_groupable(): the problem runs on the plain 32x32-tile kernel when

@@ -21,6 +21,7 @@
 #include <array>
 #include <chrono>
 #include <cstdio>
+#include <cstring>
 #include <map>
 #include <mutex>
 
@@ -3223,16 +3224,26 @@ int ttk_svd_tol(void *stream, const double *A, int m, int n, double *U, double *
   return svd_tol_impl(stream, A, m, n, U, S, Vt, work, defl, nullptr);
 }
 
-}  // extern "C"
-namespace ttk {
-// ttk_svd_tol that also stores S into `host_s` (a device pointer to host-coherent memory) from the
-// SVD kernel itself; TTK_ERR_ARG, nothing launched, for shapes that take the multi-workgroup SVD
-int svd_tol_host(void *stream, const double *A, int m, int n, double *U, double *S, double *Vt, double *work,
-                 double defl, double *host_s) {
-  return svd_tol_impl(stream, A, m, n, U, S, Vt, work, defl, host_s);
+
+int ttk_svd_tol_read(void *stream, const double *A, int m, int n, double *U, double *S, double *Vt,
+                     double *work, double defl, double *s_host) {
+  if (!s_host) {
+    ttk::set_error("ttk_svd_tol_read: null host buffer");
+    return TTK_ERR_ARG;
+  }
+  const int64_t k = m < n ? m : n;
+  double *hdev = nullptr, *h = k > 0 && k <= 65536 ? ttk::mapped_stage((size_t)k, &hdev) : nullptr;
+  int rc = h ? svd_tol_impl(stream, A, m, n, U, S, Vt, work, defl, hdev) : TTK_ERR_ARG;
+  if (rc == TTK_OK) {
+    ttk::note_sync();
+    TTK_HIP(hipStreamSynchronize(TTK_STREAM(stream)));
+    std::memcpy(s_host, h, (size_t)k * sizeof(double));
+    return TTK_OK;
+  }
+  if (rc != TTK_ERR_ARG || m <= 0 || n <= 0) return rc;
+  rc = svd_tol_impl(stream, A, m, n, U, S, Vt, work, defl, nullptr);  // the multi-workgroup path
+  return rc ? rc : ttk_read_sync(stream, S, s_host, k);
 }
-}  // namespace ttk
-extern "C" {
 
 static int svd_tol_impl(void *stream, const double *A, int m, int n, double *U, double *S, double *Vt,
                         double *work, double defl, double *host_s) {

@@ -641,6 +641,9 @@ _DUMP = {"min": int(os.environ.get("TTIPM_DUMP_SVD", "0")), "max": int(os.enviro
          "qmin": int(os.environ.get("TTIPM_DUMP_SVD_QMIN", "0")), "n": 0}
 
 
+_SVD_READ = hasattr(lib, "ttk_svd_tol_read")  # False only for an older library under TTK_LIB_PATH
+
+
 def svd(A, defl=0.0, host=True, S_out=None):
     """Thin SVD of a 2-D device matrix.  Returns (U, S, Vt, s_host).  `defl` > 0 lets the large-
     matrix path deflate directions whose total Frobenius norm is <= defl (S = 0 there).
@@ -660,8 +663,13 @@ def svd(A, defl=0.0, host=True, S_out=None):
     work = empty(int(lib.ttk_svd_work(m, n)))
     # p > 96 takes the multi-launch path (host loops over Jacobi rounds): release the GIL meanwhile
     L = lib_release if min(m, n) > 96 else lib
-    check(L.ttk_svd_tol(_stream(), _p(A), m, n, _p(U), _p(S), _p(Vt), _p(work), float(defl)), "svd")
-    sh = read(S) if host else None
+    if host and _SVD_READ:  # the SVD and the host read of S in one call (the kernel stores S itself)
+        sh = np.empty(k, dtype=np.float64)
+        check(lib.ttk_svd_tol_read(_stream(), _p(A), m, n, _p(U), _p(S), _p(Vt), _p(work), float(defl),
+                                 sh.ctypes.data_as(c_dp)), "svd")
+    else:
+        check(L.ttk_svd_tol(_stream(), _p(A), m, n, _p(U), _p(S), _p(Vt), _p(work), float(defl)), "svd")
+        sh = read(S) if host else None
     if OPSTATS is not None:
         _stat("svd", (m, n), t0, site_min=min(m, n) >= 64)
     return U, S, Vt, sh

@@ -374,6 +374,10 @@ class EmuLib:
     def ttk_svd_tol(self, s, A, m, n, U, S, Vt, work, defl):
         return self.ttk_svd(s, A, m, n, U, S, Vt, work)
 
+    def ttk_svd_tol_read(self, s, A, m, n, U, S, Vt, work, defl, s_host):
+        rc = self.ttk_svd_tol(s, A, m, n, U, S, Vt, work, defl)
+        return rc or self.ttk_read_sync(s, S, s_host, min(m, n))
+
     def ttk_svd_set_big_threshold(self, p):
         return 64
 

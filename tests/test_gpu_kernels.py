@@ -570,6 +570,27 @@ def test_svd_sweep_one_launch_bit_identical(dev, m, n, graded):
     dev.check_handoffs()
 
 
+@pytest.mark.parametrize("m,n", [(16, 4), (4, 16), (32, 32), (96, 40), (200, 97), (130, 300)])
+def test_svd_tol_read_equals_svd_then_read(dev, m, n):
+    """ttk_svd_tol_read (the one-workgroup SVD kernel storing S into host-coherent memory itself; the
+    multi-workgroup path for min(m,n) > 96 reading S afterwards) = ttk_svd_tol + ttk_read_sync, bit
+    for bit: U, S, Vt on the device and the host copy of S"""
+    rng = _rng(11 * m + n)
+    A = dev.from_numpy(rng.standard_normal((m, n)) * np.logspace(0, -8, n))
+    old = dev._SVD_READ
+    out = []
+    try:
+        for v in (True, False):
+            dev._SVD_READ = v
+            U, S, Vt, s = dev.svd(A, defl=1e-10)
+            out.append((dev.read(U), dev.read(S), dev.read(Vt), s))
+    finally:
+        dev._SVD_READ = old
+    for a, b in zip(*out):
+        assert a.shape == b.shape and np.array_equal(a, b)
+    assert np.array_equal(out[0][3], out[0][1])
+
+
 def test_elementwise_and_reductions(dev):
     rng = _rng(5)
     a = rng.standard_normal((3, 4, 5))
