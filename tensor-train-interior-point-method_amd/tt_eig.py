@@ -501,7 +501,8 @@ def _native_eig():
         B.bind_eig([ctypes.cast(f, ctypes.c_void_p).value for f in (
             L.ttk_svd_work, L.ttk_svd_tol, L.ttk_qr_work, L.ttk_qr, L.ttk_syev_extreme_work, L.ttk_syev_extreme,
             L.ttk_read_sync, L.ttk_upload, L.ttk_cholesky_sync, L.ttk_trsm_lower, L.ttk_rayleigh_tail_dev,
-            L.ttk_rayleigh_tail_sync, L.ttk_einsum_batch_begin, L.ttk_einsum_batch_end)])
+            L.ttk_rayleigh_tail_sync, L.ttk_einsum_batch_begin, L.ttk_einsum_batch_end)
+            + ((L.ttk_svd_tol_read,) if D._SVD_READ else ())])
         _NATIVE_BOUND.append(True)
     D._stream()
     D._fast()  # binds this thread's launch stream in the binder

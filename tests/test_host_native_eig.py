@@ -62,7 +62,7 @@ def native(pkg):
     b3 = [cb(n) if n != "ttk_rayleigh_tail_sync" else cb(n, ray_sync) for n in (
         "ttk_svd_work", "ttk_svd_tol", "ttk_qr_work", "ttk_qr", "ttk_syev_extreme_work", "ttk_syev_extreme",
         "ttk_read_sync", "ttk_upload", "ttk_cholesky_sync", "ttk_trsm_lower", "ttk_rayleigh_tail_dev",
-        "ttk_rayleigh_tail_sync", "ttk_einsum_batch_begin", "ttk_einsum_batch_end")]
+        "ttk_rayleigh_tail_sync", "ttk_einsum_batch_begin", "ttk_einsum_batch_end", "ttk_svd_tol_read")]
 
     def rebind():  # the binder's entry points are process-wide: (re)bind before each use
         mod.bind(*b1)
